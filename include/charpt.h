@@ -1,0 +1,149 @@
+/*
+ * charpt -- MI355X-native (gfx950/CDNA4) kernels for the char-level GPT hot path of
+ * ChaitIITB/ReplicatingGPT GPT1.py.  C ABI of libcharpt_hip.so.
+ *
+ * The reference has no native plugin API: its replaceable seam is the nn.Module surface and
+ * the aten ops those modules call.  Every entry point below replaces one or
+ * more of those aten call sites; the citation on each names the GPT1.py line(s) it stands in
+ * for.  Python binds these through ctypes (replicatinggpt_amd/_lib.py) and registers them as
+ * torch.library custom ops (replicatinggpt_amd/ops.py).
+ *
+ * Conventions
+ *   - all pointers are DEVICE pointers unless noted; the caller (PyTorch's caching allocator)
+ *     owns every buffer; the library never allocates, frees or synchronises the host.
+ *   - every function is stream-ordered on `stream` (a hipStream_t, passed as void*), so it is
+ *     capturable into a hipGraph.
+ *   - return CG_OK (0) or an error code; cg_last_error_string() gives the message.
+ *   - dtype codes: CG_F32 = 0 (float), CG_BF16 = 1 (bfloat16 bits, RNE rounding).
+ *   - dropout: Philox4x32-10 counter RNG, spec in oracle/philox.py and DESIGN.md; the stream id
+ *     is ((*rng_call) << 8) | site, with rng_call a device uint64 snapshot per forward call.
+ */
+#ifndef CHARPT_H
+#define CHARPT_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { CG_OK = 0, CG_EINVAL = 1, CG_EHIP = 2, CG_EUNSUPPORTED = 3 };
+enum { CG_F32 = 0, CG_BF16 = 1 };
+
+/* GEMM epilogues (applied to acc = sum_k A(m,k) B(n,k), per output element (m,n)) */
+enum {
+    CG_EPI_STORE = 0,        /* out = acc                                                       */
+    CG_EPI_BIAS = 1,         /* out = acc + bias[n]                                             */
+    CG_EPI_BIAS_RELU = 2,    /* out = relu(acc + bias[n])               (GPT1.py:143-144)       */
+    CG_EPI_BIAS_RESID = 3,   /* out = resid[m,n] + acc + bias[n]  (resid NULL: no add; :136,163) */
+    CG_EPI_BIAS_DROP_RESID = 4, /* out = resid + dropout(acc + bias)    (GPT1.py:145-146,164)   */
+    CG_EPI_RELU_BWD = 5      /* out = acc * (aux[m,n] > 0)              (ReLU backward, :144)   */
+};
+
+typedef struct {
+    int kind;                 /* CG_EPI_*                                                    */
+    const float* bias;        /* [N] fp32 or NULL                                            */
+    const float* resid;       /* fp32, row stride ld_resid                                   */
+    int64_t ld_resid;
+    const void* aux;          /* CG_EPI_RELU_BWD: relu output, dtype aux_dtype, stride ld_aux */
+    int aux_dtype;
+    int64_t ld_aux;
+    double dropout_p;         /* CG_EPI_BIAS_DROP_RESID                                      */
+    uint64_t seed;
+    const uint64_t* rng_call; /* device scalar                                               */
+    int site;
+    float beta;               /* out = epi(acc) + beta * out   (beta in {0,1}: grad accumulate) */
+} cg_epilogue_t;
+
+const char* cg_last_error_string(void);
+int cg_version(void);
+int cg_device_info(int* n_cu, int* arch_major, int* arch_minor);
+
+/* ---- utility ------------------------------------------------------------------------ */
+/* *counter += delta (one thread); snapshot variant: *snap = *counter, *counter += 1.       */
+int cg_counter_add(int64_t* counter, int64_t delta, void* stream);
+int cg_rng_snapshot(uint64_t* counter, uint64_t* snap, void* stream);
+/* dst[i] = dropout keep-mask (1.0 / 0.0) for element i in [0,n), for tests of the RNG.    */
+int cg_dropout_mask(float* dst, int64_t n, double p, uint64_t seed, const uint64_t* rng_call, int site,
+                    void* stream);
+/* y[r,c] = x[r,c] * keep(r*C+c) * 1/(1-p)  (dropout backward / apply; p=0 -> plain cast);
+   x fp32 [rows, C] (row stride ldx), y dtype y_dtype [rows, C] contiguous.                  */
+int cg_dropout_apply(const float* x, int64_t rows, int64_t C, int64_t ldx, void* y, int y_dtype, double p,
+                     uint64_t seed, const uint64_t* rng_call, int site, void* stream);
+/* deterministic sum of n floats into *out (two-pass); ws >= 1024 floats; out = scale*sum   */
+int cg_sum_f32(const float* x, int64_t n, float scale, float* out, float* ws, void* stream);
+/* fp32 -> bf16 cast (RNE), n elements                                                       */
+int cg_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, void* stream);
+
+/* ---- data: get_batch on device (GPT1.py:75-83) ---------------------------------------- */
+/* x[b,t] = data[ix[b]+t], y[b,t] = data[ix[b]+t+1]; data is the token stream (int64 or uint8) */
+int cg_gather_batch(const void* data, int data_is_u8, const int64_t* ix, int64_t* x, int64_t* y,
+                    int64_t B, int64_t T, void* stream);
+
+/* ---- embeddings (GPT1.py:179-181) ------------------------------------------------------ */
+/* x[b,t,:] = wte[idx[b,t],:] + wpe[t,:]  (fp32)                                          */
+int cg_embed_fwd(const int64_t* idx, const float* wte, const float* wpe, float* x, int64_t B, int64_t T,
+                 int64_t C, int64_t V, void* stream);
+/* dwte[v,:] (=|+=) sum_{idx=v} dx ; dwpe[t,:] (=|+=) sum_b dx[b,t,:]   deterministic.
+   workspace: cg_embed_bwd_workspace(B,T,C,V) bytes.                                          */
+int64_t cg_embed_bwd_workspace(int64_t B, int64_t T, int64_t C, int64_t V);
+int cg_embed_bwd(const int64_t* idx, const float* dx, float* dwte, float* dwpe, int64_t B, int64_t T,
+                 int64_t C, int64_t V, int accumulate, void* workspace, void* stream);
+
+/* ---- LayerNorm (nn.LayerNorm, GPT1.py:159-160,173) -------------------------------------- */
+/* y = (x-mu)*rstd*w + b, biased variance, eps; y dtype y_dtype; saves mean/rstd [rows]     */
+int cg_layernorm_fwd(const float* x, const float* w, const float* b, void* y, int y_dtype, float* mean,
+                     float* rstd, int64_t rows, int64_t C, float eps, void* stream);
+/* dx = dres + LN'(dy)  (dres may be NULL); dx_bf16 optional bf16 copy of dx;
+   dw/db (=|+=) column sums; workspace: cg_layernorm_bwd_workspace(rows,C) bytes.           */
+int64_t cg_layernorm_bwd_workspace(int64_t rows, int64_t C);
+int cg_layernorm_bwd(const void* dy, int dy_dtype, const float* x, const float* w, const float* mean,
+                     const float* rstd, const float* dres, float* dx, uint16_t* dx_bf16, float* dw, float* db,
+                     int accumulate, void* workspace, int64_t rows, int64_t C, void* stream);
+
+/* ---- GEMM (nn.Linear fwd/dgrad/wgrad: GPT1.py:111-112,121,136,143,145,184) -------------
+   C[m,n] = epilogue( sum_k A(m,k) * B(n,k) )
+   A(m,k) = A[m*lda+k] (a_trans=0) or A[k*lda+m] (a_trans=1); same for B with b_trans.
+   op_dtype: CG_BF16 (bf16 MFMA, fp32 accumulate) or CG_F32 (exact-f32 MFMA).
+   c_dtype: output dtype.  split_k > 1 (CG_EPI_STORE/BIAS only) needs workspace of
+   cg_gemm_workspace(M,N,split_k) bytes; results are deterministic for any split_k.            */
+int64_t cg_gemm_workspace(int64_t M, int64_t N, int split_k);
+int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+            const void* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const cg_epilogue_t* epi, int split_k,
+            void* workspace, void* stream);
+/* column sums of a [rows, N] matrix (bias gradients): out[n] (=|+=) sum_m X[m,n]            */
+int64_t cg_colsum_workspace(int64_t rows, int64_t N);
+int cg_colsum(const void* X, int x_dtype, int64_t rows, int64_t N, int64_t ldx, float* out, int accumulate,
+              void* workspace, void* stream);
+
+/* ---- causal self-attention, all heads (Head.forward GPT1.py:109-123 x n_head, :135) -------
+   q/k/v element (b,t,h,e) at ptr[(b*T+t)*ld_qkv + h*D + e]; o at o[(b*T+t)*ld_o + h*D + e].
+   P = softmax(mask(q k^T * scale)); P = dropout(P); o = P v.  lse[b,h,t] (fp32) saved.      */
+int cg_attn_fwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const void* q, const void* k,
+                const void* v, int64_t ld_qkv, void* o, int64_t ld_o, float* lse, float scale, double dropout_p,
+                uint64_t seed, const uint64_t* rng_call, int site, void* stream);
+/* dq/dk/dv written (not accumulated) with stride ld_dqkv; workspace cg_attn_bwd_workspace. */
+int64_t cg_attn_bwd_workspace(int64_t B, int64_t T, int64_t H, int64_t D);
+int cg_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const void* q, const void* k,
+                const void* v, int64_t ld_qkv, const void* o, int64_t ld_o, const void* dout, int64_t ld_do,
+                const float* lse, void* dq, void* dk, void* dv, int64_t ld_dqkv, float scale, double dropout_p,
+                uint64_t seed, const uint64_t* rng_call, int site, void* workspace, void* stream);
+
+/* ---- cross entropy over the char vocabulary (F.cross_entropy, GPT1.py:189-192) ----------
+   logits fp32 [rows, V] (row stride ld); loss_rows[r] = lse_r - logit[r, tgt_r]; lse saved.
+   bwd: dlogits = (*g) * g_mult * (softmax - onehot)   (g = dLoss, g_mult = 1/rows).                    */
+int cg_ce_fwd(const float* logits, int64_t rows, int64_t V, int64_t ld, const int64_t* targets, float* loss_rows,
+              float* lse, void* stream);
+int cg_ce_bwd(const float* logits, int64_t rows, int64_t V, int64_t ld, const int64_t* targets, const float* lse,
+              const float* g, float g_mult, float* dlogits, int64_t ld_d, void* dst_lp /* optional bf16 copy */,
+              void* stream);
+
+/* ---- fused AdamW over a flat fp32 buffer (torch.optim.AdamW, GPT1.py:218,233) ------------
+   step_ptr: device int64 step count (already incremented for this step).
+   p_bf16: optional bf16 shadow written after the update (GEMM operands).                    */
+int cg_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, double lr, double beta1,
+             double beta2, double eps, double weight_decay, const int64_t* step_ptr, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CHARPT_H */

@@ -1,0 +1,106 @@
+"""ctypes binding of libcharpt_hip.so (the C ABI declared in include/charpt.h).
+
+The library is built in-tree (``python __graft_entry__.py`` / ``make -C replicatinggpt_amd/csrc``)
+and must be present: there is no CPU or eager-PyTorch fallback for the product path.
+"""
+import ctypes
+import os
+import re
+
+import torch  # noqa: F401  -- load torch's HIP runtime first so the library binds to the same one
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcharpt_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "charpt.h")
+
+CG_F32, CG_BF16 = 0, 1
+EPI_STORE, EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_RESID, EPI_BIAS_DROP_RESID, EPI_RELU_BWD = range(6)
+
+c_i64, c_int, c_dbl, c_flt, c_u64, P = ctypes.c_int64, ctypes.c_int, ctypes.c_double, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p
+
+
+class Epilogue(ctypes.Structure):
+    _fields_ = [("kind", c_int), ("bias", P), ("resid", P), ("ld_resid", c_i64), ("aux", P), ("aux_dtype", c_int),
+                ("ld_aux", c_i64), ("dropout_p", c_dbl), ("seed", c_u64), ("rng_call", P), ("site", c_int),
+                ("beta", c_flt)]
+
+
+_SIGS = {
+    "cg_last_error_string": (ctypes.c_char_p, []),
+    "cg_version": (c_int, []),
+    "cg_device_info": (c_int, [P, P, P]),
+    "cg_counter_add": (c_int, [P, c_i64, P]),
+    "cg_rng_snapshot": (c_int, [P, P, P]),
+    "cg_dropout_mask": (c_int, [P, c_i64, c_dbl, c_u64, P, c_int, P]),
+    "cg_dropout_apply": (c_int, [P, c_i64, c_i64, c_i64, P, c_int, c_dbl, c_u64, P, c_int, P]),
+    "cg_sum_f32": (c_int, [P, c_i64, c_flt, P, P, P]),
+    "cg_cast_f32_bf16": (c_int, [P, P, c_i64, P]),
+    "cg_gather_batch": (c_int, [P, c_int, P, P, P, c_i64, c_i64, P]),
+    "cg_embed_fwd": (c_int, [P, P, P, P, c_i64, c_i64, c_i64, c_i64, P]),
+    "cg_embed_bwd_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
+    "cg_embed_bwd": (c_int, [P, P, P, P, c_i64, c_i64, c_i64, c_i64, c_int, P, P]),
+    "cg_layernorm_fwd": (c_int, [P, P, P, P, c_int, P, P, c_i64, c_i64, c_flt, P]),
+    "cg_layernorm_bwd_workspace": (c_i64, [c_i64, c_i64]),
+    "cg_layernorm_bwd": (c_int, [P, c_int, P, P, P, P, P, P, P, P, P, c_int, P, c_i64, c_i64, P]),
+    "cg_gemm_workspace": (c_i64, [c_i64, c_i64, c_int]),
+    "cg_gemm": (c_int, [c_int, c_int, c_int, c_i64, c_i64, c_i64, P, c_i64, P, c_i64, P, c_int, c_i64,
+                        ctypes.POINTER(Epilogue), c_int, P, P]),
+    "cg_colsum_workspace": (c_i64, [c_i64, c_i64]),
+    "cg_colsum": (c_int, [P, c_int, c_i64, c_i64, c_i64, P, c_int, P, P]),
+    "cg_attn_fwd": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, P, P, P, c_i64, P, c_i64, P, c_flt, c_dbl, c_u64, P,
+                            c_int, P]),
+    "cg_attn_bwd_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
+    "cg_attn_bwd": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, P, P, P, c_i64, P, c_i64, P, c_i64, P, P, P, P, c_i64,
+                            c_flt, c_dbl, c_u64, P, c_int, P, P]),
+    "cg_ce_fwd": (c_int, [P, c_i64, c_i64, c_i64, P, P, P, P]),
+    "cg_ce_bwd": (c_int, [P, c_i64, c_i64, c_i64, P, P, P, c_flt, P, c_i64, P, P]),
+    "cg_adamw": (c_int, [P, P, P, P, P, c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, P, P]),
+}
+
+_lib = None
+
+
+def header_symbols():
+    """Every cg_* function declared in include/charpt.h."""
+    src = open(HEADER_PATH).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(cg_\w+)\s*\(", src)))
+
+
+def load():
+    """Load (once) and return the ctypes library; raises if it is missing -- no fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"charpt: {LIB_PATH} is not built; run `python __graft_entry__.py` (build()) first. "
+                           "There is no CPU fallback for the HIP hot path.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = load().cg_last_error_string().decode(errors="replace")
+        raise RuntimeError(f"charpt {what} failed (code {rc}): {msg}")
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def dtype_code(dt):
+    if dt == torch.float32:
+        return CG_F32
+    if dt == torch.bfloat16:
+        return CG_BF16
+    raise TypeError(f"charpt: unsupported dtype {dt}")
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

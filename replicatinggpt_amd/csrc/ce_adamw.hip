@@ -1,0 +1,141 @@
+// charpt: cross entropy over the character vocabulary (F.cross_entropy, GPT1.py:189-192) and
+// the fused AdamW step over flat fp32 buffers (torch.optim.AdamW, GPT1.py:218,233).
+#include <math.h>
+
+#include "common.h"
+
+using namespace cg;
+
+// ---- cross entropy: one wave per row, V <= 64*16 ------------------------------------------
+__global__ __launch_bounds__(256) void k_ce_fwd(const float* __restrict__ logits, int64_t rows, int V, int64_t ld,
+                                                const int64_t* __restrict__ targets, float* __restrict__ loss_rows,
+                                                float* __restrict__ lse) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const float* x = logits + r * ld;
+    float mx = -INFINITY;
+    for (int v = lane; v < V; v += 64) mx = fmaxf(mx, x[v]);
+    mx = wave_max(mx);
+    float s = 0.f;
+    for (int v = lane; v < V; v += 64) s += expf(x[v] - mx);
+    s = wave_sum(s);
+    const float l = mx + logf(s);
+    if (lane == 0) {
+        lse[r] = l;
+        if (targets && loss_rows) {
+            int64_t t = targets[r];
+            t = t < 0 ? 0 : (t >= V ? V - 1 : t);
+            loss_rows[r] = l - x[t];
+        }
+    }
+}
+
+extern "C" int cg_ce_fwd(const float* logits, int64_t rows, int64_t V, int64_t ld, const int64_t* targets,
+                         float* loss_rows, float* lse, void* stream) {
+    CG_REQUIRE(rows > 0 && V > 0 && V <= 1024, "cg_ce_fwd: bad shape");
+    k_ce_fwd<<<ceil_div(rows, 4), 256, 0, (hipStream_t)stream>>>(logits, rows, (int)V, ld, targets, loss_rows, lse);
+    CG_LAUNCH_CHECK("cg_ce_fwd");
+    return CG_OK;
+}
+
+__global__ void k_ce_bwd(const float* __restrict__ logits, int64_t rows, int V, int64_t ld,
+                         const int64_t* __restrict__ targets, const float* __restrict__ lse,
+                         const float* __restrict__ gp, float g_mult, float* __restrict__ dlogits, int64_t ldd,
+                         bf16_t* __restrict__ dlp) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows * V) return;
+    const int64_t r = i / V;
+    const int v = (int)(i % V);
+    const float g = *gp * g_mult;
+    int64_t t = targets[r];
+    t = t < 0 ? 0 : (t >= V ? V - 1 : t);
+    const float p = expf(logits[r * ld + v] - lse[r]);
+    const float d = g * (p - (v == t ? 1.f : 0.f));
+    if (dlogits) dlogits[r * ldd + v] = d;
+    if (dlp) dlp[r * ldd + v] = f2bf(d);
+}
+
+extern "C" int cg_ce_bwd(const float* logits, int64_t rows, int64_t V, int64_t ld, const int64_t* targets,
+                         const float* lse, const float* g, float g_mult, float* dlogits, int64_t ld_d,
+                         void* dst_lp, void* stream) {
+    CG_REQUIRE(rows > 0 && V > 0, "cg_ce_bwd: bad shape");
+    k_ce_bwd<<<ceil_div(rows * V, 256), 256, 0, (hipStream_t)stream>>>(logits, rows, (int)V, ld, targets, lse, g, g_mult,
+                                                                       dlogits, ld_d, (bf16_t*)dst_lp);
+    CG_LAUNCH_CHECK("cg_ce_bwd");
+    return CG_OK;
+}
+
+// ---- AdamW ------------------------------------------------------------------------------
+// Same fp32 operation order as torch/optim/adam.py _single_tensor_adam (decoupled decay):
+//   p *= 1 - lr*wd ; m = m + (1-b1)*(g - m) [lerp, w<0.5] ; v = v*b2 + (1-b2)*g*g ;
+//   denom = sqrt(v)/sqrt(bc2) + eps ; p += (-lr/bc1)*m / denom
+// Explicit _rn intrinsics keep the compiler from contracting into FMAs.
+struct AdamScalars {
+    float decay, w1, b2, omb2, eps, neg_step, bc2_sqrt;
+};
+
+__device__ __forceinline__ float adam_one(float p, float g, float& m, float& v, const AdamScalars& s) {
+    p = __fmul_rn(p, s.decay);
+    m = __fadd_rn(m, __fmul_rn(s.w1, __fsub_rn(g, m)));
+    v = __fadd_rn(__fmul_rn(v, s.b2), __fmul_rn(__fmul_rn(s.omb2, g), g));
+    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), s.bc2_sqrt), s.eps);
+    return __fadd_rn(p, __fdiv_rn(__fmul_rn(s.neg_step, m), denom));
+}
+
+__global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const float* __restrict__ g,
+                                               float* __restrict__ m, float* __restrict__ v, bf16_t* __restrict__ pb,
+                                               int64_t n, double lr, double beta1, double beta2, double eps,
+                                               double wd, const int64_t* __restrict__ step_ptr) {
+    const double t = (double)*step_ptr;
+    AdamScalars s;
+    s.decay = (float)(1.0 - lr * wd);
+    s.w1 = (float)(1.0 - beta1);
+    s.b2 = (float)beta2;
+    s.omb2 = (float)(1.0 - beta2);
+    s.eps = (float)eps;
+    const double bc1 = 1.0 - pow(beta1, t);
+    const double bc2 = 1.0 - pow(beta2, t);
+    s.neg_step = (float)(-(lr / bc1));
+    s.bc2_sqrt = (float)sqrt(bc2);
+    const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+    for (int64_t i = i0; i < n; i += stride) {
+        if (i + 3 < n) {
+            float4 pv = *(float4*)(p + i), gv = *(const float4*)(g + i), mv = *(float4*)(m + i), vv = *(float4*)(v + i);
+            pv.x = adam_one(pv.x, gv.x, mv.x, vv.x, s);
+            pv.y = adam_one(pv.y, gv.y, mv.y, vv.y, s);
+            pv.z = adam_one(pv.z, gv.z, mv.z, vv.z, s);
+            pv.w = adam_one(pv.w, gv.w, mv.w, vv.w, s);
+            *(float4*)(p + i) = pv;
+            *(float4*)(m + i) = mv;
+            *(float4*)(v + i) = vv;
+            if (pb) *(uint2*)(pb + i) = make_uint2(pack_bf2(pv.x, pv.y), pack_bf2(pv.z, pv.w));
+        } else {
+            for (int64_t j = i; j < n; ++j) {
+                float mm = m[j], vv = v[j];
+                const float np = adam_one(p[j], g[j], mm, vv, s);
+                p[j] = np;
+                m[j] = mm;
+                v[j] = vv;
+                if (pb) pb[j] = f2bf(np);
+            }
+        }
+    }
+}
+
+extern "C" int cg_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, double lr,
+                        double beta1, double beta2, double eps, double weight_decay, const int64_t* step_ptr,
+                        void* stream) {
+    CG_REQUIRE(n >= 0, "cg_adamw: n < 0");
+    if (n == 0) return CG_OK;
+    CG_REQUIRE((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0 &&
+                   (((uintptr_t)p_bf16) & 7) == 0,
+               "cg_adamw: buffers must be 16-B aligned");
+    int grid = ceil_div((n + 3) / 4, 256);
+    grid = grid > 8192 ? 8192 : grid;
+    k_adamw<<<grid, 256, 0, (hipStream_t)stream>>>(p, g, m, v, (bf16_t*)p_bf16, n, lr, beta1, beta2, eps,
+                                                   weight_decay, step_ptr);
+    CG_LAUNCH_CHECK("cg_adamw");
+    return CG_OK;
+}

@@ -1,0 +1,137 @@
+// charpt HIP library -- shared device/host helpers (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/charpt.h"
+
+// ---------------------------------------------------------------------------------------
+// error convention: every entry point returns CG_OK or an error code and records a message
+// retrievable through cg_last_error_string() (thread-local).
+// ---------------------------------------------------------------------------------------
+namespace cg {
+void set_error(const char* fmt, ...);
+}  // namespace cg
+
+#define CG_REQUIRE(cond, ...)                \
+    do {                                     \
+        if (!(cond)) {                       \
+            cg::set_error(__VA_ARGS__);      \
+            return CG_EINVAL;                \
+        }                                    \
+    } while (0)
+
+#define CG_LAUNCH_CHECK(name)                                                        \
+    do {                                                                             \
+        hipError_t e_ = hipGetLastError();                                           \
+        if (e_ != hipSuccess) {                                                      \
+            cg::set_error("%s: launch failed: %s", name, hipGetErrorString(e_));      \
+            return CG_EHIP;                                                          \
+        }                                                                            \
+    } while (0)
+
+namespace cg {
+
+typedef unsigned short bf16_t;  // raw bf16 bits in memory
+typedef short sv8 __attribute__((ext_vector_type(8)));
+typedef short sv4 __attribute__((ext_vector_type(4)));
+typedef float fv4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bfv8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+// round-to-nearest-even f32 -> bf16 (NaN kept NaN)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (bf16_t)(u >> 16);
+}
+
+__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
+    return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+template <typename T>
+__device__ __forceinline__ float ld_as_f32(const T* p);
+template <>
+__device__ __forceinline__ float ld_as_f32<float>(const float* p) { return *p; }
+template <>
+__device__ __forceinline__ float ld_as_f32<bf16_t>(const bf16_t* p) { return bf2f(*p); }
+
+template <typename T>
+__device__ __forceinline__ void st_from_f32(T* p, float v);
+template <>
+__device__ __forceinline__ void st_from_f32<float>(float* p, float v) { *p = v; }
+template <>
+__device__ __forceinline__ void st_from_f32<bf16_t>(bf16_t* p, float v) { *p = f2bf(v); }
+
+// ---------------------------------------------------------------------------------------
+// wave64 reductions
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// ---------------------------------------------------------------------------------------
+// Philox4x32-10 counter-based dropout RNG (spec: oracle/philox.py; DESIGN.md "Dropout").
+//   element idx -> ctr = (idx>>2 lo, idx>>2 hi, stream lo, stream hi), key = seed, word idx&3
+// ---------------------------------------------------------------------------------------
+struct u32x4 {
+    uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ u32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                               uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0;
+        c1 = lo1;
+        c2 = n2;
+        c3 = lo0;
+    }
+    return {c0, c1, c2, c3};
+}
+
+// the four consecutive elements [4*group, 4*group+4)
+__device__ __forceinline__ u32x4 philox_group(uint64_t seed, uint64_t stream, uint64_t group) {
+    return philox4x32_10((uint32_t)group, (uint32_t)(group >> 32), (uint32_t)stream, (uint32_t)(stream >> 32),
+                         (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+__device__ __forceinline__ uint32_t philox_word(const u32x4& r, int w) {
+    return w == 0 ? r.x : (w == 1 ? r.y : (w == 2 ? r.z : r.w));
+}
+
+__device__ __forceinline__ uint64_t dropout_stream(const uint64_t* rng_call, int site) {
+    return (rng_call ? (*rng_call << 8) : 0ull) | (uint64_t)(site & 0xff);
+}
+
+inline uint32_t dropout_threshold(double p) {
+    double t = p * 4294967296.0;
+    t = t < 0 ? 0 : t;
+    double r = __builtin_nearbyint(t);
+    return r >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)r;
+}
+
+inline float dropout_scale(double p) { return (float)(1.0 / (1.0 - p)); }
+
+inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+}  // namespace cg

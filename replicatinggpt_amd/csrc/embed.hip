@@ -1,0 +1,100 @@
+// charpt: token + position embeddings (GPT1.py:179-181) forward and deterministic backward.
+#include "common.h"
+
+using namespace cg;
+
+// x[b,t,:] = wte[idx[b,t],:] + wpe[t,:]   -- one block per (b,t) row, coalesced over C
+__global__ void k_embed_fwd(const int64_t* __restrict__ idx, const float* __restrict__ wte,
+                            const float* __restrict__ wpe, float* __restrict__ x, int64_t T, int64_t C, int64_t V) {
+    const int64_t row = blockIdx.x;
+    const int64_t t = row % T;
+    int64_t tok = idx[row];
+    tok = tok < 0 ? 0 : (tok >= V ? V - 1 : tok);  // out-of-range ids are a caller error (torch raises)
+    const float* a = wte + tok * C;
+    const float* p = wpe + t * C;
+    float* o = x + row * C;
+    if ((C & 3) == 0) {
+        for (int64_t c = threadIdx.x * 4; c < C; c += blockDim.x * 4) {
+            float4 u = *(const float4*)(a + c), w = *(const float4*)(p + c);
+            *(float4*)(o + c) = make_float4(u.x + w.x, u.y + w.y, u.z + w.z, u.w + w.w);
+        }
+    } else {
+        for (int64_t c = threadIdx.x; c < C; c += blockDim.x) o[c] = a[c] + p[c];
+    }
+}
+
+extern "C" int cg_embed_fwd(const int64_t* idx, const float* wte, const float* wpe, float* x, int64_t B, int64_t T,
+                            int64_t C, int64_t V, void* stream) {
+    CG_REQUIRE(B > 0 && T > 0 && C > 0 && V > 0, "cg_embed_fwd: bad shape");
+    k_embed_fwd<<<(unsigned)(B * T), 128, 0, (hipStream_t)stream>>>(idx, wte, wpe, x, T, C, V);
+    CG_LAUNCH_CHECK("cg_embed_fwd");
+    return CG_OK;
+}
+
+// ---- backward -------------------------------------------------------------------------
+// dwpe[t,c] = sum_b dx[b,t,c]   (fixed b order)
+__global__ void k_embed_bwd_pos(const float* __restrict__ dx, float* __restrict__ dwpe, int64_t B, int64_t T,
+                                int64_t C, int accumulate) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= T * C) return;
+    float s = 0.f;
+    for (int64_t b = 0; b < B; ++b) s += dx[b * T * C + i];
+    dwpe[i] = accumulate ? dwpe[i] + s : s;
+}
+
+// per row-chunk partial histogram-sum: part[chunk][v][c] = sum_{rows in chunk, idx=v} dx[row][c].
+// Each thread owns one column and walks the chunk's rows in order (deterministic, no atomics).
+constexpr int EMB_CHUNK = 256;
+
+__global__ void k_embed_bwd_tok_partial(const int64_t* __restrict__ idx, const float* __restrict__ dx,
+                                        float* __restrict__ part, int64_t rows, int64_t C, int64_t V) {
+    extern __shared__ __attribute__((aligned(16))) float acc[];  // [V][blockDim.x]
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t chunk = blockIdx.y;
+    for (int64_t v = 0; v < V; ++v) acc[v * blockDim.x + threadIdx.x] = 0.f;
+    const int64_t r0 = chunk * EMB_CHUNK;
+    const int64_t r1 = r0 + EMB_CHUNK < rows ? r0 + EMB_CHUNK : rows;
+    if (c < C) {
+        for (int64_t r = r0; r < r1; ++r) {
+            int64_t tok = idx[r];
+            tok = tok < 0 ? 0 : (tok >= V ? V - 1 : tok);
+            acc[tok * blockDim.x + threadIdx.x] += dx[r * C + c];
+        }
+        float* out = part + chunk * V * C;
+        for (int64_t v = 0; v < V; ++v) out[v * C + c] = acc[v * blockDim.x + threadIdx.x];
+    }
+}
+
+__global__ void k_embed_bwd_tok_reduce(const float* __restrict__ part, float* __restrict__ dwte, int64_t nchunk,
+                                       int64_t VC, int accumulate) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= VC) return;
+    float s = 0.f;
+    for (int64_t k = 0; k < nchunk; ++k) s += part[k * VC + i];
+    dwte[i] = accumulate ? dwte[i] + s : s;
+}
+
+extern "C" int64_t cg_embed_bwd_workspace(int64_t B, int64_t T, int64_t C, int64_t V) {
+    int64_t nchunk = (B * T + EMB_CHUNK - 1) / EMB_CHUNK;
+    return nchunk * V * C * (int64_t)sizeof(float);
+}
+
+extern "C" int cg_embed_bwd(const int64_t* idx, const float* dx, float* dwte, float* dwpe, int64_t B, int64_t T,
+                            int64_t C, int64_t V, int accumulate, void* workspace, void* stream) {
+    CG_REQUIRE(B > 0 && T > 0 && C > 0 && V > 0, "cg_embed_bwd: bad shape");
+    CG_REQUIRE(V * 128 * 4 <= 160 * 1024, "cg_embed_bwd: vocab %lld too large for the LDS histogram", (long long)V);
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t rows = B * T;
+    if (dwpe) k_embed_bwd_pos<<<ceil_div(T * C, 256), 256, 0, st>>>(dx, dwpe, B, T, C, accumulate);
+    if (dwte) {
+        const int64_t nchunk = (rows + EMB_CHUNK - 1) / EMB_CHUNK;
+        const int threads = 128;
+        dim3 grid(ceil_div(C, threads), (unsigned)nchunk);
+        size_t lds = (size_t)V * threads * sizeof(float);
+        k_embed_bwd_tok_partial<<<grid, threads, lds, st>>>(idx, dx, (float*)workspace, rows, C, V);
+        k_embed_bwd_tok_reduce<<<ceil_div(V * C, 256), 256, 0, st>>>((const float*)workspace, dwte, nchunk, V * C,
+                                                                      accumulate);
+    }
+    CG_LAUNCH_CHECK("cg_embed_bwd");
+    return CG_OK;
+}

@@ -1,0 +1,285 @@
+// charpt: LayerNorm forward/backward (nn.LayerNorm, GPT1.py:159-160,173), fp32 statistics.
+// One wave64 per row; the row lives in registers: lane owns NJ chunks of VEC consecutive
+// floats at e = (j*64 + lane)*VEC.  Specialised shapes: C = 384 (VEC 2, NJ 3), 768 (4, 3),
+// 512 (4, 2), 1024 (4, 4); any other C <= 2048 uses (1, 32) with bounds checks.
+#include "common.h"
+
+using namespace cg;
+
+namespace {
+
+template <int VEC>
+struct VecIO;
+template <>
+struct VecIO<1> {
+    static __device__ __forceinline__ void ld(const float* p, float* v) { v[0] = *p; }
+    static __device__ __forceinline__ void st(float* p, const float* v) { *p = v[0]; }
+    static __device__ __forceinline__ void st(bf16_t* p, const float* v) { *p = f2bf(v[0]); }
+};
+template <>
+struct VecIO<2> {
+    static __device__ __forceinline__ void ld(const float* p, float* v) {
+        float2 t = *(const float2*)p;
+        v[0] = t.x;
+        v[1] = t.y;
+    }
+    static __device__ __forceinline__ void st(float* p, const float* v) { *(float2*)p = make_float2(v[0], v[1]); }
+    static __device__ __forceinline__ void st(bf16_t* p, const float* v) { *(uint32_t*)p = pack_bf2(v[0], v[1]); }
+};
+template <>
+struct VecIO<4> {
+    static __device__ __forceinline__ void ld(const float* p, float* v) {
+        float4 t = *(const float4*)p;
+        v[0] = t.x;
+        v[1] = t.y;
+        v[2] = t.z;
+        v[3] = t.w;
+    }
+    static __device__ __forceinline__ void st(float* p, const float* v) {
+        *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+    }
+    static __device__ __forceinline__ void st(bf16_t* p, const float* v) {
+        *(uint2*)p = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+    }
+};
+
+template <typename T>
+__device__ __forceinline__ void ld_vec_any(const T* p, float* v, int n);
+template <>
+__device__ __forceinline__ void ld_vec_any<float>(const float* p, float* v, int n) {
+    if (n == 4) VecIO<4>::ld(p, v);
+    else if (n == 2) VecIO<2>::ld(p, v);
+    else VecIO<1>::ld(p, v);
+}
+template <>
+__device__ __forceinline__ void ld_vec_any<bf16_t>(const bf16_t* p, float* v, int n) {
+    for (int i = 0; i < n; ++i) v[i] = bf2f(p[i]);
+}
+
+}  // namespace
+
+template <int VEC, int NJ, typename TY>
+__global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ x, const float* __restrict__ w,
+                                                const float* __restrict__ b, TY* __restrict__ y,
+                                                float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                int64_t rows, int C, float eps) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const float invC = 1.0f / (float)C;
+    for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < rows; r += (int64_t)gridDim.x * 4) {
+        const float* xr = x + r * C;
+        float v[NJ][VEC];
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int e = (j * 64 + lane) * VEC;
+            if (e < C) {
+                VecIO<VEC>::ld(xr + e, v[j]);
+            } else {
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) v[j][q] = 0.f;
+            }
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) s += v[j][q];
+        }
+        const float mu = wave_sum(s) * invC;
+        float ss = 0.f;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int e = (j * 64 + lane) * VEC;
+            if (e < C) {
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) {
+                    const float d = v[j][q] - mu;
+                    ss += d * d;
+                }
+            }
+        }
+        const float var = wave_sum(ss) * invC;
+        const float rs = 1.0f / sqrtf(var + eps);
+        TY* yr = y + r * C;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int e = (j * 64 + lane) * VEC;
+            if (e < C) {
+                float wv[VEC], bv[VEC], o[VEC];
+                VecIO<VEC>::ld(w + e, wv);
+                VecIO<VEC>::ld(b + e, bv);
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) o[q] = (v[j][q] - mu) * rs * wv[q] + bv[q];
+                VecIO<VEC>::st(yr + e, o);
+            }
+        }
+        if (lane == 0) {
+            mean_out[r] = mu;
+            rstd_out[r] = rs;
+        }
+    }
+}
+
+constexpr int LN_BWD_ROWS = 64;  // rows per block in the backward (16 per wave)
+
+template <int VEC, int NJ, typename TDY>
+__global__ __launch_bounds__(256) void k_ln_bwd(const TDY* __restrict__ dy, const float* __restrict__ x,
+                                                const float* __restrict__ w, const float* __restrict__ mean,
+                                                const float* __restrict__ rstd, const float* __restrict__ dres,
+                                                float* __restrict__ dx, bf16_t* __restrict__ dx_lp,
+                                                float* __restrict__ part, int64_t rows, int C) {
+    extern __shared__ __attribute__((aligned(16))) float red[];  // [4][2][C]
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const float invC = 1.0f / (float)C;
+    float adw[NJ][VEC], adb[NJ][VEC], wv[NJ][VEC];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int e = (j * 64 + lane) * VEC;
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) adw[j][q] = adb[j][q] = 0.f;
+        if (e < C) VecIO<VEC>::ld(w + e, wv[j]);
+        else {
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) wv[j][q] = 0.f;
+        }
+    }
+    const int64_t r0 = (int64_t)blockIdx.x * LN_BWD_ROWS;
+    for (int i = wave; i < LN_BWD_ROWS; i += 4) {
+        const int64_t r = r0 + i;
+        if (r >= rows) break;
+        const float mu = mean[r], rs = rstd[r];
+        float xh[NJ][VEC], g[NJ][VEC], d[NJ][VEC];
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int e = (j * 64 + lane) * VEC;
+            if (e < C) {
+                float xv[VEC];
+                VecIO<VEC>::ld(x + r * C + e, xv);
+                ld_vec_any<TDY>(dy + r * C + e, d[j], VEC);
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) {
+                    xh[j][q] = (xv[q] - mu) * rs;
+                    g[j][q] = d[j][q] * wv[j][q];
+                    s1 += g[j][q];
+                    s2 += g[j][q] * xh[j][q];
+                    adw[j][q] += d[j][q] * xh[j][q];
+                    adb[j][q] += d[j][q];
+                }
+            }
+        }
+        const float c1 = wave_sum(s1) * invC;
+        const float c2 = wave_sum(s2) * invC;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int e = (j * 64 + lane) * VEC;
+            if (e < C) {
+                float o[VEC], rv[VEC];
+                if (dres) VecIO<VEC>::ld(dres + r * C + e, rv);
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) {
+                    o[q] = rs * (g[j][q] - c1 - xh[j][q] * c2);
+                    if (dres) o[q] += rv[q];
+                }
+                VecIO<VEC>::st(dx + r * C + e, o);
+                if (dx_lp) VecIO<VEC>::st(dx_lp + r * C + e, o);
+            }
+        }
+    }
+    // block reduction of the column partials in a fixed wave order
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int e = (j * 64 + lane) * VEC;
+        if (e < C) {
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) {
+                red[(wave * 2 + 0) * C + e + q] = adw[j][q];
+                red[(wave * 2 + 1) * C + e + q] = adb[j][q];
+            }
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) {
+        const int which = c / C, e = c % C;
+        float s = 0.f;
+        for (int wv2 = 0; wv2 < 4; ++wv2) s += red[(wv2 * 2 + which) * C + e];
+        part[(int64_t)blockIdx.x * 2 * C + c] = s;
+    }
+}
+
+__global__ void k_ln_bwd_reduce(const float* __restrict__ part, int64_t nblk, int C, float* __restrict__ dw,
+                                float* __restrict__ db, int accumulate) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= 2 * C) return;
+    float s = 0.f;
+    for (int64_t k = 0; k < nblk; ++k) s += part[k * 2 * C + c];
+    float* o = c < C ? dw + c : db + (c - C);
+    if (c < C && !dw) return;
+    if (c >= C && !db) return;
+    *o = accumulate ? *o + s : s;
+}
+
+namespace {
+template <typename TY>
+int launch_ln_fwd(const float* x, const float* w, const float* b, TY* y, float* mean, float* rstd, int64_t rows,
+                  int C, float eps, hipStream_t st) {
+    const bool al16 = (((uintptr_t)x | (uintptr_t)w | (uintptr_t)b) & 15) == 0;
+    int grid = ceil_div(rows, 4);
+    grid = grid > 4096 ? 4096 : grid;
+#define LNF(V, N) k_ln_fwd<V, N, TY><<<grid, 256, 0, st>>>(x, w, b, y, mean, rstd, rows, C, eps)
+    if (C == 384 && al16) LNF(2, 3);
+    else if (C == 768 && al16) LNF(4, 3);
+    else if (C == 512 && al16) LNF(4, 2);
+    else if (C == 1024 && al16) LNF(4, 4);
+    else LNF(1, 32);
+#undef LNF
+    return CG_OK;
+}
+
+template <typename TDY>
+int launch_ln_bwd(const TDY* dy, const float* x, const float* w, const float* mean, const float* rstd,
+                  const float* dres, float* dx, bf16_t* dx_lp, float* dw, float* db, int accumulate, float* part,
+                  int64_t rows, int C, hipStream_t st) {
+    const bool al16 = (((uintptr_t)x | (uintptr_t)w | (uintptr_t)dx | (uintptr_t)(dres ? dres : x)) & 15) == 0 &&
+                      (((uintptr_t)dy) & 7) == 0;
+    const int64_t nblk = (rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
+    const size_t lds = (size_t)8 * C * sizeof(float);
+#define LNB(V, N) \
+    k_ln_bwd<V, N, TDY><<<(unsigned)nblk, 256, lds, st>>>(dy, x, w, mean, rstd, dres, dx, dx_lp, part, rows, C)
+    if (C == 384 && al16) LNB(2, 3);
+    else if (C == 768 && al16) LNB(4, 3);
+    else if (C == 512 && al16) LNB(4, 2);
+    else if (C == 1024 && al16) LNB(4, 4);
+    else LNB(1, 32);
+#undef LNB
+    if (dw || db) k_ln_bwd_reduce<<<ceil_div(2 * C, 256), 256, 0, st>>>(part, nblk, C, dw, db, accumulate);
+    return CG_OK;
+}
+}  // namespace
+
+extern "C" int cg_layernorm_fwd(const float* x, const float* w, const float* b, void* y, int y_dtype, float* mean,
+                                float* rstd, int64_t rows, int64_t C, float eps, void* stream) {
+    CG_REQUIRE(rows > 0 && C > 0 && C <= 2048, "cg_layernorm_fwd: need 0 < C <= 2048 (got %lld)", (long long)C);
+    hipStream_t st = (hipStream_t)stream;
+    if (y_dtype == CG_BF16) launch_ln_fwd<bf16_t>(x, w, b, (bf16_t*)y, mean, rstd, rows, (int)C, eps, st);
+    else launch_ln_fwd<float>(x, w, b, (float*)y, mean, rstd, rows, (int)C, eps, st);
+    CG_LAUNCH_CHECK("cg_layernorm_fwd");
+    return CG_OK;
+}
+
+extern "C" int64_t cg_layernorm_bwd_workspace(int64_t rows, int64_t C) {
+    return ((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS) * 2 * C * (int64_t)sizeof(float);
+}
+
+extern "C" int cg_layernorm_bwd(const void* dy, int dy_dtype, const float* x, const float* w, const float* mean,
+                                const float* rstd, const float* dres, float* dx, uint16_t* dx_bf16, float* dw,
+                                float* db, int accumulate, void* workspace, int64_t rows, int64_t C, void* stream) {
+    CG_REQUIRE(rows > 0 && C > 0 && C <= 2048, "cg_layernorm_bwd: need 0 < C <= 2048");
+    hipStream_t st = (hipStream_t)stream;
+    if (dy_dtype == CG_BF16)
+        launch_ln_bwd<bf16_t>((const bf16_t*)dy, x, w, mean, rstd, dres, dx, (bf16_t*)dx_bf16, dw, db, accumulate,
+                              (float*)workspace, rows, (int)C, st);
+    else
+        launch_ln_bwd<float>((const float*)dy, x, w, mean, rstd, dres, dx, (bf16_t*)dx_bf16, dw, db, accumulate,
+                             (float*)workspace, rows, (int)C, st);
+    CG_LAUNCH_CHECK("cg_layernorm_bwd");
+    return CG_OK;
+}

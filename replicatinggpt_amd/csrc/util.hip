@@ -1,0 +1,201 @@
+// charpt: error plumbing, counters, RNG helpers, reductions, batch gather.
+#include <stdarg.h>
+
+#include "common.h"
+
+namespace cg {
+static thread_local char g_err[1024] = "";
+void set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+}  // namespace cg
+
+using namespace cg;
+
+extern "C" const char* cg_last_error_string(void) { return g_err; }
+extern "C" int cg_version(void) { return 1; }
+
+extern "C" int cg_device_info(int* n_cu, int* major, int* minor) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) {
+        set_error("cg_device_info: no HIP device");
+        return CG_EHIP;
+    }
+    *n_cu = prop.multiProcessorCount;
+    *major = prop.major;
+    *minor = prop.minor;
+    return CG_OK;
+}
+
+// --------------------------------------------------------------------------------------
+__global__ void k_counter_add(int64_t* c, int64_t d) { *c += d; }
+__global__ void k_rng_snapshot(uint64_t* c, uint64_t* s) {
+    uint64_t v = *c;
+    *s = v;
+    *c = v + 1;
+}
+
+extern "C" int cg_counter_add(int64_t* counter, int64_t delta, void* stream) {
+    k_counter_add<<<1, 1, 0, (hipStream_t)stream>>>(counter, delta);
+    CG_LAUNCH_CHECK("cg_counter_add");
+    return CG_OK;
+}
+
+extern "C" int cg_rng_snapshot(uint64_t* counter, uint64_t* snap, void* stream) {
+    k_rng_snapshot<<<1, 1, 0, (hipStream_t)stream>>>(counter, snap);
+    CG_LAUNCH_CHECK("cg_rng_snapshot");
+    return CG_OK;
+}
+
+__global__ void k_dropout_mask(float* dst, int64_t n, uint32_t thr, uint64_t seed, const uint64_t* rng_call,
+                               int site) {
+    const uint64_t stream = dropout_stream(rng_call, site);
+    int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t i0 = g * 4;
+    if (i0 >= n) return;
+    u32x4 r = philox_group(seed, stream, (uint64_t)g);
+    uint32_t w[4] = {r.x, r.y, r.z, r.w};
+    for (int j = 0; j < 4 && i0 + j < n; ++j) dst[i0 + j] = w[j] >= thr ? 1.f : 0.f;
+}
+
+extern "C" int cg_dropout_mask(float* dst, int64_t n, double p, uint64_t seed, const uint64_t* rng_call, int site,
+                               void* stream) {
+    CG_REQUIRE(n >= 0, "cg_dropout_mask: n < 0");
+    if (n == 0) return CG_OK;
+    int64_t groups = (n + 3) / 4;
+    k_dropout_mask<<<ceil_div(groups, 256), 256, 0, (hipStream_t)stream>>>(dst, n, dropout_threshold(p),
+                                                                                 seed, rng_call, site);
+    CG_LAUNCH_CHECK("cg_dropout_mask");
+    return CG_OK;
+}
+
+// y = x * keep * 1/(1-p), element index r*C + c (FFN dropout backward, GPT1.py:146)
+template <typename TY>
+__global__ void k_dropout_apply(const float* __restrict__ x, int64_t rows, int64_t C, int64_t ldx, TY* __restrict__ y,
+                                uint32_t thr, float dscale, uint64_t seed, const uint64_t* rng_call, int site) {
+    const uint64_t stream = thr ? dropout_stream(rng_call, site) : 0;
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // group of 4 consecutive elements
+    const int64_t n = rows * C;
+    const int64_t i0 = g * 4;
+    if (i0 >= n) return;
+    u32x4 r = {0, 0, 0, 0};
+    if (thr) r = philox_group(seed, stream, (uint64_t)g);
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int64_t i = i0 + j;
+        if (i < n) {
+            const int64_t row = i / C, col = i % C;
+            float v = x[row * ldx + col];
+            if (thr) v = w[j] >= thr ? v * dscale : 0.f;
+            st_from_f32<TY>(y + i, v);
+        }
+    }
+}
+
+extern "C" int cg_dropout_apply(const float* x, int64_t rows, int64_t C, int64_t ldx, void* y, int y_dtype, double p,
+                                uint64_t seed, const uint64_t* rng_call, int site, void* stream) {
+    CG_REQUIRE(rows >= 0 && C > 0 && p >= 0 && p < 1, "cg_dropout_apply: bad args");
+    const int64_t n = rows * C;
+    if (n == 0) return CG_OK;
+    const uint32_t thr = p > 0 ? dropout_threshold(p) : 0u;
+    const float ds = p > 0 ? dropout_scale(p) : 1.f;
+    const int grid = ceil_div((n + 3) / 4, 256);
+    if (y_dtype == CG_BF16)
+        k_dropout_apply<bf16_t><<<grid, 256, 0, (hipStream_t)stream>>>(x, rows, C, ldx, (bf16_t*)y, thr, ds, seed,
+                                                                        rng_call, site);
+    else
+        k_dropout_apply<float><<<grid, 256, 0, (hipStream_t)stream>>>(x, rows, C, ldx, (float*)y, thr, ds, seed,
+                                                                       rng_call, site);
+    CG_LAUNCH_CHECK("cg_dropout_apply");
+    return CG_OK;
+}
+
+// --------------------------------------------------------------------------------------
+// deterministic two-pass sum: pass 1 -> one partial per block (fixed order), pass 2 one block
+__global__ void k_sum_partial(const float* x, int64_t n, float* part) {
+    __shared__ float red[16];
+    float s = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        s += x[i];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float t = 0.f;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+        part[blockIdx.x] = t;
+    }
+}
+__global__ void k_sum_final(const float* part, int np, float scale, float* out) {
+    __shared__ float red[16];
+    float s = 0.f;
+    for (int i = threadIdx.x; i < np; i += blockDim.x) s += part[i];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float t = 0.f;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+        *out = t * scale;
+    }
+}
+
+extern "C" int cg_sum_f32(const float* x, int64_t n, float scale, float* out, float* ws, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    int nb = (int)(n / 4096);
+    nb = nb < 1 ? 1 : (nb > 1024 ? 1024 : nb);
+    k_sum_partial<<<nb, 256, 0, st>>>(x, n, ws);
+    k_sum_final<<<1, 256, 0, st>>>(ws, nb, scale, out);
+    CG_LAUNCH_CHECK("cg_sum_f32");
+    return CG_OK;
+}
+
+__global__ void k_cast_f32_bf16(const float* x, bf16_t* y, int64_t n) {
+    int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (i + 3 < n) {
+        float4 v = *(const float4*)(x + i);
+        uint2 o;
+        o.x = pack_bf2(v.x, v.y);
+        o.y = pack_bf2(v.z, v.w);
+        *(uint2*)(y + i) = o;
+    } else {
+        for (; i < n; ++i) y[i] = f2bf(x[i]);
+    }
+}
+
+extern "C" int cg_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, void* stream) {
+    if (n == 0) return CG_OK;
+    CG_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 7) == 0, "cg_cast_f32_bf16: misaligned");
+    k_cast_f32_bf16<<<ceil_div((n + 3) / 4, 256), 256, 0, (hipStream_t)stream>>>(x, (bf16_t*)y, n);
+    CG_LAUNCH_CHECK("cg_cast_f32_bf16");
+    return CG_OK;
+}
+
+// --------------------------------------------------------------------------------------
+// get_batch windows on device (GPT1.py:79-80)
+template <typename D>
+__global__ void k_gather_batch(const D* data, const int64_t* ix, int64_t* x, int64_t* y, int64_t B, int64_t T) {
+    int64_t b = blockIdx.y;
+    int64_t base = ix[b];
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < T; t += (int64_t)gridDim.x * blockDim.x) {
+        x[b * T + t] = (int64_t)data[base + t];
+        y[b * T + t] = (int64_t)data[base + t + 1];
+    }
+}
+
+extern "C" int cg_gather_batch(const void* data, int data_is_u8, const int64_t* ix, int64_t* x, int64_t* y,
+                               int64_t B, int64_t T, void* stream) {
+    CG_REQUIRE(B > 0 && T > 0 && B < 65536, "cg_gather_batch: bad shape");
+    dim3 grid(ceil_div(T, 256), (unsigned)B);
+    if (data_is_u8)
+        k_gather_batch<uint8_t><<<grid, 256, 0, (hipStream_t)stream>>>((const uint8_t*)data, ix, x, y, B, T);
+    else
+        k_gather_batch<int64_t><<<grid, 256, 0, (hipStream_t)stream>>>((const int64_t*)data, ix, x, y, B, T);
+    CG_LAUNCH_CHECK("cg_gather_batch");
+    return CG_OK;
+}

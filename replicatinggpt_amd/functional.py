@@ -1,0 +1,584 @@
+"""Autograd functions for the char-GPT hot path, each a fixed sequence of charpt kernels.
+
+The fused training path is two autograd nodes per Block (GPT1.py:162-165):
+
+  AttnSublayer:  x + proj(attn(qkv(ln1(x))))            (GPT1.py:163, 134-136, 109-123)
+  FFNSublayer:   x + drop(W2 relu(W1 ln2(x) + b1) + b2)  (GPT1.py:164, 142-147)
+
+plus the embedding (GPT1.py:179-181) and the ln_f + lm_head + cross-entropy tail
+(GPT1.py:183-192).  Standalone module calls (Head, MultiHeadAttention, FeedForward, LayerNorm
+outside a model) use the elementary functions at the bottom.
+
+Parameter gradients are written by the kernels straight into the model's flat fp32 gradient
+buffer ("grad slots"), see ``Region``; the residual-stream gradient is fp32, activations and
+GEMM operands are bf16 (or fp32 in exact mode).
+"""
+import math
+
+import torch
+
+from . import _lib as L
+from . import ops
+
+EPI = {"store": L.EPI_STORE, "bias": L.EPI_BIAS, "bias_relu": L.EPI_BIAS_RELU, "bias_resid": L.EPI_BIAS_RESID,
+       "bias_drop_resid": L.EPI_BIAS_DROP_RESID, "relu_bwd": L.EPI_RELU_BWD}
+
+
+def site_stream(call, site):
+    """Dropout stream id (mirrors csrc/common.h dropout_stream and oracle.site_stream)."""
+    return (int(call) << 8) | int(site)
+
+
+# ---------------------------------------------------------------------------------------
+# parameters as the kernels see them
+# ---------------------------------------------------------------------------------------
+class Region:
+    """A contiguous fp32 weight region made of one or more nn.Parameters (e.g. all heads'
+    query/key/value weights form one [3d, d] QKV region).
+
+    master : fp32 tensor of the whole region (a view of the model's flat buffer when packed,
+             else a temporary concatenation)
+    slot   : matching view of the flat fp32 gradient buffer (None when not packed)
+    shadow : matching view of the flat bf16 shadow (None when not packed)
+    parts  : [(param, element_offset)] in region order
+    """
+
+    __slots__ = ("master", "slot", "shadow", "parts")
+
+    def __init__(self, master, parts, slot=None, shadow=None):
+        self.master, self.parts, self.slot, self.shadow = master, parts, slot, shadow
+
+    @staticmethod
+    def of(*params):
+        """Unpacked region built from loose parameters (standalone module use)."""
+        parts, off = [], 0
+        for p in params:
+            parts.append((p, off))
+            off += p.numel()
+        if len(params) == 1:
+            master = params[0].detach()
+        else:
+            master = torch.cat([p.detach().reshape(-1) for p in params]).view(-1, params[0].shape[-1])
+        return Region(master, parts)
+
+    @property
+    def params(self):
+        return [p for p, _ in self.parts]
+
+    def needs_grad(self):
+        return any(p.requires_grad for p, _ in self.parts)
+
+    def operand(self, dtype):
+        """The weight as a GEMM operand in ``dtype``."""
+        if dtype == torch.float32:
+            return self.master
+        if self.shadow is not None:
+            return self.shadow
+        out = torch.empty(self.master.shape, dtype=torch.bfloat16, device=self.master.device)
+        ops.cast_bf16(self.master.contiguous(), out)
+        return out
+
+    # -- gradient destination ----------------------------------------------------------
+    def grad_target(self):
+        """Decide where this region's gradient goes; returns (tensor, beta, finish) where
+        ``finish()`` returns the per-param values the autograd Function must return."""
+        if not self.needs_grad():
+            return None, 0.0, lambda: [None] * len(self.parts)
+        if self.slot is not None:
+            grads = [p.grad for p, _ in self.parts]
+            if all(g is None for g in grads):
+                def assign():
+                    with torch.no_grad():
+                        for p, off in self.parts:
+                            if p.requires_grad:
+                                p.grad = self.slot.view(-1)[off:off + p.numel()].view(p.shape)
+                    return [None] * len(self.parts)
+                return self.slot, 0.0, assign
+            if all(g is not None and g.data_ptr() == self.slot.view(-1)[off:].data_ptr() and g.shape == p.shape
+                   for (p, off), g in zip(self.parts, grads)):
+                return self.slot, 1.0, lambda: [None] * len(self.parts)
+        tmp = torch.empty(self.master.shape, dtype=torch.float32, device=self.master.device)
+
+        def ret():
+            return [tmp.view(-1)[off:off + p.numel()].view(p.shape) if p.requires_grad else None
+                    for p, off in self.parts]
+        return tmp, 0.0, ret
+
+
+def _flat2(t):
+    return t.reshape(-1, t.shape[-1])
+
+
+def _is_bf16(dt):
+    return dt == torch.bfloat16
+
+
+# ---------------------------------------------------------------------------------------
+# GEMM helpers (all three nn.Linear products)
+# ---------------------------------------------------------------------------------------
+def linear_fwd(x2, w, out, epi="store", bias=None, resid=None, aux=None, dropout_p=0.0, seed=0, rng_call=None,
+               site=0):
+    """out[M,N] = epi(x2[M,K] @ w[N,K]^T)"""
+    M, K = x2.shape
+    N = w.shape[0]
+    ops.gemm(x2, w, out, _is_bf16(x2.dtype), False, False, M, N, K, K, K, out.stride(0), EPI[epi], bias, resid,
+             resid.stride(0) if resid is not None else 0, aux, aux.stride(0) if aux is not None else 0,
+             float(dropout_p), int(seed), rng_call, int(site), 0.0, 1, None)
+    return out
+
+
+def linear_dgrad(dy2, w, out, epi="store", aux=None):
+    """out[M,K] = epi(dy2[M,N] @ w[N,K])"""
+    M, N = dy2.shape
+    K = w.shape[1]
+    ops.gemm(dy2, w, out, _is_bf16(dy2.dtype), False, True, M, K, N, N, K, out.stride(0), EPI[epi], None, None, 0,
+             aux, aux.stride(0) if aux is not None else 0, 0.0, 0, None, 0, 0.0, 1, None)
+    return out
+
+
+def _wgrad_split(M, N, K, fast):
+    tiles = (-(-M // 128) * -(-N // 128)) if fast else (-(-M // 64) * -(-N // 64))
+    split = 1
+    while tiles * split * 2 <= 1024 and split < 32 and K % (64 * split * 2) == 0 and K // (split * 2) >= 256:
+        split *= 2
+    return split
+
+
+def linear_wgrad(dy2, x2, out, beta):
+    """out[N,K] (+)= dy2[M,N]^T @ x2[M,K]   (fp32, deterministic split-K)"""
+    M, N = dy2.shape
+    K = x2.shape[1]
+    fast = _is_bf16(dy2.dtype) and N % 128 == 0 and K % 128 == 0 and M % 64 == 0
+    split = _wgrad_split(N, K, M, fast)
+    ws = None
+    if split > 1:
+        ws = torch.empty(ops.gemm_workspace(N, K, split) // 4, dtype=torch.float32, device=dy2.device)
+    ops.gemm(dy2, x2, out, _is_bf16(dy2.dtype), True, True, N, K, M, N, K, out.stride(0), L.EPI_STORE, None, None, 0,
+             None, 0, 0.0, 0, None, 0, float(beta), split, ws)
+    return out
+
+
+def colsum_into(x2, out, beta):
+    ws = torch.empty(ops.colsum_workspace(x2.shape[0], x2.shape[1]) // 4 + 1, dtype=torch.float32, device=x2.device)
+    ops.colsum(x2, out, bool(beta), ws)
+
+
+def layernorm(x2, w, b, out_dtype, eps=1e-5):
+    rows, C = x2.shape
+    y = torch.empty((rows, C), dtype=out_dtype, device=x2.device)
+    mean = torch.empty(rows, dtype=torch.float32, device=x2.device)
+    rstd = torch.empty(rows, dtype=torch.float32, device=x2.device)
+    ops.layernorm_fwd(x2, w, b, y, mean, rstd, float(eps))
+    return y, mean, rstd
+
+
+def layernorm_bwd(dy2, x2, w_reg, b_reg, mean, rstd, dres=None, want_lp=False):
+    """dx (fp32) = dres + LN'(dy); LN weight/bias grads into their regions."""
+    rows, C = x2.shape
+    dx = torch.empty((rows, C), dtype=torch.float32, device=x2.device)
+    dx_lp = torch.empty((rows, C), dtype=torch.bfloat16, device=x2.device) if want_lp else None
+    gw, bw, fw = w_reg.grad_target()
+    gb, bb, fb = b_reg.grad_target()
+    ws = torch.empty(ops.layernorm_bwd_workspace(rows, C) // 4 + 1, dtype=torch.float32, device=x2.device)
+    ops.layernorm_bwd(dy2, x2, w_reg.master, mean, rstd, dres, dx, dx_lp, gw, gb, bool(bw or bb), ws)
+    return dx, dx_lp, fw() + fb()
+
+
+def attention_fwd(qkv, B, T, H, D, out, scale, p, seed, rng_call, site):
+    d = H * D
+    lse = torch.empty((B, H, T), dtype=torch.float32, device=qkv.device)
+    ops.attn_fwd(qkv, B, T, H, D, 0, d, 2 * d, qkv.stride(0), out, out.stride(0), lse, float(scale), float(p),
+                 int(seed), rng_call, int(site))
+    return lse
+
+
+def attention_bwd(qkv, B, T, H, D, o, do, lse, scale, p, seed, rng_call, site):
+    d = H * D
+    dqkv = torch.empty_like(qkv)
+    ws = torch.empty(ops.attn_bwd_workspace(B, T, H, D) // 4 + 1, dtype=torch.float32, device=qkv.device)
+    ops.attn_bwd(qkv, B, T, H, D, 0, d, 2 * d, qkv.stride(0), o, o.stride(0), do, do.stride(0), lse, dqkv,
+                 dqkv.stride(0), float(scale), float(p), int(seed), rng_call, int(site), ws)
+    return dqkv
+
+
+def to_act(x2, dtype):
+    """fp32 activation -> GEMM operand dtype (bf16 copy through the cast kernel)."""
+    if x2.dtype == dtype:
+        return x2
+    out = torch.empty(x2.shape, dtype=dtype, device=x2.device)
+    ops.cast_bf16(x2.contiguous(), out)
+    return out
+
+
+def _regions_params(regs):
+    out = []
+    for r in regs:
+        out += r.params
+    return out
+
+
+class LayerCtx:
+    """Per-call context for a sublayer: geometry, dropout and dtype."""
+    __slots__ = ("n_head", "head_size", "scale", "p", "seed", "rng_call", "site", "act")
+
+    def __init__(self, n_head, head_size, scale, p, seed, rng_call, site, act):
+        self.n_head, self.head_size, self.scale, self.p = n_head, head_size, scale, p
+        self.seed, self.rng_call, self.site, self.act = seed, rng_call, site, act
+
+
+# ---------------------------------------------------------------------------------------
+# fused training nodes
+# ---------------------------------------------------------------------------------------
+class EmbeddingFn(torch.autograd.Function):
+    """x = wte[idx] + wpe[arange(T)]  (GPT1.py:179-181)"""
+
+    @staticmethod
+    def forward(ctx, idx, wte_reg, wpe_reg, *params):
+        B, T = idx.shape
+        V, C = wte_reg.master.shape
+        x = torch.empty((B, T, C), dtype=torch.float32, device=idx.device)
+        ops.embed_fwd(idx, wte_reg.master, wpe_reg.master, x)
+        ctx.save_for_backward(idx)
+        ctx.regs = (wte_reg, wpe_reg)
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        (idx,) = ctx.saved_tensors
+        wte_reg, wpe_reg = ctx.regs
+        B, T = idx.shape
+        V, C = wte_reg.master.shape
+        gt, bt, ft = wte_reg.grad_target()
+        gp, bp, fp = wpe_reg.grad_target()
+        if gt is not None or gp is not None:
+            ws = torch.empty(ops.embed_bwd_workspace(B, T, C, V) // 4 + 1, dtype=torch.float32, device=dx.device)
+            if bt != bp and gt is not None and gp is not None:
+                ops.embed_bwd(idx, dx.contiguous(), gt, None, bool(bt), ws)
+                ops.embed_bwd(idx, dx.contiguous(), None, gp[:T], bool(bp), ws)
+            else:
+                ops.embed_bwd(idx, dx.contiguous(), gt, gp[:T] if gp is not None else None, bool(bt or bp), ws)
+            if gp is not None and not bp and T < gp.shape[0]:
+                gp[T:].zero_()  # positions beyond T get no gradient (overwrite mode)
+        return (None, None, None, *ft(), *fp())
+
+
+class AttnSublayerFn(torch.autograd.Function):
+    """x + proj(MultiHeadAttention(ln1(x)))   (GPT1.py:163, 134-136, 109-123)."""
+
+    @staticmethod
+    def forward(ctx, x, lc, ln_w, ln_b, qkv_w, proj_w, proj_b, *params):
+        B, T, C = x.shape
+        x2 = x.reshape(B * T, C)
+        act = lc.act
+        a, mean, rstd = layernorm(x2, ln_w.master, ln_b.master, act)
+        qkv = torch.empty((B * T, 3 * C), dtype=act, device=x.device)
+        linear_fwd(a, qkv_w.operand(act), qkv)
+        o = torch.empty((B * T, C), dtype=act, device=x.device)
+        lse = attention_fwd(qkv, B, T, lc.n_head, lc.head_size, o, lc.scale, lc.p, lc.seed, lc.rng_call, lc.site)
+        out = torch.empty((B * T, C), dtype=torch.float32, device=x.device)
+        linear_fwd(o, proj_w.operand(act), out, "bias_resid", bias=proj_b.master, resid=x2)
+        ctx.save_for_backward(x2, a, mean, rstd, qkv, o, lse)
+        ctx.lc, ctx.regs, ctx.shape = lc, (ln_w, ln_b, qkv_w, proj_w, proj_b), (B, T, C)
+        return out.view(B, T, C)
+
+    @staticmethod
+    def backward(ctx, dout):
+        x2, a, mean, rstd, qkv, o, lse = ctx.saved_tensors
+        lc = ctx.lc
+        ln_w, ln_b, qkv_w, proj_w, proj_b = ctx.regs
+        B, T, C = ctx.shape
+        act = lc.act
+        d32 = dout.reshape(B * T, C).contiguous()
+        dy = to_act(d32, act)
+        # proj: dW = dy^T o, db = colsum(dy), do = dy W
+        g, beta, f_pw = proj_w.grad_target()
+        if g is not None:
+            linear_wgrad(dy, o, g, beta)
+        g, beta, f_pb = proj_b.grad_target()
+        if g is not None:
+            colsum_into(dy, g, beta)
+        do = torch.empty((B * T, C), dtype=act, device=x2.device)
+        linear_dgrad(dy, proj_w.operand(act), do)
+        dqkv = attention_bwd(qkv, B, T, lc.n_head, lc.head_size, o, do, lse, lc.scale, lc.p, lc.seed, lc.rng_call,
+                             lc.site)
+        g, beta, f_qkv = qkv_w.grad_target()
+        if g is not None:
+            linear_wgrad(dqkv, a, g, beta)
+        da = torch.empty((B * T, C), dtype=act, device=x2.device)
+        linear_dgrad(dqkv, qkv_w.operand(act), da)
+        dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd, dres=d32)
+        return (dx.view(B, T, C), None, None, None, None, None, None, *f_ln, *f_qkv(), *f_pw(), *f_pb())
+
+
+class FFNSublayerFn(torch.autograd.Function):
+    """x + Dropout(W2 relu(W1 ln2(x) + b1) + b2)   (GPT1.py:164, 142-147)."""
+
+    @staticmethod
+    def forward(ctx, x, lc, ln_w, ln_b, w1, b1, w2, b2, *params):
+        B, T, C = x.shape
+        x2 = x.reshape(B * T, C)
+        act = lc.act
+        a, mean, rstd = layernorm(x2, ln_w.master, ln_b.master, act)
+        F4 = w1.master.shape[0]
+        h = torch.empty((B * T, F4), dtype=act, device=x.device)
+        linear_fwd(a, w1.operand(act), h, "bias_relu", bias=b1.master)
+        out = torch.empty((B * T, C), dtype=torch.float32, device=x.device)
+        linear_fwd(h, w2.operand(act), out, "bias_drop_resid", bias=b2.master, resid=x2, dropout_p=lc.p,
+                   seed=lc.seed, rng_call=lc.rng_call, site=lc.site)
+        ctx.save_for_backward(x2, a, mean, rstd, h)
+        ctx.lc, ctx.regs, ctx.shape = lc, (ln_w, ln_b, w1, b1, w2, b2), (B, T, C)
+        return out.view(B, T, C)
+
+    @staticmethod
+    def backward(ctx, dout):
+        x2, a, mean, rstd, h = ctx.saved_tensors
+        lc = ctx.lc
+        ln_w, ln_b, w1, b1, w2, b2 = ctx.regs
+        B, T, C = ctx.shape
+        act = lc.act
+        d32 = dout.reshape(B * T, C).contiguous()
+        dz2 = torch.empty((B * T, C), dtype=act, device=x2.device)
+        ops.dropout_apply(d32, dz2, float(lc.p), int(lc.seed), lc.rng_call, int(lc.site))
+        g, beta, f_w2 = w2.grad_target()
+        if g is not None:
+            linear_wgrad(dz2, h, g, beta)
+        g, beta, f_b2 = b2.grad_target()
+        if g is not None:
+            colsum_into(dz2, g, beta)
+        dz1 = torch.empty_like(h)
+        linear_dgrad(dz2, w2.operand(act), dz1, "relu_bwd", aux=h)
+        g, beta, f_w1 = w1.grad_target()
+        if g is not None:
+            linear_wgrad(dz1, a, g, beta)
+        g, beta, f_b1 = b1.grad_target()
+        if g is not None:
+            colsum_into(dz1, g, beta)
+        da = torch.empty((B * T, C), dtype=act, device=x2.device)
+        linear_dgrad(dz1, w1.operand(act), da)
+        dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd, dres=d32)
+        return (dx.view(B, T, C), None, None, None, None, None, None, None, *f_ln, *f_w1(), *f_b1(), *f_w2(),
+                *f_b2())
+
+
+class HeadLossFn(torch.autograd.Function):
+    """ln_f -> lm_head -> (optional) mean cross entropy   (GPT1.py:183-192)."""
+
+    @staticmethod
+    def forward(ctx, x, targets, act, ln_w, ln_b, lm_w, lm_b, *params):
+        B, T, C = x.shape
+        M = B * T
+        x2 = x.reshape(M, C)
+        a, mean, rstd = layernorm(x2, ln_w.master, ln_b.master, act)
+        V = lm_w.master.shape[0]
+        logits = torch.empty((M, V), dtype=torch.float32, device=x.device)
+        linear_fwd(a, lm_w.operand(act), logits, "bias", bias=lm_b.master)
+        lse = torch.empty(M, dtype=torch.float32, device=x.device)
+        ctx.regs, ctx.shape, ctx.act = (ln_w, ln_b, lm_w, lm_b), (B, T, C), act
+        ctx.set_materialize_grads(False)
+        if targets is None:
+            ctx.save_for_backward(x2, a, mean, rstd, logits, lse)
+            ctx.has_targets = False
+            return logits.view(B, T, V)
+        t1 = targets.reshape(M)
+        loss_rows = torch.empty(M, dtype=torch.float32, device=x.device)
+        ops.ce_fwd(logits, t1, loss_rows, lse)
+        loss = torch.empty((), dtype=torch.float32, device=x.device)
+        ws = torch.empty(1024, dtype=torch.float32, device=x.device)
+        ops.sum_scaled(loss_rows, 1.0 / M, loss, ws)
+        ctx.save_for_backward(x2, a, mean, rstd, logits, lse, t1)
+        ctx.has_targets = True
+        return logits, loss
+
+    @staticmethod
+    def backward(ctx, *grads):
+        ln_w, ln_b, lm_w, lm_b = ctx.regs
+        B, T, C = ctx.shape
+        act = ctx.act
+        M = B * T
+        if ctx.has_targets:
+            x2, a, mean, rstd, logits, lse, t1 = ctx.saved_tensors
+            g_logits, g_loss = grads
+        else:
+            x2, a, mean, rstd, logits, lse = ctx.saved_tensors
+            g_logits, g_loss = grads[0], None
+        V = logits.shape[-1]
+        dl = torch.empty((M, V), dtype=torch.float32, device=x2.device)
+        if g_loss is not None:
+            ops.ce_bwd(logits, t1, lse, g_loss.reshape(1).float().contiguous(), 1.0 / M, dl, None)
+            if g_logits is not None:
+                dl.add_(g_logits.reshape(M, V))
+        else:
+            dl.copy_(g_logits.reshape(M, V))
+        dl_op = dl if act == torch.float32 else to_act(dl, act)
+        g, beta, f_lw = lm_w.grad_target()
+        if g is not None:
+            linear_wgrad(dl_op, a, g, beta)
+        g, beta, f_lb = lm_b.grad_target()
+        if g is not None:
+            colsum_into(dl, g, beta)
+        da = torch.empty((M, C), dtype=act, device=x2.device)
+        linear_dgrad(dl_op, lm_w.operand(act), da)
+        dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd)
+        return (dx.view(B, T, C), None, None, None, None, None, None, *f_ln, *f_lw(), *f_lb())
+
+
+# ---------------------------------------------------------------------------------------
+# standalone module paths (GPT1.py classes used on their own)
+# ---------------------------------------------------------------------------------------
+class LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w_reg, b_reg, eps, *params):
+        shp = x.shape
+        x2 = _flat2(x.float().contiguous())
+        y, mean, rstd = layernorm(x2, w_reg.master, b_reg.master, torch.float32, eps)
+        ctx.save_for_backward(x2, mean, rstd)
+        ctx.regs = (w_reg, b_reg)
+        return y.view(shp)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, mean, rstd = ctx.saved_tensors
+        w_reg, b_reg = ctx.regs
+        dx, _, f = layernorm_bwd(_flat2(dy.float().contiguous()), x2, w_reg, b_reg, mean, rstd)
+        return (dx.view(dy.shape), None, None, None, *f)
+
+
+class MHAFn(torch.autograd.Function):
+    """MultiHeadAttention.forward / Head.forward on an arbitrary (already normalised) input:
+    out = [proj](cat_h softmax(mask(q_h k_h^T * C^-0.5)) v_h)  (GPT1.py:109-123,134-136).
+    proj_w None -> single Head (no projection)."""
+
+    @staticmethod
+    def forward(ctx, x, lc, qkv_w, proj_w, proj_b, *params):
+        B, T, C = x.shape
+        act = lc.act
+        x2 = to_act(_flat2(x.float().contiguous()), act)
+        d = lc.n_head * lc.head_size
+        qkv = torch.empty((B * T, 3 * d), dtype=act, device=x.device)
+        linear_fwd(x2, qkv_w.operand(act), qkv)
+        o = torch.empty((B * T, d), dtype=act, device=x.device)
+        lse = attention_fwd(qkv, B, T, lc.n_head, lc.head_size, o, lc.scale, lc.p, lc.seed, lc.rng_call, lc.site)
+        if proj_w is not None:
+            out = torch.empty((B * T, proj_w.master.shape[0]), dtype=torch.float32, device=x.device)
+            linear_fwd(o, proj_w.operand(act), out, "bias", bias=proj_b.master)
+        else:
+            out = o.float()
+        ctx.save_for_backward(x2, qkv, o, lse)
+        ctx.lc, ctx.regs, ctx.shape = lc, (qkv_w, proj_w, proj_b), (B, T, C)
+        return out.view(B, T, -1)
+
+    @staticmethod
+    def backward(ctx, dout):
+        x2, qkv, o, lse = ctx.saved_tensors
+        lc = ctx.lc
+        qkv_w, proj_w, proj_b = ctx.regs
+        B, T, C = ctx.shape
+        act = lc.act
+        d32 = _flat2(dout.float().contiguous())
+        rets = []
+        if proj_w is not None:
+            dy = to_act(d32, act)
+            g, beta, f_pw = proj_w.grad_target()
+            if g is not None:
+                linear_wgrad(dy, o, g, beta)
+            g, beta, f_pb = proj_b.grad_target()
+            if g is not None:
+                colsum_into(dy, g, beta)
+            do = torch.empty(o.shape, dtype=act, device=o.device)
+            linear_dgrad(dy, proj_w.operand(act), do)
+            rets = [*f_pw(), *f_pb()]
+        else:
+            do = to_act(d32, act)
+        dqkv = attention_bwd(qkv, B, T, lc.n_head, lc.head_size, o, do, lse, lc.scale, lc.p, lc.seed, lc.rng_call,
+                             lc.site)
+        g, beta, f_qkv = qkv_w.grad_target()
+        if g is not None:
+            linear_wgrad(dqkv, x2, g, beta)
+        dx = torch.empty((B * T, C), dtype=torch.float32, device=o.device)
+        linear_dgrad(dqkv, qkv_w.operand(act), dx)
+        return (dx.view(B, T, C), None, None, None, None, *f_qkv(), *rets)
+
+
+class FFNFn(torch.autograd.Function):
+    """FeedForward.forward (GPT1.py:142-150) on an arbitrary input: Dropout(W2 relu(W1 x + b1) + b2)."""
+
+    @staticmethod
+    def forward(ctx, x, lc, w1, b1, w2, b2, *params):
+        B, T, C = x.shape
+        act = lc.act
+        x2 = to_act(_flat2(x.float().contiguous()), act)
+        h = torch.empty((B * T, w1.master.shape[0]), dtype=act, device=x.device)
+        linear_fwd(x2, w1.operand(act), h, "bias_relu", bias=b1.master)
+        out = torch.empty((B * T, C), dtype=torch.float32, device=x.device)
+        linear_fwd(h, w2.operand(act), out, "bias_drop_resid", bias=b2.master, resid=None, dropout_p=lc.p,
+                   seed=lc.seed, rng_call=lc.rng_call, site=lc.site)
+        ctx.save_for_backward(x2, h)
+        ctx.lc, ctx.regs, ctx.shape = lc, (w1, b1, w2, b2), (B, T, C)
+        return out.view(B, T, C)
+
+    @staticmethod
+    def backward(ctx, dout):
+        x2, h = ctx.saved_tensors
+        lc = ctx.lc
+        w1, b1, w2, b2 = ctx.regs
+        B, T, C = ctx.shape
+        act = lc.act
+        d32 = _flat2(dout.float().contiguous())
+        dz2 = torch.empty((B * T, C), dtype=act, device=h.device)
+        ops.dropout_apply(d32, dz2, float(lc.p), int(lc.seed), lc.rng_call, int(lc.site))
+        g, beta, f_w2 = w2.grad_target()
+        if g is not None:
+            linear_wgrad(dz2, h, g, beta)
+        g, beta, f_b2 = b2.grad_target()
+        if g is not None:
+            colsum_into(dz2, g, beta)
+        dz1 = torch.empty_like(h)
+        linear_dgrad(dz2, w2.operand(act), dz1, "relu_bwd", aux=h)
+        g, beta, f_w1 = w1.grad_target()
+        if g is not None:
+            linear_wgrad(dz1, x2, g, beta)
+        g, beta, f_b1 = b1.grad_target()
+        if g is not None:
+            colsum_into(dz1, g, beta)
+        dx = torch.empty((B * T, C), dtype=torch.float32, device=h.device)
+        linear_dgrad(dz1, w1.operand(act), dx)
+        return (dx.view(B, T, C), None, None, None, None, None, *f_w1(), *f_b1(), *f_w2(), *f_b2())
+
+
+class LinearFn(torch.autograd.Function):
+    """nn.Linear on its own (exact fp32 GEMMs): y = x W^T + b."""
+
+    @staticmethod
+    def forward(ctx, x, w_reg, b_reg, *params):
+        shp = x.shape
+        x2 = _flat2(x.float().contiguous())
+        N = w_reg.master.shape[0]
+        out = torch.empty((x2.shape[0], N), dtype=torch.float32, device=x.device)
+        linear_fwd(x2, w_reg.master, out, "bias" if b_reg is not None else "store",
+                   bias=b_reg.master if b_reg is not None else None)
+        ctx.save_for_backward(x2)
+        ctx.regs = (w_reg, b_reg)
+        return out.view(*shp[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x2,) = ctx.saved_tensors
+        w_reg, b_reg = ctx.regs
+        d2 = _flat2(dy.float().contiguous())
+        g, beta, fw = w_reg.grad_target()
+        if g is not None:
+            linear_wgrad(d2, x2, g, beta)
+        rets = fw()
+        if b_reg is not None:
+            g, beta, fb = b_reg.grad_target()
+            if g is not None:
+                colsum_into(d2, g, beta)
+            rets = rets + fb()
+        dx = torch.empty(x2.shape, dtype=torch.float32, device=x2.device)
+        linear_dgrad(d2, w_reg.master, dx)
+        return (dx.view(*dy.shape[:-1], x2.shape[-1]), None, None, *rets)
+
+
+def attention_scale(n_embd):
+    """Q1: the reference scales by C ** -0.5 with C = n_embd (GPT1.py:110,114), not head_size."""
+    return float(n_embd) ** -0.5

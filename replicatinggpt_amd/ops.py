@@ -1,0 +1,195 @@
+"""torch.library custom ops over the charpt C ABI (include/charpt.h).
+
+Each op is a thin, out-style wrapper: the caller (replicatinggpt_amd.functional) allocates every
+output/workspace through PyTorch's caching allocator, and the op launches the HIP kernel on the
+current stream (so whole training steps are capturable into a hipGraph).  Ops are registered for
+the "cuda" (= HIP on ROCm) device only: calling them on CPU tensors raises -- the product has no
+CPU fallback.
+"""
+from typing import Optional
+
+import torch
+from torch import Tensor
+
+from . import _lib as L
+
+_NS = "charpt"
+
+
+def _s(t):
+    return L.stream_ptr(t.device)
+
+
+def _op(name, mutates):
+    return torch.library.custom_op(f"{_NS}::{name}", mutates_args=mutates, device_types="cuda")
+
+
+# ---------------------------------------------------------------------------------------
+@_op("rng_snapshot", ("counter", "snap"))
+def rng_snapshot(counter: Tensor, snap: Tensor) -> None:
+    L.check(L.load().cg_rng_snapshot(L.ptr(counter), L.ptr(snap), _s(counter)), "rng_snapshot")
+
+
+@_op("counter_add", ("counter",))
+def counter_add(counter: Tensor, delta: int) -> None:
+    L.check(L.load().cg_counter_add(L.ptr(counter), delta, _s(counter)), "counter_add")
+
+
+@_op("dropout_mask", ("out",))
+def dropout_mask(out: Tensor, p: float, seed: int, rng_call: Optional[Tensor], site: int) -> None:
+    L.check(L.load().cg_dropout_mask(L.ptr(out), out.numel(), p, seed, L.ptr(rng_call), site, _s(out)), "dropout_mask")
+
+
+@_op("dropout_apply", ("out",))
+def dropout_apply(x: Tensor, out: Tensor, p: float, seed: int, rng_call: Optional[Tensor], site: int) -> None:
+    C = x.shape[-1]
+    rows = x.numel() // C
+    L.check(L.load().cg_dropout_apply(L.ptr(x), rows, C, C, L.ptr(out), L.dtype_code(out.dtype), p, seed,
+                                      L.ptr(rng_call), site, _s(x)), "dropout_apply")
+
+
+@_op("sum_scaled", ("out", "ws"))
+def sum_scaled(x: Tensor, scale: float, out: Tensor, ws: Tensor) -> None:
+    L.check(L.load().cg_sum_f32(L.ptr(x), x.numel(), scale, L.ptr(out), L.ptr(ws), _s(x)), "sum_f32")
+
+
+@_op("cast_bf16", ("out",))
+def cast_bf16(x: Tensor, out: Tensor) -> None:
+    L.check(L.load().cg_cast_f32_bf16(L.ptr(x), L.ptr(out), x.numel(), _s(x)), "cast_f32_bf16")
+
+
+@_op("gather_batch", ("x", "y"))
+def gather_batch(data: Tensor, ix: Tensor, x: Tensor, y: Tensor) -> None:
+    B, T = x.shape
+    L.check(L.load().cg_gather_batch(L.ptr(data), int(data.dtype == torch.uint8), L.ptr(ix), L.ptr(x), L.ptr(y), B,
+                                     T, _s(x)), "gather_batch")
+
+
+# ---------------------------------------------------------------------------------------
+@_op("embed_fwd", ("x",))
+def embed_fwd(idx: Tensor, wte: Tensor, wpe: Tensor, x: Tensor) -> None:
+    B, T = idx.shape
+    V, C = wte.shape
+    L.check(L.load().cg_embed_fwd(L.ptr(idx), L.ptr(wte), L.ptr(wpe), L.ptr(x), B, T, C, V, _s(x)), "embed_fwd")
+
+
+@_op("embed_bwd", ("dwte", "dwpe", "ws"))
+def embed_bwd(idx: Tensor, dx: Tensor, dwte: Optional[Tensor], dwpe: Optional[Tensor], accumulate: bool,
+              ws: Tensor) -> None:
+    B, T = idx.shape
+    C = dx.shape[-1]
+    V = dwte.shape[0] if dwte is not None else 1
+    L.check(L.load().cg_embed_bwd(L.ptr(idx), L.ptr(dx), L.ptr(dwte), L.ptr(dwpe), B, T, C, V, int(accumulate),
+                                  L.ptr(ws), _s(dx)), "embed_bwd")
+
+
+def embed_bwd_workspace(B, T, C, V):
+    return L.load().cg_embed_bwd_workspace(B, T, C, V)
+
+
+# ---------------------------------------------------------------------------------------
+@_op("layernorm_fwd", ("y", "mean", "rstd"))
+def layernorm_fwd(x: Tensor, w: Tensor, b: Tensor, y: Tensor, mean: Tensor, rstd: Tensor, eps: float) -> None:
+    C = x.shape[-1]
+    rows = x.numel() // C
+    L.check(L.load().cg_layernorm_fwd(L.ptr(x), L.ptr(w), L.ptr(b), L.ptr(y), L.dtype_code(y.dtype), L.ptr(mean),
+                                      L.ptr(rstd), rows, C, eps, _s(x)), "layernorm_fwd")
+
+
+@_op("layernorm_bwd", ("dx", "dx_lp", "dw", "db", "ws"))
+def layernorm_bwd(dy: Tensor, x: Tensor, w: Tensor, mean: Tensor, rstd: Tensor, dres: Optional[Tensor], dx: Tensor,
+                  dx_lp: Optional[Tensor], dw: Optional[Tensor], db: Optional[Tensor], accumulate: bool,
+                  ws: Tensor) -> None:
+    C = x.shape[-1]
+    rows = x.numel() // C
+    L.check(L.load().cg_layernorm_bwd(L.ptr(dy), L.dtype_code(dy.dtype), L.ptr(x), L.ptr(w), L.ptr(mean), L.ptr(rstd),
+                                      L.ptr(dres), L.ptr(dx), L.ptr(dx_lp), L.ptr(dw), L.ptr(db), int(accumulate),
+                                      L.ptr(ws), rows, C, _s(x)), "layernorm_bwd")
+
+
+def layernorm_bwd_workspace(rows, C):
+    return L.load().cg_layernorm_bwd_workspace(rows, C)
+
+
+# ---------------------------------------------------------------------------------------
+@_op("gemm", ("out", "ws"))
+def gemm(a: Tensor, b: Tensor, out: Tensor, op_bf16: bool, a_trans: bool, b_trans: bool, M: int, N: int, K: int,
+         lda: int, ldb: int, ldc: int, epi: int, bias: Optional[Tensor], resid: Optional[Tensor], ld_resid: int,
+         aux: Optional[Tensor], ld_aux: int, dropout_p: float, seed: int, rng_call: Optional[Tensor], site: int,
+         beta: float, split_k: int, ws: Optional[Tensor]) -> None:
+    e = L.Epilogue(epi, L.ptr(bias), L.ptr(resid), ld_resid, L.ptr(aux),
+                   L.dtype_code(aux.dtype) if aux is not None else 0, ld_aux, dropout_p, seed, L.ptr(rng_call), site,
+                   beta)
+    L.check(L.load().cg_gemm(L.CG_BF16 if op_bf16 else L.CG_F32, int(a_trans), int(b_trans), M, N, K, L.ptr(a), lda,
+                             L.ptr(b), ldb, L.ptr(out), L.dtype_code(out.dtype), ldc, e, split_k, L.ptr(ws), _s(out)),
+            "gemm")
+
+
+def gemm_workspace(M, N, split_k):
+    return L.load().cg_gemm_workspace(M, N, split_k)
+
+
+@_op("colsum", ("out", "ws"))
+def colsum(x: Tensor, out: Tensor, accumulate: bool, ws: Tensor) -> None:
+    N = x.shape[-1]
+    rows = x.numel() // N
+    L.check(L.load().cg_colsum(L.ptr(x), L.dtype_code(x.dtype), rows, N, N, L.ptr(out), int(accumulate), L.ptr(ws),
+                               _s(x)), "colsum")
+
+
+def colsum_workspace(rows, N):
+    return L.load().cg_colsum_workspace(rows, N)
+
+
+# ---------------------------------------------------------------------------------------
+@_op("attn_fwd", ("o", "lse"))
+def attn_fwd(qkv: Tensor, B: int, T: int, H: int, D: int, q_off: int, k_off: int, v_off: int, ld: int, o: Tensor,
+             ld_o: int, lse: Tensor, scale: float, dropout_p: float, seed: int, rng_call: Optional[Tensor],
+             site: int) -> None:
+    es = qkv.element_size()
+    base = qkv.data_ptr()
+    L.check(L.load().cg_attn_fwd(L.dtype_code(qkv.dtype), B, T, H, D, base + q_off * es, base + k_off * es,
+                                 base + v_off * es, ld, L.ptr(o), ld_o, L.ptr(lse), scale, dropout_p, seed,
+                                 L.ptr(rng_call), site, _s(qkv)), "attn_fwd")
+
+
+@_op("attn_bwd", ("dqkv", "ws"))
+def attn_bwd(qkv: Tensor, B: int, T: int, H: int, D: int, q_off: int, k_off: int, v_off: int, ld: int, o: Tensor,
+             ld_o: int, dout: Tensor, ld_do: int, lse: Tensor, dqkv: Tensor, ld_d: int, scale: float,
+             dropout_p: float, seed: int, rng_call: Optional[Tensor], site: int, ws: Tensor) -> None:
+    es = qkv.element_size()
+    base, dbase = qkv.data_ptr(), dqkv.data_ptr()
+    L.check(L.load().cg_attn_bwd(L.dtype_code(qkv.dtype), B, T, H, D, base + q_off * es, base + k_off * es,
+                                 base + v_off * es, ld, L.ptr(o), ld_o, L.ptr(dout), ld_do, L.ptr(lse),
+                                 dbase + q_off * es, dbase + k_off * es, dbase + v_off * es, ld_d, scale, dropout_p,
+                                 seed, L.ptr(rng_call), site, L.ptr(ws), _s(qkv)), "attn_bwd")
+
+
+def attn_bwd_workspace(B, T, H, D):
+    return L.load().cg_attn_bwd_workspace(B, T, H, D)
+
+
+# ---------------------------------------------------------------------------------------
+@_op("ce_fwd", ("loss_rows", "lse"))
+def ce_fwd(logits: Tensor, targets: Optional[Tensor], loss_rows: Optional[Tensor], lse: Tensor) -> None:
+    V = logits.shape[-1]
+    rows = logits.numel() // V
+    L.check(L.load().cg_ce_fwd(L.ptr(logits), rows, V, V, L.ptr(targets), L.ptr(loss_rows), L.ptr(lse),
+                               _s(logits)), "ce_fwd")
+
+
+@_op("ce_bwd", ("dlogits", "dlogits_lp"))
+def ce_bwd(logits: Tensor, targets: Tensor, lse: Tensor, g: Tensor, g_mult: float, dlogits: Optional[Tensor],
+           dlogits_lp: Optional[Tensor]) -> None:
+    V = logits.shape[-1]
+    rows = logits.numel() // V
+    L.check(L.load().cg_ce_bwd(L.ptr(logits), rows, V, V, L.ptr(targets), L.ptr(lse), L.ptr(g), g_mult,
+                               L.ptr(dlogits), V, L.ptr(dlogits_lp), _s(logits)), "ce_bwd")
+
+
+# ---------------------------------------------------------------------------------------
+@_op("adamw", ("p", "m", "v", "p_bf16"))
+def adamw(p: Tensor, g: Tensor, m: Tensor, v: Tensor, p_bf16: Optional[Tensor], lr: float, beta1: float, beta2: float,
+          eps: float, weight_decay: float, step: Tensor) -> None:
+    L.check(L.load().cg_adamw(L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), L.ptr(p_bf16), p.numel(), lr, beta1, beta2, eps,
+                              weight_decay, L.ptr(step), _s(p)), "adamw")

@@ -1,0 +1,169 @@
+"""Model-level parity on the MI355X against vectors produced by the reference GPT1.py
+(tests/golden) and against the CPU oracle (same Philox dropout masks)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_path, ROOT
+from oracle import gpt1_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+
+
+def relerr(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-30))
+
+
+def build_model(cfg_t, dtype="fp32", dropout=0.0, sd=None):
+    from replicatinggpt_amd import BigramLanguageModel, GPTConfig
+    B, T, C, H, L = [int(v) for v in cfg_t]
+    cfg = GPTConfig(block_size=T, n_embd=C, n_head=H, n_layers=L, dropout=dropout, dtype=dtype)
+    m = BigramLanguageModel(cfg)
+    if sd is not None:
+        missing, unexpected = m.load_state_dict(sd, strict=False)
+        assert not unexpected and all("tril" in k for k in missing)
+    return m.to(DEV), cfg, B
+
+
+@pytest.mark.parametrize("tag", ["S", "S_odd"])
+def test_model_fp32_matches_reference(tag):
+    g = torch.load(golden_path("ops_small.pt"), weights_only=True)[tag]
+    m, cfg, B = build_model(g["config"], sd=g["state_dict"])
+    ref = g["model"]
+    logits, loss = m(ref["idx"].to(DEV), ref["targets"].to(DEV))
+    loss.backward()
+    assert abs(float(loss) - float(ref["loss"])) < 1e-5
+    assert relerr(logits, ref["logits"]) < 1e-5
+    for name, p in m.named_parameters():
+        assert relerr(p.grad, ref["grad." + name]) < 1e-4, name
+    with torch.no_grad():
+        lg, ls = m(ref["idx"][:, : cfg.block_size - 3].to(DEV))
+    assert ls is None and tuple(lg.shape) == tuple(ref["logits_notarget_short"].shape)
+    assert relerr(lg, ref["logits_notarget_short"]) < 1e-5
+
+
+@pytest.mark.parametrize("tag", ["S", "S_odd"])
+def test_modules_fp32_match_reference(tag):
+    g = torch.load(golden_path("ops_small.pt"), weights_only=True)[tag]
+    m, cfg, B = build_model(g["config"], sd=g["state_dict"])
+    blk = m.blocks[0]
+    for case, mod in [("ln1", blk.ln1), ("head0", blk.sa_heads.heads[0]), ("head0_short", blk.sa_heads.heads[0]),
+                      ("mha", blk.sa_heads), ("ffwd", blk.ffwd), ("block0", blk)]:
+        c = g[case]
+        m.zero_grad(set_to_none=True)
+        x = c["x"].to(DEV).requires_grad_(True)
+        out = mod(x)
+        out.backward(c["grad_out"].to(DEV))
+        assert relerr(out, c["out"]) < 1e-5, case
+        assert relerr(x.grad, c["grad_x"]) < 1e-4, case
+        for n, p in mod.named_parameters():
+            assert relerr(p.grad, c["grad." + n]) < 1e-4, (case, n)
+
+
+def test_c1_shape_grads_match_reference():
+    g = torch.load(golden_path("model_c1_grads.pt"), weights_only=True)
+    from replicatinggpt_amd import BigramLanguageModel, GPTConfig
+    torch.manual_seed(1337)
+    m = BigramLanguageModel(GPTConfig(dropout=0.0, dtype="fp32")).to(DEV)
+    logits, loss = m(g["idx"].to(DEV), g["targets"].to(DEV))
+    loss.backward()
+    assert abs(float(loss) - float(g["loss"])) < 1e-5
+    assert relerr(logits[:8], g["logits_head"]) < 1e-5
+    grads = dict(m.named_parameters())
+    for k, n in g["grad_norms"].items():
+        assert abs(float(grads[k].grad.double().norm()) - n) <= 1e-4 * n + 1e-7, k
+    for k, gr in g["grads"].items():
+        assert relerr(grads[k].grad, gr) < 1e-4, k
+
+
+def test_dropout_model_matches_oracle_fp32():
+    """p = 0.2: the HIP model and the CPU oracle draw identical Philox masks."""
+    from replicatinggpt_amd import BigramLanguageModel, GPTConfig
+    cfg = GPTConfig(block_size=64, n_embd=64, n_head=2, n_layers=2, dropout=0.2, dtype="fp32")
+    torch.manual_seed(1337)
+    m = BigramLanguageModel(cfg).to(DEV)
+    ocfg = O.OracleConfig(block_size=64, n_embd=64, n_head=2, n_layers=2, dropout=0.2)
+    torch.manual_seed(1337)
+    P = O.init_params(ocfg)
+    gen = torch.Generator().manual_seed(5)
+    idx = torch.randint(0, 65, (3, 64), generator=gen)
+    tgt = torch.randint(0, 65, (3, 64), generator=gen)
+    for call in range(2):
+        m.zero_grad(set_to_none=True)
+        logits, loss = m(idx.to(DEV), tgt.to(DEV))
+        loss.backward()
+        _, rl, rg = O.loss_and_grads(P, idx, tgt, ocfg, train=True, seed=cfg.dropout_seed, call=call)
+        assert abs(float(loss) - float(rl)) < 1e-5, call
+        for name, p in m.named_parameters():
+            assert relerr(p.grad, rg[name]) < 1e-4, (call, name)
+
+
+@pytest.mark.parametrize("T,C,H", [(256, 384, 6), (128, 128, 2)])
+def test_bf16_model_close_to_fp32(T, C, H):
+    from replicatinggpt_amd import BigramLanguageModel, GPTConfig
+    cfg = GPTConfig(block_size=T, n_embd=C, n_head=H, n_layers=2, dropout=0.0, dtype="fp32")
+    torch.manual_seed(0)
+    m32 = BigramLanguageModel(cfg).to(DEV)
+    torch.manual_seed(0)
+    m16 = BigramLanguageModel(cfg.with_(dtype="bf16")).to(DEV)
+    idx = torch.randint(0, 65, (4, T), device=DEV)
+    tgt = torch.randint(0, 65, (4, T), device=DEV)
+    _, l32 = m32(idx, tgt)
+    l32.backward()
+    _, l16 = m16(idx, tgt)
+    l16.backward()
+    assert abs(float(l16) - float(l32)) < 2e-2 * float(l32)
+    g32 = dict(m32.named_parameters())
+    for n, p in m16.named_parameters():
+        assert relerr(p.grad, g32[n].grad) < 5e-2, n
+
+
+def test_train_steps_match_reference_p0():
+    """GPT1.py:221-233 with Dropout=0: same batch indices, fp32 HIP path, per-step losses."""
+    from replicatinggpt_amd import AdamW, BigramLanguageModel, GPTConfig
+    from replicatinggpt_amd.data import BatchSampler, TokenStream
+    g = torch.load(golden_path("train_c1_p0.pt"), weights_only=True)
+    for key, lr in [("lr0.0002", 2e-4), ("lr0.5", 0.5)]:
+        want = g[key]
+        torch.manual_seed(1337)
+        m = BigramLanguageModel(GPTConfig(dropout=0.0, dtype="fp32")).to(DEV)
+        tok, ts = TokenStream.from_file(device=DEV)
+        sampler = BatchSampler(ts, 256, 64)
+        opt = AdamW(m.parameters(), lr=lr).attach(m)
+        n = len(want) if key == "lr0.0002" else 3
+        for i in range(n):
+            xb, yb = sampler.get_batch("train")
+            _, loss = m(xb, yb)
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
+            opt.step()
+            tol = 1e-4 * (i + 1) * max(1.0, float(want[i]))
+            assert abs(float(loss) - float(want[i])) < tol, (key, i, float(loss), float(want[i]))
+
+
+def test_greedy_generate_matches_reference():
+    """Greedy 500-token stream from the reference-trained C1 weights, fp32 (north_star check)."""
+    from safetensors.torch import load_file
+    from replicatinggpt_amd import BigramLanguageModel, GPTConfig
+    sd = load_file(golden_path("model_c1_trained.safetensors"))
+    gold = torch.load(golden_path("trained_c1.pt"), weights_only=True)
+    m = BigramLanguageModel(GPTConfig(dtype="fp32"))
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    assert not unexpected and all("tril" in k for k in missing)
+    m = m.to(DEV).eval()
+    with torch.no_grad():
+        for tag in ["zeros", "batch4"]:
+            want = gold["streams"][tag]["tokens"]
+            out = m.generate(want[:, :1].to(DEV), 500, greedy=True)
+            assert torch.equal(out.cpu(), want), tag

@@ -1,0 +1,288 @@
+"""Per-kernel parity on the MI355X: each charpt op against a plain fp32/fp64 torch CPU
+reference (and the numpy Philox oracle for dropout masks).  Tolerances: fp32 path rtol 1e-5
+(relative to the output scale), bf16 path 2e-2 -- the north_star's bars."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import philox
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    from replicatinggpt_amd import _lib as L
+    L.load()
+    yield
+
+
+def ops():
+    from replicatinggpt_amd import ops as O
+    return O
+
+
+def F():
+    from replicatinggpt_amd import functional as Fn
+    return Fn
+
+
+def relerr(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-30))
+
+
+def test_device_is_gfx950():
+    from replicatinggpt_amd import _lib as L
+    import ctypes
+    n, ma, mi = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    L.check(L.load().cg_device_info(ctypes.byref(n), ctypes.byref(ma), ctypes.byref(mi)))
+    assert (ma.value, mi.value) == (9, 5) and n.value >= 64
+
+
+@pytest.mark.parametrize("p", [0.2, 0.5])
+def test_dropout_mask_matches_oracle(p):
+    n = 10007
+    call = torch.tensor([5], dtype=torch.int64, device=DEV)
+    out = torch.empty(n, dtype=torch.float32, device=DEV)
+    ops().dropout_mask(out, p, 0x1337, call, 3)
+    want = philox.keep_mask(0x1337, (5 << 8) | 3, np.arange(n), p)
+    assert np.array_equal(out.cpu().numpy() > 0.5, want)
+
+
+@pytest.mark.parametrize("C", [126, 384, 768, 33])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_layernorm(C, out_dtype):
+    torch.manual_seed(0)
+    rows = 300
+    x = torch.randn(rows, C) * 2 + 0.5
+    w = torch.randn(C) * 0.1 + 1
+    b = torch.randn(C) * 0.1
+    xr = x.clone().double().requires_grad_(True)
+    wr, br = w.double().requires_grad_(True), b.double().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (C,), wr, br, 1e-5)
+    gy = torch.randn(rows, C)
+    yr.backward(gy.double())
+    Fn = F()
+    y, mean, rstd = Fn.layernorm(x.to(DEV), w.to(DEV), b.to(DEV), out_dtype)
+    tol = 1e-5 if out_dtype == torch.float32 else 1e-2
+    assert relerr(y, yr) < tol
+    dres = torch.randn(rows, C)
+    wreg, breg = Fn.Region.of(torch.nn.Parameter(w.to(DEV))), Fn.Region.of(torch.nn.Parameter(b.to(DEV)))
+    dx, _, grads = Fn.layernorm_bwd(gy.to(DEV).to(out_dtype), x.to(DEV), wreg, breg, mean, rstd, dres=dres.to(DEV))
+    gyq = gy.to(out_dtype).double()
+    yr2 = torch.nn.functional.layer_norm(x.double().requires_grad_(True), (C,), w.double(), b.double(), 1e-5)
+    xr2 = x.double().requires_grad_(True)
+    wr2, br2 = w.double().requires_grad_(True), b.double().requires_grad_(True)
+    torch.nn.functional.layer_norm(xr2, (C,), wr2, br2, 1e-5).backward(gyq)
+    assert relerr(dx, xr2.grad + dres.double()) < 1e-5
+    assert relerr(grads[0], wr2.grad) < 1e-5
+    assert relerr(grads[1], br2.grad) < 1e-5
+
+
+def _ref_gemm(A, B, at, bt):
+    a = A.double().t() if at else A.double()
+    b = B.double().t() if bt else B.double()
+    return a @ b.t()
+
+
+@pytest.mark.parametrize("at,bt", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("shape", [(37, 65, 126), (128, 384, 192), (256, 128, 1536)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gemm_layouts(at, bt, shape, dt):
+    M, N, K = shape
+    torch.manual_seed(1)
+    A = (torch.randn(K, M) if at else torch.randn(M, K)).to(dt)
+    B = (torch.randn(K, N) if bt else torch.randn(N, K)).to(dt)
+    ref = _ref_gemm(A, B, at, bt)
+    out = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    lda = A.shape[1]
+    ldb = B.shape[1]
+    ops().gemm(A.to(DEV), B.to(DEV), out, dt == torch.bfloat16, bool(at), bool(bt), M, N, K, lda, ldb, N, 0, None,
+               None, 0, None, 0, 0.0, 0, None, 0, 0.0, 1, None)
+    assert relerr(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("split", [2, 4, 8])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gemm_splitk_deterministic(split, dt):
+    M, N, K = 128, 256, 2048
+    torch.manual_seed(2)
+    A = torch.randn(K, M).to(dt).to(DEV)
+    B = torch.randn(K, N).to(dt).to(DEV)
+    ref = _ref_gemm(A.cpu(), B.cpu(), 1, 1)
+    outs = []
+    for _ in range(2):
+        out = torch.empty(M, N, dtype=torch.float32, device=DEV)
+        ws = torch.empty(ops().gemm_workspace(M, N, split) // 4, dtype=torch.float32, device=DEV)
+        ops().gemm(A, B, out, dt == torch.bfloat16, True, True, M, N, K, M, N, N, 0, None, None, 0, None, 0, 0.0,
+                   0, None, 0, 0.0, split, ws)
+        outs.append(out.clone())
+    assert torch.equal(outs[0], outs[1])
+    assert relerr(outs[0], ref) < 1e-5
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(256, 384, 128), (96, 70, 40)])
+def test_gemm_epilogues(dt, M, N, K):
+    Fn = F()
+    torch.manual_seed(3)
+    x = torch.randn(M, K).to(dt)
+    w = torch.randn(N, K).to(dt)
+    bias = torch.randn(N)
+    resid = torch.randn(M, N)
+    acc = x.double() @ w.double().t()
+    xd, wd = x.to(DEV), w.to(DEV)
+    tol = 1e-5 if dt == torch.float32 else 8e-3
+    # bias + relu
+    h = torch.empty(M, N, dtype=dt, device=DEV)
+    Fn.linear_fwd(xd, wd, h, "bias_relu", bias=bias.to(DEV))
+    assert relerr(h, torch.relu(acc + bias.double())) < tol
+    # bias + residual (fp32 out)
+    o = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    Fn.linear_fwd(xd, wd, o, "bias_resid", bias=bias.to(DEV), resid=resid.to(DEV))
+    assert relerr(o, acc + bias.double() + resid.double()) < 1e-5
+    # bias + dropout + residual against the oracle mask
+    call = torch.tensor([9], dtype=torch.int64, device=DEV)
+    Fn.linear_fwd(xd, wd, o, "bias_drop_resid", bias=bias.to(DEV), resid=resid.to(DEV), dropout_p=0.2, seed=77,
+                  rng_call=call, site=5)
+    keep = philox.keep_mask(77, (9 << 8) | 5, np.arange(M * N), 0.2).reshape(M, N)
+    want = resid.double() + torch.from_numpy(keep).double() * (acc + bias.double()) * float(np.float32(1 / 0.8))
+    assert relerr(o, want) < 1e-5
+    # relu backward with an aux mask
+    aux = torch.randn(M, N).to(dt)
+    g = torch.empty(M, N, dtype=dt, device=DEV)
+    ops().gemm(xd, wd, g, dt == torch.bfloat16, False, False, M, N, K, K, K, N, 5, None, None, 0, aux.to(DEV), N,
+               0.0, 0, None, 0, 0.0, 1, None)
+    assert relerr(g, acc * (aux.double() > 0)) < tol
+
+
+def _attn_ref(q, k, v, scale, p=0.0, seed=0, stream=0):
+    """q,k,v [B,T,H,D] float64; reference softmax attention with the oracle dropout mask."""
+    B, T, H, D = q.shape
+    s = torch.einsum("bthd,bshd->bhts", q, k) * scale
+    mask = torch.tril(torch.ones(T, T, dtype=torch.bool))
+    s = s.masked_fill(~mask, float("-inf"))
+    P = torch.softmax(s, dim=-1)
+    if p > 0:
+        idx = np.arange(B * H * T * T, dtype=np.uint64).reshape(B, H, T, T)
+        keep = torch.from_numpy(philox.keep_mask(seed, stream, idx, p)).double()
+        P = P * keep * float(np.float32(1 / (1 - p)))
+    return torch.einsum("bhts,bshd->bthd", P, v)
+
+
+@pytest.mark.parametrize("B,T,H,D", [(2, 37, 3, 21), (2, 64, 2, 64), (1, 256, 2, 64), (2, 96, 1, 8)])
+@pytest.mark.parametrize("p", [0.0, 0.2])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_attention_fwd_bwd(B, T, H, D, p, dt):
+    Fn = F()
+    torch.manual_seed(4)
+    d = H * D
+    qkv = (torch.randn(B * T, 3 * d) * 0.7).to(dt)
+    scale = (3.0 * D) ** -0.5
+    q = qkv[:, :d].double().view(B, T, H, D).requires_grad_(True)
+    k = qkv[:, d:2 * d].double().view(B, T, H, D).requires_grad_(True)
+    v = qkv[:, 2 * d:].double().view(B, T, H, D).requires_grad_(True)
+    call = torch.tensor([2], dtype=torch.int64, device=DEV)
+    ref = _attn_ref(q, k, v, scale, p, 11, (2 << 8) | 7)
+    dout = torch.randn(B, T, H, D).to(dt)
+    ref.backward(dout.double())
+    qkv_d = qkv.to(DEV)
+    o = torch.empty(B * T, d, dtype=dt, device=DEV)
+    lse = Fn.attention_fwd(qkv_d, B, T, H, D, o, scale, p, 11, call, 7)
+    tol = 1e-5 if dt == torch.float32 else 2e-2
+    assert relerr(o, ref.reshape(B * T, d)) < tol
+    dqkv = Fn.attention_bwd(qkv_d, B, T, H, D, o, dout.reshape(B * T, d).to(DEV), lse, scale, p, 11, call, 7)
+    dq, dk, dv = dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:]
+    assert relerr(dq, q.grad.reshape(B * T, d)) < (1e-5 if dt == torch.float32 else 3e-2)
+    assert relerr(dk, k.grad.reshape(B * T, d)) < (1e-5 if dt == torch.float32 else 3e-2)
+    assert relerr(dv, v.grad.reshape(B * T, d)) < (1e-5 if dt == torch.float32 else 3e-2)
+
+
+def test_attention_fast_matches_generic_bf16():
+    """The MFMA head_size-64 kernels against the generic kernels on identical bf16 inputs."""
+    Fn = F()
+    B, T, H, D = 2, 256, 3, 64
+    torch.manual_seed(5)
+    d = H * D
+    qkv = (torch.randn(B * T, 3 * d)).to(torch.bfloat16).to(DEV)
+    call = torch.tensor([1], dtype=torch.int64, device=DEV)
+    o_fast = torch.empty(B * T, d, dtype=torch.bfloat16, device=DEV)
+    lse_fast = Fn.attention_fwd(qkv, B, T, H, D, o_fast, 0.05, 0.2, 3, call, 1)
+    # generic path: a non-16B-aligned leading dimension forces it
+    wide = torch.zeros(B * T, 3 * d + 4, dtype=torch.bfloat16, device=DEV)
+    wide[:, :3 * d] = qkv
+    view = wide[:, :3 * d]
+    o_gen = torch.empty(B * T, d, dtype=torch.bfloat16, device=DEV)
+    lse = torch.empty(B, H, T, dtype=torch.float32, device=DEV)
+    ops().attn_fwd(view, B, T, H, D, 0, d, 2 * d, view.stride(0), o_gen, d, lse, 0.05, 0.2, 3, call, 1)
+    assert relerr(o_fast, o_gen) < 2e-2
+    assert relerr(lse_fast, lse) < 1e-4
+
+
+def test_embedding_fwd_bwd():
+    Fn = F()
+    V, T, C, B = 65, 40, 126, 3
+    torch.manual_seed(6)
+    wte = torch.randn(V, C)
+    wpe = torch.randn(64, C)
+    idx = torch.randint(0, V, (B, T))
+    x = torch.empty(B, T, C, device=DEV)
+    ops().embed_fwd(idx.to(DEV), wte.to(DEV), wpe.to(DEV), x)
+    ref = wte[idx] + wpe[:T]
+    assert relerr(x, ref) < 1e-6
+    dx = torch.randn(B, T, C)
+    dwte = torch.empty(V, C, device=DEV)
+    dwpe = torch.empty(64, C, device=DEV)
+    ws = torch.empty(ops().embed_bwd_workspace(B, T, C, V) // 4 + 1, device=DEV)
+    ops().embed_bwd(idx.to(DEV), dx.to(DEV), dwte, dwpe[:T], False, ws)
+    want_te = torch.zeros(V, C, dtype=torch.float64).index_add_(0, idx.reshape(-1), dx.reshape(-1, C).double())
+    assert relerr(dwte, want_te) < 1e-6
+    assert relerr(dwpe[:T], dx.double().sum(0)) < 1e-6
+
+
+def test_cross_entropy():
+    M, V = 300, 65
+    torch.manual_seed(7)
+    logits = torch.randn(M, V) * 3
+    tgt = torch.randint(0, V, (M,))
+    lr = logits.double().requires_grad_(True)
+    loss = torch.nn.functional.cross_entropy(lr, tgt)
+    loss.backward()
+    ld, td = logits.to(DEV), tgt.to(DEV)
+    rows = torch.empty(M, device=DEV)
+    lse = torch.empty(M, device=DEV)
+    ops().ce_fwd(ld, td, rows, lse)
+    out = torch.empty((), device=DEV)
+    ops().sum_scaled(rows, 1.0 / M, out, torch.empty(1024, device=DEV))
+    assert abs(float(out) - float(loss)) < 1e-5
+    dl = torch.empty(M, V, device=DEV)
+    ops().ce_bwd(ld, td, lse, torch.ones(1, device=DEV), 1.0 / M, dl, None)
+    assert relerr(dl, lr.grad) < 1e-5
+
+
+def test_adamw_matches_torch():
+    n = 1000
+    torch.manual_seed(8)
+    p = torch.randn(n)
+    ref = p.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([ref], lr=2e-4)
+    pd = p.clone().to(DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    sh = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    step = torch.zeros(1, dtype=torch.int64, device=DEV)
+    for i in range(5):
+        g = torch.randn(n)
+        ref.grad = g.clone()
+        opt.step()
+        ops().counter_add(step, 1)
+        ops().adamw(pd, g.to(DEV), m, v, sh, 2e-4, 0.9, 0.999, 1e-8, 1e-2, step)
+    assert relerr(pd, ref.detach()) < 1e-6
+    assert torch.equal(sh.cpu(), pd.cpu().to(torch.bfloat16))
