@@ -1,0 +1,208 @@
+"""charpt training-throughput benchmark (BASELINE.json metric: train tokens/sec at 1/2/4/8
+MI355X + MFMA util, char-GPT block 256).
+
+Workload (default, --config c2): BASELINE configs[1] -- the char-GPT shape 6L/6H/384d, block 256,
+batch 64 per GPU, bf16 activations/GEMM operands with fp32 master weights, dropout 0.2 as the model
+does, synthetic char tokens (randint(65) stream, seed 1337), AdamW.  One "step" = one iteration of
+GPT1.py:227-233 (get_batch, forward, zero_grad, backward, [grad all-reduce], optimizer step),
+replayed from a hipGraph.  N > 1 GPUs: data parallel, weak scaling (64 sequences per GPU),
+bucketed RCCL all-reduce of the fp32 gradient buffer.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0         # MI355X HBM3E
+
+
+def flops_per_token(cfg, T):
+    """F = 6 (L 12 d^2 + d V) + 6 L (T+1) d   (fwd+bwd, causal attention)."""
+    L, d, V = cfg.n_layers, cfg.n_embd, cfg.vocab_size
+    return 6 * (L * 12 * d * d + d * V) + 6 * L * (T + 1) * d
+
+
+def cpu_baseline(cfg, seconds=12.0):
+    """The oracle (CPU fp32 restatement of GPT1.py, 'port') timed on this host, bounded sample:
+    batch 4 x block 256 of the same model, fwd+bwd+AdamW per step."""
+    from oracle import gpt1_oracle as O
+    torch.set_num_threads(min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+    ocfg = O.OracleConfig(vocab_size=cfg.vocab_size, block_size=cfg.block_size, n_embd=cfg.n_embd,
+                          n_head=cfg.n_head, n_layers=cfg.n_layers, dropout=0.0)
+    torch.manual_seed(1337)
+    P = O.init_params(ocfg)
+    opt = O.AdamWOracle(P, lr=2e-4)
+    Bc = 4
+    g = torch.Generator().manual_seed(1)
+    x = torch.randint(0, 65, (Bc, cfg.block_size), generator=g)
+    y = torch.randint(0, 65, (Bc, cfg.block_size), generator=g)
+    _, _, gr = O.loss_and_grads(P, x, y, ocfg)   # warm-up
+    opt.step(gr)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        _, _, gr = O.loss_and_grads(P, x, y, ocfg)
+        opt.step(gr)
+        n += 1
+        if time.perf_counter() - t0 > seconds and n >= 2:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(n * Bc * cfg.block_size / dt, 1), "unit": "tokens/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle fp32 fwd+bwd+AdamW, {n} steps of batch {Bc} x block {cfg.block_size}, "
+                      f"{cfg.n_layers}L/{cfg.n_head}H/{cfg.n_embd}d, dropout 0 (CPU cost of dropout excluded)"}
+
+
+def time_gemm(M, N, K, at, bt, epi, dev, reps=30):
+    """Average duration (ms) of one charpt bf16 GEMM launch of this shape, HIP events on the
+    launch stream."""
+    from replicatinggpt_amd import functional as Fn, ops
+    A = torch.randn((K, M) if at else (M, K), device=dev).to(torch.bfloat16)
+    B = torch.randn((K, N) if bt else (N, K), device=dev).to(torch.bfloat16)
+    out = torch.empty(M, N, dtype=torch.bfloat16 if epi != "wgrad" else torch.float32, device=dev)
+    split, ws = 1, None
+    if epi == "wgrad":
+        split = Fn._wgrad_split(M, N, K, True)
+        if split > 1:
+            ws = torch.empty(ops.gemm_workspace(M, N, split) // 4, dtype=torch.float32, device=dev)
+
+    def run():
+        ops.gemm(A, B, out, True, bool(at), bool(bt), M, N, K, A.shape[1], B.shape[1], N, 0, None, None, 0, None, 0,
+                 0.0, 0, None, 0, 0.0, split, ws)
+    for _ in range(3):
+        run()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        run()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def gemm_census(cfg, Bsz, T, dev):
+    """Every GEMM launch of one training step: (name, M, N, K, a_trans, b_trans, kind, launches/step)."""
+    M, d, L = Bsz * T, cfg.n_embd, cfg.n_layers
+    F4 = 4 * d
+    shapes = [
+        ("qkv_fwd", M, 3 * d, d, 0, 0, "fwd", L), ("proj_fwd", M, d, d, 0, 0, "fwd", L),
+        ("ffn1_fwd", M, F4, d, 0, 0, "fwd", L), ("ffn2_fwd", M, d, F4, 0, 0, "fwd", L),
+        ("proj_dgrad", M, d, d, 0, 1, "fwd", L), ("qkv_dgrad", M, d, 3 * d, 0, 1, "fwd", L),
+        ("ffn2_dgrad", M, F4, d, 0, 1, "fwd", L), ("ffn1_dgrad", M, d, F4, 0, 1, "fwd", L),
+        ("proj_wgrad", d, d, M, 1, 1, "wgrad", L), ("qkv_wgrad", 3 * d, d, M, 1, 1, "wgrad", L),
+        ("ffn2_wgrad", d, F4, M, 1, 1, "wgrad", L), ("ffn1_wgrad", F4, d, M, 1, 1, "wgrad", L),
+    ]
+    out = []
+    for name, m, n, k, at, bt, epi, cnt in shapes:
+        ms = time_gemm(m, n, k, at, bt, epi, dev)
+        out.append({"name": name, "M": m, "N": n, "K": k, "ms": ms, "launches": cnt, "flops": 2.0 * m * n * k})
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c1"])
+    ap.add_argument("--batch", type=int, default=None, help="sequences per GPU (default: config)")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-census", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from replicatinggpt_amd import AdamW, BigramLanguageModel, PRESETS
+    from replicatinggpt_amd.data import BatchSampler, TokenStream
+    from replicatinggpt_amd.engine import GradReducer, TrainStep
+
+    cfg = PRESETS[args.config].with_(dtype="bf16" if args.config != "c1" else "fp32")
+    Bsz = args.batch or cfg.batch_size
+    T = cfg.block_size
+    torch.manual_seed(cfg.seed)
+    model = BigramLanguageModel(cfg).to(dev)
+    model.config.dropout_seed = cfg.dropout_seed + 7919 * rank
+    opt = AdamW(model.parameters(), lr=cfg.learning_rate).attach(model)
+    stream = TokenStream.synthetic(device=dev)
+    sampler = BatchSampler(stream, T, Bsz, world_size=world, rank=rank,
+                           generator=torch.Generator().manual_seed(cfg.seed))
+    reducer = GradReducer(model.flat.grad) if world > 1 else None
+    step = TrainStep(model, opt, sampler, reducer, use_graph=not args.no_graph)
+    step.capture()
+    for _ in range(args.warmup):
+        step.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    final_loss = float(loss)
+    tokens = world * Bsz * T * args.steps
+    value = tokens / elapsed
+    ms_step = elapsed / args.steps * 1e3
+    F = flops_per_token(cfg, T)
+    mfu = value * F / (world * PEAK_BF16_TFLOPS * 1e12)
+
+    result = None
+    if rank == 0:
+        roofline, census = None, None
+        if not args.no_census:
+            census = gemm_census(cfg, Bsz, T, dev)
+            dom = max(census, key=lambda c: c["ms"] * c["launches"])
+            achieved = dom["flops"] / (dom["ms"] * 1e-3) / 1e12
+            roofline = {"bound": "mfma", "kernel": f"k_gemm_bf16 {dom['name']} M={dom['M']} N={dom['N']} K={dom['K']}",
+                        "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                        "avg_launch_ms": round(dom["ms"], 5)}
+        result = {
+            "metric": "train tokens/sec at 1/2/4/8 MI355X + MFMA util, char-GPT block 256",
+            "value": round(value, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "config": {"workload": f"{args.config}: char-GPT {cfg.n_layers}L/{cfg.n_head}H/{cfg.n_embd}d, "
+                                   f"block {T}, batch {Bsz}/GPU, dropout {cfg.dropout}, AdamW, full train step",
+                       "global_batch": Bsz * world, "seq_len": T, "parallelism": f"dp{world}",
+                       "graph": step.g_fb is not None},
+            "mfu_step": round(mfu, 4), "flops_per_token": F, "final_loss": round(final_loss, 4),
+            "roofline": roofline,
+        }
+        if census is not None:
+            result["gemm_census_ms"] = {c["name"]: round(c["ms"], 4) for c in census}
+        if world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(cfg)
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

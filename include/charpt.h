@@ -56,6 +56,9 @@ typedef struct {
 
 const char* cg_last_error_string(void);
 int cg_version(void);
+/* process-wide tuning knobs (benchmarking / autotuning): "gemm_variant" 0 = automatic,
+   1 = 128x128 tile, 2 = 128x128 two K-tiles in flight, 3 = 256x128, 4 = 256x128 two in flight. */
+int cg_set_tuning(const char* key, int value);
 int cg_device_info(int* n_cu, int* arch_major, int* arch_minor);
 
 /* ---- utility ------------------------------------------------------------------------ */

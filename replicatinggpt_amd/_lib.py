@@ -28,6 +28,7 @@ class Epilogue(ctypes.Structure):
 _SIGS = {
     "cg_last_error_string": (ctypes.c_char_p, []),
     "cg_version": (c_int, []),
+    "cg_set_tuning": (c_int, [ctypes.c_char_p, c_int]),
     "cg_device_info": (c_int, [P, P, P]),
     "cg_counter_add": (c_int, [P, c_i64, P]),
     "cg_rng_snapshot": (c_int, [P, P, P]),

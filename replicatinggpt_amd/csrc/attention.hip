@@ -141,20 +141,32 @@ __global__ __launch_bounds__(256) void k_attn_fwd_generic(int64_t T_, int H, int
     }
 }
 
-// delta[bh, t] = sum_e dO * O
+// delta[bh, t] = sum_e dO * O  -- one thread per (b, t, h) row
 template <typename T>
 __global__ void k_attn_delta(int64_t B, int64_t T_, int H, int D, const T* __restrict__ o, int64_t ldo,
                              const T* __restrict__ dout, int64_t ldd, float* __restrict__ delta) {
-    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // (b, t, h) flattened as (b*T+t)*H + h
-    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (b*T + t)*H + h
     if (row >= B * T_ * H) return;
     const int64_t bt = row / H;
     const int h = (int)(row % H);
     const int64_t b = bt / T_, t = bt % T_;
+    const T* op = o + bt * ldo + h * D;
+    const T* dp = dout + bt * ldd + h * D;
     float s = 0.f;
-    for (int e = lane; e < D; e += 64) s += ld_as_f32<T>(o + bt * ldo + h * D + e) * ld_as_f32<T>(dout + bt * ldd + h * D + e);
-    s = wave_sum(s);
-    if (lane == 0) delta[(b * H + h) * T_ + t] = s;
+    if (sizeof(T) == 2 && D % 8 == 0 && ((((uintptr_t)op) | ((uintptr_t)dp)) & 15) == 0) {
+        for (int e = 0; e < D; e += 8) {
+            const uint4 a = *(const uint4*)(op + e), c = *(const uint4*)(dp + e);
+            const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, cw[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                s += __uint_as_float(aw[q] << 16) * __uint_as_float(cw[q] << 16);
+                s += __uint_as_float(aw[q] & 0xffff0000u) * __uint_as_float(cw[q] & 0xffff0000u);
+            }
+        }
+    } else {
+        for (int e = 0; e < D; ++e) s += ld_as_f32<T>(op + e) * ld_as_f32<T>(dp + e);
+    }
+    delta[(b * H + h) * T_ + t] = s;
 }
 
 template <typename T>
@@ -875,10 +887,10 @@ extern "C" int cg_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D
     float* delta = (float*)workspace;
     const int64_t nrows = B * T * H;
     if (dtype == CG_BF16)
-        k_attn_delta<bf16_t><<<ceil_div(nrows, 4), 256, 0, st>>>(B, T, (int)H, (int)D, (const bf16_t*)o, ld_o,
+        k_attn_delta<bf16_t><<<ceil_div(nrows, 256), 256, 0, st>>>(B, T, (int)H, (int)D, (const bf16_t*)o, ld_o,
                                                                  (const bf16_t*)dout, ld_do, delta);
     else
-        k_attn_delta<float><<<ceil_div(nrows, 4), 256, 0, st>>>(B, T, (int)H, (int)D, (const float*)o, ld_o,
+        k_attn_delta<float><<<ceil_div(nrows, 256), 256, 0, st>>>(B, T, (int)H, (int)D, (const float*)o, ld_o,
                                                                 (const float*)dout, ld_do, delta);
     const bool fast = fast_attn_ok(dtype, T, D, q, dout, dq, ld_qkv, ld_do) && ld_dqkv % 8 == 0 &&
                       ((((uintptr_t)dk) | ((uintptr_t)dv)) & 15) == 0;

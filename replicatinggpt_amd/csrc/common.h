@@ -13,6 +13,10 @@
 // ---------------------------------------------------------------------------------------
 namespace cg {
 void set_error(const char* fmt, ...);
+// out[n] (=|+=) sum_k part[k*N + n] in a fixed order (deterministic); columns n >= S go to
+// out_b[n - S] (either output may be NULL to drop it).  Defined in util.hip.
+void launch_reduce_partials(const float* part, int64_t K, int64_t N, float* out_a, float* out_b, int64_t S,
+                            int accumulate, hipStream_t st);
 }  // namespace cg
 
 #define CG_REQUIRE(cond, ...)                \

@@ -1,0 +1,75 @@
+// charpt GEMM internals shared by gemm.hip (generic path, dispatch) and gemm_bf16.hip (MFMA path).
+#pragma once
+#include "common.h"
+
+namespace cg {
+
+struct EpiArgs {
+    int kind;
+    const float* bias;
+    const float* resid;
+    int64_t ld_resid;
+    const void* aux;
+    int aux_dtype;
+    int64_t ld_aux;
+    uint32_t thr;
+    float dscale;
+    uint64_t seed;
+    const uint64_t* rng_call;
+    int site;
+    float beta;
+};
+
+__device__ __forceinline__ float aux_at(const EpiArgs& e, int64_t m, int64_t n) {
+    return e.aux_dtype == CG_BF16 ? bf2f(((const bf16_t*)e.aux)[m * e.ld_aux + n])
+                                  : ((const float*)e.aux)[m * e.ld_aux + n];
+}
+
+// scalar epilogue (generic path and split-K reduce); idx for dropout = m*N + n
+__device__ __forceinline__ float epi_scalar(const EpiArgs& e, float v, int64_t m, int64_t n, int64_t N,
+                                            uint64_t stream) {
+    switch (e.kind) {
+        case CG_EPI_BIAS:
+            if (e.bias) v += e.bias[n];
+            break;
+        case CG_EPI_BIAS_RELU:
+            if (e.bias) v += e.bias[n];
+            v = fmaxf(v, 0.f);
+            break;
+        case CG_EPI_BIAS_RESID:
+            if (e.bias) v += e.bias[n];
+            if (e.resid) v = e.resid[m * e.ld_resid + n] + v;
+            break;
+        case CG_EPI_BIAS_DROP_RESID: {
+            if (e.bias) v += e.bias[n];
+            const uint64_t idx = (uint64_t)m * (uint64_t)N + (uint64_t)n;
+            const u32x4 r = philox_group(e.seed, stream, idx >> 2);
+            if (e.thr) v = philox_word(r, (int)(idx & 3)) >= e.thr ? v * e.dscale : 0.f;
+            if (e.resid) v = e.resid[m * e.ld_resid + n] + v;
+            break;
+        }
+        case CG_EPI_RELU_BWD:
+            v = aux_at(e, m, n) > 0.f ? v : 0.f;
+            break;
+        default:
+            break;
+    }
+    return v;
+}
+
+template <typename TC>
+__device__ __forceinline__ void store_out(TC* C, int64_t off, float v, float beta) {
+    if (beta != 0.f) v += beta * ld_as_f32<TC>(C + off);
+    st_from_f32<TC>(C + off, v);
+}
+
+
+// tuning knob (cg_set_tuning("gemm_variant", v)); 0 = automatic choice
+extern int g_gemm_variant;
+
+// launches the bf16 MFMA kernel if the problem qualifies; returns false (nothing launched) if not
+bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
+                      int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, float* ws,
+                      hipStream_t st);
+
+}  // namespace cg

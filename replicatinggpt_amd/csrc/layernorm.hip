@@ -117,15 +117,17 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ x, con
     }
 }
 
-constexpr int LN_BWD_ROWS = 64;  // rows per block in the backward (16 per wave)
+constexpr int LN_BWD_ROWS = 64;   // rows per block in the backward
+// waves per block: 16 (1024 threads, 4 rows per wave) for the register-light specialised shapes,
+// 4 for the generic (VEC 1, NJ 32) row-in-registers variant
 
-template <int VEC, int NJ, typename TDY>
-__global__ __launch_bounds__(256) void k_ln_bwd(const TDY* __restrict__ dy, const float* __restrict__ x,
+template <int VEC, int NJ, typename TDY, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ dy, const float* __restrict__ x,
                                                 const float* __restrict__ w, const float* __restrict__ mean,
                                                 const float* __restrict__ rstd, const float* __restrict__ dres,
                                                 float* __restrict__ dx, bf16_t* __restrict__ dx_lp,
                                                 float* __restrict__ part, int64_t rows, int C) {
-    extern __shared__ __attribute__((aligned(16))) float red[];  // [4][2][C]
+    extern __shared__ __attribute__((aligned(16))) float red[];  // [WAVES][2][C]
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const float invC = 1.0f / (float)C;
@@ -142,7 +144,7 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const TDY* __restrict__ dy, cons
         }
     }
     const int64_t r0 = (int64_t)blockIdx.x * LN_BWD_ROWS;
-    for (int i = wave; i < LN_BWD_ROWS; i += 4) {
+    for (int i = wave; i < LN_BWD_ROWS; i += WAVES) {
         const int64_t r = r0 + i;
         if (r >= rows) break;
         const float mu = mean[r], rs = rstd[r];
@@ -200,21 +202,9 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const TDY* __restrict__ dy, cons
     for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) {
         const int which = c / C, e = c % C;
         float s = 0.f;
-        for (int wv2 = 0; wv2 < 4; ++wv2) s += red[(wv2 * 2 + which) * C + e];
+        for (int wv2 = 0; wv2 < WAVES; ++wv2) s += red[(wv2 * 2 + which) * C + e];
         part[(int64_t)blockIdx.x * 2 * C + c] = s;
     }
-}
-
-__global__ void k_ln_bwd_reduce(const float* __restrict__ part, int64_t nblk, int C, float* __restrict__ dw,
-                                float* __restrict__ db, int accumulate) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= 2 * C) return;
-    float s = 0.f;
-    for (int64_t k = 0; k < nblk; ++k) s += part[k * 2 * C + c];
-    float* o = c < C ? dw + c : db + (c - C);
-    if (c < C && !dw) return;
-    if (c >= C && !db) return;
-    *o = accumulate ? *o + s : s;
 }
 
 namespace {
@@ -241,16 +231,16 @@ int launch_ln_bwd(const TDY* dy, const float* x, const float* w, const float* me
     const bool al16 = (((uintptr_t)x | (uintptr_t)w | (uintptr_t)dx | (uintptr_t)(dres ? dres : x)) & 15) == 0 &&
                       (((uintptr_t)dy) & 7) == 0;
     const int64_t nblk = (rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
-    const size_t lds = (size_t)8 * C * sizeof(float);
-#define LNB(V, N) \
-    k_ln_bwd<V, N, TDY><<<(unsigned)nblk, 256, lds, st>>>(dy, x, w, mean, rstd, dres, dx, dx_lp, part, rows, C)
-    if (C == 384 && al16) LNB(2, 3);
-    else if (C == 768 && al16) LNB(4, 3);
-    else if (C == 512 && al16) LNB(4, 2);
-    else if (C == 1024 && al16) LNB(4, 4);
-    else LNB(1, 32);
+#define LNB(V, N, W)                                                                                    \
+    k_ln_bwd<V, N, TDY, W><<<(unsigned)nblk, 64 * W, (size_t)2 * W * C * sizeof(float), st>>>(dy, x, w, mean, rstd, \
+                                                                                            dres, dx, dx_lp, part, rows, C)
+    if (C == 384 && al16) LNB(2, 3, 16);
+    else if (C == 768 && al16) LNB(4, 3, 16);
+    else if (C == 512 && al16) LNB(4, 2, 16);
+    else if (C == 1024 && al16) LNB(4, 4, 8);
+    else LNB(1, 32, 4);
 #undef LNB
-    if (dw || db) k_ln_bwd_reduce<<<ceil_div(2 * C, 256), 256, 0, st>>>(part, nblk, C, dw, db, accumulate);
+    if (dw || db) launch_reduce_partials(part, nblk, 2 * C, dw, db, C, accumulate, st);
     return CG_OK;
 }
 }  // namespace
@@ -272,7 +262,7 @@ extern "C" int64_t cg_layernorm_bwd_workspace(int64_t rows, int64_t C) {
 extern "C" int cg_layernorm_bwd(const void* dy, int dy_dtype, const float* x, const float* w, const float* mean,
                                 const float* rstd, const float* dres, float* dx, uint16_t* dx_bf16, float* dw,
                                 float* db, int accumulate, void* workspace, int64_t rows, int64_t C, void* stream) {
-    CG_REQUIRE(rows > 0 && C > 0 && C <= 2048, "cg_layernorm_bwd: need 0 < C <= 2048");
+    CG_REQUIRE(rows > 0 && C > 0 && C <= 1024, "cg_layernorm_bwd: need 0 < C <= 1024");
     hipStream_t st = (hipStream_t)stream;
     if (dy_dtype == CG_BF16)
         launch_ln_bwd<bf16_t>((const bf16_t*)dy, x, w, mean, rstd, dres, dx, (bf16_t*)dx_bf16, dw, db, accumulate,

@@ -116,6 +116,44 @@ extern "C" int cg_dropout_apply(const float* x, int64_t rows, int64_t C, int64_t
 }
 
 // --------------------------------------------------------------------------------------
+// column reduction of per-block partials: 32 columns x 8 k-lanes per block, 8 loads in flight
+__global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict__ part, int64_t K, int64_t N,
+                                                         float* __restrict__ out_a, float* __restrict__ out_b,
+                                                         int64_t S, int accumulate) {
+    __shared__ float red[8][33];
+    const int c = threadIdx.x & 31, kl = threadIdx.x >> 5;
+    const int64_t n = (int64_t)blockIdx.x * 32 + c;
+    float s = 0.f;
+    if (n < N) {
+        int64_t k = kl;
+        for (; k + 56 < K; k += 64) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = part[(k + 8 * j) * N + n];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s += v[j];
+        }
+        for (; k < K; k += 8) s += part[k * N + n];
+    }
+    red[kl][c] = s;
+    __syncthreads();
+    if (kl == 0 && n < N) {
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t += red[j][c];
+        float* dst = n < S ? (out_a ? out_a + n : nullptr) : (out_b ? out_b + (n - S) : nullptr);
+        if (dst) *dst = accumulate ? *dst + t : t;
+    }
+}
+
+namespace cg {
+void launch_reduce_partials(const float* part, int64_t K, int64_t N, float* out_a, float* out_b, int64_t S,
+                            int accumulate, hipStream_t st) {
+    k_reduce_partials<<<ceil_div(N, 32), 256, 0, st>>>(part, K, N, out_a, out_b, S, accumulate);
+}
+}  // namespace cg
+
+// --------------------------------------------------------------------------------------
 // deterministic two-pass sum: pass 1 -> one partial per block (fixed order), pass 2 one block
 __global__ void k_sum_partial(const float* x, int64_t n, float* part) {
     __shared__ float red[16];

@@ -398,6 +398,9 @@ class BigramLanguageModel(nn.Module):
     def forward(self, idx, targets=None):
         _require_hip(idx)
         cfg = self.config
+        idx = idx.contiguous()          # generate() passes a column slice idx[:, -block_size:]
+        if targets is not None:
+            targets = targets.contiguous()
         B, T = idx.shape
         if T > cfg.block_size:
             raise ValueError(f"sequence length {T} exceeds block_size {cfg.block_size}")

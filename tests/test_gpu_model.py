@@ -123,10 +123,14 @@ def test_bf16_model_close_to_fp32(T, C, H):
     l32.backward()
     _, l16 = m16(idx, tgt)
     l16.backward()
-    assert abs(float(l16) - float(l32)) < 2e-2 * float(l32)
+    assert abs(float(l16) - float(l32)) < 1e-2 * float(l32)
+    # bf16 rounding flips a few ReLU / attention-mask-adjacent terms, so compare gradients by
+    # norm (per element they are O(1%) apart, with rare flipped terms)
     g32 = dict(m32.named_parameters())
     for n, p in m16.named_parameters():
-        assert relerr(p.grad, g32[n].grad) < 5e-2, n
+        a, b = p.grad.double(), g32[n].grad.double()
+        assert float((a - b).norm() / b.norm()) < 5e-2, n
+        assert float(torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0)) > 0.998, n
 
 
 def test_train_steps_match_reference_p0():
