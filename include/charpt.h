@@ -123,13 +123,18 @@ int cg_colsum(const void* X, int x_dtype, int64_t rows, int64_t N, int64_t ldx, 
    P = softmax(mask(q k^T * scale)); P = dropout(P); o = P v.  lse[b,h,t] (fp32) saved.      */
 int cg_attn_fwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const void* q, const void* k,
                 const void* v, int64_t ld_qkv, void* o, int64_t ld_o, float* lse, float scale, double dropout_p,
-                uint64_t seed, const uint64_t* rng_call, int site, void* stream);
+                uint64_t seed, const uint64_t* rng_call, int site, uint64_t* mask, void* stream);
+/* keep-bit buffer for dropout on the MFMA (bf16, head_size 64) path: the forward fills it from the
+   Philox stream (cg_attn_fwd `mask`, may be NULL on the generic path or with p = 0) and the
+   backward reads it (cg_attn_bwd `mask`; NULL -> regenerated inside the workspace).            */
+int64_t cg_attn_mask_bytes(int64_t B, int64_t H, int64_t T);
 /* dq/dk/dv written (not accumulated) with stride ld_dqkv; workspace cg_attn_bwd_workspace. */
 int64_t cg_attn_bwd_workspace(int64_t B, int64_t T, int64_t H, int64_t D);
 int cg_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const void* q, const void* k,
                 const void* v, int64_t ld_qkv, const void* o, int64_t ld_o, const void* dout, int64_t ld_do,
                 const float* lse, void* dq, void* dk, void* dv, int64_t ld_dqkv, float scale, double dropout_p,
-                uint64_t seed, const uint64_t* rng_call, int site, void* workspace, void* stream);
+                uint64_t seed, const uint64_t* rng_call, int site, const uint64_t* mask, void* workspace,
+                void* stream);
 
 /* ---- cross entropy over the char vocabulary (F.cross_entropy, GPT1.py:189-192) ----------
    logits fp32 [rows, V] (row stride ld); loss_rows[r] = lse_r - logit[r, tgt_r]; lse saved.

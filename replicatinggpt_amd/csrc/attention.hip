@@ -30,7 +30,38 @@ struct DropArgs {
     uint64_t seed;
     const uint64_t* rng_call;
     int site;
+    const uint64_t* mask;  // fast kernels: precomputed keep bits (k_attn_dropmask), NULL = no dropout
 };
+
+// Keep-bit image for the MFMA kernels, per (b*H + h) and 16x16 (query tile, key tile):
+// 4 uint64 words, bit l of word w = keep(query = 16*qt + (l & 15), key = 16*kt + 4*(l >> 4) + w).
+// Generated once per forward from the canonical Philox stream (same bits as keep_elem), read by
+// the forward, dQ and dK/dV kernels instead of re-running Philox in their inner loops.
+__device__ __forceinline__ const uint64_t* mask_tile(const uint64_t* mask, int bh, int NT, int qt, int kt) {
+    return mask + ((((int64_t)bh * NT + qt) * NT + kt) << 2);
+}
+
+__global__ __launch_bounds__(256) void k_attn_dropmask(int64_t T_, uint64_t* __restrict__ mask, DropArgs d) {
+    const int NT = (int)(T_ >> 4);
+    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile >= NT * NT) return;
+    const int qt = tile / NT, kt = tile % NT;
+    if (kt > qt) return;  // strictly above the diagonal: fully causal-masked, never read
+    const int lane = threadIdx.x & 63;
+    const uint64_t bh = blockIdx.y;
+    const uint64_t stream = dropout_stream(d.rng_call, d.site);
+    const uint64_t q = (uint64_t)qt * 16 + (lane & 15), key0 = (uint64_t)kt * 16 + 4 * (lane >> 4);
+    const u32x4 r = philox_group(d.seed, stream, ((bh * T_ + q) * T_ + key0) >> 2);
+    const uint64_t b0 = __ballot(r.x >= d.thr), b1 = __ballot(r.y >= d.thr);
+    const uint64_t b2 = __ballot(r.z >= d.thr), b3 = __ballot(r.w >= d.thr);
+    if (lane == 0) {
+        uint64_t* o = mask + (((bh * NT + qt) * NT + kt) << 2);
+        o[0] = b0;
+        o[1] = b1;
+        o[2] = b2;
+        o[3] = b3;
+    }
+}
 
 __device__ __forceinline__ bool keep_elem(const DropArgs& d, uint64_t stream, uint64_t idx) {
     const u32x4 r = philox_group(d.seed, stream, idx >> 2);
@@ -436,7 +467,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd_d64(int64_t T_, int H, const b
 #pragma unroll
         for (int j = 0; j < 2; ++j) oacc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
     float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
-    const uint64_t stream = drop.thr ? dropout_stream(drop.rng_call, drop.site) : 0;
+    const int NT = (int)(T_ >> 4);
 
     const int64_t qlast = (qblk0 + FQ - 1) < (T_ - 1) ? (qblk0 + FQ - 1) : (T_ - 1);
     const int nkv = (int)(qlast / 64) + 1;
@@ -487,16 +518,14 @@ __global__ __launch_bounds__(256) void k_attn_fwd_d64(int64_t T_, int H, const b
                 float ls = 0.f;
 #pragma unroll
                 for (int kt = 0; kt < 4; ++kt) {
-                    u32x4 rr;
-                    if (drop.thr)
-                        rr = philox_group(drop.seed, stream,
-                                          ((((uint64_t)bh * T_ + qa) * T_) + (uint64_t)(k0 + 16 * kt + 4 * g)) >> 2);
+                    const uint64_t* mw = nullptr;
+                    if (drop.mask) mw = mask_tile(drop.mask, bh, NT, (int)((qw0 + 16 * qt) >> 4), (int)((k0 + 16 * kt) >> 4));
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const float p = exp2f(sacc[kt][qt][r] - m_new);
                         ls += p;
                         float pd = p;
-                        if (drop.thr) pd = philox_word(rr, r) >= drop.thr ? p * drop.dscale : 0.f;
+                        if (drop.mask) pd = ((mw[r] >> lane) & 1ull) ? p * drop.dscale : 0.f;
                         sacc[kt][qt][r] = pd;
                     }
                 }
@@ -579,7 +608,7 @@ __global__ __launch_bounds__(256) void k_attn_dq_d64(int64_t T_, int H, const bf
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) dqacc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
-    const uint64_t stream = drop.thr ? dropout_stream(drop.rng_call, drop.site) : 0;
+    const int NT = (int)(T_ >> 4);
     const bf16_t* kb_ = k + boff * ld + h * 64;
     const bf16_t* vb_ = v + boff * ld + h * 64;
     const int64_t qlast = (qblk0 + FQ - 1) < (T_ - 1) ? (qblk0 + FQ - 1) : (T_ - 1);
@@ -617,16 +646,14 @@ __global__ __launch_bounds__(256) void k_attn_dq_d64(int64_t T_, int H, const bf
                 const int64_t qa = qw0 + 16 * qt + li;
 #pragma unroll
                 for (int kt = 0; kt < 4; ++kt) {
-                    u32x4 rr;
-                    if (drop.thr)
-                        rr = philox_group(drop.seed, stream,
-                                          ((((uint64_t)bh * T_ + qa) * T_) + (uint64_t)(k0 + 16 * kt + 4 * g)) >> 2);
+                    const uint64_t* mw = nullptr;
+                    if (drop.mask) mw = mask_tile(drop.mask, bh, NT, (int)((qw0 + 16 * qt) >> 4), (int)((k0 + 16 * kt) >> 4));
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int64_t key = k0 + 16 * kt + 4 * g + r;
                         float p = key > qa ? 0.f : exp2f(sa[kt][qt][r] * scale_log2 - lq[qt]);
                         float dp = pa[kt][qt][r];
-                        if (drop.thr) dp = philox_word(rr, r) >= drop.thr ? dp * drop.dscale : 0.f;
+                        if (drop.mask) dp = ((mw[r] >> lane) & 1ull) ? dp * drop.dscale : 0.f;
                         sa[kt][qt][r] = p * (dp - dl[qt]);
                     }
                 }
@@ -702,7 +729,7 @@ __global__ __launch_bounds__(256) void k_attn_dkdv_d64(int64_t T_, int H, const 
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) dka[i][j] = dva[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
-    const uint64_t stream = drop.thr ? dropout_stream(drop.rng_call, drop.site) : 0;
+    const int NT = (int)(T_ >> 4);
     const bf16_t* qb_ = q + boff * ld + h * 64;
     const bf16_t* ob_ = dout + boff * ldd + h * 64;
     const int nq = (int)(T_ / 64);
@@ -753,15 +780,13 @@ __global__ __launch_bounds__(256) void k_attn_dkdv_d64(int64_t T_, int H, const 
                     for (int kt = 0; kt < 2; ++kt) {
                         const int64_t key = kw0 + 16 * kt + li;
                         uint64_t keepbits = ~0ull;  // bit r set -> keep (query 4g + r)
-                        if (drop.thr) {
-                            // this lane generates group (query = q0+qr0+16qt+li, keys kw0+16kt+4g..+3)
-                            const int64_t gq = q0 + qr0 + 16 * qt + li;
-                            const u32x4 rr = philox_group(
-                                drop.seed, stream, ((((uint64_t)bh * T_ + gq) * T_) + (uint64_t)(kw0 + 16 * kt + 4 * g)) >> 2);
-                            const uint64_t b0 = __ballot(rr.x >= drop.thr), b1 = __ballot(rr.y >= drop.thr);
-                            const uint64_t b2 = __ballot(rr.z >= drop.thr), b3 = __ballot(rr.w >= drop.thr);
+                        if (drop.mask) {
+                            // tile words are in the forward's (query-on-lane) order: word w, bit l =
+                            // keep(query l&15, key 4(l>>4) + w); transpose through the bit index
+                            const uint64_t* mw =
+                                mask_tile(drop.mask, bh, NT, (int)((q0 + qr0 + 16 * qt) >> 4), (int)((kw0 + 16 * kt) >> 4));
                             const int w = li & 3;  // my key's word within its group
-                            const uint64_t bw = w == 0 ? b0 : (w == 1 ? b1 : (w == 2 ? b2 : b3));
+                            const uint64_t bw = w == 0 ? mw[0] : (w == 1 ? mw[1] : (w == 2 ? mw[2] : mw[3]));
                             // source lane for (query 4g + r, key li): (4g + r) + 16 * (li >> 2)
                             keepbits = 0;
 #pragma unroll
@@ -776,7 +801,7 @@ __global__ __launch_bounds__(256) void k_attn_dkdv_d64(int64_t T_, int H, const 
                                 key > qa ? 0.f : exp2f(sa[qt][kt][r] * scale_log2 - stat[st][0][qrel]);
                             float dp = pa[qt][kt][r];
                             float zz = p;
-                            if (drop.thr) {
+                            if (drop.mask) {
                                 const bool kp = (keepbits >> r) & 1ull;
                                 dp = kp ? dp * drop.dscale : 0.f;
                                 zz = kp ? p * drop.dscale : 0.f;
@@ -829,7 +854,16 @@ DropArgs make_drop(double p, uint64_t seed, const uint64_t* rng_call, int site) 
     d.seed = seed;
     d.rng_call = rng_call;
     d.site = site;
+    d.mask = nullptr;
     return d;
+}
+
+int64_t mask_bytes(int64_t B, int64_t H, int64_t T) { return B * H * (T / 16) * (T / 16) * 32; }
+
+void launch_dropmask(int64_t B, int64_t H, int64_t T, uint64_t* mask, const DropArgs& d, hipStream_t st) {
+    const int64_t NT = T / 16;
+    dim3 grid(ceil_div(NT * NT, 4), (unsigned)(B * H));
+    k_attn_dropmask<<<grid, 256, 0, st>>>(T, mask, d);
 }
 
 bool fast_attn_ok(int dtype, int64_t T, int64_t D, const void* a, const void* b, const void* c, int64_t ld1,
@@ -847,12 +881,18 @@ size_t generic_lds(int D, int nrows_blocks, int nsq) {
 
 extern "C" int cg_attn_fwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const void* q, const void* k,
                            const void* v, int64_t ld_qkv, void* o, int64_t ld_o, float* lse, float scale,
-                           double dropout_p, uint64_t seed, const uint64_t* rng_call, int site, void* stream) {
+                           double dropout_p, uint64_t seed, const uint64_t* rng_call, int site, uint64_t* mask,
+                           void* stream) {
     CG_REQUIRE(B > 0 && T > 0 && H > 0 && D > 0 && D <= 128, "cg_attn_fwd: bad shape (D must be <= 128)");
     CG_REQUIRE(dropout_p >= 0 && dropout_p < 1, "cg_attn_fwd: dropout_p must be in [0,1)");
     hipStream_t st = (hipStream_t)stream;
-    const DropArgs d = make_drop(dropout_p, seed, rng_call, site);
+    DropArgs d = make_drop(dropout_p, seed, rng_call, site);
     if (fast_attn_ok(dtype, T, D, q, k, o, ld_qkv, ld_o)) {
+        if (d.thr) {
+            CG_REQUIRE(mask, "cg_attn_fwd: dropout on the MFMA path needs a mask buffer (cg_attn_mask_bytes)");
+            launch_dropmask(B, H, T, mask, d, st);
+            d.mask = mask;
+        }
         dim3 grid(ceil_div(T, FQ), (unsigned)(B * H));
         k_attn_fwd_d64<<<grid, 256, 0, st>>>(T, (int)H, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ld_qkv,
                                              (bf16_t*)o, ld_o, lse, scale * LOG2E, d);
@@ -870,20 +910,23 @@ extern "C" int cg_attn_fwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D
     return CG_OK;
 }
 
+extern "C" int64_t cg_attn_mask_bytes(int64_t B, int64_t H, int64_t T) { return mask_bytes(B, H, T); }
+
 extern "C" int64_t cg_attn_bwd_workspace(int64_t B, int64_t T, int64_t H, int64_t D) {
     (void)D;
-    return B * H * T * (int64_t)sizeof(float);
+    const int64_t delta = (B * H * T * (int64_t)sizeof(float) + 255) / 256 * 256;
+    return delta + mask_bytes(B, H, T);
 }
 
 extern "C" int cg_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const void* q, const void* k,
                            const void* v, int64_t ld_qkv, const void* o, int64_t ld_o, const void* dout, int64_t ld_do,
                            const float* lse, void* dq, void* dk, void* dv, int64_t ld_dqkv, float scale,
-                           double dropout_p, uint64_t seed, const uint64_t* rng_call, int site, void* workspace,
-                           void* stream) {
+                           double dropout_p, uint64_t seed, const uint64_t* rng_call, int site, const uint64_t* mask,
+                           void* workspace, void* stream) {
     CG_REQUIRE(B > 0 && T > 0 && H > 0 && D > 0 && D <= 128, "cg_attn_bwd: bad shape (D must be <= 128)");
     CG_REQUIRE(workspace, "cg_attn_bwd: workspace required");
     hipStream_t st = (hipStream_t)stream;
-    const DropArgs d = make_drop(dropout_p, seed, rng_call, site);
+    DropArgs d = make_drop(dropout_p, seed, rng_call, site);
     float* delta = (float*)workspace;
     const int64_t nrows = B * T * H;
     if (dtype == CG_BF16)
@@ -895,6 +938,14 @@ extern "C" int cg_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D
     const bool fast = fast_attn_ok(dtype, T, D, q, dout, dq, ld_qkv, ld_do) && ld_dqkv % 8 == 0 &&
                       ((((uintptr_t)dk) | ((uintptr_t)dv)) & 15) == 0;
     if (fast) {
+        if (d.thr) {
+            if (!mask) {  // regenerate the forward's keep bits (identical Philox stream)
+                uint64_t* m = (uint64_t*)((char*)workspace + (B * H * T * (int64_t)sizeof(float) + 255) / 256 * 256);
+                launch_dropmask(B, H, T, m, d, st);
+                mask = m;
+            }
+            d.mask = mask;
+        }
         const bf16_t *Q = (const bf16_t*)q, *K = (const bf16_t*)k, *V = (const bf16_t*)v, *DO = (const bf16_t*)dout;
         k_attn_dq_d64<<<dim3(ceil_div(T, FQ), (unsigned)(B * H)), 256, 0, st>>>(T, (int)H, Q, K, V, ld_qkv, DO, ld_do, lse,
                                                                                delta, (bf16_t*)dq, ld_dqkv, scale, d);

@@ -185,19 +185,24 @@ def layernorm_bwd(dy2, x2, w_reg, b_reg, mean, rstd, dres=None, want_lp=False):
 
 
 def attention_fwd(qkv, B, T, H, D, out, scale, p, seed, rng_call, site):
+    """Returns (lse, mask): mask holds the dropout keep bits of the MFMA path (None when p == 0
+    or when the generic kernels, which regenerate Philox in place, are used)."""
     d = H * D
     lse = torch.empty((B, H, T), dtype=torch.float32, device=qkv.device)
+    mask = None
+    if p > 0 and T % 16 == 0:
+        mask = torch.empty(ops.attn_mask_bytes(B, H, T) // 8, dtype=torch.int64, device=qkv.device)
     ops.attn_fwd(qkv, B, T, H, D, 0, d, 2 * d, qkv.stride(0), out, out.stride(0), lse, float(scale), float(p),
-                 int(seed), rng_call, int(site))
-    return lse
+                 int(seed), rng_call, int(site), mask)
+    return lse, mask
 
 
-def attention_bwd(qkv, B, T, H, D, o, do, lse, scale, p, seed, rng_call, site):
+def attention_bwd(qkv, B, T, H, D, o, do, lse, scale, p, seed, rng_call, site, mask=None):
     d = H * D
     dqkv = torch.empty_like(qkv)
     ws = torch.empty(ops.attn_bwd_workspace(B, T, H, D) // 4 + 1, dtype=torch.float32, device=qkv.device)
     ops.attn_bwd(qkv, B, T, H, D, 0, d, 2 * d, qkv.stride(0), o, o.stride(0), do, do.stride(0), lse, dqkv,
-                 dqkv.stride(0), float(scale), float(p), int(seed), rng_call, int(site), ws)
+                 dqkv.stride(0), float(scale), float(p), int(seed), rng_call, int(site), mask, ws)
     return dqkv
 
 
@@ -274,7 +279,8 @@ class AttnSublayerFn(torch.autograd.Function):
         qkv = torch.empty((B * T, 3 * C), dtype=act, device=x.device)
         linear_fwd(a, qkv_w.operand(act), qkv)
         o = torch.empty((B * T, C), dtype=act, device=x.device)
-        lse = attention_fwd(qkv, B, T, lc.n_head, lc.head_size, o, lc.scale, lc.p, lc.seed, lc.rng_call, lc.site)
+        lse, ctx.mask = attention_fwd(qkv, B, T, lc.n_head, lc.head_size, o, lc.scale, lc.p, lc.seed, lc.rng_call,
+                                      lc.site)
         out = torch.empty((B * T, C), dtype=torch.float32, device=x.device)
         linear_fwd(o, proj_w.operand(act), out, "bias_resid", bias=proj_b.master, resid=x2)
         ctx.save_for_backward(x2, a, mean, rstd, qkv, o, lse)
@@ -300,7 +306,7 @@ class AttnSublayerFn(torch.autograd.Function):
         do = torch.empty((B * T, C), dtype=act, device=x2.device)
         linear_dgrad(dy, proj_w.operand(act), do)
         dqkv = attention_bwd(qkv, B, T, lc.n_head, lc.head_size, o, do, lse, lc.scale, lc.p, lc.seed, lc.rng_call,
-                             lc.site)
+                             lc.site, ctx.mask)
         g, beta, f_qkv = qkv_w.grad_target()
         if g is not None:
             linear_wgrad(dqkv, a, g, beta)
@@ -457,7 +463,8 @@ class MHAFn(torch.autograd.Function):
         qkv = torch.empty((B * T, 3 * d), dtype=act, device=x.device)
         linear_fwd(x2, qkv_w.operand(act), qkv)
         o = torch.empty((B * T, d), dtype=act, device=x.device)
-        lse = attention_fwd(qkv, B, T, lc.n_head, lc.head_size, o, lc.scale, lc.p, lc.seed, lc.rng_call, lc.site)
+        lse, ctx.mask = attention_fwd(qkv, B, T, lc.n_head, lc.head_size, o, lc.scale, lc.p, lc.seed, lc.rng_call,
+                                      lc.site)
         if proj_w is not None:
             out = torch.empty((B * T, proj_w.master.shape[0]), dtype=torch.float32, device=x.device)
             linear_fwd(o, proj_w.operand(act), out, "bias", bias=proj_b.master)
@@ -490,7 +497,7 @@ class MHAFn(torch.autograd.Function):
         else:
             do = to_act(d32, act)
         dqkv = attention_bwd(qkv, B, T, lc.n_head, lc.head_size, o, do, lse, lc.scale, lc.p, lc.seed, lc.rng_call,
-                             lc.site)
+                             lc.site, ctx.mask)
         g, beta, f_qkv = qkv_w.grad_target()
         if g is not None:
             linear_wgrad(dqkv, x2, g, beta)

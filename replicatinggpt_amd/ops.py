@@ -142,27 +142,32 @@ def colsum_workspace(rows, N):
 
 
 # ---------------------------------------------------------------------------------------
-@_op("attn_fwd", ("o", "lse"))
+@_op("attn_fwd", ("o", "lse", "mask"))
 def attn_fwd(qkv: Tensor, B: int, T: int, H: int, D: int, q_off: int, k_off: int, v_off: int, ld: int, o: Tensor,
              ld_o: int, lse: Tensor, scale: float, dropout_p: float, seed: int, rng_call: Optional[Tensor],
-             site: int) -> None:
+             site: int, mask: Optional[Tensor]) -> None:
     es = qkv.element_size()
     base = qkv.data_ptr()
     L.check(L.load().cg_attn_fwd(L.dtype_code(qkv.dtype), B, T, H, D, base + q_off * es, base + k_off * es,
                                  base + v_off * es, ld, L.ptr(o), ld_o, L.ptr(lse), scale, dropout_p, seed,
-                                 L.ptr(rng_call), site, _s(qkv)), "attn_fwd")
+                                 L.ptr(rng_call), site, L.ptr(mask), _s(qkv)), "attn_fwd")
+
+
+def attn_mask_bytes(B, H, T):
+    return L.load().cg_attn_mask_bytes(B, H, T)
 
 
 @_op("attn_bwd", ("dqkv", "ws"))
 def attn_bwd(qkv: Tensor, B: int, T: int, H: int, D: int, q_off: int, k_off: int, v_off: int, ld: int, o: Tensor,
              ld_o: int, dout: Tensor, ld_do: int, lse: Tensor, dqkv: Tensor, ld_d: int, scale: float,
-             dropout_p: float, seed: int, rng_call: Optional[Tensor], site: int, ws: Tensor) -> None:
+             dropout_p: float, seed: int, rng_call: Optional[Tensor], site: int, mask: Optional[Tensor],
+             ws: Tensor) -> None:
     es = qkv.element_size()
     base, dbase = qkv.data_ptr(), dqkv.data_ptr()
     L.check(L.load().cg_attn_bwd(L.dtype_code(qkv.dtype), B, T, H, D, base + q_off * es, base + k_off * es,
                                  base + v_off * es, ld, L.ptr(o), ld_o, L.ptr(dout), ld_do, L.ptr(lse),
                                  dbase + q_off * es, dbase + k_off * es, dbase + v_off * es, ld_d, scale, dropout_p,
-                                 seed, L.ptr(rng_call), site, L.ptr(ws), _s(qkv)), "attn_bwd")
+                                 seed, L.ptr(rng_call), site, L.ptr(mask), L.ptr(ws), _s(qkv)), "attn_bwd")
 
 
 def attn_bwd_workspace(B, T, H, D):

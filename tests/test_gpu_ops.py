@@ -195,10 +195,10 @@ def test_attention_fwd_bwd(B, T, H, D, p, dt):
     ref.backward(dout.double())
     qkv_d = qkv.to(DEV)
     o = torch.empty(B * T, d, dtype=dt, device=DEV)
-    lse = Fn.attention_fwd(qkv_d, B, T, H, D, o, scale, p, 11, call, 7)
+    lse, mask = Fn.attention_fwd(qkv_d, B, T, H, D, o, scale, p, 11, call, 7)
     tol = 1e-5 if dt == torch.float32 else 2e-2
     assert relerr(o, ref.reshape(B * T, d)) < tol
-    dqkv = Fn.attention_bwd(qkv_d, B, T, H, D, o, dout.reshape(B * T, d).to(DEV), lse, scale, p, 11, call, 7)
+    dqkv = Fn.attention_bwd(qkv_d, B, T, H, D, o, dout.reshape(B * T, d).to(DEV), lse, scale, p, 11, call, 7, mask)
     dq, dk, dv = dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:]
     assert relerr(dq, q.grad.reshape(B * T, d)) < (1e-5 if dt == torch.float32 else 3e-2)
     assert relerr(dk, k.grad.reshape(B * T, d)) < (1e-5 if dt == torch.float32 else 3e-2)
@@ -221,9 +221,26 @@ def test_attention_fast_matches_generic_bf16():
     view = wide[:, :3 * d]
     o_gen = torch.empty(B * T, d, dtype=torch.bfloat16, device=DEV)
     lse = torch.empty(B, H, T, dtype=torch.float32, device=DEV)
-    ops().attn_fwd(view, B, T, H, D, 0, d, 2 * d, view.stride(0), o_gen, d, lse, 0.05, 0.2, 3, call, 1)
+    ops().attn_fwd(view, B, T, H, D, 0, d, 2 * d, view.stride(0), o_gen, d, lse, 0.05, 0.2, 3, call, 1, None)
     assert relerr(o_fast, o_gen) < 2e-2
-    assert relerr(lse_fast, lse) < 1e-4
+    assert relerr(lse_fast[0], lse) < 1e-4
+
+
+def test_attention_bwd_regenerates_mask():
+    """cg_attn_bwd with mask=NULL regenerates the forward's keep bits: identical gradients."""
+    Fn = F()
+    B, T, H, D = 2, 128, 2, 64
+    torch.manual_seed(9)
+    d = H * D
+    qkv = torch.randn(B * T, 3 * d).to(torch.bfloat16).to(DEV)
+    call = torch.tensor([4], dtype=torch.int64, device=DEV)
+    o = torch.empty(B * T, d, dtype=torch.bfloat16, device=DEV)
+    lse, mask = Fn.attention_fwd(qkv, B, T, H, D, o, 0.1, 0.2, 5, call, 2)
+    assert mask is not None
+    do = torch.randn(B * T, d).to(torch.bfloat16).to(DEV)
+    g1 = Fn.attention_bwd(qkv, B, T, H, D, o, do, lse, 0.1, 0.2, 5, call, 2, mask)
+    g2 = Fn.attention_bwd(qkv, B, T, H, D, o, do, lse, 0.1, 0.2, 5, call, 2, None)
+    assert torch.equal(g1, g2)
 
 
 def test_embedding_fwd_bwd():
