@@ -1,0 +1,479 @@
+// charpt: fused causal self-attention over all heads -- Head.forward (GPT1.py:109-123) run for
+// every head of MultiHeadAttention (GPT1.py:134-135) without materialising the T x T scores.
+//
+//   S = q k^T * scale (scale = n_embd^-0.5); S[j > i] = -inf (tril, GPT1.py:115);
+//   P = softmax(S) (GPT1.py:116); P = dropout(P) (GPT1.py:117); out = P v (GPT1.py:122).
+//
+// Online softmax, logsumexp saved for the backward, dropout regenerated from the Philox
+// counter (element idx = ((b*H + h)*T + i)*T + j).  Backward = FlashAttention-2 style
+// recompute split in two deterministic kernels (dK/dV per key block, dQ per query block), so no
+// float atomics are needed.
+//
+// Kernels:
+//   *_generic : fp32 math, any head size D <= 128 and any T; the fp32 parity path and the
+//               as-shipped head_size 21.  32x32 blocks, VALU dot products.
+//   *_d64     : bf16 MFMA (16x16x32), D = 64, T % 64 == 0 -- the C2/C4 perf path.
+#include <math.h>
+
+#include "attention_common.h"
+
+using namespace cg;
+
+namespace {
+
+
+__global__ __launch_bounds__(256) void k_attn_dropmask(int64_t T_, uint64_t* __restrict__ mask, DropArgs d) {
+    const int NT = (int)(T_ >> 4);
+    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile >= NT * NT) return;
+    const int qt = tile / NT, kt = tile % NT;
+    if (kt > qt) return;  // strictly above the diagonal: fully causal-masked, never read
+    const int lane = threadIdx.x & 63;
+    const uint64_t bh = blockIdx.y;
+    const uint64_t stream = dropout_stream(d.rng_call, d.site);
+    const uint64_t q = (uint64_t)qt * 16 + (lane & 15), key0 = (uint64_t)kt * 16 + 4 * (lane >> 4);
+    const u32x4 r = philox_group(d.seed, stream, ((bh * T_ + q) * T_ + key0) >> 2);
+    const uint64_t b0 = __ballot(r.x >= d.thr), b1 = __ballot(r.y >= d.thr);
+    const uint64_t b2 = __ballot(r.z >= d.thr), b3 = __ballot(r.w >= d.thr);
+    if (lane == 0) {
+        uint64_t* o = mask + (((bh * NT + qt) * NT + kt) << 2);
+        o[0] = b0;
+        o[1] = b1;
+        o[2] = b2;
+        o[3] = b3;
+    }
+}
+
+__device__ __forceinline__ bool keep_elem(const DropArgs& d, uint64_t stream, uint64_t idx) {
+    const u32x4 r = philox_group(d.seed, stream, idx >> 2);
+    return philox_word(r, (int)(idx & 3)) >= d.thr;
+}
+
+// =====================================================================================
+// generic fp32 kernels
+// =====================================================================================
+constexpr int GB = 32;  // rows per block (queries or keys)
+
+template <typename T>
+__device__ __forceinline__ void load_rows(float* dst, int DP, const T* base, int64_t ld, int64_t row0, int64_t T_,
+                                          int D, int tid) {
+    for (int i = tid; i < GB * D; i += 256) {
+        const int r = i / D, e = i % D;
+        const int64_t t = row0 + r;
+        dst[r * DP + e] = t < T_ ? ld_as_f32<T>(base + t * ld + e) : 0.f;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_attn_fwd_generic(int64_t T_, int H, int D, const T* __restrict__ q,
+                                                          const T* __restrict__ k, const T* __restrict__ v, int64_t ld,
+                                                          T* __restrict__ o, int64_t ldo, float* __restrict__ lse,
+                                                          float scale, DropArgs drop) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int DP = D + 1;
+    float* Qs = sm;
+    float* Ks = Qs + GB * DP;
+    float* Vs = Ks + GB * DP;
+    float* Ps = Vs + GB * DP;  // [GB][GB+1]
+    const int bh = blockIdx.y, b = bh / H, h = bh % H;
+    const int qb = blockIdx.x;
+    const int64_t q0 = (int64_t)qb * GB;
+    const int tid = threadIdx.x, qi = tid >> 3, sub = tid & 7;
+    const int64_t qa = q0 + qi;
+    const T* qbase = q + (int64_t)b * T_ * ld + h * D;
+    const T* kbase = k + (int64_t)b * T_ * ld + h * D;
+    const T* vbase = v + (int64_t)b * T_ * ld + h * D;
+    load_rows<T>(Qs, DP, qbase, ld, q0, T_, D, tid);
+    const uint64_t stream = drop.thr ? dropout_stream(drop.rng_call, drop.site) : 0;
+    float m_run = -INFINITY, l_run = 0.f;
+    float oacc[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) oacc[j] = 0.f;
+    for (int kb = 0; kb <= qb; ++kb) {
+        const int64_t k0 = (int64_t)kb * GB;
+        __syncthreads();
+        load_rows<T>(Ks, DP, kbase, ld, k0, T_, D, tid);
+        load_rows<T>(Vs, DP, vbase, ld, k0, T_, D, tid);
+        __syncthreads();
+        float s[4], mx = -INFINITY;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int j = sub + 8 * jj;
+            const int64_t key = k0 + j;
+            float acc = 0.f;
+            for (int e = 0; e < D; ++e) acc += Qs[qi * DP + e] * Ks[j * DP + e];
+            acc *= scale;
+            if (key > qa || key >= T_) acc = -INFINITY;
+            s[jj] = acc;
+            mx = fmaxf(mx, acc);
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 4, 64));
+        const float m_new = fmaxf(m_run, mx);
+        const float alpha = m_new == -INFINITY ? 1.f : expf(m_run - m_new);
+        float psum = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int j = sub + 8 * jj;
+            const float p = s[jj] == -INFINITY ? 0.f : expf(s[jj] - m_new);
+            psum += p;
+            float pd = p;
+            if (drop.thr && p != 0.f) {
+                const uint64_t idx = (((uint64_t)bh * T_ + qa) * T_ + (k0 + j));
+                pd = keep_elem(drop, stream, idx) ? p * drop.dscale : 0.f;
+            }
+            Ps[qi * (GB + 1) + j] = pd;
+        }
+        psum += __shfl_xor(psum, 1, 64);
+        psum += __shfl_xor(psum, 2, 64);
+        psum += __shfl_xor(psum, 4, 64);
+        l_run = l_run * alpha + psum;
+        m_run = m_new;
+        __syncthreads();
+#pragma unroll
+        for (int j8 = 0; j8 < 16; ++j8) {
+            const int e = sub + 8 * j8;
+            if (e < D) {
+                float a = oacc[j8] * alpha;
+                for (int j = 0; j < GB; ++j) a += Ps[qi * (GB + 1) + j] * Vs[j * DP + e];
+                oacc[j8] = a;
+            }
+        }
+    }
+    if (qa < T_) {
+        const float inv = 1.f / l_run;
+        T* orow = o + ((int64_t)b * T_ + qa) * ldo + h * D;
+#pragma unroll
+        for (int j8 = 0; j8 < 16; ++j8) {
+            const int e = sub + 8 * j8;
+            if (e < D) st_from_f32<T>(orow + e, oacc[j8] * inv);
+        }
+        if (sub == 0) lse[(int64_t)bh * T_ + qa] = m_run + logf(l_run);
+    }
+}
+
+// delta[bh, t] = sum_e dO * O  -- one thread per (b, t, h) row
+template <typename T>
+__global__ void k_attn_delta(int64_t B, int64_t T_, int H, int D, const T* __restrict__ o, int64_t ldo,
+                             const T* __restrict__ dout, int64_t ldd, float* __restrict__ delta) {
+    const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (b*T + t)*H + h
+    if (row >= B * T_ * H) return;
+    const int64_t bt = row / H;
+    const int h = (int)(row % H);
+    const int64_t b = bt / T_, t = bt % T_;
+    const T* op = o + bt * ldo + h * D;
+    const T* dp = dout + bt * ldd + h * D;
+    float s = 0.f;
+    if (sizeof(T) == 2 && D % 8 == 0 && ((((uintptr_t)op) | ((uintptr_t)dp)) & 15) == 0) {
+        for (int e = 0; e < D; e += 8) {
+            const uint4 a = *(const uint4*)(op + e), c = *(const uint4*)(dp + e);
+            const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, cw[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                s += __uint_as_float(aw[q] << 16) * __uint_as_float(cw[q] << 16);
+                s += __uint_as_float(aw[q] & 0xffff0000u) * __uint_as_float(cw[q] & 0xffff0000u);
+            }
+        }
+    } else {
+        for (int e = 0; e < D; ++e) s += ld_as_f32<T>(op + e) * ld_as_f32<T>(dp + e);
+    }
+    delta[(b * H + h) * T_ + t] = s;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_attn_dq_generic(int64_t T_, int H, int D, const T* __restrict__ q,
+                                                         const T* __restrict__ k, const T* __restrict__ v, int64_t ld,
+                                                         const T* __restrict__ dout, int64_t ldd,
+                                                         const float* __restrict__ lse,
+                                                         const float* __restrict__ delta, T* __restrict__ dq,
+                                                         int64_t lddq, float scale, DropArgs drop) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int DP = D + 1;
+    float* Qs = sm;
+    float* Os = Qs + GB * DP;  // dO rows
+    float* Ks = Os + GB * DP;
+    float* Vs = Ks + GB * DP;
+    float* Ss = Vs + GB * DP;  // dS [GB][GB+1]
+    const int bh = blockIdx.y, b = bh / H, h = bh % H;
+    const int qb = blockIdx.x;
+    const int64_t q0 = (int64_t)qb * GB;
+    const int tid = threadIdx.x, qi = tid >> 3, sub = tid & 7;
+    const int64_t qa = q0 + qi;
+    const int64_t boff = (int64_t)b * T_;
+    load_rows<T>(Qs, DP, q + boff * ld + h * D, ld, q0, T_, D, tid);
+    load_rows<T>(Os, DP, dout + boff * ldd + h * D, ldd, q0, T_, D, tid);
+    const bool valid_q = qa < T_;
+    const float lq = valid_q ? lse[(int64_t)bh * T_ + qa] : 0.f;
+    const float dq_ = valid_q ? delta[(int64_t)bh * T_ + qa] : 0.f;
+    const uint64_t stream = drop.thr ? dropout_stream(drop.rng_call, drop.site) : 0;
+    float acc[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+    for (int kb = 0; kb <= qb; ++kb) {
+        const int64_t k0 = (int64_t)kb * GB;
+        __syncthreads();
+        load_rows<T>(Ks, DP, k + boff * ld + h * D, ld, k0, T_, D, tid);
+        load_rows<T>(Vs, DP, v + boff * ld + h * D, ld, k0, T_, D, tid);
+        __syncthreads();
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int j = sub + 8 * jj;
+            const int64_t key = k0 + j;
+            float ds = 0.f;
+            if (valid_q && key <= qa) {
+                float s = 0.f, dp = 0.f;
+                for (int e = 0; e < D; ++e) {
+                    s += Qs[qi * DP + e] * Ks[j * DP + e];
+                    dp += Os[qi * DP + e] * Vs[j * DP + e];
+                }
+                const float p = expf(s * scale - lq);
+                if (drop.thr) {
+                    const uint64_t idx = (((uint64_t)bh * T_ + qa) * T_ + key);
+                    dp = keep_elem(drop, stream, idx) ? dp * drop.dscale : 0.f;
+                }
+                ds = p * (dp - dq_);
+            }
+            Ss[qi * (GB + 1) + j] = ds;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j8 = 0; j8 < 16; ++j8) {
+            const int e = sub + 8 * j8;
+            if (e < D) {
+                float a = acc[j8];
+                for (int j = 0; j < GB; ++j) a += Ss[qi * (GB + 1) + j] * Ks[j * DP + e];
+                acc[j8] = a;
+            }
+        }
+    }
+    if (valid_q) {
+        T* row = dq + (boff + qa) * lddq + h * D;
+#pragma unroll
+        for (int j8 = 0; j8 < 16; ++j8) {
+            const int e = sub + 8 * j8;
+            if (e < D) st_from_f32<T>(row + e, acc[j8] * scale);
+        }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_attn_dkdv_generic(int64_t T_, int H, int D, const T* __restrict__ q,
+                                                           const T* __restrict__ k, const T* __restrict__ v,
+                                                           int64_t ld, const T* __restrict__ dout, int64_t ldd,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ delta, T* __restrict__ dk,
+                                                           T* __restrict__ dv, int64_t lddkv, float scale,
+                                                           DropArgs drop) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int DP = D + 1;
+    float* Ks = sm;
+    float* Vs = Ks + GB * DP;
+    float* Qs = Vs + GB * DP;
+    float* Os = Qs + GB * DP;
+    float* Zs = Os + GB * DP;        // [key][q]
+    float* Ds = Zs + GB * (GB + 1);  // [key][q]
+    float* Ls = Ds + GB * (GB + 1);  // lse[GB], delta[GB]
+    const int bh = blockIdx.y, b = bh / H, h = bh % H;
+    const int kb = blockIdx.x;
+    const int64_t k0 = (int64_t)kb * GB;
+    const int tid = threadIdx.x, kj = tid >> 3, sub = tid & 7;
+    const int64_t ka = k0 + kj;
+    const int64_t boff = (int64_t)b * T_;
+    load_rows<T>(Ks, DP, k + boff * ld + h * D, ld, k0, T_, D, tid);
+    load_rows<T>(Vs, DP, v + boff * ld + h * D, ld, k0, T_, D, tid);
+    const uint64_t stream = drop.thr ? dropout_stream(drop.rng_call, drop.site) : 0;
+    float adk[16], adv[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) adk[j] = adv[j] = 0.f;
+    const int nqb = (int)((T_ + GB - 1) / GB);
+    for (int qb = kb; qb < nqb; ++qb) {
+        const int64_t q0 = (int64_t)qb * GB;
+        __syncthreads();
+        load_rows<T>(Qs, DP, q + boff * ld + h * D, ld, q0, T_, D, tid);
+        load_rows<T>(Os, DP, dout + boff * ldd + h * D, ldd, q0, T_, D, tid);
+        if (tid < GB) {
+            const int64_t t = q0 + tid;
+            Ls[tid] = t < T_ ? lse[(int64_t)bh * T_ + t] : 0.f;
+            Ls[GB + tid] = t < T_ ? delta[(int64_t)bh * T_ + t] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+            const int qi = sub + 8 * ii;
+            const int64_t qa = q0 + qi;
+            float z = 0.f, ds = 0.f;
+            if (ka < T_ && qa < T_ && ka <= qa) {
+                float s = 0.f, dp = 0.f;
+                for (int e = 0; e < D; ++e) {
+                    s += Ks[kj * DP + e] * Qs[qi * DP + e];
+                    dp += Vs[kj * DP + e] * Os[qi * DP + e];
+                }
+                const float p = expf(s * scale - Ls[qi]);
+                z = p;
+                if (drop.thr) {
+                    const uint64_t idx = (((uint64_t)bh * T_ + qa) * T_ + ka);
+                    const bool kp = keep_elem(drop, stream, idx);
+                    z = kp ? p * drop.dscale : 0.f;
+                    dp = kp ? dp * drop.dscale : 0.f;
+                }
+                ds = p * (dp - Ls[GB + qi]);
+            }
+            Zs[kj * (GB + 1) + qi] = z;
+            Ds[kj * (GB + 1) + qi] = ds;
+        }
+        __syncthreads();
+#pragma unroll 1
+        for (int i = 0; i < GB; ++i) {
+            const float zi = Zs[kj * (GB + 1) + i], di = Ds[kj * (GB + 1) + i];
+#pragma unroll
+            for (int j8 = 0; j8 < 16; ++j8) {
+                const int e = sub + 8 * j8;
+                if (e < D) {
+                    adv[j8] += zi * Os[i * DP + e];
+                    adk[j8] += di * Qs[i * DP + e];
+                }
+            }
+        }
+    }
+    if (ka < T_) {
+        T* krow = dk + (boff + ka) * lddkv + h * D;
+        T* vrow = dv + (boff + ka) * lddkv + h * D;
+#pragma unroll
+        for (int j8 = 0; j8 < 16; ++j8) {
+            const int e = sub + 8 * j8;
+            if (e < D) {
+                st_from_f32<T>(krow + e, adk[j8] * scale);
+                st_from_f32<T>(vrow + e, adv[j8]);
+            }
+        }
+    }
+}
+
+DropArgs make_drop(double p, uint64_t seed, const uint64_t* rng_call, int site) {
+    DropArgs d;
+    d.thr = p > 0 ? dropout_threshold(p) : 0u;
+    d.dscale = p > 0 ? dropout_scale(p) : 1.f;
+    d.seed = seed;
+    d.rng_call = rng_call;
+    d.site = site;
+    d.mask = nullptr;
+    return d;
+}
+
+int64_t mask_bytes(int64_t B, int64_t H, int64_t T) { return B * H * (T / 16) * (T / 16) * 32; }
+
+void launch_dropmask(int64_t B, int64_t H, int64_t T, uint64_t* mask, const DropArgs& d, hipStream_t st) {
+    const int64_t NT = T / 16;
+    dim3 grid(ceil_div(NT * NT, 4), (unsigned)(B * H));
+    k_attn_dropmask<<<grid, 256, 0, st>>>(T, mask, d);
+}
+
+bool fast_attn_ok(int dtype, int64_t T, int64_t D, const void* a, const void* b, const void* c, int64_t ld1,
+                  int64_t ld2) {
+    return dtype == CG_BF16 && D == 64 && T % 64 == 0 && (((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) & 15) == 0 &&
+           ld1 % 8 == 0 && ld2 % 8 == 0;
+}
+
+template <typename T>
+size_t generic_lds(int D, int nrows_blocks, int nsq) {
+    return (size_t)(nrows_blocks * GB * (D + 1) + nsq * GB * (GB + 1) + 2 * GB) * sizeof(float);
+}
+
+}  // namespace
+
+extern "C" int cg_attn_fwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const void* q, const void* k,
+                           const void* v, int64_t ld_qkv, void* o, int64_t ld_o, float* lse, float scale,
+                           double dropout_p, uint64_t seed, const uint64_t* rng_call, int site, uint64_t* mask,
+                           void* stream) {
+    CG_REQUIRE(B > 0 && T > 0 && H > 0 && D > 0 && D <= 128, "cg_attn_fwd: bad shape (D must be <= 128)");
+    CG_REQUIRE(dropout_p >= 0 && dropout_p < 1, "cg_attn_fwd: dropout_p must be in [0,1)");
+    hipStream_t st = (hipStream_t)stream;
+    DropArgs d = make_drop(dropout_p, seed, rng_call, site);
+    if (fast_attn_ok(dtype, T, D, q, k, o, ld_qkv, ld_o)) {
+        if (d.thr) {
+            CG_REQUIRE(mask, "cg_attn_fwd: dropout on the MFMA path needs a mask buffer (cg_attn_mask_bytes)");
+            launch_dropmask(B, H, T, mask, d, st);
+            d.mask = mask;
+        }
+        attn::launch_fwd_d64(B, T, (int)H, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ld_qkv, (bf16_t*)o,
+                             ld_o, lse, scale, d, st);
+    } else {
+        dim3 grid(ceil_div(T, GB), (unsigned)(B * H));
+        const size_t lds = generic_lds<float>((int)D, 3, 1);
+        if (dtype == CG_BF16)
+            k_attn_fwd_generic<bf16_t><<<grid, 256, lds, st>>>(T, (int)H, (int)D, (const bf16_t*)q, (const bf16_t*)k,
+                                                               (const bf16_t*)v, ld_qkv, (bf16_t*)o, ld_o, lse, scale, d);
+        else
+            k_attn_fwd_generic<float><<<grid, 256, lds, st>>>(T, (int)H, (int)D, (const float*)q, (const float*)k,
+                                                              (const float*)v, ld_qkv, (float*)o, ld_o, lse, scale, d);
+    }
+    CG_LAUNCH_CHECK("cg_attn_fwd");
+    return CG_OK;
+}
+
+extern "C" int64_t cg_attn_mask_bytes(int64_t B, int64_t H, int64_t T) { return mask_bytes(B, H, T); }
+
+extern "C" int64_t cg_attn_bwd_workspace(int64_t B, int64_t T, int64_t H, int64_t D) {
+    (void)D;
+    const int64_t delta = (B * H * T * (int64_t)sizeof(float) + 255) / 256 * 256;
+    return delta + mask_bytes(B, H, T);
+}
+
+extern "C" int cg_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const void* q, const void* k,
+                           const void* v, int64_t ld_qkv, const void* o, int64_t ld_o, const void* dout, int64_t ld_do,
+                           const float* lse, void* dq, void* dk, void* dv, int64_t ld_dqkv, float scale,
+                           double dropout_p, uint64_t seed, const uint64_t* rng_call, int site, const uint64_t* mask,
+                           void* workspace, void* stream) {
+    CG_REQUIRE(B > 0 && T > 0 && H > 0 && D > 0 && D <= 128, "cg_attn_bwd: bad shape (D must be <= 128)");
+    CG_REQUIRE(workspace, "cg_attn_bwd: workspace required");
+    hipStream_t st = (hipStream_t)stream;
+    DropArgs d = make_drop(dropout_p, seed, rng_call, site);
+    float* delta = (float*)workspace;
+    const int64_t nrows = B * T * H;
+    if (dtype == CG_BF16)
+        k_attn_delta<bf16_t><<<ceil_div(nrows, 256), 256, 0, st>>>(B, T, (int)H, (int)D, (const bf16_t*)o, ld_o,
+                                                                 (const bf16_t*)dout, ld_do, delta);
+    else
+        k_attn_delta<float><<<ceil_div(nrows, 256), 256, 0, st>>>(B, T, (int)H, (int)D, (const float*)o, ld_o,
+                                                                (const float*)dout, ld_do, delta);
+    const bool fast = fast_attn_ok(dtype, T, D, q, dout, dq, ld_qkv, ld_do) && ld_dqkv % 8 == 0 &&
+                      ((((uintptr_t)dk) | ((uintptr_t)dv)) & 15) == 0;
+    if (fast) {
+        if (d.thr) {
+            if (!mask) {  // regenerate the forward's keep bits (identical Philox stream)
+                uint64_t* m = (uint64_t*)((char*)workspace + (B * H * T * (int64_t)sizeof(float) + 255) / 256 * 256);
+                launch_dropmask(B, H, T, m, d, st);
+                mask = m;
+            }
+            d.mask = mask;
+        }
+        const bf16_t *Q = (const bf16_t*)q, *K = (const bf16_t*)k, *V = (const bf16_t*)v, *DO = (const bf16_t*)dout;
+        attn::launch_dq_d64(B, T, (int)H, Q, K, V, ld_qkv, DO, ld_do, lse, delta, (bf16_t*)dq, ld_dqkv, scale, d, st);
+        attn::launch_dkdv_d64(B, T, (int)H, Q, K, V, ld_qkv, DO, ld_do, lse, delta, (bf16_t*)dk, (bf16_t*)dv, ld_dqkv,
+                              scale, d, st);
+    } else {
+        dim3 grid(ceil_div(T, GB), (unsigned)(B * H));
+        const size_t lds_dq = generic_lds<float>((int)D, 4, 1);
+        const size_t lds_kv = generic_lds<float>((int)D, 4, 2);
+        if (dtype == CG_BF16) {
+            k_attn_dq_generic<bf16_t><<<grid, 256, lds_dq, st>>>(T, (int)H, (int)D, (const bf16_t*)q, (const bf16_t*)k,
+                                                                 (const bf16_t*)v, ld_qkv, (const bf16_t*)dout, ld_do,
+                                                                 lse, delta, (bf16_t*)dq, ld_dqkv, scale, d);
+            k_attn_dkdv_generic<bf16_t><<<grid, 256, lds_kv, st>>>(T, (int)H, (int)D, (const bf16_t*)q,
+                                                                   (const bf16_t*)k, (const bf16_t*)v, ld_qkv,
+                                                                   (const bf16_t*)dout, ld_do, lse, delta,
+                                                                   (bf16_t*)dk, (bf16_t*)dv, ld_dqkv, scale, d);
+        } else {
+            k_attn_dq_generic<float><<<grid, 256, lds_dq, st>>>(T, (int)H, (int)D, (const float*)q, (const float*)k,
+                                                                (const float*)v, ld_qkv, (const float*)dout, ld_do,
+                                                                lse, delta, (float*)dq, ld_dqkv, scale, d);
+            k_attn_dkdv_generic<float><<<grid, 256, lds_kv, st>>>(T, (int)H, (int)D, (const float*)q, (const float*)k,
+                                                                  (const float*)v, ld_qkv, (const float*)dout, ld_do,
+                                                                  lse, delta, (float*)dk, (float*)dv, ld_dqkv, scale,
+                                                                  d);
+        }
+    }
+    CG_LAUNCH_CHECK("cg_attn_bwd");
+    return CG_OK;
+}

@@ -201,12 +201,17 @@ int launch_generic(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, co
 
 namespace cg {
 int g_gemm_variant = 0;
+extern int g_attn_variant;  // attention_d64.hip
 }
 
 extern "C" int cg_set_tuning(const char* key, int value) {
     CG_REQUIRE(key, "cg_set_tuning: null key");
     if (!strcmp(key, "gemm_variant")) {
         g_gemm_variant = value;
+        return CG_OK;
+    }
+    if (!strcmp(key, "attn_variant")) {
+        g_attn_variant = value;
         return CG_OK;
     }
     set_error("cg_set_tuning: unknown key %s", key);

@@ -226,6 +226,40 @@ def test_attention_fast_matches_generic_bf16():
     assert relerr(lse_fast[0], lse) < 1e-4
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_attention_fast_variants(variant):
+    """Every per-wave width of the MFMA kernels (16/32 queries, 16/32 keys) against the fp64
+    reference, at a T that leaves the 128-wide blocks partially filled."""
+    from replicatinggpt_amd import _lib as L
+    Fn = F()
+    B, T, H, D, p = 2, 192, 3, 64, 0.2
+    torch.manual_seed(6)
+    d = H * D
+    qkv = (torch.randn(B * T, 3 * d) * 0.7).to(torch.bfloat16)
+    q = qkv[:, :d].double().view(B, T, H, D).requires_grad_(True)
+    k = qkv[:, d:2 * d].double().view(B, T, H, D).requires_grad_(True)
+    v = qkv[:, 2 * d:].double().view(B, T, H, D).requires_grad_(True)
+    scale = (3.0 * D) ** -0.5
+    ref = _attn_ref(q, k, v, scale, p, 21, (3 << 8) | 4)
+    dout = torch.randn(B, T, H, D).to(torch.bfloat16)
+    ref.backward(dout.double())
+    lib = L.load()
+    L.check(lib.cg_set_tuning(b"attn_variant", variant))
+    try:
+        call = torch.tensor([3], dtype=torch.int64, device=DEV)
+        qkv_d = qkv.to(DEV)
+        o = torch.empty(B * T, d, dtype=torch.bfloat16, device=DEV)
+        lse, mask = Fn.attention_fwd(qkv_d, B, T, H, D, o, scale, p, 21, call, 4)
+        dqkv = Fn.attention_bwd(qkv_d, B, T, H, D, o, dout.reshape(B * T, d).to(DEV), lse, scale, p, 21, call, 4,
+                                mask)
+        torch.cuda.synchronize()
+    finally:
+        L.check(lib.cg_set_tuning(b"attn_variant", 0))
+    assert relerr(o, ref.reshape(B * T, d)) < 2e-2
+    for i, t in enumerate((q, k, v)):
+        assert relerr(dqkv[:, i * d:(i + 1) * d], t.grad.reshape(B * T, d)) < 3e-2
+
+
 def test_attention_bwd_regenerates_mask():
     """cg_attn_bwd with mask=NULL regenerates the forward's keep bits: identical gradients."""
     Fn = F()
