@@ -201,6 +201,7 @@ int launch_generic(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, co
 
 namespace cg {
 int g_gemm_variant = 0;
+int g_gemm_max_grid = 0;
 extern int g_attn_variant;  // attention_d64.hip
 }
 
@@ -208,6 +209,10 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     CG_REQUIRE(key, "cg_set_tuning: null key");
     if (!strcmp(key, "gemm_variant")) {
         g_gemm_variant = value;
+        return CG_OK;
+    }
+    if (!strcmp(key, "gemm_max_grid")) {
+        g_gemm_max_grid = value;
         return CG_OK;
     }
     if (!strcmp(key, "attn_variant")) {

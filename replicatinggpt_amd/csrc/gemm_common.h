@@ -66,10 +66,20 @@ __device__ __forceinline__ void store_out(TC* C, int64_t off, float v, float bet
 
 // tuning knob (cg_set_tuning("gemm_variant", v)); 0 = automatic choice
 extern int g_gemm_variant;
+// test knob (cg_set_tuning("gemm_max_grid", n)): cap on persistent-kernel blocks; 0 = resident slots
+extern int g_gemm_max_grid;
 
 // launches the bf16 MFMA kernel if the problem qualifies; returns false (nothing launched) if not
 bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
                       int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, float* ws,
                       hipStream_t st);
+// LDS-DMA (global_load_lds) kernels, variant >= 5 (gemm_glds.hip); false if the variant/shape does not apply
+bool glds_gemm_launch(int variant, int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda,
+                      const bf16_t* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k,
+                      float* ws, hipStream_t st);
+// persistent LDS-DMA kernels with register epilogues, variant >= 9 (gemm_pk.hip)
+bool pk_gemm_launch(int variant, int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda,
+                    const bf16_t* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k,
+                    float* ws, hipStream_t st);
 
 }  // namespace cg

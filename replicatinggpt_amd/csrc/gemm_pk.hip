@@ -1,0 +1,243 @@
+// charpt: persistent LDS-DMA bf16 MFMA GEMM (gfx950) -- the default kernel behind cg_gemm for the
+// nn.Linear forward / dgrad / wgrad products of GPT1.py:111-112,121,136,143,145.
+//
+// Measured on MI355X (tools/gemm_diag.hip): with one 128x128 tile per block, a K=384 launch spends
+// ~0.7 us waiting for its first K-tile and ~2.5 us in an LDS-staged epilogue against ~3 us of
+// MFMA loop.  This kernel removes both:
+//  * persistent blocks (grid = resident slots) walk a flattened (item, K-tile) sequence; the
+//    LDS-DMA stream (global_load_lds_dwordx4, NBUF stages, NBUF-1 tiles in flight) runs straight
+//    across item boundaries, so the next item's first tiles land while this item finishes;
+//  * the MFMA operands are swapped (D = B_tile x A_tile^T), so each lane's accumulator holds four
+//    consecutive output COLUMNS of one row: bias / ReLU / Philox dropout (exactly one Philox group
+//    per 4 columns) / residual / ReLU-backward are applied in registers and stored as one 8-B
+//    (bf16) or 16-B (fp32) store -- no LDS staging, no epilogue barriers.
+// An item is one BM x BN output tile of one K-split; items are ordered split-major and remapped
+// so that consecutive items (same row panel / same split) share an XCD's L2.
+#include "gemm_tile.h"
+
+namespace cg {
+namespace {
+using namespace gt;
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// per-lane part of one operand's LDS-DMA sources: R rows (K-contiguous) or R columns (TR) x 64 k
+template <bool TR, int R, int WAVES>
+struct DmaP {
+    static constexpr int INSTR = R * FBK * 2 / 1024;  // 1-KB wave instructions per K-tile
+    static constexpr int PER_WAVE = INSTR / WAVES;
+    static_assert(PER_WAVE * WAVES == INSTR, "tile/wave mismatch");
+    static_assert(!TR || R >= 128, "transposed image swizzle needs >= 16 chunks per row");
+    int off[PER_WAVE];  // element offset of this lane's 16-B chunk from the tile origin
+    int64_t kstep;
+
+    __device__ __forceinline__ void init(int64_t ld, int wave, int lane) {
+#pragma unroll
+        for (int i = 0; i < PER_WAVE; ++i) {
+            const int pos = (wave * PER_WAVE + i) * 1024 + lane * 16;
+            if (!TR) {
+                const int r = pos >> 7, c = ((pos >> 4) & 7) ^ row_swz(r);
+                off[i] = (int)(r * ld) + c * 8;
+            } else {
+                const int k = pos / (2 * R), c = ((pos % (2 * R)) >> 4) ^ col_swz(k);
+                off[i] = (int)(k * ld) + c * 8;
+            }
+        }
+        kstep = TR ? (int64_t)FBK * ld : (int64_t)FBK;
+    }
+    __device__ __forceinline__ void issue(const bf16_t* origin, int kt, char* img, int wave) const {
+        const bf16_t* base = origin + kt * kstep;
+#pragma unroll
+        for (int i = 0; i < PER_WAVE; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(base + off[i]),
+                                             (lds_void*)(img + (wave * PER_WAVE + i) * 1024), 16, 0, 0);
+    }
+};
+
+template <int BM, int BN, int NBUF>
+struct GeoP {
+    static constexpr int WM = BM / 64, WN = BN / 64, WAVES = WM * WN, THREADS = WAVES * 64;
+    static constexpr int IMG_A = BM * FBK * 2, IMG_B = BN * FBK * 2, STAGE = IMG_A + IMG_B;
+    static constexpr int LDS = NBUF * STAGE;
+    static constexpr int OCC = LDS <= 80 * 1024 ? 2 : 1;  // resident blocks per CU (LDS-bound)
+};
+
+template <bool AT, bool BT, int BM, int BN, int NBUF>
+__global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, ((BM + BN) * 128 * NBUF <= 80 * 1024 ? 2 : 1))
+void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
+               const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype, int64_t ldc,
+               EpiArgs epi, int split_k, int64_t kchunk, float* __restrict__ ws) {
+    using G = GeoP<BM, BN, NBUF>;
+    using DA = DmaP<AT, BM, G::WAVES>;
+    using DB = DmaP<BT, BN, G::WAVES>;
+    constexpr int LPT = DA::PER_WAVE + DB::PER_WAVE;  // DMA instructions per thread per K-tile
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / G::WN, wn = wave % G::WN;
+    const int tilesN = (int)(N / BN);
+    const int ntiles = (int)(M / BM) * tilesN;
+    const int nitems = ntiles * split_k;
+    const int nk = (int)(kchunk / FBK);
+    const int P = gridDim.x, b = blockIdx.x;
+    const int my_items = b < nitems ? (nitems - 1 - b) / P + 1 : 0;
+    const int total = my_items * nk;
+    const uint64_t stream =
+        (epi.kind == CG_EPI_BIAS_DROP_RESID && epi.thr && split_k == 1) ? dropout_stream(epi.rng_call, epi.site) : 0;
+
+    DA da;
+    DB db;
+    da.init(lda, wave, lane);
+    db.init(ldb, wave, lane);
+
+    auto decode = [&](int j, int64_t& m0, int64_t& n0, int& split) {
+        const int it = xcd_remap(b + j * P, nitems);
+        split = it / ntiles;
+        const int t = it - split * ntiles;
+        m0 = (int64_t)(t / tilesN) * BM;
+        n0 = (int64_t)(t % tilesN) * BN;
+    };
+
+    // DMA issue cursor (item ij, K-tile ikt) and its operand origins
+    int ij = 0, ikt = 0;
+    const bf16_t* oa = A;
+    const bf16_t* ob = B;
+    auto issue_next = [&](int buf) {
+        if (ikt == 0) {
+            int64_t m0, n0;
+            int sp;
+            decode(ij, m0, n0, sp);
+            const int64_t kb = sp * kchunk;
+            oa = AT ? A + kb * lda + m0 : A + m0 * lda + kb;
+            ob = BT ? B + kb * ldb + n0 : B + n0 * ldb + kb;
+        }
+        char* img = smem + buf * G::STAGE;
+        da.issue(oa, ikt, img, wave);
+        db.issue(ob, ikt, img + G::IMG_A, wave);
+        if (++ikt == nk) {
+            ikt = 0;
+            ++ij;
+        }
+    };
+
+    fv4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+    for (int s = 0; s < NBUF - 1; ++s)
+        if (s < total) issue_next(s);
+
+    int cur = 0, cj = 0, ckt = 0;
+    for (int g = 0; g < total; ++g) {
+        const int ahead = total - 1 - g;  // steps issued after g that may stay in flight: min(NBUF-2, ahead)
+        if constexpr (NBUF >= 4) {
+            if (ahead >= 2) wait_vm<2 * LPT>();
+            else if (ahead == 1) wait_vm<LPT>();
+            else wait_vm<0>();
+        } else if constexpr (NBUF == 3) {
+            if (ahead >= 1) wait_vm<LPT>();
+            else wait_vm<0>();
+        } else {
+            wait_vm<0>();
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (g + NBUF - 1 < total) {
+            int nb = cur + NBUF - 1;
+            if (nb >= NBUF) nb -= NBUF;
+            issue_next(nb);
+        }
+        const char* imgA = smem + cur * G::STAGE;
+        const char* imgB = imgA + G::IMG_A;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            sv8 af[4], bf[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) af[i] = frag<AT, BM>(imgA, wm * 64 + i * 16, s, lane);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bf[j] = frag<BT, BN>(imgB, wn * 64 + j * 16, s, lane);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = mfma_bf16(bf[j], af[i], acc[i][j]);
+        }
+        cur = cur + 1 == NBUF ? 0 : cur + 1;
+        if (++ckt == nk) {
+            // item done: acc[i][j][r] = C[mw + 16i + (lane&15)][nw + 16j + 4(lane>>4) + r]
+            int64_t m0, n0;
+            int sp;
+            decode(cj, m0, n0, sp);
+            const int64_t mr = m0 + wm * 64 + (lane & 15), nc = n0 + wn * 64 + 4 * (lane >> 4);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int64_t m = mr + 16 * i, n = nc + 16 * j;
+                    if (split_k > 1)
+                        *(fv4*)(ws + ((int64_t)sp * M + m) * N + n) = acc[i][j];
+                    else
+                        epi_store4(acc[i][j], m, n, N, Cv, c_dtype, ldc, epi, stream);
+                    acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
+                }
+            ckt = 0;
+            ++cj;
+        }
+    }
+}
+
+int cu_count() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+    }
+    return n;
+}
+
+template <int BM, int BN, int NBUF>
+void launch_p(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
+              int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, float* ws,
+              hipStream_t st) {
+    using G = GeoP<BM, BN, NBUF>;
+    const int64_t kchunk = K / split_k;
+    const int64_t nitems = (M / BM) * (N / BN) * split_k;
+    int64_t slots = (int64_t)cu_count() * G::OCC;
+    if (g_gemm_max_grid > 0 && g_gemm_max_grid < slots) slots = g_gemm_max_grid;
+    const unsigned grid = (unsigned)(nitems < slots ? nitems : slots);
+#define FG(AT_, BT_)                                                                                             \
+    k_gemm_pk<AT_, BT_, BM, BN, NBUF><<<grid, G::THREADS, G::LDS, st>>>(M, N, K, A, lda, B, ldb, C, c_dtype, ldc, \
+                                                                      e, split_k, kchunk, ws)
+    if (!at && !bt) FG(false, false);
+    else if (!at && bt) FG(false, true);
+    else if (at && !bt) FG(true, false);
+    else FG(true, true);
+#undef FG
+}
+
+}  // namespace
+
+bool pk_gemm_launch(int v, int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda,
+                    const bf16_t* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k,
+                    float* ws, hipStream_t st) {
+    switch (v) {
+        case 9: launch_p<128, 128, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st); return true;
+        case 10: launch_p<128, 128, 3>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st); return true;
+        case 11:
+            if (M % 256) return false;
+            launch_p<256, 128, 3>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
+            return true;
+        case 12: launch_p<128, 128, 4>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st); return true;
+        default: return false;
+    }
+}
+
+}  // namespace cg

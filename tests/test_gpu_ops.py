@@ -109,6 +109,52 @@ def test_gemm_layouts(at, bt, shape, dt):
     assert relerr(out, ref) < 1e-5
 
 
+@pytest.mark.parametrize("variant,max_grid", [(1, 0), (2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (7, 0), (8, 0), (9, 0),
+                                              (9, 5), (10, 0), (10, 7), (11, 0), (11, 3), (12, 0)])
+@pytest.mark.parametrize("at,bt", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_kernel_variants(variant, max_grid, at, bt):
+    """Every bf16 MFMA kernel variant (register-staged 1-4, LDS-DMA 5-8, persistent LDS-DMA 9-12 --
+    with the grid capped so that each block walks several tiles) on all four layouts, with split-K
+    and the fused bias+ReLU and bias+dropout+residual epilogues."""
+    from replicatinggpt_amd import _lib as L
+    lib = L.load()
+    M, N, K = 512, 384, 768
+    torch.manual_seed(7)
+    A = (torch.randn(K, M) if at else torch.randn(M, K)).to(torch.bfloat16)
+    B = (torch.randn(K, N) if bt else torch.randn(N, K)).to(torch.bfloat16)
+    bias = torch.randn(N)
+    ref = _ref_gemm(A, B, at, bt)
+    Ad, Bd = A.to(DEV), B.to(DEV)
+    L.check(lib.cg_set_tuning(b"gemm_variant", variant))
+    L.check(lib.cg_set_tuning(b"gemm_max_grid", max_grid))
+    try:
+        out = torch.empty(M, N, dtype=torch.float32, device=DEV)
+        ops().gemm(Ad, Bd, out, True, bool(at), bool(bt), M, N, K, A.shape[1], B.shape[1], N, 0, None, None, 0,
+                   None, 0, 0.0, 0, None, 0, 0.0, 1, None)
+        ws = torch.empty(ops().gemm_workspace(M, N, 3) // 4, dtype=torch.float32, device=DEV)
+        out3 = torch.empty(M, N, dtype=torch.float32, device=DEV)
+        ops().gemm(Ad, Bd, out3, True, bool(at), bool(bt), M, N, K, A.shape[1], B.shape[1], N, 0, None, None, 0,
+                   None, 0, 0.0, 0, None, 0, 0.0, 3, ws)
+        h = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        ops().gemm(Ad, Bd, h, True, bool(at), bool(bt), M, N, K, A.shape[1], B.shape[1], N, 2, bias.to(DEV), None,
+                   0, None, 0, 0.0, 0, None, 0, 0.0, 1, None)
+        resid = torch.randn(M, N)
+        call = torch.tensor([6], dtype=torch.int64, device=DEV)
+        o = torch.empty(M, N, dtype=torch.float32, device=DEV)
+        ops().gemm(Ad, Bd, o, True, bool(at), bool(bt), M, N, K, A.shape[1], B.shape[1], N, 4, bias.to(DEV),
+                   resid.to(DEV), N, None, 0, 0.2, 99, call, 3, 0.0, 1, None)
+        torch.cuda.synchronize()
+    finally:
+        L.check(lib.cg_set_tuning(b"gemm_variant", 0))
+        L.check(lib.cg_set_tuning(b"gemm_max_grid", 0))
+    assert relerr(out, ref) < 1e-5
+    assert relerr(out3, ref) < 1e-5
+    assert relerr(h, torch.relu(ref + bias.double())) < 8e-3
+    keep = philox.keep_mask(99, (6 << 8) | 3, np.arange(M * N), 0.2).reshape(M, N)
+    want = resid.double() + torch.from_numpy(keep).double() * (ref + bias.double()) * float(np.float32(1 / 0.8))
+    assert relerr(o, want) < 1e-5
+
+
 @pytest.mark.parametrize("split", [2, 4, 8])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_gemm_splitk_deterministic(split, dt):
