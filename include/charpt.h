@@ -124,6 +124,15 @@ int cg_colsum(const void* X, int x_dtype, int64_t rows, int64_t N, int64_t ldx, 
 int cg_attn_fwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const void* q, const void* k,
                 const void* v, int64_t ld_qkv, void* o, int64_t ld_o, float* lse, float scale, double dropout_p,
                 uint64_t seed, const uint64_t* rng_call, int site, uint64_t* mask, void* stream);
+/* the same with the keep bits already in `mask` (cg_attn_dropmask, e.g. launched ahead on another
+   stream so the Philox work overlaps earlier kernels); identical results to cg_attn_fwd.        */
+int cg_attn_fwd_premasked(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const void* q, const void* k,
+                          const void* v, int64_t ld_qkv, void* o, int64_t ld_o, float* lse, float scale,
+                          double dropout_p, uint64_t seed, const uint64_t* rng_call, int site, uint64_t* mask,
+                          void* stream);
+/* fill the MFMA path's keep-bit buffer for one attention call (0 < p < 1, T % 16 == 0)          */
+int cg_attn_dropmask(int64_t B, int64_t H, int64_t T, double dropout_p, uint64_t seed, const uint64_t* rng_call,
+                     int site, uint64_t* mask, void* stream);
 /* keep-bit buffer for dropout on the MFMA (bf16, head_size 64) path: the forward fills it from the
    Philox stream (cg_attn_fwd `mask`, may be NULL on the generic path or with p = 0) and the
    backward reads it (cg_attn_bwd `mask`; NULL -> regenerated inside the workspace).            */
@@ -144,6 +153,20 @@ int cg_ce_fwd(const float* logits, int64_t rows, int64_t V, int64_t ld, const in
 int cg_ce_bwd(const float* logits, int64_t rows, int64_t V, int64_t ld, const int64_t* targets, const float* lse,
               const float* g, float g_mult, float* dlogits, int64_t ld_d, void* dst_lp /* optional bf16 copy */,
               void* stream);
+
+/* ---- fused LM head for the bf16 path (ln_f output -> lm_head -> cross entropy, GPT1.py:174,183-192)
+   a bf16 [M, C]; wpad bf16 [wpad_rows, C] = lm_head.weight with zero rows V..wpad_rows-1
+   (wpad_rows >= 16*ceil(V/16), V <= 128, M % 16 == 0, C % 32 == 0); bias fp32 [V].
+   fwd: logits fp32 [M, V] = a wpad^T + b, lse [M]; with targets also *loss = mean CE (workspace
+   cg_head_workspace).  bwd: dl bf16 [M, ld_dl] = (*g_loss) g_mult (softmax - onehot) [+ g_logits],
+   zero in columns V..ld_dl-1 (the K-padded operand of the dgrad/wgrad GEMMs); db (+)= colsum(dl). */
+int64_t cg_head_workspace(int64_t M, int64_t V);
+int cg_head_fwd(const void* a, const void* wpad, int64_t wpad_rows, const float* bias, const int64_t* targets,
+                float* logits, float* lse, float* loss, void* workspace, int64_t M, int64_t C, int64_t V,
+                void* stream);
+int cg_head_bwd(const float* logits, const float* lse, const int64_t* targets, const float* g_loss, float g_mult,
+                const float* g_logits, void* dl, int64_t ld_dl, float* db, int db_accumulate, void* workspace,
+                int64_t M, int64_t V, void* stream);
 
 /* ---- fused AdamW over a flat fp32 buffer (torch.optim.AdamW, GPT1.py:218,233) ------------
    step_ptr: device int64 step count (already incremented for this step).

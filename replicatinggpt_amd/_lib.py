@@ -50,12 +50,18 @@ _SIGS = {
     "cg_colsum": (c_int, [P, c_int, c_i64, c_i64, c_i64, P, c_int, P, P]),
     "cg_attn_fwd": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, P, P, P, c_i64, P, c_i64, P, c_flt, c_dbl, c_u64, P,
                             c_int, P, P]),
+    "cg_attn_fwd_premasked": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, P, P, P, c_i64, P, c_i64, P, c_flt, c_dbl,
+                                      c_u64, P, c_int, P, P]),
+    "cg_attn_dropmask": (c_int, [c_i64, c_i64, c_i64, c_dbl, c_u64, P, c_int, P, P]),
     "cg_attn_mask_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "cg_attn_bwd_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
     "cg_attn_bwd": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, P, P, P, c_i64, P, c_i64, P, c_i64, P, P, P, P, c_i64,
                             c_flt, c_dbl, c_u64, P, c_int, P, P, P]),
     "cg_ce_fwd": (c_int, [P, c_i64, c_i64, c_i64, P, P, P, P]),
     "cg_ce_bwd": (c_int, [P, c_i64, c_i64, c_i64, P, P, P, c_flt, P, c_i64, P, P]),
+    "cg_head_workspace": (c_i64, [c_i64, c_i64]),
+    "cg_head_fwd": (c_int, [P, P, c_i64, P, P, P, P, P, P, c_i64, c_i64, c_i64, P]),
+    "cg_head_bwd": (c_int, [P, P, P, P, c_flt, P, P, c_i64, P, c_int, P, c_i64, c_i64, P]),
     "cg_adamw": (c_int, [P, P, P, P, P, c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, P, P]),
 }
 

@@ -30,9 +30,10 @@ namespace attn {
 // bf16 MFMA kernels, head_size 64, T % 64 == 0 (attention_d64.hip)
 void launch_fwd_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                     bf16_t* o, int64_t ldo, float* lse, float scale, const DropArgs& d, hipStream_t st);
+// also computes delta = rowsum(dO * O) for its queries and writes it (read by launch_dkdv_d64 next)
 void launch_dq_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
-                   const bf16_t* dout, int64_t ldd, const float* lse, const float* delta, bf16_t* dq, int64_t lddq,
-                   float scale, const DropArgs& d, hipStream_t st);
+                   const bf16_t* o, int64_t ldo, const bf16_t* dout, int64_t ldd, const float* lse, float* delta,
+                   bf16_t* dq, int64_t lddq, float scale, const DropArgs& d, hipStream_t st);
 void launch_dkdv_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                      const bf16_t* dout, int64_t ldd, const float* lse, const float* delta, bf16_t* dk, bf16_t* dv,
                      int64_t lddkv, float scale, const DropArgs& d, hipStream_t st);

@@ -264,8 +264,8 @@ __global__ __launch_bounds__(256, QW == 16 ? 3 : 2) void k_attn_fwd_d64(
 template <int QW>
 __global__ __launch_bounds__(256, QW == 16 ? 3 : 2) void k_attn_dq_d64(
     int64_t T_, int H, const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-    int64_t ld, const bf16_t* __restrict__ dout, int64_t ldd, const float* __restrict__ lse,
-    const float* __restrict__ delta, bf16_t* __restrict__ dq, int64_t lddq, float scale,
+    int64_t ld, const bf16_t* __restrict__ o, int64_t ldo, const bf16_t* __restrict__ dout, int64_t ldd,
+    const float* __restrict__ lse, float* __restrict__ delta, bf16_t* __restrict__ dq, int64_t lddq, float scale,
     const uint64_t* __restrict__ mask, float dscale) {
     constexpr int QT = QW / 16, FQ = 4 * QW, QROWS = FQ / 16;
     constexpr int MB = QROWS * 128;
@@ -292,7 +292,27 @@ __global__ __launch_bounds__(256, QW == 16 ? 3 : 2) void k_attn_dq_d64(
             of[qt][s] = wave_active ? *(const sv8*)(dout + (boff + qrow) * ldd + h * 64 + 32 * s + 8 * g) : sv8{};
         }
         lq[qt] = wave_active ? lse[(int64_t)bh * T_ + qrow] * LOG2E : 0.f;
-        dl[qt] = wave_active ? delta[(int64_t)bh * T_ + qrow] : 0.f;
+        // delta = rowsum(dO * O) (dropout-invariant: O already holds the dropped P); lane group g
+        // holds elements 32s + 8g .. +7 of the row: reduce over s in-lane, then across g
+        float dsum = 0.f;
+        if (wave_active) {
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const uint4 ov = *(const uint4*)(o + (boff + qrow) * ldo + h * 64 + 32 * s + 8 * g);
+                const sv8 dv8 = of[qt][s];
+                const uint32_t ow[4] = {ov.x, ov.y, ov.z, ov.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    dsum += __uint_as_float(ow[e] << 16) * __uint_as_float(((uint32_t)(uint16_t)dv8[2 * e]) << 16);
+                    dsum += __uint_as_float(ow[e] & 0xffff0000u) *
+                            __uint_as_float(((uint32_t)(uint16_t)dv8[2 * e + 1]) << 16);
+                }
+            }
+        }
+        dsum += __shfl_xor(dsum, 16, 64);
+        dsum += __shfl_xor(dsum, 32, 64);
+        dl[qt] = dsum;
+        if (wave_active && g == 0) delta[(int64_t)bh * T_ + qrow] = dsum;
     }
     fv4 dqacc[4][QT];
 #pragma unroll
@@ -561,15 +581,15 @@ void launch_fwd_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* 
                                                                                     scale * LOG2E, d.mask, ds);
 }
 void launch_dq_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
-                   const bf16_t* dout, int64_t ldd, const float* lse, const float* delta, bf16_t* dq, int64_t lddq,
-                   float scale, const DropArgs& d, hipStream_t st) {
+                   const bf16_t* o, int64_t ldo, const bf16_t* dout, int64_t ldd, const float* lse, float* delta,
+                   bf16_t* dq, int64_t lddq, float scale, const DropArgs& d, hipStream_t st) {
     const float ds = d.mask ? d.dscale : 1.f;
     if (qw_of() == 32)
-        k_attn_dq_d64<32><<<dim3(ceil_div(T, 128), (unsigned)(B * H)), 256, 0, st>>>(T, H, q, k, v, ld, dout, ldd, lse,
-                                                                                    delta, dq, lddq, scale, d.mask, ds);
+        k_attn_dq_d64<32><<<dim3(ceil_div(T, 128), (unsigned)(B * H)), 256, 0, st>>>(
+            T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale, d.mask, ds);
     else
-        k_attn_dq_d64<16><<<dim3(ceil_div(T, 64), (unsigned)(B * H)), 256, 0, st>>>(T, H, q, k, v, ld, dout, ldd, lse,
-                                                                                   delta, dq, lddq, scale, d.mask, ds);
+        k_attn_dq_d64<16><<<dim3(ceil_div(T, 64), (unsigned)(B * H)), 256, 0, st>>>(
+            T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale, d.mask, ds);
 }
 void launch_dkdv_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                      const bf16_t* dout, int64_t ldd, const float* lse, const float* delta, bf16_t* dk, bf16_t* dv,

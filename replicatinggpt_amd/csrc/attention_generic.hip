@@ -22,25 +22,37 @@ using namespace cg;
 namespace {
 
 
-__global__ __launch_bounds__(256) void k_attn_dropmask(int64_t T_, uint64_t* __restrict__ mask, DropArgs d) {
+// one wave per 16x16 (query tile, key tile) on or below the diagonal, DM_TPW tiles per wave over
+// the flattened (b*H + h, lower-triangle tile) sequence: no idle waves above the diagonal and
+// enough work per wave that the launch is not dispatch-bound (B*H*NT(NT+1)/2 tiles in all).
+constexpr int DM_TPW = 8;
+__global__ __launch_bounds__(256) void k_attn_dropmask(int64_t T_, int64_t nbh, uint64_t* __restrict__ mask,
+                                                       DropArgs d) {
     const int NT = (int)(T_ >> 4);
-    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (tile >= NT * NT) return;
-    const int qt = tile / NT, kt = tile % NT;
-    if (kt > qt) return;  // strictly above the diagonal: fully causal-masked, never read
+    const int64_t ntri = (int64_t)NT * (NT + 1) / 2;
+    const int64_t total = nbh * ntri;
     const int lane = threadIdx.x & 63;
-    const uint64_t bh = blockIdx.y;
     const uint64_t stream = dropout_stream(d.rng_call, d.site);
-    const uint64_t q = (uint64_t)qt * 16 + (lane & 15), key0 = (uint64_t)kt * 16 + 4 * (lane >> 4);
-    const u32x4 r = philox_group(d.seed, stream, ((bh * T_ + q) * T_ + key0) >> 2);
-    const uint64_t b0 = __ballot(r.x >= d.thr), b1 = __ballot(r.y >= d.thr);
-    const uint64_t b2 = __ballot(r.z >= d.thr), b3 = __ballot(r.w >= d.thr);
-    if (lane == 0) {
-        uint64_t* o = mask + (((bh * NT + qt) * NT + kt) << 2);
-        o[0] = b0;
-        o[1] = b1;
-        o[2] = b2;
-        o[3] = b3;
+    const int64_t t0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * DM_TPW;
+#pragma unroll 1
+    for (int i = 0; i < DM_TPW; ++i) {
+        const int64_t t = t0 + i;
+        if (t >= total) return;
+        const uint64_t bh = (uint64_t)(t / ntri);
+        const int tri = (int)(t - (int64_t)bh * ntri);
+        int qt = (int)((sqrtf(8.f * tri + 1.f) - 1.f) * 0.5f);
+        while ((qt + 1) * (qt + 2) / 2 <= tri) ++qt;
+        while (qt * (qt + 1) / 2 > tri) --qt;
+        const int kt = tri - qt * (qt + 1) / 2;
+        const uint64_t q = (uint64_t)qt * 16 + (lane & 15), key0 = (uint64_t)kt * 16 + 4 * (lane >> 4);
+        const u32x4 r = philox_group(d.seed, stream, ((bh * T_ + q) * T_ + key0) >> 2);
+        const uint64_t b0 = __ballot(r.x >= d.thr), b1 = __ballot(r.y >= d.thr);
+        const uint64_t b2 = __ballot(r.z >= d.thr), b3 = __ballot(r.w >= d.thr);
+        if (lane == 0) {
+            uint64_t* o = mask + (((bh * NT + qt) * NT + kt) << 2);
+            *(uint4*)o = make_uint4((uint32_t)b0, (uint32_t)(b0 >> 32), (uint32_t)b1, (uint32_t)(b1 >> 32));
+            *(uint4*)(o + 2) = make_uint4((uint32_t)b2, (uint32_t)(b2 >> 32), (uint32_t)b3, (uint32_t)(b3 >> 32));
+        }
     }
 }
 
@@ -365,8 +377,8 @@ int64_t mask_bytes(int64_t B, int64_t H, int64_t T) { return B * H * (T / 16) * 
 
 void launch_dropmask(int64_t B, int64_t H, int64_t T, uint64_t* mask, const DropArgs& d, hipStream_t st) {
     const int64_t NT = T / 16;
-    dim3 grid(ceil_div(NT * NT, 4), (unsigned)(B * H));
-    k_attn_dropmask<<<grid, 256, 0, st>>>(T, mask, d);
+    const int64_t tiles = B * H * NT * (NT + 1) / 2;
+    k_attn_dropmask<<<ceil_div(tiles, 4 * DM_TPW), 256, 0, st>>>(T, B * H, mask, d);
 }
 
 bool fast_attn_ok(int dtype, int64_t T, int64_t D, const void* a, const void* b, const void* c, int64_t ld1,
@@ -382,10 +394,42 @@ size_t generic_lds(int D, int nrows_blocks, int nsq) {
 
 }  // namespace
 
+namespace {
+int attn_fwd_impl(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const void* q, const void* k, const void* v,
+                  int64_t ld_qkv, void* o, int64_t ld_o, float* lse, float scale, double dropout_p, uint64_t seed,
+                  const uint64_t* rng_call, int site, uint64_t* mask, bool mask_ready, void* stream);
+}
+
 extern "C" int cg_attn_fwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const void* q, const void* k,
                            const void* v, int64_t ld_qkv, void* o, int64_t ld_o, float* lse, float scale,
                            double dropout_p, uint64_t seed, const uint64_t* rng_call, int site, uint64_t* mask,
                            void* stream) {
+    return attn_fwd_impl(dtype, B, T, H, D, q, k, v, ld_qkv, o, ld_o, lse, scale, dropout_p, seed, rng_call, site,
+                         mask, false, stream);
+}
+
+extern "C" int cg_attn_fwd_premasked(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const void* q,
+                                     const void* k, const void* v, int64_t ld_qkv, void* o, int64_t ld_o, float* lse,
+                                     float scale, double dropout_p, uint64_t seed, const uint64_t* rng_call, int site,
+                                     uint64_t* mask, void* stream) {
+    return attn_fwd_impl(dtype, B, T, H, D, q, k, v, ld_qkv, o, ld_o, lse, scale, dropout_p, seed, rng_call, site,
+                         mask, true, stream);
+}
+
+extern "C" int cg_attn_dropmask(int64_t B, int64_t H, int64_t T, double dropout_p, uint64_t seed,
+                                const uint64_t* rng_call, int site, uint64_t* mask, void* stream) {
+    CG_REQUIRE(B > 0 && H > 0 && T > 0 && T % 16 == 0, "cg_attn_dropmask: bad shape (T %% 16 == 0 required)");
+    CG_REQUIRE(dropout_p > 0 && dropout_p < 1 && mask, "cg_attn_dropmask: needs 0 < p < 1 and a mask buffer");
+    DropArgs d = make_drop(dropout_p, seed, rng_call, site);
+    launch_dropmask(B, H, T, mask, d, (hipStream_t)stream);
+    CG_LAUNCH_CHECK("cg_attn_dropmask");
+    return CG_OK;
+}
+
+namespace {
+int attn_fwd_impl(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const void* q, const void* k, const void* v,
+                  int64_t ld_qkv, void* o, int64_t ld_o, float* lse, float scale, double dropout_p, uint64_t seed,
+                  const uint64_t* rng_call, int site, uint64_t* mask, bool mask_ready, void* stream) {
     CG_REQUIRE(B > 0 && T > 0 && H > 0 && D > 0 && D <= 128, "cg_attn_fwd: bad shape (D must be <= 128)");
     CG_REQUIRE(dropout_p >= 0 && dropout_p < 1, "cg_attn_fwd: dropout_p must be in [0,1)");
     hipStream_t st = (hipStream_t)stream;
@@ -393,7 +437,7 @@ extern "C" int cg_attn_fwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D
     if (fast_attn_ok(dtype, T, D, q, k, o, ld_qkv, ld_o)) {
         if (d.thr) {
             CG_REQUIRE(mask, "cg_attn_fwd: dropout on the MFMA path needs a mask buffer (cg_attn_mask_bytes)");
-            launch_dropmask(B, H, T, mask, d, st);
+            if (!mask_ready) launch_dropmask(B, H, T, mask, d, st);
             d.mask = mask;
         }
         attn::launch_fwd_d64(B, T, (int)H, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ld_qkv, (bf16_t*)o,
@@ -411,6 +455,7 @@ extern "C" int cg_attn_fwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D
     CG_LAUNCH_CHECK("cg_attn_fwd");
     return CG_OK;
 }
+}  // namespace
 
 extern "C" int64_t cg_attn_mask_bytes(int64_t B, int64_t H, int64_t T) { return mask_bytes(B, H, T); }
 
@@ -431,14 +476,16 @@ extern "C" int cg_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D
     DropArgs d = make_drop(dropout_p, seed, rng_call, site);
     float* delta = (float*)workspace;
     const int64_t nrows = B * T * H;
-    if (dtype == CG_BF16)
+    const bool fast = fast_attn_ok(dtype, T, D, q, dout, dq, ld_qkv, ld_do) && ld_dqkv % 8 == 0 &&
+                      ((((uintptr_t)dk) | ((uintptr_t)dv) | ((uintptr_t)o)) & 15) == 0 && ld_o % 8 == 0;
+    if (fast) {
+        // delta = rowsum(dO * O) is computed inside the dQ kernel (which runs before dK/dV)
+    } else if (dtype == CG_BF16)
         k_attn_delta<bf16_t><<<ceil_div(nrows, 256), 256, 0, st>>>(B, T, (int)H, (int)D, (const bf16_t*)o, ld_o,
                                                                  (const bf16_t*)dout, ld_do, delta);
     else
         k_attn_delta<float><<<ceil_div(nrows, 256), 256, 0, st>>>(B, T, (int)H, (int)D, (const float*)o, ld_o,
                                                                 (const float*)dout, ld_do, delta);
-    const bool fast = fast_attn_ok(dtype, T, D, q, dout, dq, ld_qkv, ld_do) && ld_dqkv % 8 == 0 &&
-                      ((((uintptr_t)dk) | ((uintptr_t)dv)) & 15) == 0;
     if (fast) {
         if (d.thr) {
             if (!mask) {  // regenerate the forward's keep bits (identical Philox stream)
@@ -449,7 +496,8 @@ extern "C" int cg_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D
             d.mask = mask;
         }
         const bf16_t *Q = (const bf16_t*)q, *K = (const bf16_t*)k, *V = (const bf16_t*)v, *DO = (const bf16_t*)dout;
-        attn::launch_dq_d64(B, T, (int)H, Q, K, V, ld_qkv, DO, ld_do, lse, delta, (bf16_t*)dq, ld_dqkv, scale, d, st);
+        attn::launch_dq_d64(B, T, (int)H, Q, K, V, ld_qkv, (const bf16_t*)o, ld_o, DO, ld_do, lse, delta, (bf16_t*)dq,
+                            ld_dqkv, scale, d, st);
         attn::launch_dkdv_d64(B, T, (int)H, Q, K, V, ld_qkv, DO, ld_do, lse, delta, (bf16_t*)dk, (bf16_t*)dv, ld_dqkv,
                               scale, d, st);
     } else {

@@ -185,7 +185,10 @@ bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf1
     if (e.resid && ((((uintptr_t)e.resid) & 15) || e.ld_resid % 4)) return false;
     if (e.aux && ((((uintptr_t)e.aux) & 15) || e.ld_aux % 8)) return false;
     int v = g_gemm_variant;
-    if (v == 0) v = 2;  // measured best on MI355X for every C2/C4 shape (tools/gemm_tune.py)
+    if (v == 0) v = 9;  // persistent 128x128 LDS-DMA: measured best on the C2 shapes (profiles/r1_gemm_scan.txt)
+    if (v >= 20 && p8_gemm_launch(v, at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st))
+        return true;
+    if (v >= 20) v = 2;
     if (v >= 5 && glds_gemm_launch(v, at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st))
         return true;
     if ((v == 3 || v == 4) && M % 256) v = 1;

@@ -82,4 +82,9 @@ bool pk_gemm_launch(int variant, int at, int bt, int64_t M, int64_t N, int64_t K
                     const bf16_t* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k,
                     float* ws, hipStream_t st);
 
+// persistent 8-wave LDS-DMA kernels (gemm_p8.hip), variant >= 20 (20 = automatic tile choice)
+bool p8_gemm_launch(int variant, int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda,
+                    const bf16_t* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k,
+                    float* ws, hipStream_t st);
+
 }  // namespace cg

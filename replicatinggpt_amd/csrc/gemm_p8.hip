@@ -1,0 +1,296 @@
+// charpt: persistent 8-wave LDS-DMA bf16 MFMA GEMM (gfx950) -- the default kernel behind cg_gemm
+// for the nn.Linear forward / dgrad / wgrad products of GPT1.py:111-112,121,136,143,145.
+//
+// Why this shape (measured with tools/gemm_diag.hip on MI355X):
+//  * a 128x128 block tile needs (BM+BN)*BK*2 B of operands per 2*BM*BN*BK FLOP = 64 FLOP/B, i.e.
+//    ~31 TB/s of L2->LDS traffic at the MFMA peak -- the chip's whole L2 bandwidth.  256x128 tiles
+//    halve that per FLOP (85 FLOP/B), 256x256 tiles quarter it (128 FLOP/B);
+//  * with one tile per block every CU runs load -> MFMA -> store in lockstep with every other CU,
+//    so a short-K launch (K = 384: 6 K-tiles) pays the HBM-bound first load and the HBM-bound
+//    output store in series with the MFMA loop.  Here blocks are persistent (one per CU, 8 waves =
+//    2 per SIMD) and walk a flattened (item, K-tile) sequence; the LDS-DMA ring
+//    (global_load_lds_dwordx4, NBUF stages, NBUF-1 K-tiles in flight, counted vmcnt, raw
+//    s_barrier) runs straight across item boundaries, and the epilogue is register-direct
+//    (swapped MFMA operands: each lane holds 4 consecutive output columns of one row), so the
+//    output stores of item j drain while item j+1's MFMAs run.
+// An item is one BM x BN output tile of one K-split; items are ordered split-major and remapped so
+// that consecutive items (same row panel) share an XCD's L2.
+#include "gemm_tile.h"
+
+namespace cg {
+namespace {
+using namespace gt;
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+constexpr int P8_WAVES = 8, P8_THREADS = 512;
+
+// per-lane LDS-DMA sources of one operand image: R rows (K-contiguous) or R columns (TR) x 64 k.
+// Wave-instruction i writes LDS bytes [1024 i, 1024 i + 1024) lane-linearly; the XOR swizzle of
+// gemm_tile.h is applied to the SOURCE address (cdna guide §5.4 rule 21).
+template <bool TR, int R>
+struct Dma8 {
+    static constexpr int INSTR = R * FBK * 2 / 1024;
+    static constexpr int PER_WAVE = INSTR / P8_WAVES;
+    static_assert(PER_WAVE * P8_WAVES == INSTR, "tile/wave mismatch");
+    static_assert(!TR || R >= 128, "transposed image swizzle needs >= 16 chunks per row");
+    int off[PER_WAVE];
+    int64_t kstep;
+
+    __device__ __forceinline__ void init(int64_t ld, int wave, int lane) {
+#pragma unroll
+        for (int i = 0; i < PER_WAVE; ++i) {
+            const int pos = (wave * PER_WAVE + i) * 1024 + lane * 16;
+            if (!TR) {
+                const int r = pos >> 7, c = ((pos >> 4) & 7) ^ row_swz(r);
+                off[i] = (int)(r * ld) + c * 8;
+            } else {
+                const int k = pos / (2 * R), c = ((pos % (2 * R)) >> 4) ^ col_swz(k);
+                off[i] = (int)(k * ld) + c * 8;
+            }
+        }
+        kstep = TR ? (int64_t)FBK * ld : (int64_t)FBK;
+    }
+    __device__ __forceinline__ void issue(const bf16_t* origin, int kt, char* img, int wave) const {
+        const bf16_t* base = origin + kt * kstep;
+#pragma unroll
+        for (int i = 0; i < PER_WAVE; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(base + off[i]),
+                                             (lds_void*)(img + (wave * PER_WAVE + i) * 1024), 16, 0, 0);
+    }
+};
+
+template <int BM, int BN, int NBUF>
+struct Geo8 {
+    static constexpr int IMG_A = BM * FBK * 2, IMG_B = BN * FBK * 2, STAGE = IMG_A + IMG_B;
+    static constexpr int LDS = NBUF * STAGE;
+};
+
+// WM = waves along M (8 / WM along N); per-wave tile (BM/WM) x (BN/(8/WM)) in 16x16 fragments
+template <bool AT, bool BT, int BM, int BN, int WM, int NBUF>
+__global__ __launch_bounds__(P8_THREADS, 2)
+void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
+               const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype, int64_t ldc,
+               EpiArgs epi, int split_k, int64_t kchunk, float* __restrict__ ws) {
+    using G = Geo8<BM, BN, NBUF>;
+    using DA = Dma8<AT, BM>;
+    using DB = Dma8<BT, BN>;
+    constexpr int WN = P8_WAVES / WM, FM = BM / WM / 16, FN = BN / WN / 16;
+    constexpr int LPT = DA::PER_WAVE + DB::PER_WAVE;  // DMA instructions per lane per K-tile
+    constexpr int EPI_OPS = FM * FN;                  // vector-memory stores per lane per item
+    static_assert(NBUF >= 2 && NBUF <= 4, "ring depth");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int tilesN = (int)(N / BN);
+    const int ntiles = (int)(M / BM) * tilesN;
+    const int nitems = ntiles * split_k;
+    const int nk = (int)(kchunk / FBK);
+    const int P = gridDim.x, b = blockIdx.x;
+    const int my_items = b < nitems ? (nitems - 1 - b) / P + 1 : 0;
+    const int total = my_items * nk;
+    const uint64_t stream =
+        (epi.kind == CG_EPI_BIAS_DROP_RESID && epi.thr && split_k == 1) ? dropout_stream(epi.rng_call, epi.site) : 0;
+
+    DA da;
+    DB db;
+    da.init(lda, wave, lane);
+    db.init(ldb, wave, lane);
+
+    auto decode = [&](int j, int64_t& m0, int64_t& n0, int& split) {
+        const int it = xcd_remap(b + j * P, nitems);
+        split = it / ntiles;
+        const int t = it - split * ntiles;
+        m0 = (int64_t)(t / tilesN) * BM;
+        n0 = (int64_t)(t % tilesN) * BN;
+    };
+
+    // DMA issue cursor (item ij, K-tile ikt) and its operand origins
+    int ij = 0, ikt = 0;
+    const bf16_t* oa = A;
+    const bf16_t* ob = B;
+    auto issue_next = [&](int buf) {
+        if (ikt == 0) {
+            int64_t m0, n0;
+            int sp;
+            decode(ij, m0, n0, sp);
+            const int64_t kb = sp * kchunk;
+            oa = AT ? A + kb * lda + m0 : A + m0 * lda + kb;
+            ob = BT ? B + kb * ldb + n0 : B + n0 * ldb + kb;
+        }
+        char* img = smem + buf * G::STAGE;
+        da.issue(oa, ikt, img, wave);
+        db.issue(ob, ikt, img + G::IMG_A, wave);
+        if (++ikt == nk) {
+            ikt = 0;
+            ++ij;
+        }
+    };
+
+    fv4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+    for (int s = 0; s < NBUF - 1; ++s)
+        if (s < total) issue_next(s);
+
+    int cur = 0, cj = 0, ckt = 0;
+    bool stored = false;  // the previous step ended an item: EPI_OPS stores are the youngest VMEM ops
+    for (int g = 0; g < total; ++g) {
+        // DMA steps issued after step g (they may stay in flight): min(NBUF-2, total-1-g)
+        const int ahead = total - 1 - g;
+        if (stored) {
+            if constexpr (NBUF >= 4) {
+                if (ahead >= 2) wait_vm<2 * LPT + EPI_OPS>();
+                else if (ahead == 1) wait_vm<LPT + EPI_OPS>();
+                else wait_vm<EPI_OPS>();
+            } else if constexpr (NBUF == 3) {
+                if (ahead >= 1) wait_vm<LPT + EPI_OPS>();
+                else wait_vm<EPI_OPS>();
+            } else {
+                wait_vm<EPI_OPS>();
+            }
+        } else {
+            if constexpr (NBUF >= 4) {
+                if (ahead >= 2) wait_vm<2 * LPT>();
+                else if (ahead == 1) wait_vm<LPT>();
+                else wait_vm<0>();
+            } else if constexpr (NBUF == 3) {
+                if (ahead >= 1) wait_vm<LPT>();
+                else wait_vm<0>();
+            } else {
+                wait_vm<0>();
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (g + NBUF - 1 < total) {
+            int nb = cur + NBUF - 1;
+            if (nb >= NBUF) nb -= NBUF;
+            issue_next(nb);
+        }
+        const char* imgA = smem + cur * G::STAGE;
+        const char* imgB = imgA + G::IMG_A;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            sv8 af[FM], bf[FN];
+#pragma unroll
+            for (int i = 0; i < FM; ++i) af[i] = frag<AT, BM>(imgA, wm * (BM / WM) + i * 16, s, lane);
+#pragma unroll
+            for (int j = 0; j < FN; ++j) bf[j] = frag<BT, BN>(imgB, wn * (BN / WN) + j * 16, s, lane);
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j) acc[i][j] = mfma_bf16(bf[j], af[i], acc[i][j]);
+        }
+        cur = cur + 1 == NBUF ? 0 : cur + 1;
+        stored = false;
+        if (++ckt == nk) {
+            // item done: acc[i][j][r] = C[mw + 16i + (lane&15)][nw + 16j + 4(lane>>4) + r]
+            int64_t m0, n0;
+            int sp;
+            decode(cj, m0, n0, sp);
+            const int64_t mr = m0 + wm * (BM / WM) + (lane & 15), nc = n0 + wn * (BN / WN) + 4 * (lane >> 4);
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const int64_t m = mr + 16 * i, n = nc + 16 * j;
+                    if (split_k > 1)
+                        *(fv4*)(ws + ((int64_t)sp * M + m) * N + n) = acc[i][j];
+                    else
+                        epi_store4(acc[i][j], m, n, N, Cv, c_dtype, ldc, epi, stream);
+                    acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
+                }
+            ckt = 0;
+            ++cj;
+            stored = true;
+        }
+    }
+}
+
+int cu_count8() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+    }
+    return n;
+}
+
+template <int BM, int BN, int WM, int NBUF>
+void launch8(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
+             int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, float* ws,
+             hipStream_t st) {
+    using G = Geo8<BM, BN, NBUF>;
+    const int64_t kchunk = K / split_k;
+    const int64_t nitems = (M / BM) * (N / BN) * split_k;
+    const int occ = G::LDS <= 80 * 1024 ? 2 : 1;
+    int64_t slots = (int64_t)cu_count8() * occ;
+    if (g_gemm_max_grid > 0 && g_gemm_max_grid < slots) slots = g_gemm_max_grid;
+    const unsigned grid = (unsigned)(nitems < slots ? nitems : slots);
+#define FG(AT_, BT_)                                                                                     \
+    k_gemm_p8<AT_, BT_, BM, BN, WM, NBUF><<<grid, P8_THREADS, G::LDS, st>>>(M, N, K, A, lda, B, ldb, C, c_dtype, \
+                                                                            ldc, e, split_k, kchunk, ws)
+    if (!at && !bt) FG(false, false);
+    else if (!at && bt) FG(false, true);
+    else if (at && !bt) FG(true, false);
+    else FG(true, true);
+#undef FG
+}
+
+}  // namespace
+
+// variants: 20 = automatic tile choice; 21 = 256x128 (NBUF 3); 22 = 128x256 (NBUF 3);
+// 23 = 128x128 (NBUF 4); 24 = 256x256 (NBUF 2); 25 = 256x128 (NBUF 2)
+// Returns false (nothing launched) if the chosen tile does not divide the problem.
+bool p8_gemm_launch(int v, int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda,
+                    const bf16_t* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k,
+                    float* ws, hipStream_t st) {
+    if (K % (FBK * split_k)) return false;
+    if (v == 20) {
+        // largest tile that divides the problem and still yields >= ~3/4 of a block per CU
+        const int64_t cus = cu_count8();
+        auto items = [&](int bm, int bn) { return (M / bm) * (N / bn) * split_k; };
+        if (M % 256 == 0 && N % 128 == 0 && items(256, 128) >= (cus * 3) / 4) v = 21;
+        else if (M % 128 == 0 && N % 256 == 0 && items(128, 256) >= (cus * 3) / 4) v = 22;
+        else if (M % 128 == 0 && N % 128 == 0) v = 23;
+        else return false;
+    }
+    switch (v) {
+        case 21:
+            if (M % 256 || N % 128) return false;
+            launch8<256, 128, 4, 3>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
+            return true;
+        case 22:
+            if (M % 128 || N % 256) return false;
+            launch8<128, 256, 2, 3>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
+            return true;
+        case 23:
+            if (M % 128 || N % 128) return false;
+            launch8<128, 128, 2, 4>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
+            return true;
+        case 24:
+            if (M % 256 || N % 256) return false;
+            launch8<256, 256, 2, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
+            return true;
+        case 25:
+            if (M % 256 || N % 128) return false;
+            launch8<256, 128, 4, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
+            return true;
+        default:
+            return false;
+    }
+}
+
+}  // namespace cg

@@ -13,6 +13,7 @@ Parameter gradients are written by the kernels straight into the model's flat fp
 buffer ("grad slots"), see ``Region``; the residual-stream gradient is fp32, activations and
 GEMM operands are bf16 (or fp32 in exact mode).
 """
+import contextlib
 import math
 
 import torch
@@ -22,6 +23,52 @@ from . import ops
 
 EPI = {"store": L.EPI_STORE, "bias": L.EPI_BIAS, "bias_relu": L.EPI_BIAS_RELU, "bias_resid": L.EPI_BIAS_RESID,
        "bias_drop_resid": L.EPI_BIAS_DROP_RESID, "relu_bwd": L.EPI_RELU_BWD}
+
+
+class SideStream:
+    """A second HIP stream for work off the backward's critical path (weight gradients, bias column
+    sums, their split-K reductions) and for the forward's dropout keep bits.  The dgrad chain keeps
+    the main stream; these kernels overlap it (hipGraph replay keeps the fork/join as graph edges,
+    so the two branches run concurrently on the device).  Tensors read by side work are kept alive
+    until ``join()``, which makes the main stream wait for everything forked so far; the model's
+    embedding backward (the last autograd node), AdamW.step and TrainStep call it."""
+
+    def __init__(self):
+        self.enabled = True
+        self._streams = {}
+        self._keep = []
+        self._pending = set()
+
+    def stream(self, device):
+        s = self._streams.get(device)
+        if s is None:
+            s = self._streams[device] = torch.cuda.Stream(device=device)
+        return s
+
+    @contextlib.contextmanager
+    def run(self, device, *keep):
+        if not self.enabled or device.type != "cuda":
+            yield
+            return
+        cur = torch.cuda.current_stream(device)
+        s = self.stream(device)
+        s.wait_stream(cur)
+        with torch.cuda.stream(s):
+            yield
+        self._keep.extend(t for t in keep if t is not None)
+        self._pending.add(device)
+
+    def join(self, device=None):
+        devs = [device] if device is not None else list(self._pending)
+        for d in devs:
+            if d in self._pending:
+                torch.cuda.current_stream(d).wait_stream(self.stream(d))
+                self._pending.discard(d)
+        if not self._pending:
+            self._keep.clear()
+
+
+SIDE = SideStream()
 
 
 def site_stream(call, site):
@@ -43,10 +90,13 @@ class Region:
     parts  : [(param, element_offset)] in region order
     """
 
-    __slots__ = ("master", "slot", "shadow", "parts")
+    __slots__ = ("master", "slot", "shadow", "parts", "padded")
 
-    def __init__(self, master, parts, slot=None, shadow=None):
+    def __init__(self, master, parts, slot=None, shadow=None, padded=None):
         self.master, self.parts, self.slot, self.shadow = master, parts, slot, shadow
+        # (shadow, slot) views of a row-padded allocation (zero rows past the weight): the LM head's
+        # K-padded GEMM operand / gradient destination (FlatStore pad_rows)
+        self.padded = padded
 
     @staticmethod
     def of(*params):
@@ -184,17 +234,28 @@ def layernorm_bwd(dy2, x2, w_reg, b_reg, mean, rstd, dres=None, want_lp=False):
     return dx, dx_lp, fw() + fb()
 
 
-def attention_fwd(qkv, B, T, H, D, out, scale, p, seed, rng_call, site):
+def attention_fwd(qkv, B, T, H, D, out, scale, p, seed, rng_call, site, premask=None):
     """Returns (lse, mask): mask holds the dropout keep bits of the MFMA path (None when p == 0
-    or when the generic kernels, which regenerate Philox in place, are used)."""
+    or when the generic kernels, which regenerate Philox in place, are used).  ``premask`` =
+    (mask, event): keep bits already generated on the side stream (the main stream waits on the
+    event instead of generating them)."""
     d = H * D
     lse = torch.empty((B, H, T), dtype=torch.float32, device=qkv.device)
-    mask = None
-    if p > 0 and T % 16 == 0:
+    mask, ready = None, False
+    if p > 0 and premask is not None:
+        mask, ev = premask
+        torch.cuda.current_stream(qkv.device).wait_event(ev)
+        ready = True
+    elif p > 0 and T % 16 == 0:
         mask = torch.empty(ops.attn_mask_bytes(B, H, T) // 8, dtype=torch.int64, device=qkv.device)
     ops.attn_fwd(qkv, B, T, H, D, 0, d, 2 * d, qkv.stride(0), out, out.stride(0), lse, float(scale), float(p),
-                 int(seed), rng_call, int(site), mask)
+                 int(seed), rng_call, int(site), mask, ready)
     return lse, mask
+
+
+def premask_ok(act, T, D):
+    """The bf16 MFMA attention path (csrc fast_attn_ok) reads precomputed keep bits."""
+    return act == torch.bfloat16 and D == 64 and T % 64 == 0
 
 
 def attention_bwd(qkv, B, T, H, D, o, do, lse, scale, p, seed, rng_call, site, mask=None):
@@ -224,11 +285,12 @@ def _regions_params(regs):
 
 class LayerCtx:
     """Per-call context for a sublayer: geometry, dropout and dtype."""
-    __slots__ = ("n_head", "head_size", "scale", "p", "seed", "rng_call", "site", "act")
+    __slots__ = ("n_head", "head_size", "scale", "p", "seed", "rng_call", "site", "act", "premask")
 
-    def __init__(self, n_head, head_size, scale, p, seed, rng_call, site, act):
+    def __init__(self, n_head, head_size, scale, p, seed, rng_call, site, act, premask=None):
         self.n_head, self.head_size, self.scale, self.p = n_head, head_size, scale, p
         self.seed, self.rng_call, self.site, self.act = seed, rng_call, site, act
+        self.premask = premask   # (mask tensor, event) from BigramLanguageModel._launch_premasks
 
 
 # ---------------------------------------------------------------------------------------
@@ -264,6 +326,7 @@ class EmbeddingFn(torch.autograd.Function):
                 ops.embed_bwd(idx, dx.contiguous(), gt, gp[:T] if gp is not None else None, bool(bt or bp), ws)
             if gp is not None and not bp and T < gp.shape[0]:
                 gp[T:].zero_()  # positions beyond T get no gradient (overwrite mode)
+        SIDE.join(dx.device)   # last node of the model backward: every gradient is final after this
         return (None, None, None, *ft(), *fp())
 
 
@@ -280,7 +343,7 @@ class AttnSublayerFn(torch.autograd.Function):
         linear_fwd(a, qkv_w.operand(act), qkv)
         o = torch.empty((B * T, C), dtype=act, device=x.device)
         lse, ctx.mask = attention_fwd(qkv, B, T, lc.n_head, lc.head_size, o, lc.scale, lc.p, lc.seed, lc.rng_call,
-                                      lc.site)
+                                      lc.site, lc.premask)
         out = torch.empty((B * T, C), dtype=torch.float32, device=x.device)
         linear_fwd(o, proj_w.operand(act), out, "bias_resid", bias=proj_b.master, resid=x2)
         ctx.save_for_backward(x2, a, mean, rstd, qkv, o, lse)
@@ -296,20 +359,23 @@ class AttnSublayerFn(torch.autograd.Function):
         act = lc.act
         d32 = dout.reshape(B * T, C).contiguous()
         dy = to_act(d32, act)
-        # proj: dW = dy^T o, db = colsum(dy), do = dy W
-        g, beta, f_pw = proj_w.grad_target()
-        if g is not None:
-            linear_wgrad(dy, o, g, beta)
-        g, beta, f_pb = proj_b.grad_target()
-        if g is not None:
-            colsum_into(dy, g, beta)
+        dev = x2.device
+        # proj: dW = dy^T o, db = colsum(dy) (side stream), do = dy W (critical path)
+        g_pw, beta_pw, f_pw = proj_w.grad_target()
+        g_pb, beta_pb, f_pb = proj_b.grad_target()
+        with SIDE.run(dev, dy, o):
+            if g_pw is not None:
+                linear_wgrad(dy, o, g_pw, beta_pw)
+            if g_pb is not None:
+                colsum_into(dy, g_pb, beta_pb)
         do = torch.empty((B * T, C), dtype=act, device=x2.device)
         linear_dgrad(dy, proj_w.operand(act), do)
         dqkv = attention_bwd(qkv, B, T, lc.n_head, lc.head_size, o, do, lse, lc.scale, lc.p, lc.seed, lc.rng_call,
                              lc.site, ctx.mask)
         g, beta, f_qkv = qkv_w.grad_target()
         if g is not None:
-            linear_wgrad(dqkv, a, g, beta)
+            with SIDE.run(dev, dqkv, a):
+                linear_wgrad(dqkv, a, g, beta)
         da = torch.empty((B * T, C), dtype=act, device=x2.device)
         linear_dgrad(dqkv, qkv_w.operand(act), da)
         dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd, dres=d32)
@@ -345,20 +411,23 @@ class FFNSublayerFn(torch.autograd.Function):
         d32 = dout.reshape(B * T, C).contiguous()
         dz2 = torch.empty((B * T, C), dtype=act, device=x2.device)
         ops.dropout_apply(d32, dz2, float(lc.p), int(lc.seed), lc.rng_call, int(lc.site))
-        g, beta, f_w2 = w2.grad_target()
-        if g is not None:
-            linear_wgrad(dz2, h, g, beta)
-        g, beta, f_b2 = b2.grad_target()
-        if g is not None:
-            colsum_into(dz2, g, beta)
+        dev = x2.device
+        g_w2, beta_w2, f_w2 = w2.grad_target()
+        g_b2, beta_b2, f_b2 = b2.grad_target()
+        with SIDE.run(dev, dz2, h):
+            if g_w2 is not None:
+                linear_wgrad(dz2, h, g_w2, beta_w2)
+            if g_b2 is not None:
+                colsum_into(dz2, g_b2, beta_b2)
         dz1 = torch.empty_like(h)
         linear_dgrad(dz2, w2.operand(act), dz1, "relu_bwd", aux=h)
-        g, beta, f_w1 = w1.grad_target()
-        if g is not None:
-            linear_wgrad(dz1, a, g, beta)
-        g, beta, f_b1 = b1.grad_target()
-        if g is not None:
-            colsum_into(dz1, g, beta)
+        g_w1, beta_w1, f_w1 = w1.grad_target()
+        g_b1, beta_b1, f_b1 = b1.grad_target()
+        with SIDE.run(dev, dz1, a):
+            if g_w1 is not None:
+                linear_wgrad(dz1, a, g_w1, beta_w1)
+            if g_b1 is not None:
+                colsum_into(dz1, g_b1, beta_b1)
         da = torch.empty((B * T, C), dtype=act, device=x2.device)
         linear_dgrad(dz1, w1.operand(act), da)
         dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd, dres=d32)
@@ -376,6 +445,9 @@ class HeadLossFn(torch.autograd.Function):
         x2 = x.reshape(M, C)
         a, mean, rstd = layernorm(x2, ln_w.master, ln_b.master, act)
         V = lm_w.master.shape[0]
+        ctx.fused = _head_fused_ok(act, lm_w, M, C, V)
+        if ctx.fused:
+            return HeadLossFn._fused_forward(ctx, x, x2, targets, act, a, mean, rstd, (ln_w, ln_b, lm_w, lm_b))
         logits = torch.empty((M, V), dtype=torch.float32, device=x.device)
         linear_fwd(a, lm_w.operand(act), logits, "bias", bias=lm_b.master)
         lse = torch.empty(M, dtype=torch.float32, device=x.device)
@@ -408,6 +480,9 @@ class HeadLossFn(torch.autograd.Function):
             x2, a, mean, rstd, logits, lse = ctx.saved_tensors
             g_logits, g_loss = grads[0], None
         V = logits.shape[-1]
+        if ctx.fused:
+            return HeadLossFn._fused_backward(ctx, x2, a, mean, rstd, logits, lse, t1 if ctx.has_targets else None,
+                                              g_logits, g_loss)
         dl = torch.empty((M, V), dtype=torch.float32, device=x2.device)
         if g_loss is not None:
             ops.ce_bwd(logits, t1, lse, g_loss.reshape(1).float().contiguous(), 1.0 / M, dl, None)
@@ -426,6 +501,67 @@ class HeadLossFn(torch.autograd.Function):
         linear_dgrad(dl_op, lm_w.operand(act), da)
         dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd)
         return (dx.view(B, T, C), None, None, None, None, None, None, *f_ln, *f_lw(), *f_lb())
+
+    # -- bf16 fast path: cg_head_fwd/bwd + K-padded MFMA GEMMs (csrc/head.hip) -------------
+    @staticmethod
+    def _fused_forward(ctx, x, x2, targets, act, a, mean, rstd, regs):
+        ln_w, ln_b, lm_w, lm_b = regs
+        B, T, C = x.shape
+        M, V = B * T, lm_w.master.shape[0]
+        wpad = lm_w.padded[0]
+        logits = torch.empty((M, V), dtype=torch.float32, device=x.device)
+        lse = torch.empty(M, dtype=torch.float32, device=x.device)
+        ctx.regs, ctx.shape, ctx.act = regs, (B, T, C), act
+        ctx.set_materialize_grads(False)
+        if targets is None:
+            ops.head_fwd(a, wpad, lm_b.master, None, logits, lse, None, None)
+            ctx.save_for_backward(x2, a, mean, rstd, logits, lse)
+            ctx.has_targets = False
+            return logits.view(B, T, V)
+        t1 = targets.reshape(M)
+        loss = torch.empty((), dtype=torch.float32, device=x.device)
+        ws = torch.empty(ops.head_workspace(M, V) // 4, dtype=torch.float32, device=x.device)
+        ops.head_fwd(a, wpad, lm_b.master, t1, logits, lse, loss, ws)
+        ctx.save_for_backward(x2, a, mean, rstd, logits, lse, t1)
+        ctx.has_targets = True
+        return logits, loss
+
+    @staticmethod
+    def _fused_backward(ctx, x2, a, mean, rstd, logits, lse, t1, g_logits, g_loss):
+        ln_w, ln_b, lm_w, lm_b = ctx.regs
+        B, T, C = ctx.shape
+        M, V = logits.shape
+        wpad, gpad = lm_w.padded
+        KP = wpad.shape[0]
+        dl = torch.empty((M, KP), dtype=torch.bfloat16, device=x2.device)
+        gb, beta_b, f_lb = lm_b.grad_target()
+        ws = torch.empty(ops.head_workspace(M, V) // 4, dtype=torch.float32, device=x2.device)
+        gl = None if g_logits is None else g_logits.reshape(M, V).float().contiguous()
+        if g_loss is None:
+            t1 = None
+        ops.head_bwd(logits, lse, t1, None if g_loss is None else g_loss.reshape(1).float().contiguous(), 1.0 / M,
+                     gl, dl, gb, bool(beta_b), ws)
+        g, beta, f_lw = lm_w.grad_target()
+        if g is not None:
+            if g.data_ptr() == lm_w.slot.data_ptr():
+                with SIDE.run(x2.device, dl, a):
+                    linear_wgrad(dl, a, gpad, beta)   # rows >= V get exact zeros (dl pad columns are 0)
+            else:
+                tmp = torch.empty((KP, C), dtype=torch.float32, device=x2.device)
+                linear_wgrad(dl, a, tmp, 0.0)
+                if beta:
+                    g.add_(tmp[:V])
+                else:
+                    g.copy_(tmp[:V])
+        da = torch.empty((M, C), dtype=torch.bfloat16, device=x2.device)
+        linear_dgrad(dl, wpad, da)
+        dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd)
+        return (dx.view(B, T, C), None, None, None, None, None, None, *f_ln, *f_lw(), *f_lb())
+
+
+def _head_fused_ok(act, lm_w, M, C, V):
+    return (act == torch.bfloat16 and lm_w.padded is not None and lm_w.slot is not None and V <= 128
+            and M % 16 == 0 and C % 32 == 0)
 
 
 # ---------------------------------------------------------------------------------------
@@ -464,7 +600,7 @@ class MHAFn(torch.autograd.Function):
         linear_fwd(x2, qkv_w.operand(act), qkv)
         o = torch.empty((B * T, d), dtype=act, device=x.device)
         lse, ctx.mask = attention_fwd(qkv, B, T, lc.n_head, lc.head_size, o, lc.scale, lc.p, lc.seed, lc.rng_call,
-                                      lc.site)
+                                      lc.site, lc.premask)
         if proj_w is not None:
             out = torch.empty((B * T, proj_w.master.shape[0]), dtype=torch.float32, device=x.device)
             linear_fwd(o, proj_w.operand(act), out, "bias", bias=proj_b.master)

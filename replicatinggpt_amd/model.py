@@ -123,8 +123,10 @@ class MultiHeadAttention(nn.Module):
     def layer_ctx(self, x, C):
         p = self.heads[0].dropout.p if self.training else 0.0
         rng = _snapshot_for(self, x) if p > 0 else None
+        root = getattr(self, "_charpt_root", None)
+        pm = root._premasks.get(self.site) if (p > 0 and root is not None and root._premasks) else None
         return Fn.LayerCtx(len(self.heads), self.heads[0].key.out_features, Fn.attention_scale(C), p,
-                           self.config.dropout_seed, rng, self.site, _act_dtype(self.config))
+                           self.config.dropout_seed, rng, self.site, _act_dtype(self.config), pm)
 
     def forward(self, x):
         _require_hip(x)
@@ -227,15 +229,23 @@ def _snapshot_for(module, x):
 class FlatStore:
     """One fp32 master buffer, one fp32 gradient buffer and one bf16 shadow for all parameters."""
 
-    def __init__(self, plan, device):
-        # plan: list of (key, [(module, attr)]) -- parameters of a region are concatenated
+    def __init__(self, plan, device, pad_rows=None):
+        # plan: list of (key, [(module, attr)]) -- parameters of a region are concatenated.
+        # pad_rows: {key: rows} -- allocate the (single-parameter, 2-D) region with that many rows,
+        # the extra rows zero forever (zero gradient, zero AdamW update): the LM head's K-padded
+        # GEMM operand (functional.HeadLossFn) lives in the shadow without a copy.
         self.plan = plan
+        self.pad_rows = dict(pad_rows or {})
         self.offsets = {}
         off = 0
         for key, members in plan:
             n = sum(getattr(m, a).numel() for m, a in members)
             self.offsets[key] = (off, n)
-            off += -(-n // ALIGN) * ALIGN
+            alloc = n
+            if key in self.pad_rows:
+                cols = getattr(*members[0]).shape[-1]
+                alloc = max(n, self.pad_rows[key] * cols)
+            off += -(-alloc // ALIGN) * ALIGN
         self.numel = off
         master = torch.zeros(self.numel, dtype=torch.float32, device=device)
         with torch.no_grad():
@@ -272,8 +282,13 @@ class FlatStore:
                     newp = old
                 parts.append((newp, po))
                 po += old.numel()
+            padded = None
+            if key in self.pad_rows and self.pad_rows[key] >= shape[0]:
+                pr = self.pad_rows[key]
+                padded = (self.shadow[o:o + pr * shape[1]].view(pr, shape[1]),
+                          self.grad[o:o + pr * shape[1]].view(pr, shape[1]))
             self.regions[key] = Fn.Region(mview, parts, self.grad[o:o + n].view(shape),
-                                          self.shadow[o:o + n].view(shape))
+                                          self.shadow[o:o + n].view(shape), padded)
         self.refresh_shadow()
 
     @staticmethod
@@ -326,6 +341,7 @@ class BigramLanguageModel(nn.Module):
         for l, blk in enumerate(self.blocks):
             blk.set_layer_index(l)
         self._fwd_rng = None
+        self._premasks = None
         self.register_buffer("_rng_counter", torch.zeros(1, dtype=torch.int64), persistent=False)
         self._store = None
         self._pack()
@@ -349,7 +365,9 @@ class BigramLanguageModel(nn.Module):
 
     def _pack(self):
         dev = self.token_embedding_table.weight.device
-        self._store = FlatStore(self._plan(), dev)
+        V = self.config.vocab_size
+        pad = {"lm_w": 128} if V <= 128 else None   # K-padded operand of the fused head (HeadLossFn)
+        self._store = FlatStore(self._plan(), dev, pad)
         self._attach_regions()
 
     def _attach_regions(self):
@@ -413,6 +431,9 @@ class BigramLanguageModel(nn.Module):
             snap = torch.empty(1, dtype=torch.int64, device=idx.device)
             ops.rng_snapshot(self._rng_counter, snap)
             self._fwd_rng = snap
+            hs = cfg.n_embd // cfg.n_head
+            if Fn.SIDE.enabled and Fn.premask_ok(act, T, hs) and self.blocks[0].sa_heads.heads[0].dropout.p > 0:
+                self._launch_premasks(idx.device, B, T)
         try:
             wte, wpe = R["wte"], R["wpe"]
             x = Fn.EmbeddingFn.apply(idx, wte, wpe, *wte.params, *wpe.params)
@@ -422,9 +443,33 @@ class BigramLanguageModel(nn.Module):
                                       *hb.params)
         finally:
             self._fwd_rng = None
+            self._premasks = None
         if targets is None:
             return out, None
         return out
+
+    def _launch_premasks(self, dev, B, T):
+        """Every layer's attention-dropout keep bits, generated on the side stream at the start of
+        the forward (Philox is VALU work that overlaps the embedding / LN / QKV GEMM kernels); each
+        attention forward waits on its layer's event."""
+        cfg = self.config
+        H = cfg.n_head
+        n = ops.attn_mask_bytes(B, H, T) // 8
+        cur = torch.cuda.current_stream(dev)
+        side = Fn.SIDE.stream(dev)
+        side.wait_stream(cur)
+        pm = {}
+        with torch.cuda.stream(side):
+            for blk in self.blocks:
+                site = blk.sa_heads.site
+                p = blk.sa_heads.heads[0].dropout.p
+                mask = torch.empty(n, dtype=torch.int64, device=dev)
+                ops.attn_dropmask(B, H, T, float(p), int(cfg.dropout_seed), self._fwd_rng, int(site), mask)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                mask.record_stream(cur)   # read by the main stream (forward + backward)
+                pm[site] = (mask, ev)
+        self._premasks = pm
 
     # -- generate (GPT1.py:196-212) ----------------------------------------------------
     def generate(self, idx, max_new_tokens, greedy=False, generator=None):

@@ -145,12 +145,20 @@ def colsum_workspace(rows, N):
 @_op("attn_fwd", ("o", "lse", "mask"))
 def attn_fwd(qkv: Tensor, B: int, T: int, H: int, D: int, q_off: int, k_off: int, v_off: int, ld: int, o: Tensor,
              ld_o: int, lse: Tensor, scale: float, dropout_p: float, seed: int, rng_call: Optional[Tensor],
-             site: int, mask: Optional[Tensor]) -> None:
+             site: int, mask: Optional[Tensor], mask_ready: bool = False) -> None:
     es = qkv.element_size()
     base = qkv.data_ptr()
-    L.check(L.load().cg_attn_fwd(L.dtype_code(qkv.dtype), B, T, H, D, base + q_off * es, base + k_off * es,
-                                 base + v_off * es, ld, L.ptr(o), ld_o, L.ptr(lse), scale, dropout_p, seed,
-                                 L.ptr(rng_call), site, L.ptr(mask), _s(qkv)), "attn_fwd")
+    fn = L.load().cg_attn_fwd_premasked if mask_ready else L.load().cg_attn_fwd
+    L.check(fn(L.dtype_code(qkv.dtype), B, T, H, D, base + q_off * es, base + k_off * es, base + v_off * es, ld,
+               L.ptr(o), ld_o, L.ptr(lse), scale, dropout_p, seed, L.ptr(rng_call), site, L.ptr(mask), _s(qkv)),
+            "attn_fwd")
+
+
+@_op("attn_dropmask", ("mask",))
+def attn_dropmask(B: int, H: int, T: int, dropout_p: float, seed: int, rng_call: Optional[Tensor], site: int,
+                  mask: Tensor) -> None:
+    L.check(L.load().cg_attn_dropmask(B, H, T, dropout_p, seed, L.ptr(rng_call), site, L.ptr(mask), _s(mask)),
+            "attn_dropmask")
 
 
 def attn_mask_bytes(B, H, T):
@@ -190,6 +198,28 @@ def ce_bwd(logits: Tensor, targets: Tensor, lse: Tensor, g: Tensor, g_mult: floa
     rows = logits.numel() // V
     L.check(L.load().cg_ce_bwd(L.ptr(logits), rows, V, V, L.ptr(targets), L.ptr(lse), L.ptr(g), g_mult,
                                L.ptr(dlogits), V, L.ptr(dlogits_lp), _s(logits)), "ce_bwd")
+
+
+def head_workspace(M: int, V: int) -> int:
+    return int(L.load().cg_head_workspace(M, V))
+
+
+@_op("head_fwd", ("logits", "lse", "loss", "ws"))
+def head_fwd(a: Tensor, wpad: Tensor, bias: Tensor, targets: Optional[Tensor], logits: Tensor, lse: Tensor,
+             loss: Optional[Tensor], ws: Optional[Tensor]) -> None:
+    M, C = a.shape
+    V = logits.shape[-1]
+    L.check(L.load().cg_head_fwd(L.ptr(a), L.ptr(wpad), wpad.shape[0], L.ptr(bias), L.ptr(targets), L.ptr(logits),
+                                 L.ptr(lse), L.ptr(loss), L.ptr(ws), M, C, V, _s(a)), "head_fwd")
+
+
+@_op("head_bwd", ("dl", "db", "ws"))
+def head_bwd(logits: Tensor, lse: Tensor, targets: Optional[Tensor], g_loss: Optional[Tensor], g_mult: float,
+             g_logits: Optional[Tensor], dl: Tensor, db: Optional[Tensor], db_accumulate: bool, ws: Tensor) -> None:
+    M, V = logits.shape
+    L.check(L.load().cg_head_bwd(L.ptr(logits), L.ptr(lse), L.ptr(targets), L.ptr(g_loss), g_mult, L.ptr(g_logits),
+                                 L.ptr(dl), dl.stride(0), L.ptr(db), int(db_accumulate), L.ptr(ws), M, V, _s(logits)),
+            "head_bwd")
 
 
 # ---------------------------------------------------------------------------------------

@@ -7,6 +7,7 @@ bias-corrected moments, same fp32 operation order).
 """
 import torch
 
+from . import functional as Fn
 from . import ops
 
 
@@ -66,6 +67,7 @@ class AdamW(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         self._ensure()
+        Fn.SIDE.join()   # weight gradients computed on the side stream must be final
         st = self._store
         grp = self.param_groups[0]
         b1, b2 = grp["betas"]

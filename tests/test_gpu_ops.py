@@ -110,15 +110,17 @@ def test_gemm_layouts(at, bt, shape, dt):
 
 
 @pytest.mark.parametrize("variant,max_grid", [(1, 0), (2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (7, 0), (8, 0), (9, 0),
-                                              (9, 5), (10, 0), (10, 7), (11, 0), (11, 3), (12, 0)])
+                                              (9, 5), (10, 0), (10, 7), (11, 0), (11, 3), (12, 0),
+                                              (20, 0), (21, 0), (21, 3), (22, 0), (22, 5), (23, 0), (23, 7),
+                                              (24, 0), (24, 1), (25, 0), (25, 2)])
 @pytest.mark.parametrize("at,bt", [(0, 0), (0, 1), (1, 0), (1, 1)])
-def test_gemm_kernel_variants(variant, max_grid, at, bt):
-    """Every bf16 MFMA kernel variant (register-staged 1-4, LDS-DMA 5-8, persistent LDS-DMA 9-12 --
-    with the grid capped so that each block walks several tiles) on all four layouts, with split-K
-    and the fused bias+ReLU and bias+dropout+residual epilogues."""
+@pytest.mark.parametrize("M,N,K", [(512, 384, 768), (512, 512, 640)])
+def test_gemm_kernel_variants(variant, max_grid, at, bt, M, N, K):
+    """Every bf16 MFMA kernel variant (register-staged 1-4, LDS-DMA 5-8, persistent LDS-DMA 9-12,
+    persistent 8-wave LDS-DMA 20-25 -- with the grid capped so that each block walks several tiles)
+    on all four layouts, with split-K and the fused bias+ReLU and bias+dropout+residual epilogues."""
     from replicatinggpt_amd import _lib as L
     lib = L.load()
-    M, N, K = 512, 384, 768
     torch.manual_seed(7)
     A = (torch.randn(K, M) if at else torch.randn(M, K)).to(torch.bfloat16)
     B = (torch.randn(K, N) if bt else torch.randn(N, K)).to(torch.bfloat16)
@@ -362,6 +364,46 @@ def test_cross_entropy():
     dl = torch.empty(M, V, device=DEV)
     ops().ce_bwd(ld, td, lse, torch.ones(1, device=DEV), 1.0 / M, dl, None)
     assert relerr(dl, lr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("M,C,V", [(256, 384, 65), (1024, 128, 65), (64, 96, 16), (128, 64, 128)])
+def test_head_fused(M, C, V):
+    """cg_head_fwd/bwd (bf16 LM head + cross entropy, csrc/head.hip) against torch fp64 on the same
+    bf16-rounded operands: logits/lse/loss/dlogits/dbias at the bf16 bar (2e-2)."""
+    torch.manual_seed(11)
+    a = torch.randn(M, C).to(torch.bfloat16)
+    W = (torch.randn(V, C) / math.sqrt(C)).to(torch.bfloat16)
+    b = torch.randn(V)
+    tgt = torch.randint(0, V, (M,))
+    KP = 128
+    wpad = torch.zeros(KP, C, dtype=torch.bfloat16)
+    wpad[:V] = W
+    lg = (a.double() @ W.double().t() + b.double()).requires_grad_(True)
+    loss = torch.nn.functional.cross_entropy(lg, tgt)
+    loss.backward()
+    logits = torch.empty(M, V, device=DEV)
+    lse = torch.empty(M, device=DEV)
+    out = torch.empty((), device=DEV)
+    ws = torch.empty(ops().head_workspace(M, V) // 4, device=DEV)
+    ops().head_fwd(a.to(DEV), wpad.to(DEV), b.to(DEV), tgt.to(DEV), logits, lse, out, ws)
+    assert relerr(logits, lg) < 1e-5      # same bf16 operands, fp32 accumulate
+    assert relerr(lse, torch.logsumexp(lg.detach(), 1)) < 1e-5
+    assert abs(float(out) - float(loss)) < 1e-4 * max(1.0, abs(float(loss)))
+    dl = torch.empty(M, KP, dtype=torch.bfloat16, device=DEV)
+    db = torch.full((V,), 0.5, device=DEV)
+    ops().head_bwd(logits, lse, tgt.to(DEV), torch.full((1,), 2.0, device=DEV), 1.0 / M, None, dl, db, True, ws)
+    want = 2.0 * lg.grad
+    assert relerr(dl[:, :V], want) < 2e-2
+    if V < KP:
+        assert float(dl[:, V:].float().abs().max()) == 0.0
+    assert relerr(db, 0.5 + want.sum(0)) < 1e-5
+    # logits-only forward (generate path) and logits-gradient backward
+    logits2 = torch.empty(M, V, device=DEV)
+    ops().head_fwd(a.to(DEV), wpad.to(DEV), b.to(DEV), None, logits2, lse, None, None)
+    assert torch.equal(logits2, logits)
+    gl = torch.randn(M, V)
+    ops().head_bwd(logits, lse, None, None, 1.0 / M, gl.to(DEV), dl, None, False, ws)
+    assert relerr(dl[:, :V], gl) < 1e-2
 
 
 def test_adamw_matches_torch():
