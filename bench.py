@@ -119,6 +119,10 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-census", action="store_true")
+    ap.add_argument("--overlap", type=int, default=None, choices=[0, 1],
+                    help="force the segmented (DP-overlap) backward on/off (default: on when N > 1)")
+    ap.add_argument("--seg-layers", type=int, default=2,
+                    help="DP: blocks per backward graph segment (gradient all-reduce overlaps the next segment)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -143,8 +147,9 @@ def main():
     stream = TokenStream.synthetic(device=dev)
     sampler = BatchSampler(stream, T, Bsz, world_size=world, rank=rank,
                            generator=torch.Generator().manual_seed(cfg.seed))
-    reducer = GradReducer(model.flat.grad) if world > 1 else None
-    step = TrainStep(model, opt, sampler, reducer, use_graph=not args.no_graph)
+    reducer = GradReducer(model.flat.grad) if (world > 1 or args.overlap) else None
+    step = TrainStep(model, opt, sampler, reducer, use_graph=not args.no_graph, seg_layers=args.seg_layers,
+                     overlap=None if args.overlap is None else bool(args.overlap))
     step.capture()
     for _ in range(args.warmup):
         step.step()
@@ -164,7 +169,7 @@ def main():
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
-    final_loss = float(loss)
+    final_loss = float(loss.detach())
     tokens = world * Bsz * T * args.steps
     value = tokens / elapsed
     ms_step = elapsed / args.steps * 1e3
@@ -190,7 +195,9 @@ def main():
             "config": {"workload": f"{args.config}: char-GPT {cfg.n_layers}L/{cfg.n_head}H/{cfg.n_embd}d, "
                                    f"block {T}, batch {Bsz}/GPU, dropout {cfg.dropout}, AdamW, full train step",
                        "global_batch": Bsz * world, "seq_len": T, "parallelism": f"dp{world}",
-                       "graph": step.g_fb is not None},
+                       "graph": step.g_fb is not None or bool(step.g_seg),
+                       "grad_allreduce": (f"RCCL AVG overlapped: {len(step.ranges)} backward segments"
+                                          if step.overlap else ("RCCL AVG after backward" if world > 1 else None))},
             "mfu_step": round(mfu, 4), "flops_per_token": F, "final_loss": round(final_loss, 4),
             "roofline": roofline,
         }

@@ -1,14 +1,25 @@
 """Training-step executor: one iteration of GPT1.py's loop (GPT1.py:227-233) -- get_batch,
 forward, zero_grad, backward, [data-parallel gradient all-reduce], AdamW -- replayed from
-hipGraphs so the ~150 kernel launches of a step cost one graph launch instead of ~150 Python
+hipGraphs so the ~230 kernel launches of a step cost a few graph launches instead of ~230 Python
 dispatches.
 
 Single GPU: the whole step (forward + backward + optimizer) is one graph.
-Data parallel: forward + backward is one graph; the flat fp32 gradient buffer is averaged with
-bucketed RCCL all-reduces (dist.ReduceOp.AVG over xGMI); the optimizer step is a second graph.
+
+Data parallel (one process per GPU, RCCL over xGMI): the backward is captured as SEGMENTS cut at
+block boundaries (``torch.autograd.backward(..., inputs=[block input])`` stops the backward at a
+residual-stream tensor; the next segment resumes from its gradient).  Parameters live in one flat
+buffer laid out [embeddings | block 0 | ... | block L-1 | ln_f + lm_head], so the gradients a
+segment finishes form one contiguous range of the flat gradient buffer.  After segment i's graph
+is replayed, that range's ``all_reduce(AVG)`` is enqueued (async, RCCL's own stream) and segment
+i+1's graph replays on the compute stream meanwhile -- the gradient all-reduce overlaps the rest
+of the backward with only eager collectives (no collective is captured in a graph, so nothing
+here depends on RCCL graph capture).  The optimizer is a final graph replayed after the
+collectives have been waited on.
 """
 import torch
 import torch.distributed as dist
+
+from . import functional as Fn
 
 
 class GradReducer:
@@ -17,28 +28,58 @@ class GradReducer:
     def __init__(self, flat_grad, bucket_bytes=32 << 20, group=None):
         self.flat = flat_grad
         self.group = group
+        self.per = max(1, bucket_bytes // flat_grad.element_size())
         n = flat_grad.numel()
-        per = max(1, bucket_bytes // flat_grad.element_size())
         # reverse order: the backward finishes the last layers' gradients first
-        self.buckets = [(max(0, e - per), e) for e in range(n, 0, -per)]
-        self.world = dist.get_world_size(group)
-        self.avg_native = dist.get_backend(group) == "nccl"
+        self.buckets = [(max(0, e - self.per), e) for e in range(n, 0, -self.per)]
+        init = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if init else 1
+        self.avg_native = init and dist.get_backend(group) == "nccl"
+
+    def launch(self, start, end):
+        """Async all-reduce of flat[start:end] (bucket-sized pieces); returns the work handles.
+        RCCL's stream waits for the work already queued on the current stream, so this runs
+        behind the graph segment that produced the range and beside whatever is queued next."""
+        works = []
+        if self.world == 1 or end <= start:
+            return works
+        op = dist.ReduceOp.AVG if self.avg_native else dist.ReduceOp.SUM
+        for s in range(start, end, self.per):
+            e = min(end, s + self.per)
+            works.append(dist.all_reduce(self.flat[s:e], op=op, group=self.group, async_op=True))
+        return works
+
+    def finish(self, works, ranges=None):
+        for w in works:
+            w.wait()
+        if not self.avg_native and self.world > 1:
+            for s, e in (ranges or [(0, self.flat.numel())]):
+                self.flat[s:e].div_(self.world)
 
     def all_reduce(self):
         if self.world == 1:
             return
         works = []
         for s, e in self.buckets:
-            op = dist.ReduceOp.AVG if self.avg_native else dist.ReduceOp.SUM
-            works.append(dist.all_reduce(self.flat[s:e], op=op, group=self.group, async_op=True))
-        for w in works:
-            w.wait()
-        if not self.avg_native:
-            self.flat.div_(self.world)
+            works += self.launch(s, e)
+        self.finish(works)
+
+
+def segment_plan(model, seg_layers):
+    """Block indices where the backward is cut (descending) and, per segment, the contiguous flat
+    gradient range it finalizes: segment 0 = forward + loss .. block cuts[0] (ln_f/lm_head and
+    blocks cuts[0]..L-1), ..., last = blocks 0..cuts[-1]-1 + embeddings."""
+    L = len(model.blocks)
+    cuts = list(range(L - seg_layers, 0, -seg_layers)) if seg_layers > 0 else []
+    starts = model.flat.block_starts()            # flat offset of block l's first region
+    numel = model.flat.numel
+    bounds = [numel] + [starts[c] for c in cuts] + [0]
+    ranges = [(bounds[i + 1], bounds[i]) for i in range(len(bounds) - 1)]
+    return cuts, ranges
 
 
 class TrainStep:
-    def __init__(self, model, optimizer, sampler, reducer=None, use_graph=True):
+    def __init__(self, model, optimizer, sampler, reducer=None, use_graph=True, overlap=None, seg_layers=2):
         self.model, self.opt, self.sampler, self.reducer = model, optimizer, sampler, reducer
         dev = model.flat.master.device
         B, T = sampler.B, sampler.T
@@ -46,8 +87,12 @@ class TrainStep:
         self.y = torch.empty((B, T), dtype=torch.int64, device=dev)
         self.use_graph = use_graph and dev.type == "cuda"
         self.g_fb = self.g_opt = None
+        self.g_seg = []
         self.loss = None
+        self.overlap = (reducer is not None and reducer.world > 1) if overlap is None else bool(overlap)
+        self.cuts, self.ranges = segment_plan(model, seg_layers) if self.overlap else ([], [])
 
+    # -- eager ----------------------------------------------------------------------------
     def _fwd_bwd(self):
         _, loss = self.model(self.x, self.y)           # GPT1.py:230
         self.opt.zero_grad(set_to_none=True)           # GPT1.py:231
@@ -61,6 +106,50 @@ class TrainStep:
         self.opt.step()                                # GPT1.py:233
         return loss
 
+    # -- segmented backward (DP overlap) ------------------------------------------------------
+    def _forward_with_cuts(self):
+        """Forward with the residual stream cut at the segment boundaries: block j (j in cuts)
+        receives a detached leaf copy-free alias of its input, so each backward segment ends at a
+        leaf (autograd would still run the grad_fn of a non-leaf ``inputs=`` target).
+        Returns (loss, {j: (block input, leaf alias)})."""
+        xs = {}
+
+        def grab(j):
+            def hook(mod, args):
+                leaf = args[0].detach().requires_grad_(True)
+                xs[j] = (args[0], leaf)
+                return (leaf,) + tuple(args[1:])
+            return hook
+        hooks = [self.model.blocks[j].register_forward_pre_hook(grab(j)) for j in self.cuts]
+        try:
+            _, loss = self.model(self.x, self.y)
+        finally:
+            for h in hooks:
+                h.remove()
+        return loss, xs
+
+    def _segment(self, i, loss, xs):
+        """Backward of segment i (0 = from the loss): stops at the next cut's leaf alias, whose
+        .grad the following segment feeds into the real block-input tensor."""
+        if i == 0:
+            torch.autograd.backward(loss)
+        else:
+            src, leaf = xs[self.cuts[i - 1]]
+            torch.autograd.backward(src, grad_tensors=leaf.grad)
+        Fn.SIDE.join()
+
+    def _eager_segmented(self):
+        loss, xs = self._forward_with_cuts()
+        self.opt.zero_grad(set_to_none=True)
+        works = []
+        for i in range(len(self.cuts) + 1):
+            self._segment(i, loss, xs)
+            works += self.reducer.launch(*self.ranges[i])
+        self.reducer.finish(works, self.ranges)
+        self.opt.step()
+        return loss
+
+    # -- capture ------------------------------------------------------------------------------
     def capture(self, warmup=2):
         if not self.use_graph:
             return
@@ -69,10 +158,16 @@ class TrainStep:
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 self.sampler.get_batch("train", out=(self.x, self.y))
-                self._eager()
+                if self.overlap:
+                    self._eager_segmented()
+                else:
+                    self._eager()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         self.opt.zero_grad(set_to_none=True)
+        if self.overlap:
+            self._capture_segmented()
+            return
         self.g_fb = torch.cuda.CUDAGraph()
         if self.reducer is None:
             with torch.cuda.graph(self.g_fb):
@@ -86,10 +181,38 @@ class TrainStep:
                 self.opt.step()
         torch.cuda.synchronize()
 
+    def _capture_segmented(self):
+        g0 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g0):
+            loss, xs = self._forward_with_cuts()
+            self.opt.zero_grad(set_to_none=True)
+            self._segment(0, loss, xs)
+        self.g_seg = [g0]
+        for i in range(1, len(self.cuts) + 1):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=g0.pool()):
+                self._segment(i, loss, xs)
+            self.g_seg.append(g)
+        self.g_opt = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_opt, pool=g0.pool()):
+            self.opt.step()
+        self.loss = loss
+        self._xs = xs   # keep the segment boundary tensors (and their .grad) alive
+        torch.cuda.synchronize()
+
+    # -- one training step ----------------------------------------------------------------
     def step(self):
         self.sampler.get_batch("train", out=(self.x, self.y))   # GPT1.py:227
+        if self.g_seg:
+            works = []
+            for i, g in enumerate(self.g_seg):
+                g.replay()
+                works += self.reducer.launch(*self.ranges[i])
+            self.reducer.finish(works, self.ranges)
+            self.g_opt.replay()
+            return self.loss
         if self.g_fb is None:
-            self.loss = self._eager()
+            self.loss = self._eager_segmented() if self.overlap else self._eager()
             return self.loss
         self.g_fb.replay()
         if self.reducer is not None:

@@ -299,6 +299,15 @@ class FlatStore:
         rows = sum(s[0] for s in shapes)
         return torch.Size([rows, shapes[0][1]])
 
+    def block_starts(self):
+        """Flat offset of each transformer block's first region (the plan keeps a block's
+        parameters contiguous: [embeddings | block 0 | ... | block L-1 | ln_f + lm_head])."""
+        out, l = [], 0
+        while f"{l}.qkv" in self.offsets:
+            out.append(self.offsets[f"{l}.qkv"][0])
+            l += 1
+        return out
+
     def params(self):
         out = []
         for r in self.regions.values():

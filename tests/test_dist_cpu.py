@@ -34,7 +34,15 @@ def _worker(rank, world, port, q):
         g = torch.arange(1000, dtype=torch.float32) * (rank + 1)
         red = GradReducer(g, bucket_bytes=1024)
         red.all_reduce()
-        q.put((rank, [m.tolist() for m in mine], g.tolist(), len(red.buckets)))
+        # overlapped form (engine.TrainStep DP path): per-segment ranges launched async, then finished
+        g2 = torch.arange(1000, dtype=torch.float32) * (rank + 1)
+        red2 = GradReducer(g2, bucket_bytes=1024)
+        ranges = [(700, 1000), (250, 700), (0, 250)]
+        works = []
+        for r0, r1 in ranges:
+            works += red2.launch(r0, r1)
+        red2.finish(works, ranges)
+        q.put((rank, [m.tolist() for m in mine], g.tolist(), len(red.buckets), g2.tolist(), len(works)))
     finally:
         dist.destroy_process_group()
 
@@ -49,8 +57,8 @@ def test_dp_sampler_and_reducer_gloo():
         p.start()
     res = dict()
     for _ in range(world):
-        r, ix, g, nb = q.get(timeout=120)
-        res[r] = (ix, g, nb)
+        r, ix, g, nb, g2, nw = q.get(timeout=120)
+        res[r] = (ix, g, nb, g2, nw)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -65,3 +73,29 @@ def test_dp_sampler_and_reducer_gloo():
     for r in range(world):
         assert res[r][1] == want
         assert res[r][2] == 4
+        assert res[r][3] == want          # segmented launch/finish == one-shot average
+        assert res[r][4] == 2 + 2 + 1     # 256-element buckets inside each range
+
+
+def test_segment_plan_partitions_flat_buffer():
+    """The DP overlap cuts (engine.segment_plan) give contiguous flat-gradient ranges that tile the
+    whole buffer, each ending on a block boundary, head range first (backward order)."""
+    from replicatinggpt_amd import BigramLanguageModel, GPTConfig
+    from replicatinggpt_amd.engine import segment_plan
+    cfg = GPTConfig(block_size=32, n_embd=64, n_head=2, n_layers=5, dropout=0.0, dtype="bf16")
+    m = BigramLanguageModel(cfg)
+    starts = m.flat.block_starts()
+    assert len(starts) == 5 and starts == sorted(starts)
+    for seg in (1, 2, 3):
+        cuts, ranges = segment_plan(m, seg)
+        assert cuts == list(range(5 - seg, 0, -seg))
+        assert ranges[0][1] == m.flat.numel and ranges[-1][0] == 0
+        for (a0, a1), (b0, b1) in zip(ranges, ranges[1:]):
+            assert b1 == a0 and a0 > b0
+        assert [r[0] for r in ranges[:-1]] == [starts[c] for c in cuts]
+        # every parameter falls in exactly one range, and a block's parameters in one range
+        for l, blk in enumerate(m.blocks):
+            offs = [p.data_ptr() for p in blk.parameters()]
+            base = m.flat.master.data_ptr()
+            idx = {next(i for i, (r0, r1) in enumerate(ranges) if r0 <= (o - base) // 4 < r1) for o in offs}
+            assert len(idx) == 1

@@ -171,3 +171,29 @@ def test_greedy_generate_matches_reference():
             want = gold["streams"][tag]["tokens"]
             out = m.generate(want[:, :1].to(DEV), 500, greedy=True)
             assert torch.equal(out.cpu(), want), tag
+
+
+def test_segmented_overlap_step_matches_single_graph():
+    """engine.TrainStep's DP path (backward captured as block segments, per-segment gradient
+    ranges handed to the reducer between segment replays) gives bit-identical losses and weights to
+    the single-graph step (world size 1: the reducer is a no-op, the segmentation is exercised)."""
+    from replicatinggpt_amd import AdamW, BigramLanguageModel, GPTConfig
+    from replicatinggpt_amd.data import BatchSampler, TokenStream
+    from replicatinggpt_amd.engine import GradReducer, TrainStep
+    cfg = GPTConfig(block_size=128, n_embd=128, n_head=2, n_layers=5, dropout=0.2, dtype="bf16", batch_size=8)
+    runs = []
+    for overlap in (False, True):
+        torch.manual_seed(1337)
+        model = BigramLanguageModel(cfg).to("cuda")
+        opt = AdamW(model.parameters(), lr=1e-3).attach(model)
+        stream = TokenStream.synthetic(device="cuda")
+        sampler = BatchSampler(stream, 128, 8, generator=torch.Generator().manual_seed(5))
+        red = GradReducer(model.flat.grad) if overlap else None
+        step = TrainStep(model, opt, sampler, red, use_graph=True, overlap=overlap, seg_layers=2)
+        step.capture()
+        losses = [float(step.step().detach()) for _ in range(4)]
+        torch.cuda.synchronize()
+        runs.append((losses, model.flat.master.detach().cpu().clone(), len(step.g_seg)))
+    assert runs[1][2] == 3          # 5 layers, cuts at blocks 3 and 1
+    assert runs[0][0] == runs[1][0]
+    assert torch.equal(runs[0][1], runs[1][1])
