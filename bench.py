@@ -109,6 +109,32 @@ def gemm_census(cfg, Bsz, T, dev):
     return out
 
 
+def bench_generate(dev, B=256, new=500):
+    """BASELINE configs[4] (C5): generate() batched decode, 256 sequences x 500 new tokens from
+    the reference-trained C1-shape weights (tests/golden/model_c1_trained.safetensors -- the
+    model.pth of GPT1.py:239-241 as produced by the reference), fp32, greedy, through the
+    decode engine (K/V-cached prefix phase + sliding-window phase, one hipGraph per phase)."""
+    from safetensors.torch import load_file
+    from replicatinggpt_amd import BigramLanguageModel, GPTConfig
+    sd = load_file(os.path.join(ROOT, "tests", "golden", "model_c1_trained.safetensors"))
+    m = BigramLanguageModel(GPTConfig(dtype="fp32"))
+    m.load_state_dict(sd, strict=False)
+    m = m.to(dev).eval()
+    idx = torch.zeros((B, 1), dtype=torch.long, device=dev)
+    with torch.no_grad():
+        m.generate(idx, new, greedy=True)              # capture + warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = m.generate(idx, new, greedy=True)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    T = m.config.block_size
+    return {"metric": "generate tokens/sec (C5: 256 seqs x 500 new tokens, model.pth C1 shape, fp32 greedy)",
+            "value": round(B * new / dt, 1), "unit": "tokens/s", "seconds": round(dt, 4),
+            "phases": {"kv_cached_steps": T, "sliding_window_steps": new - T},
+            "checksum": int(out.sum())}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -119,6 +145,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-census", action="store_true")
+    ap.add_argument("--no-generate", action="store_true", help="skip the C5 batched-decode measurement")
     ap.add_argument("--overlap", type=int, default=None, choices=[0, 1],
                     help="force the segmented (DP-overlap) backward on/off (default: on when N > 1)")
     ap.add_argument("--seg-layers", type=int, default=2,
@@ -203,6 +230,8 @@ def main():
         }
         if census is not None:
             result["gemm_census_ms"] = {c["name"]: round(c["ms"], 4) for c in census}
+        if world == 1 and not args.no_generate:
+            result["generate_c5"] = bench_generate(dev)
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(cfg)
         print(json.dumps(result), flush=True)

@@ -168,6 +168,28 @@ int cg_head_bwd(const float* logits, const float* lse, const int64_t* targets, c
                 const float* g_logits, void* dl, int64_t ld_dl, float* db, int db_accumulate, void* workspace,
                 int64_t M, int64_t V, void* stream);
 
+/* ---- batched decode for generate() (GPT1.py:196-212; replicatinggpt_amd/decode.py) ----------
+   len_dev: device int64 = current sequence length (tokens in idx rows, row stride ld).          */
+/* out[b, j] = idx[b, max(0, len - T) + j]: the cropped context of GPT1.py:200                   */
+int cg_decode_window(const int64_t* idx, int64_t ld, int64_t B, int64_t T, const int64_t* len_dev, int64_t* out,
+                     void* stream);
+/* x[b] = wte[idx[b, len-1]] + wpe[len-1]  (fp32, the newest token)                              */
+int cg_decode_embed(const int64_t* idx, int64_t ld, const float* wte, const float* wpe, int64_t C,
+                    const int64_t* len_dev, float* x, int64_t B, void* stream);
+/* K/V cache [B, H, Tmax, D] row len-1 <- qkv rows (k / v at column offsets k_off / v_off)        */
+int cg_decode_kv_append(const float* qkv, int64_t ld, int64_t k_off, int64_t v_off, int64_t B, int64_t H,
+                        int64_t D, int64_t Tmax, const int64_t* len_dev, float* kcache, float* vcache,
+                        void* stream);
+/* one query per (b, h) against keys 0..n-1 (n = *len_dev, or nkeys when len_dev is NULL);
+   K/V element (b, h, j, e) at base + b*sb + h*sh + j*sj + e; o[b, h*D + e]; D <= 64            */
+int cg_decode_attn(const float* q, int64_t ldq, const float* k, const float* v, int64_t sb, int64_t sh, int64_t sj,
+                   int64_t B, int64_t H, int64_t D, const int64_t* len_dev, int64_t nkeys, float scale, float* o,
+                   int64_t ldo, void* stream);
+/* idx[b, len] <- argmax(logits[b]) (greedy, first index on ties) or an inverse-CDF draw from
+   softmax(logits[b]) with u from Philox(*seed_dev, stream = len, counter = b)                     */
+int cg_decode_sample(const float* logits, int64_t ldl, int64_t V, int64_t B, int greedy, const uint64_t* seed_dev,
+                     const int64_t* len_dev, int64_t* idx, int64_t ld, void* stream);
+
 /* ---- fused AdamW over a flat fp32 buffer (torch.optim.AdamW, GPT1.py:218,233) ------------
    step_ptr: device int64 step count (already incremented for this step).
    p_bf16: optional bf16 shadow written after the update (GEMM operands).                    */

@@ -62,6 +62,12 @@ _SIGS = {
     "cg_head_workspace": (c_i64, [c_i64, c_i64]),
     "cg_head_fwd": (c_int, [P, P, c_i64, P, P, P, P, P, P, c_i64, c_i64, c_i64, P]),
     "cg_head_bwd": (c_int, [P, P, P, P, c_flt, P, P, c_i64, P, c_int, P, c_i64, c_i64, P]),
+    "cg_decode_window": (c_int, [P, c_i64, c_i64, c_i64, P, P, P]),
+    "cg_decode_embed": (c_int, [P, c_i64, P, P, c_i64, P, P, c_i64, P]),
+    "cg_decode_kv_append": (c_int, [P, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, P, P, P, P]),
+    "cg_decode_attn": (c_int, [P, c_i64, P, P, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, P, c_i64, c_flt, P, c_i64,
+                               P]),
+    "cg_decode_sample": (c_int, [P, c_i64, c_i64, c_i64, c_int, P, P, P, c_i64, P]),
     "cg_adamw": (c_int, [P, P, P, P, P, c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, P, P]),
 }
 

@@ -1,0 +1,191 @@
+// charpt: batched autoregressive decode kernels for generate() (GPT1.py:196-212).
+//
+// The reference crops the context to the last block_size tokens and re-runs the full forward
+// every step (positions are re-indexed from 0 after the crop, so once the window slides no K/V can
+// be reused -- SURVEY Q7).  The decode engine (replicatinggpt_amd/decode.py) therefore runs
+//   phase 1 (length <= block_size): one new token per step against a per-layer K/V cache
+//            (cg_decode_kv_append + cg_decode_attn), positions identical to the full recompute;
+//   phase 2 (sliding window): the full window forward (cg_decode_window gathers it), last row only
+//            through ln_f / lm_head;
+// and samples on the device (cg_decode_sample: argmax, or inverse-CDF sampling from a Philox
+// stream).  Every step's shapes are static and the current length lives in device memory, so each
+// phase is captured once as a hipGraph and replayed per token.
+#include "common.h"
+
+namespace {
+using namespace cg;
+
+// out[b, j] = idx[b, start + j], start = max(0, len - T)  (len = *len_dev; idx row stride ld)
+__global__ void k_decode_window(const int64_t* __restrict__ idx, int64_t ld, int64_t B, int64_t T,
+                                const int64_t* __restrict__ len_dev, int64_t* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B * T) return;
+    const int64_t b = i / T, j = i % T;
+    const int64_t len = *len_dev;
+    const int64_t start = len > T ? len - T : 0;
+    out[i] = start + j < ld ? idx[b * ld + start + j] : 0;   // rows shorter than T: zero padding
+}
+
+// x[b, :] = wte[idx[b, pos]] + wpe[pos]   (pos = *len_dev - 1: the newest token)
+__global__ void k_decode_embed(const int64_t* __restrict__ idx, int64_t ld, const float* __restrict__ wte,
+                               const float* __restrict__ wpe, int64_t C, const int64_t* __restrict__ len_dev,
+                               float* __restrict__ x, int64_t B) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B * C) return;
+    const int64_t b = i / C, c = i % C;
+    const int64_t pos = *len_dev - 1;
+    x[i] = wte[idx[b * ld + pos] * C + c] + wpe[pos * C + c];
+}
+
+// K/V cache [B, H, Tmax, D]: row pos = *len_dev - 1 from the qkv rows (k at k_off, v at v_off)
+__global__ void k_decode_kv_append(const float* __restrict__ qkv, int64_t ld, int64_t k_off, int64_t v_off,
+                                   int64_t B, int64_t H, int64_t D, int64_t Tmax,
+                                   const int64_t* __restrict__ len_dev, float* __restrict__ kc,
+                                   float* __restrict__ vc) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B * H * D) return;
+    const int64_t b = i / (H * D), r = i % (H * D), h = r / D, e = r % D;
+    const int64_t pos = *len_dev - 1;
+    const int64_t dst = ((b * H + h) * Tmax + pos) * D + e;
+    kc[dst] = qkv[b * ld + k_off + h * D + e];
+    vc[dst] = qkv[b * ld + v_off + h * D + e];
+}
+
+// one wave per (b, h): the newest query against cached keys 0..pos (causal by construction).
+// Scores in fp32 (scale = n_embd^-0.5), exact softmax (max + sum over the wave), then
+// o[e] = sum_j p_j v_j[e] reduced across lanes.  D <= 64.
+// K/V element (b, h, key j, e) at base + b*sb + h*sh + j*sj + e: the [B, H, Tmax, D] cache
+// (sb = H*Tmax*D, sh = Tmax*D, sj = D) or the rows of a window's qkv buffer (sb = T*ld, sh = D, sj = ld).
+__global__ __launch_bounds__(256) void k_decode_attn(const float* __restrict__ q, int64_t ldq,
+                                                     const float* __restrict__ kc, const float* __restrict__ vc,
+                                                     int64_t sb, int64_t sh, int64_t sj, int64_t B, int64_t H,
+                                                     int64_t D, const int64_t* __restrict__ len_dev, int64_t nfix,
+                                                     float scale, float* __restrict__ o, int64_t ldo) {
+    __shared__ float sq[4][64];
+    __shared__ float sp[4][1024];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t bh = (int64_t)blockIdx.x * 4 + w;
+    if (bh >= B * H) return;
+    const int64_t b = bh / H, h = bh % H;
+    const int64_t n = len_dev ? *len_dev : nfix;  // keys 0..n-1
+    if (lane < D) sq[w][lane] = q[b * ldq + h * D + lane];
+    __builtin_amdgcn_wave_barrier();
+    const float* K = kc + b * sb + h * sh;
+    const float* V = vc + b * sb + h * sh;
+    float mx = -INFINITY;
+    for (int64_t j = lane; j < n; j += 64) {
+        float s = 0.f;
+        for (int e = 0; e < D; ++e) s = fmaf(sq[w][e], K[j * sj + e], s);
+        s *= scale;
+        sp[w][j] = s;
+        mx = fmaxf(mx, s);
+    }
+    mx = wave_max(mx);
+    float sum = 0.f;
+    for (int64_t j = lane; j < n; j += 64) {
+        const float p = __expf(sp[w][j] - mx);
+        sp[w][j] = p;
+        sum += p;
+    }
+    sum = wave_sum(sum);
+    __builtin_amdgcn_wave_barrier();
+    // lane e accumulates output element e over all keys (probabilities from LDS)
+    if (lane < D) {
+        float acc = 0.f;
+        for (int64_t j = 0; j < n; ++j) acc = fmaf(sp[w][j], V[j * sj + lane], acc);
+        o[b * ldo + h * D + lane] = acc / sum;
+    }
+}
+
+// next token per row from logits [B, V]: greedy = first argmax (torch.argmax tie rule); else
+// inverse-CDF sampling of softmax(logits) with u = Philox(seed, stream = step)[b] / 2^32.
+// Writes idx[b, len] (len = *len_dev) -- the caller then advances *len_dev.
+__global__ __launch_bounds__(64) void k_decode_sample(const float* __restrict__ logits, int64_t ldl, int64_t V,
+                                                      int64_t B, int greedy, const uint64_t* __restrict__ seed_dev,
+                                                      const int64_t* __restrict__ len_dev,
+                                                      int64_t* __restrict__ idx, int64_t ld) {
+    const int64_t b = blockIdx.x;
+    if (b >= B) return;
+    const int lane = threadIdx.x;
+    const float* row = logits + b * ldl;
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int v = lane; v < V; v += 64) {
+        const float x = row[v];
+        if (x > best || (x == best && v < bi)) { best = x; bi = v; }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const float ob = __shfl_xor(best, off, 64);
+        const int oi = __shfl_xor(bi, off, 64);
+        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    const int64_t len = *len_dev;
+    int64_t tok = bi;
+    if (!greedy) {
+        float s = 0.f;
+        for (int v = lane; v < V; v += 64) s += __expf(row[v] - best);
+        s = wave_sum(s);
+        const u32x4 r = philox_group(seed_dev ? *seed_dev : 0ull, (uint64_t)len, (uint64_t)b);
+        const float u = (float)(r.x >> 8) * (1.0f / 16777216.0f) * s;  // 24-bit uniform in [0, s)
+        // sequential inverse CDF in vocabulary order (lane 0; V is the 65-char vocabulary)
+        if (lane == 0) {
+            float c = 0.f;
+            tok = V - 1;
+            for (int v = 0; v < V; ++v) {
+                c += __expf(row[v] - best);
+                if (u < c) { tok = v; break; }
+            }
+        }
+    }
+    if (lane == 0) idx[b * ld + len] = tok;
+}
+
+}  // namespace
+
+extern "C" int cg_decode_window(const int64_t* idx, int64_t ld, int64_t B, int64_t T, const int64_t* len_dev,
+                                int64_t* out, void* stream) {
+    CG_REQUIRE(B > 0 && T > 0 && ld > 0, "cg_decode_window: bad sizes");
+    k_decode_window<<<ceil_div(B * T, 256), 256, 0, (hipStream_t)stream>>>(idx, ld, B, T, len_dev, out);
+    CG_LAUNCH_CHECK("cg_decode_window");
+    return CG_OK;
+}
+
+extern "C" int cg_decode_embed(const int64_t* idx, int64_t ld, const float* wte, const float* wpe, int64_t C,
+                               const int64_t* len_dev, float* x, int64_t B, void* stream) {
+    CG_REQUIRE(B > 0 && C > 0, "cg_decode_embed: bad sizes");
+    k_decode_embed<<<ceil_div(B * C, 256), 256, 0, (hipStream_t)stream>>>(idx, ld, wte, wpe, C, len_dev, x, B);
+    CG_LAUNCH_CHECK("cg_decode_embed");
+    return CG_OK;
+}
+
+extern "C" int cg_decode_kv_append(const float* qkv, int64_t ld, int64_t k_off, int64_t v_off, int64_t B, int64_t H,
+                                   int64_t D, int64_t Tmax, const int64_t* len_dev, float* kcache, float* vcache,
+                                   void* stream) {
+    CG_REQUIRE(B > 0 && H > 0 && D > 0 && Tmax > 0, "cg_decode_kv_append: bad sizes");
+    k_decode_kv_append<<<ceil_div(B * H * D, 256), 256, 0, (hipStream_t)stream>>>(qkv, ld, k_off, v_off, B, H, D,
+                                                                                  Tmax, len_dev, kcache, vcache);
+    CG_LAUNCH_CHECK("cg_decode_kv_append");
+    return CG_OK;
+}
+
+extern "C" int cg_decode_attn(const float* q, int64_t ldq, const float* k, const float* v, int64_t sb, int64_t sh,
+                              int64_t sj, int64_t B, int64_t H, int64_t D, const int64_t* len_dev, int64_t nkeys,
+                              float scale, float* o, int64_t ldo, void* stream) {
+    CG_REQUIRE(B > 0 && H > 0 && D > 0 && D <= 64, "cg_decode_attn: needs D <= 64");
+    CG_REQUIRE(len_dev || (nkeys > 0 && nkeys <= 1024), "cg_decode_attn: 1..1024 keys");
+    k_decode_attn<<<ceil_div(B * H, 4), 256, 0, (hipStream_t)stream>>>(q, ldq, k, v, sb, sh, sj, B, H, D, len_dev,
+                                                                       nkeys, scale, o, ldo);
+    CG_LAUNCH_CHECK("cg_decode_attn");
+    return CG_OK;
+}
+
+extern "C" int cg_decode_sample(const float* logits, int64_t ldl, int64_t V, int64_t B, int greedy,
+                                const uint64_t* seed_dev, const int64_t* len_dev, int64_t* idx, int64_t ld,
+                                void* stream) {
+    CG_REQUIRE(B > 0 && V > 0, "cg_decode_sample: bad sizes");
+    k_decode_sample<<<(unsigned)B, 64, 0, (hipStream_t)stream>>>(logits, ldl, V, B, greedy, seed_dev, len_dev, idx,
+                                                                 ld);
+    CG_LAUNCH_CHECK("cg_decode_sample");
+    return CG_OK;
+}

@@ -481,9 +481,23 @@ class BigramLanguageModel(nn.Module):
         self._premasks = pm
 
     # -- generate (GPT1.py:196-212) ----------------------------------------------------
-    def generate(self, idx, max_new_tokens, greedy=False, generator=None):
-        """Autoregressive sampling exactly as GPT1.py:196-212 (window crop, full forward, last
-        row, softmax, multinomial).  ``greedy=True`` takes the argmax instead (parity tests)."""
+    def generate(self, idx, max_new_tokens, greedy=False, generator=None, engine=True):
+        """Autoregressive sampling as GPT1.py:196-212 (crop to block_size, forward, last row,
+        softmax, multinomial, append).  On the GPU this runs the batched decode engine
+        (decode.DecodeEngine: K/V-cached prefix phase, sliding-window phase, device sampling, one
+        hipGraph per phase); ``greedy=True`` takes the argmax (the parity mode).  Sampled draws use
+        a seed taken from ``generator`` (torch's CPU multinomial stream is not reproducible on a
+        GPU).  ``engine=False`` runs the reference's loop literally (one full forward per token)."""
+        if engine and idx.device.type == "cuda" and max_new_tokens > 0:
+            from .decode import DecodeEngine
+            B, L0 = idx.shape
+            key = (B, L0 + max_new_tokens, bool(greedy), idx.device)
+            cache = self.__dict__.setdefault("_decode_engines", {})
+            eng = cache.get(key)
+            if eng is None or eng.m is not self:
+                eng = cache[key] = DecodeEngine(self, B, L0 + max_new_tokens, greedy=greedy)
+            seed = None if greedy else int(torch.randint(0, 2 ** 62, (1,), generator=generator))
+            return eng.generate(idx, max_new_tokens, seed=seed)
         for _ in range(max_new_tokens):
             idx_cond = idx[:, -self.config.block_size:]                 # GPT1.py:200
             logits, _ = self(idx_cond)                                   # GPT1.py:202

@@ -223,6 +223,45 @@ def head_bwd(logits: Tensor, lse: Tensor, targets: Optional[Tensor], g_loss: Opt
 
 
 # ---------------------------------------------------------------------------------------
+# batched decode (decode.py)
+@_op("decode_window", ("out",))
+def decode_window(idx: Tensor, len_dev: Tensor, out: Tensor) -> None:
+    B, T = out.shape
+    L.check(L.load().cg_decode_window(L.ptr(idx), idx.stride(0), B, T, L.ptr(len_dev), L.ptr(out), _s(idx)),
+            "decode_window")
+
+
+@_op("decode_embed", ("x",))
+def decode_embed(idx: Tensor, wte: Tensor, wpe: Tensor, len_dev: Tensor, x: Tensor) -> None:
+    B, C = x.shape
+    L.check(L.load().cg_decode_embed(L.ptr(idx), idx.stride(0), L.ptr(wte), L.ptr(wpe), C, L.ptr(len_dev), L.ptr(x),
+                                     B, _s(x)), "decode_embed")
+
+
+@_op("decode_kv_append", ("kcache", "vcache"))
+def decode_kv_append(qkv: Tensor, k_off: int, v_off: int, len_dev: Tensor, kcache: Tensor, vcache: Tensor) -> None:
+    B, H, Tmax, D = kcache.shape
+    L.check(L.load().cg_decode_kv_append(L.ptr(qkv), qkv.stride(0), k_off, v_off, B, H, D, Tmax, L.ptr(len_dev),
+                                         L.ptr(kcache), L.ptr(vcache), _s(qkv)), "decode_kv_append")
+
+
+@_op("decode_attn", ("o",))
+def decode_attn(q: Tensor, ldq: int, k: Tensor, k_off: int, v: Tensor, v_off: int, sb: int, sh: int, sj: int, B: int,
+                H: int, D: int, len_dev: Optional[Tensor], nkeys: int, scale: float, o: Tensor) -> None:
+    es = k.element_size()
+    L.check(L.load().cg_decode_attn(L.ptr(q), ldq, k.data_ptr() + k_off * es, v.data_ptr() + v_off * es, sb, sh, sj,
+                                    B, H, D, L.ptr(len_dev), nkeys, scale, L.ptr(o), o.stride(0), _s(q)),
+            "decode_attn")
+
+
+@_op("decode_sample", ("idx",))
+def decode_sample(logits: Tensor, greedy: bool, seed: Tensor, len_dev: Tensor, idx: Tensor) -> None:
+    B, V = logits.shape
+    L.check(L.load().cg_decode_sample(L.ptr(logits), logits.stride(0), V, B, int(greedy), L.ptr(seed),
+                                      L.ptr(len_dev), L.ptr(idx), idx.stride(0), _s(logits)), "decode_sample")
+
+
+# ---------------------------------------------------------------------------------------
 @_op("adamw", ("p", "m", "v", "p_bf16"))
 def adamw(p: Tensor, g: Tensor, m: Tensor, v: Tensor, p_bf16: Optional[Tensor], lr: float, beta1: float, beta2: float,
           eps: float, weight_decay: float, step: Tensor) -> None:
