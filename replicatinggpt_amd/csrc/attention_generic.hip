@@ -18,6 +18,9 @@
 #include "attention_common.h"
 
 using namespace cg;
+namespace cg {
+extern int g_attn_variant;
+}
 
 namespace {
 
@@ -74,6 +77,121 @@ __device__ __forceinline__ void load_rows(float* dst, int DP, const T* base, int
         const int64_t t = row0 + r;
         dst[r * DP + e] = t < T_ ? ld_as_f32<T>(base + t * ld + e) : 0.f;
     }
+}
+
+// =====================================================================================
+// fp32 MFMA forward for small heads (D <= 32, e.g. the as-shipped head_size 21), no dropout:
+// the eval / generate path of the fp32 model.  v_mfma_f32_16x16x4_f32 (exact f32 products, f32
+// accumulation).  Block = 4 waves x 16 queries; 64-key K/V tiles in LDS (zero-padded to DP4 / 32
+// columns).  S^T = K Q^T puts the query on the lane column (softmax statistics lane-local + two
+// shuffles); P^T is consumed straight from the S^T accumulator as the B operand of O^T = V^T P^T in
+// the permuted key order {4g + s} (k-step s, lane group g), V read in the same order.
+// =====================================================================================
+__device__ __forceinline__ fv4 mfma_f32x4(float a, float b, fv4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <int DP4>  // D padded to a multiple of 4 (<= 32)
+__global__ __launch_bounds__(256) void k_attn_fwd_f32mfma(int64_t T_, int H, int D, const float* __restrict__ q,
+                                                          const float* __restrict__ k, const float* __restrict__ v,
+                                                          int64_t ld, float* __restrict__ o, int64_t ldo,
+                                                          float* __restrict__ lse, float scale) {
+    constexpr int KS = DP4 / 4;           // k-steps of S^T
+    constexpr int KLD = DP4 + 1, VLD = 33;
+    __shared__ float Ks[64 * KLD];
+    __shared__ float Vs[64 * VLD];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, li = lane & 15;
+    const int bh = blockIdx.y, b = bh / H, h = bh % H;
+    const int64_t qblk0 = (int64_t)blockIdx.x * 64;
+    const int64_t qw0 = qblk0 + wave * 16;
+    const int64_t qa = qw0 + li;                       // this lane's query (S^T column)
+    const float* qb = q + (int64_t)b * T_ * ld + h * D;
+    const float* kb = k + (int64_t)b * T_ * ld + h * D;
+    const float* vb = v + (int64_t)b * T_ * ld + h * D;
+    float qf[KS];                                      // Q^T B operand: Q[qa][4t + g]
+#pragma unroll
+    for (int t = 0; t < KS; ++t) {
+        const int e = 4 * t + g;
+        qf[t] = (qa < T_ && e < D) ? qb[qa * ld + e] : 0.f;
+    }
+    fv4 oacc[2] = {fv4{0.f, 0.f, 0.f, 0.f}, fv4{0.f, 0.f, 0.f, 0.f}};
+    float m_run = -INFINITY, l_run = 0.f;
+    const int64_t qlast = (qblk0 + 63) < (T_ - 1) ? (qblk0 + 63) : (T_ - 1);
+    const int nkv = (int)(qlast / 64) + 1;
+    for (int kv = 0; kv < nkv; ++kv) {
+        const int64_t k0 = (int64_t)kv * 64;
+        __syncthreads();
+        for (int i = tid; i < 64 * 32; i += 256) {
+            const int r = i >> 5, e = i & 31;
+            const int64_t key = k0 + r;
+            const bool ok = key < T_ && e < D;
+            if (e < DP4) Ks[r * KLD + e] = ok ? kb[key * ld + e] : 0.f;
+            Vs[r * VLD + e] = ok ? vb[key * ld + e] : 0.f;
+        }
+        __syncthreads();
+        if (qw0 >= T_ || k0 > qw0 + 15) continue;      // wave past the end / tile fully masked
+        fv4 st[4];
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+            fv4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int t = 0; t < KS; ++t) c = mfma_f32x4(Ks[(16 * kt + li) * KLD + 4 * t + g], qf[t], c);
+            st[kt] = c;
+        }
+        // lane: query qa, keys k0 + 16kt + 4g + r
+        float mx = -INFINITY;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t key = k0 + 16 * kt + 4 * g + r;
+                float x = st[kt][r] * scale;
+                if (key > qa || key >= T_) x = -INFINITY;
+                st[kt][r] = x;
+                mx = fmaxf(mx, x);
+            }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float m_new = fmaxf(m_run, mx);
+        const float alpha = m_new == -INFINITY ? 1.f : expf(m_run - m_new);
+        float ps = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float p = st[kt][r] == -INFINITY ? 0.f : expf(st[kt][r] - m_new);
+                st[kt][r] = p;
+                ps += p;
+            }
+        ps += __shfl_xor(ps, 16, 64);
+        ps += __shfl_xor(ps, 32, 64);
+        l_run = l_run * alpha + ps;
+        m_run = m_new;
+        oacc[0] *= alpha;
+        oacc[1] *= alpha;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int key = 16 * kt + 4 * g + s;   // permuted order: k-step s, lane group g
+#pragma unroll
+                for (int et = 0; et < 2; ++et)
+                    oacc[et] = mfma_f32x4(Vs[key * VLD + 16 * et + li], st[kt][s], oacc[et]);
+            }
+    }
+    if (qa >= T_) return;
+    // O^T accumulator: lane holds e = 16 et + 4g + r for query qa
+    const float inv = 1.f / l_run;
+    float* orow = o + ((int64_t)b * T_ + qa) * ldo + h * D;
+#pragma unroll
+    for (int et = 0; et < 2; ++et)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int e = 16 * et + 4 * g + r;
+            if (e < D) orow[e] = oacc[et][r] * inv;
+        }
+    if (g == 0) lse[(int64_t)bh * T_ + qa] = m_run + logf(l_run);
 }
 
 template <typename T>
@@ -445,7 +563,18 @@ int attn_fwd_impl(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const v
     } else {
         dim3 grid(ceil_div(T, GB), (unsigned)(B * H));
         const size_t lds = generic_lds<float>((int)D, 3, 1);
-        if (dtype == CG_BF16)
+        if (dtype == CG_F32 && !d.thr && D <= 32 && g_attn_variant != 8) {
+            dim3 g2(ceil_div(T, 64), (unsigned)(B * H));
+#define AF(dp)                                                                                                  \
+    k_attn_fwd_f32mfma<dp><<<g2, 256, 0, st>>>(T, (int)H, (int)D, (const float*)q, (const float*)k, (const float*)v, \
+                                               ld_qkv, (float*)o, ld_o, lse, scale)
+            const int dp4 = (int)((D + 3) / 4) * 4;
+            if (dp4 <= 8) AF(8);
+            else if (dp4 <= 16) AF(16);
+            else if (dp4 <= 24) AF(24);
+            else AF(32);
+#undef AF
+        } else if (dtype == CG_BF16)
             k_attn_fwd_generic<bf16_t><<<grid, 256, lds, st>>>(T, (int)H, (int)D, (const bf16_t*)q, (const bf16_t*)k,
                                                                (const bf16_t*)v, ld_qkv, (bf16_t*)o, ld_o, lse, scale, d);
         else

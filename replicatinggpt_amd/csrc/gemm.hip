@@ -111,6 +111,119 @@ __global__ __launch_bounds__(256) void k_gemm_generic(int a_trans, int b_trans, 
             }
 }
 
+// ---------------------------------------------------------------------------------------
+// fp32 MFMA GEMM (v_mfma_f32_16x16x4_f32: exact f32 products, f32 accumulation) -- the exact
+// (dtype="fp32") model path: parity runs, the as-shipped fp32 training and generate() on
+// model.pth.  128 x 64 block tile, BK = 16, 4 waves of 64 x 32; operand tiles staged k-major in
+// LDS ([k][rows], so a fragment read is 16 consecutive floats) with the next K-tile prefetched
+// into registers during the MFMAs; any M / N / K (masked), all four layouts, split-K slabs.
+// ---------------------------------------------------------------------------------------
+constexpr int FBM = 128, FBN = 64, FBKK = 16;
+
+template <bool TR, int R>
+struct F32Tile {
+    static constexpr int PER = R * FBKK / 256;  // elements per thread
+    float v[PER];
+    __device__ __forceinline__ void load(const float* __restrict__ X, int64_t ld, int64_t r0, int64_t rmax,
+                                         int64_t k0, int64_t kmax, int tid) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int lin = tid + 256 * i;
+            int r, kk;
+            if (!TR) { kk = lin % FBKK; r = lin / FBKK; }
+            else { r = lin % R; kk = lin / R; }
+            const int64_t gr = r0 + r, gk = k0 + kk;
+            v[i] = (gr < rmax && gk < kmax) ? (TR ? X[gk * ld + gr] : X[gr * ld + gk]) : 0.f;
+        }
+    }
+    __device__ __forceinline__ void store(float* Xs, int tid) const {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int lin = tid + 256 * i;
+            int r, kk;
+            if (!TR) { kk = lin % FBKK; r = lin / FBKK; }
+            else { r = lin % R; kk = lin / R; }
+            Xs[kk * (R + 4) + r] = v[i];
+        }
+    }
+};
+
+template <bool AT, bool BT>
+__global__ __launch_bounds__(256, 2) void k_gemm_f32(int64_t M, int64_t N, int64_t K, const float* __restrict__ A,
+                                                     int64_t lda, const float* __restrict__ B, int64_t ldb,
+                                                     float* __restrict__ C, int64_t ldc, EpiArgs epi, int split_k,
+                                                     int64_t kchunk, float* __restrict__ ws) {
+    __shared__ float As[FBKK * (FBM + 4)];
+    __shared__ float Bs[FBKK * (FBN + 4)];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1, g = lane >> 4, li = lane & 15;
+    const int64_t tilesN = (N + FBN - 1) / FBN;
+    const int64_t m0 = (int64_t)(blockIdx.x / tilesN) * FBM, n0 = (int64_t)(blockIdx.x % tilesN) * FBN;
+    const int split = blockIdx.y;
+    const int64_t kb = split * kchunk, ke = kb + kchunk < K ? kb + kchunk : K;
+    fv4 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = fv4{0.f, 0.f, 0.f, 0.f};
+    F32Tile<AT, FBM> ta;
+    F32Tile<BT, FBN> tb;
+    ta.load(A, lda, m0, M, kb, ke, tid);
+    tb.load(B, ldb, n0, N, kb, ke, tid);
+    for (int64_t k0 = kb; k0 < ke; k0 += FBKK) {
+        __syncthreads();
+        ta.store(As, tid);
+        tb.store(Bs, tid);
+        __syncthreads();
+        if (k0 + FBKK < ke) {
+            ta.load(A, lda, m0, M, k0 + FBKK, ke, tid);
+            tb.load(B, ldb, n0, N, k0 + FBKK, ke, tid);
+        }
+#pragma unroll
+        for (int k4 = 0; k4 < FBKK / 4; ++k4) {
+            const int kr = 4 * k4 + g;
+            float a[4], b[2];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = As[kr * (FBM + 4) + wm * 64 + 16 * i + li];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) b[j] = Bs[kr * (FBN + 4) + wn * 32 + 16 * j + li];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    const uint64_t stream = (epi.kind == CG_EPI_BIAS_DROP_RESID && epi.thr) ? dropout_stream(epi.rng_call, epi.site) : 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t m = m0 + wm * 64 + 16 * i + 4 * g + r;
+                const int64_t n = n0 + wn * 32 + 16 * j + li;
+                if (m < M && n < N) {
+                    if (split_k > 1)
+                        ws[((int64_t)split * M + m) * N + n] = acc[i][j][r];
+                    else
+                        store_out<float>(C, m * ldc + n, epi_scalar(epi, acc[i][j][r], m, n, N, stream), epi.beta);
+                }
+            }
+}
+
+void launch_f32(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                const float* B, int64_t ldb, float* C, int64_t ldc, const EpiArgs& e, int split_k, float* ws,
+                hipStream_t st) {
+    int64_t kchunk = (K + split_k - 1) / split_k;
+    kchunk = (kchunk + FBKK - 1) / FBKK * FBKK;
+    dim3 grid((unsigned)(((M + FBM - 1) / FBM) * ((N + FBN - 1) / FBN)), (unsigned)split_k);
+#define KF(at_, bt_) k_gemm_f32<at_, bt_><<<grid, 256, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, split_k, kchunk, ws)
+    if (!a_trans && !b_trans) KF(false, false);
+    else if (!a_trans && b_trans) KF(false, true);
+    else if (a_trans && !b_trans) KF(true, false);
+    else KF(true, true);
+#undef KF
+}
+
 template <typename TC>
 __global__ void k_splitk_reduce(const float* __restrict__ ws, int split_k, int64_t M, int64_t N, TC* __restrict__ C,
                                 int64_t ldc, EpiArgs epi) {
@@ -245,6 +358,9 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
     } else if (op_dtype == CG_BF16) {
         launch_generic<bf16_t, bf16_t>(a_trans, b_trans, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k,
                                        workspace, st);
+    } else if (c_dtype == CG_F32 && g_gemm_variant != 99) {  // 99: force the generic kernel (tests)
+        launch_f32(a_trans, b_trans, M, N, K, (const float*)A, lda, (const float*)B, ldb, (float*)C, ldc, e, split_k,
+                   (float*)workspace, st);
     } else {
         launch_generic<float, float>(a_trans, b_trans, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k,
                                      workspace, st);

@@ -406,6 +406,38 @@ def test_head_fused(M, C, V):
     assert relerr(dl[:, :V], gl) < 1e-2
 
 
+@pytest.mark.parametrize("at,bt", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K,split", [(300, 126, 126, 1), (257, 378, 504, 1), (126, 504, 1000, 4), (64, 65, 33, 1)])
+def test_gemm_f32_mfma_matches_generic(at, bt, M, N, K, split):
+    """fp32 MFMA GEMM (exact path) against torch fp64 and the generic fp32 kernel, odd sizes, all
+    layouts, split-K, bias+relu epilogue."""
+    from replicatinggpt_amd import _lib as L
+    lib = L.load()
+    torch.manual_seed(12)
+    A = torch.randn(K, M) if at else torch.randn(M, K)
+    B = torch.randn(K, N) if bt else torch.randn(N, K)
+    bias = torch.randn(N)
+    ref = torch.relu(_ref_gemm(A, B, at, bt) + bias.double())
+    outs = []
+    for v in (0, 99):
+        L.check(lib.cg_set_tuning(b"gemm_variant", v))
+        try:
+            out = torch.empty(M, N, device=DEV)
+            ws = torch.empty(max(1, ops().gemm_workspace(M, N, split) // 4), device=DEV)
+            if split > 1:
+                ops().gemm(A.to(DEV), B.to(DEV), out, False, bool(at), bool(bt), M, N, K, A.shape[1], B.shape[1], N,
+                           0, None, None, 0, None, 0, 0.0, 0, None, 0, 0.0, split, ws)
+                out = torch.relu(out + bias.to(DEV))
+            else:
+                ops().gemm(A.to(DEV), B.to(DEV), out, False, bool(at), bool(bt), M, N, K, A.shape[1], B.shape[1], N,
+                           2, bias.to(DEV), None, 0, None, 0, 0.0, 0, None, 0, 0.0, 1, None)
+            torch.cuda.synchronize()
+        finally:
+            L.check(lib.cg_set_tuning(b"gemm_variant", 0))
+        outs.append(out)
+        assert relerr(out, ref) < 1e-5
+
+
 def test_adamw_matches_torch():
     n = 1000
     torch.manual_seed(8)
