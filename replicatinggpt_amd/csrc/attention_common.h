@@ -37,6 +37,15 @@ void launch_dq_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k
 void launch_dkdv_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                      const bf16_t* dout, int64_t ldd, const float* lse, const float* delta, bf16_t* dk, bf16_t* dv,
                      int64_t lddkv, float scale, const DropArgs& d, hipStream_t st);
+// whole-(b, h)-resident kernels for T % 64 == 0, T <= 256 (attention_res.hip), opt-in with
+// attn_variant bit 8
+bool res_ok(int64_t T);
+void launch_fwd_res(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
+                    bf16_t* o, int64_t ldo, float* lse, float scale, const DropArgs& d, hipStream_t st);
+void launch_bwd_res(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
+                    const bf16_t* o, int64_t ldo, const bf16_t* dout, int64_t ldd, const float* lse, bf16_t* dq,
+                    bf16_t* dk, bf16_t* dv, int64_t lddqkv, float scale, const DropArgs& d, hipStream_t st);
 }  // namespace attn
+extern int g_attn_variant;
 
 }  // namespace cg

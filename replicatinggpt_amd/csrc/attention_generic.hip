@@ -18,9 +18,6 @@
 #include "attention_common.h"
 
 using namespace cg;
-namespace cg {
-extern int g_attn_variant;
-}
 
 namespace {
 
@@ -558,8 +555,12 @@ int attn_fwd_impl(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const v
             if (!mask_ready) launch_dropmask(B, H, T, mask, d, st);
             d.mask = mask;
         }
-        attn::launch_fwd_d64(B, T, (int)H, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ld_qkv, (bf16_t*)o,
-                             ld_o, lse, scale, d, st);
+        if (attn::res_ok(T))
+            attn::launch_fwd_res(B, T, (int)H, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ld_qkv,
+                                 (bf16_t*)o, ld_o, lse, scale, d, st);
+        else
+            attn::launch_fwd_d64(B, T, (int)H, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ld_qkv,
+                                 (bf16_t*)o, ld_o, lse, scale, d, st);
     } else {
         dim3 grid(ceil_div(T, GB), (unsigned)(B * H));
         const size_t lds = generic_lds<float>((int)D, 3, 1);
@@ -625,10 +626,15 @@ extern "C" int cg_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D
             d.mask = mask;
         }
         const bf16_t *Q = (const bf16_t*)q, *K = (const bf16_t*)k, *V = (const bf16_t*)v, *DO = (const bf16_t*)dout;
-        attn::launch_dq_d64(B, T, (int)H, Q, K, V, ld_qkv, (const bf16_t*)o, ld_o, DO, ld_do, lse, delta, (bf16_t*)dq,
-                            ld_dqkv, scale, d, st);
-        attn::launch_dkdv_d64(B, T, (int)H, Q, K, V, ld_qkv, DO, ld_do, lse, delta, (bf16_t*)dk, (bf16_t*)dv, ld_dqkv,
-                              scale, d, st);
+        if (attn::res_ok(T)) {
+            attn::launch_bwd_res(B, T, (int)H, Q, K, V, ld_qkv, (const bf16_t*)o, ld_o, DO, ld_do, lse, (bf16_t*)dq,
+                                 (bf16_t*)dk, (bf16_t*)dv, ld_dqkv, scale, d, st);
+        } else {
+            attn::launch_dq_d64(B, T, (int)H, Q, K, V, ld_qkv, (const bf16_t*)o, ld_o, DO, ld_do, lse, delta,
+                                (bf16_t*)dq, ld_dqkv, scale, d, st);
+            attn::launch_dkdv_d64(B, T, (int)H, Q, K, V, ld_qkv, DO, ld_do, lse, delta, (bf16_t*)dk, (bf16_t*)dv,
+                                  ld_dqkv, scale, d, st);
+        }
     } else {
         dim3 grid(ceil_div(T, GB), (unsigned)(B * H));
         const size_t lds_dq = generic_lds<float>((int)D, 4, 1);

@@ -274,10 +274,11 @@ def test_attention_fast_matches_generic_bf16():
     assert relerr(lse_fast[0], lse) < 1e-4
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 8])
 def test_attention_fast_variants(variant):
-    """Every per-wave width of the MFMA kernels (16/32 queries, 16/32 keys) against the fp64
-    reference, at a T that leaves the 128-wide blocks partially filled."""
+    """Every per-wave width of the streaming MFMA kernels (16/32 queries, 16/32 keys) and the
+    resident-(b, h) kernels (variant 8) against the fp64 reference, at a T that leaves the
+    128-wide blocks partially filled."""
     from replicatinggpt_amd import _lib as L
     Fn = F()
     B, T, H, D, p = 2, 192, 3, 64, 0.2
