@@ -102,6 +102,14 @@ int64_t cg_layernorm_bwd_workspace(int64_t rows, int64_t C);
 int cg_layernorm_bwd(const void* dy, int dy_dtype, const float* x, const float* w, const float* mean,
                      const float* rstd, const float* dres, float* dx, uint16_t* dx_bf16, float* dw, float* db,
                      int accumulate, void* workspace, int64_t rows, int64_t C, void* stream);
+/* the same, with the consumer-side extras: lp_out = bf16(keep ? dx / (1 - p) : 0) (keep from the
+   Philox stream (lp_seed, lp_rng_call, lp_site), element idx = r*C + c; p = 0: plain bf16 copy) and
+   lp_colsum (+)= column sums of that tensor (fp32, before rounding).                              */
+int cg_layernorm_bwd_ex(const void* dy, int dy_dtype, const float* x, const float* w, const float* mean,
+                        const float* rstd, const float* dres, float* dx, uint16_t* lp_out, double lp_dropout_p,
+                        uint64_t lp_seed, const uint64_t* lp_rng_call, int lp_site, float* dw, float* db,
+                        float* lp_colsum, int accumulate, int colsum_accumulate, void* workspace, int64_t rows,
+                        int64_t C, void* stream);
 
 /* ---- GEMM (nn.Linear fwd/dgrad/wgrad: GPT1.py:111-112,121,136,143,145,184) -------------
    C[m,n] = epilogue( sum_k A(m,k) * B(n,k) )

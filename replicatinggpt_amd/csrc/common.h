@@ -17,6 +17,9 @@ void set_error(const char* fmt, ...);
 // out_b[n - S] (either output may be NULL to drop it).  Defined in util.hip.
 void launch_reduce_partials(const float* part, int64_t K, int64_t N, float* out_a, float* out_b, int64_t S,
                             int accumulate, hipStream_t st);
+// three segments of S columns: out_a, out_b (accumulate), out_c (accumulate_c)
+void launch_reduce_partials3(const float* part, int64_t K, int64_t N, float* out_a, float* out_b, float* out_c,
+                             int64_t S, int accumulate, int accumulate_c, hipStream_t st);
 }  // namespace cg
 
 #define CG_REQUIRE(cond, ...)                \

@@ -118,53 +118,87 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ x, con
 }
 
 constexpr int LN_BWD_ROWS = 64;   // rows per block in the backward
-// waves per block: 16 (1024 threads, 4 rows per wave) for the register-light specialised shapes,
-// 4 for the generic (VEC 1, NJ 32) row-in-registers variant
 
+// The consumer-side extras of the backward (the residual-stream gradient dx feeds the previous
+// sublayer's backward, GPT1.py:163-164): a bf16 copy of it with that sublayer's dropout applied
+// (FeedForward's nn.Dropout, GPT1.py:146 -- keep(idx = r*C + c) from the Philox stream, scaled), or
+// a plain bf16 copy (the attention projection's input gradient), and the column sums of that
+// tensor (the consumer's bias gradient, fp32 before rounding) -- fused here so the consumer needs
+// neither a dropout / cast pass nor a column-sum pass over it.
+struct LnLp {
+    bf16_t* out;             // NULL: no copy
+    uint32_t thr;            // dropout threshold (0: none)
+    float dscale;
+    uint64_t seed;
+    const uint64_t* rng_call;
+    int site;
+    int csum;                // 1: column sums of the copy into part columns [2C, 3C)
+};
+
+// One wave per row, RPW rows per wave with every load of the wave's rows issued before any
+// reduction (the previous loop waited a full load latency per row); row in registers as in the
+// forward.  Partials [block][NP*C]: dgamma, dbeta (+ consumer bias column sums).
 template <int VEC, int NJ, typename TDY, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ dy, const float* __restrict__ x,
                                                 const float* __restrict__ w, const float* __restrict__ mean,
                                                 const float* __restrict__ rstd, const float* __restrict__ dres,
-                                                float* __restrict__ dx, bf16_t* __restrict__ dx_lp,
-                                                float* __restrict__ part, int64_t rows, int C) {
-    extern __shared__ __attribute__((aligned(16))) float red[];  // [WAVES][2][C]
+                                                float* __restrict__ dx, LnLp lp, float* __restrict__ part,
+                                                int64_t rows, int C) {
+    constexpr int RPW = LN_BWD_ROWS / WAVES;
+    extern __shared__ __attribute__((aligned(16))) float red[];  // [WAVES][NP][C]
+    const int NP = lp.csum ? 3 : 2;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const float invC = 1.0f / (float)C;
-    float adw[NJ][VEC], adb[NJ][VEC], wv[NJ][VEC];
+    const uint64_t stream = lp.thr ? dropout_stream(lp.rng_call, lp.site) : 0;
+    float adw[NJ][VEC], adb[NJ][VEC], acs[NJ][VEC], wv[NJ][VEC];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
         const int e = (j * 64 + lane) * VEC;
 #pragma unroll
-        for (int q = 0; q < VEC; ++q) adw[j][q] = adb[j][q] = 0.f;
+        for (int q = 0; q < VEC; ++q) adw[j][q] = adb[j][q] = acs[j][q] = 0.f;
         if (e < C) VecIO<VEC>::ld(w + e, wv[j]);
         else {
 #pragma unroll
             for (int q = 0; q < VEC; ++q) wv[j][q] = 0.f;
         }
     }
-    const int64_t r0 = (int64_t)blockIdx.x * LN_BWD_ROWS;
-    for (int i = wave; i < LN_BWD_ROWS; i += WAVES) {
+    const int64_t r0 = (int64_t)blockIdx.x * LN_BWD_ROWS + wave * RPW;
+    float xv[RPW][NJ][VEC], d[RPW][NJ][VEC], rv[RPW][NJ][VEC];
+    float mu[RPW], rs[RPW];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+        const int64_t r = r0 + i < rows ? r0 + i : rows - 1;
+        mu[i] = mean[r];
+        rs[i] = rstd[r];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int e = (j * 64 + lane) * VEC;
+            if (e < C) {
+                VecIO<VEC>::ld(x + r * C + e, xv[i][j]);
+                ld_vec_any<TDY>(dy + r * C + e, d[i][j], VEC);
+                if (dres) VecIO<VEC>::ld(dres + r * C + e, rv[i][j]);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
         const int64_t r = r0 + i;
         if (r >= rows) break;
-        const float mu = mean[r], rs = rstd[r];
-        float xh[NJ][VEC], g[NJ][VEC], d[NJ][VEC];
+        float xh[NJ][VEC], g[NJ][VEC];
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int e = (j * 64 + lane) * VEC;
             if (e < C) {
-                float xv[VEC];
-                VecIO<VEC>::ld(x + r * C + e, xv);
-                ld_vec_any<TDY>(dy + r * C + e, d[j], VEC);
 #pragma unroll
                 for (int q = 0; q < VEC; ++q) {
-                    xh[j][q] = (xv[q] - mu) * rs;
-                    g[j][q] = d[j][q] * wv[j][q];
+                    xh[j][q] = (xv[i][j][q] - mu[i]) * rs[i];
+                    g[j][q] = d[i][j][q] * wv[j][q];
                     s1 += g[j][q];
                     s2 += g[j][q] * xh[j][q];
-                    adw[j][q] += d[j][q] * xh[j][q];
-                    adb[j][q] += d[j][q];
+                    adw[j][q] += d[i][j][q] * xh[j][q];
+                    adb[j][q] += d[i][j][q];
                 }
             }
         }
@@ -174,15 +208,32 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
         for (int j = 0; j < NJ; ++j) {
             const int e = (j * 64 + lane) * VEC;
             if (e < C) {
-                float o[VEC], rv[VEC];
-                if (dres) VecIO<VEC>::ld(dres + r * C + e, rv);
+                float o[VEC];
 #pragma unroll
                 for (int q = 0; q < VEC; ++q) {
-                    o[q] = rs * (g[j][q] - c1 - xh[j][q] * c2);
-                    if (dres) o[q] += rv[q];
+                    o[q] = rs[i] * (g[j][q] - c1 - xh[j][q] * c2);
+                    if (dres) o[q] += rv[i][j][q];
                 }
                 VecIO<VEC>::st(dx + r * C + e, o);
-                if (dx_lp) VecIO<VEC>::st(dx_lp + r * C + e, o);
+                if (lp.out) {
+                    float z[VEC];
+                    if (lp.thr) {
+                        const uint64_t idx = (uint64_t)r * (uint64_t)C + (uint64_t)e;
+                        u32x4 ph = philox_group(lp.seed, stream, idx >> 2);
+#pragma unroll
+                        for (int q = 0; q < VEC; ++q) {
+                            const uint64_t iq = idx + q;
+                            if (q > 0 && (iq & 3) == 0) ph = philox_group(lp.seed, stream, iq >> 2);
+                            z[q] = philox_word(ph, (int)(iq & 3)) >= lp.thr ? o[q] * lp.dscale : 0.f;
+                        }
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < VEC; ++q) z[q] = o[q];
+                    }
+                    VecIO<VEC>::st(lp.out + r * C + e, z);
+#pragma unroll
+                    for (int q = 0; q < VEC; ++q) acs[j][q] += z[q];
+                }
             }
         }
     }
@@ -193,17 +244,18 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
         if (e < C) {
 #pragma unroll
             for (int q = 0; q < VEC; ++q) {
-                red[(wave * 2 + 0) * C + e + q] = adw[j][q];
-                red[(wave * 2 + 1) * C + e + q] = adb[j][q];
+                red[(wave * NP + 0) * C + e + q] = adw[j][q];
+                red[(wave * NP + 1) * C + e + q] = adb[j][q];
+                if (NP == 3) red[(wave * NP + 2) * C + e + q] = acs[j][q];
             }
         }
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) {
+    for (int c = threadIdx.x; c < NP * C; c += blockDim.x) {
         const int which = c / C, e = c % C;
         float s = 0.f;
-        for (int wv2 = 0; wv2 < WAVES; ++wv2) s += red[(wv2 * 2 + which) * C + e];
-        part[(int64_t)blockIdx.x * 2 * C + c] = s;
+        for (int wv2 = 0; wv2 < WAVES; ++wv2) s += red[(wv2 * NP + which) * C + e];
+        part[(int64_t)blockIdx.x * NP * C + c] = s;
     }
 }
 
@@ -226,21 +278,22 @@ int launch_ln_fwd(const float* x, const float* w, const float* b, TY* y, float* 
 
 template <typename TDY>
 int launch_ln_bwd(const TDY* dy, const float* x, const float* w, const float* mean, const float* rstd,
-                  const float* dres, float* dx, bf16_t* dx_lp, float* dw, float* db, int accumulate, float* part,
-                  int64_t rows, int C, hipStream_t st) {
+                  const float* dres, float* dx, const LnLp& lp, float* dw, float* db, float* dbias, int accumulate,
+                  int dbias_accumulate, float* part, int64_t rows, int C, hipStream_t st) {
     const bool al16 = (((uintptr_t)x | (uintptr_t)w | (uintptr_t)dx | (uintptr_t)(dres ? dres : x)) & 15) == 0 &&
-                      (((uintptr_t)dy) & 7) == 0;
+                      (((uintptr_t)dy) & 7) == 0 && (((uintptr_t)(lp.out ? lp.out : (bf16_t*)x)) & 7) == 0;
     const int64_t nblk = (rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
-#define LNB(V, N, W)                                                                                    \
-    k_ln_bwd<V, N, TDY, W><<<(unsigned)nblk, 64 * W, (size_t)2 * W * C * sizeof(float), st>>>(dy, x, w, mean, rstd, \
-                                                                                            dres, dx, dx_lp, part, rows, C)
+    const int NP = lp.csum ? 3 : 2;
+#define LNB(V, N, W)                                                                                         \
+    k_ln_bwd<V, N, TDY, W><<<(unsigned)nblk, 64 * W, (size_t)NP * W * C * sizeof(float), st>>>(dy, x, w, mean, rstd, \
+                                                                                             dres, dx, lp, part, rows, C)
     if (C == 384 && al16) LNB(2, 3, 16);
     else if (C == 768 && al16) LNB(4, 3, 16);
     else if (C == 512 && al16) LNB(4, 2, 16);
     else if (C == 1024 && al16) LNB(4, 4, 8);
     else LNB(1, 32, 4);
 #undef LNB
-    if (dw || db) launch_reduce_partials(part, nblk, 2 * C, dw, db, C, accumulate, st);
+    if (dw || db || dbias) launch_reduce_partials3(part, nblk, NP * C, dw, db, dbias, C, accumulate, dbias_accumulate, st);
     return CG_OK;
 }
 }  // namespace
@@ -256,20 +309,39 @@ extern "C" int cg_layernorm_fwd(const float* x, const float* w, const float* b, 
 }
 
 extern "C" int64_t cg_layernorm_bwd_workspace(int64_t rows, int64_t C) {
-    return ((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS) * 2 * C * (int64_t)sizeof(float);
+    return ((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS) * 3 * C * (int64_t)sizeof(float);
+}
+
+extern "C" int cg_layernorm_bwd_ex(const void* dy, int dy_dtype, const float* x, const float* w, const float* mean,
+                                   const float* rstd, const float* dres, float* dx, uint16_t* lp_out,
+                                   double lp_dropout_p, uint64_t lp_seed, const uint64_t* lp_rng_call, int lp_site,
+                                   float* dw, float* db, float* lp_colsum, int accumulate, int colsum_accumulate,
+                                   void* workspace, int64_t rows, int64_t C, void* stream) {
+    CG_REQUIRE(rows > 0 && C > 0 && C <= 1024, "cg_layernorm_bwd: need 0 < C <= 1024");
+    CG_REQUIRE(lp_dropout_p >= 0 && lp_dropout_p < 1, "cg_layernorm_bwd_ex: dropout p must be in [0, 1)");
+    CG_REQUIRE(!lp_colsum || lp_out, "cg_layernorm_bwd_ex: lp_colsum needs lp_out");
+    hipStream_t st = (hipStream_t)stream;
+    LnLp lp;
+    lp.out = (bf16_t*)lp_out;
+    lp.thr = lp_dropout_p > 0 ? dropout_threshold(lp_dropout_p) : 0u;
+    lp.dscale = lp_dropout_p > 0 ? dropout_scale(lp_dropout_p) : 1.f;
+    lp.seed = lp_seed;
+    lp.rng_call = lp_rng_call;
+    lp.site = lp_site;
+    lp.csum = lp_colsum != nullptr;
+    if (dy_dtype == CG_BF16)
+        launch_ln_bwd<bf16_t>((const bf16_t*)dy, x, w, mean, rstd, dres, dx, lp, dw, db, lp_colsum, accumulate,
+                              colsum_accumulate, (float*)workspace, rows, (int)C, st);
+    else
+        launch_ln_bwd<float>((const float*)dy, x, w, mean, rstd, dres, dx, lp, dw, db, lp_colsum, accumulate,
+                             colsum_accumulate, (float*)workspace, rows, (int)C, st);
+    CG_LAUNCH_CHECK("cg_layernorm_bwd");
+    return CG_OK;
 }
 
 extern "C" int cg_layernorm_bwd(const void* dy, int dy_dtype, const float* x, const float* w, const float* mean,
                                 const float* rstd, const float* dres, float* dx, uint16_t* dx_bf16, float* dw,
                                 float* db, int accumulate, void* workspace, int64_t rows, int64_t C, void* stream) {
-    CG_REQUIRE(rows > 0 && C > 0 && C <= 1024, "cg_layernorm_bwd: need 0 < C <= 1024");
-    hipStream_t st = (hipStream_t)stream;
-    if (dy_dtype == CG_BF16)
-        launch_ln_bwd<bf16_t>((const bf16_t*)dy, x, w, mean, rstd, dres, dx, (bf16_t*)dx_bf16, dw, db, accumulate,
-                              (float*)workspace, rows, (int)C, st);
-    else
-        launch_ln_bwd<float>((const float*)dy, x, w, mean, rstd, dres, dx, (bf16_t*)dx_bf16, dw, db, accumulate,
-                             (float*)workspace, rows, (int)C, st);
-    CG_LAUNCH_CHECK("cg_layernorm_bwd");
-    return CG_OK;
+    return cg_layernorm_bwd_ex(dy, dy_dtype, x, w, mean, rstd, dres, dx, dx_bf16, 0.0, 0, nullptr, 0, dw, db, nullptr,
+                               accumulate, 0, workspace, rows, C, stream);
 }

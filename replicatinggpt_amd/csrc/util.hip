@@ -116,10 +116,12 @@ extern "C" int cg_dropout_apply(const float* x, int64_t rows, int64_t C, int64_t
 }
 
 // --------------------------------------------------------------------------------------
-// column reduction of per-block partials: 32 columns x 8 k-lanes per block, 8 loads in flight
+// column reduction of per-block partials: 32 columns x 8 k-lanes per block, 8 loads in flight.
+// Column n goes to out_a[n] (n < S), out_b[n - S] (n < 2S) or out_c[n - 2S]; NULL drops it.
 __global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict__ part, int64_t K, int64_t N,
                                                          float* __restrict__ out_a, float* __restrict__ out_b,
-                                                         int64_t S, int accumulate) {
+                                                         float* __restrict__ out_c, int64_t S, int accumulate,
+                                                         int accumulate_c) {
     __shared__ float red[8][33];
     const int c = threadIdx.x & 31, kl = threadIdx.x >> 5;
     const int64_t n = (int64_t)blockIdx.x * 32 + c;
@@ -141,19 +143,29 @@ __global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict
         float t = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) t += red[j][c];
-        float* dst = n < S ? (out_a ? out_a + n : nullptr) : (out_b ? out_b + (n - S) : nullptr);
-        if (dst) *dst = accumulate ? *dst + t : t;
+        float* dst;
+        int acc = accumulate;
+        if (n < S) dst = out_a ? out_a + n : nullptr;
+        else if (n < 2 * S) dst = out_b ? out_b + (n - S) : nullptr;
+        else {
+            dst = out_c ? out_c + (n - 2 * S) : nullptr;
+            acc = accumulate_c;
+        }
+        if (dst) *dst = acc ? *dst + t : t;
     }
 }
 
 namespace cg {
 void launch_reduce_partials(const float* part, int64_t K, int64_t N, float* out_a, float* out_b, int64_t S,
                             int accumulate, hipStream_t st) {
-    k_reduce_partials<<<ceil_div(N, 32), 256, 0, st>>>(part, K, N, out_a, out_b, S, accumulate);
+    k_reduce_partials<<<ceil_div(N, 32), 256, 0, st>>>(part, K, N, out_a, out_b, nullptr, S, accumulate, 0);
+}
+void launch_reduce_partials3(const float* part, int64_t K, int64_t N, float* out_a, float* out_b, float* out_c,
+                             int64_t S, int accumulate, int accumulate_c, hipStream_t st) {
+    k_reduce_partials<<<ceil_div(N, 32), 256, 0, st>>>(part, K, N, out_a, out_b, out_c, S, accumulate, accumulate_c);
 }
 }  // namespace cg
 
-// --------------------------------------------------------------------------------------
 // deterministic two-pass sum: pass 1 -> one partial per block (fixed order), pass 2 one block
 __global__ void k_sum_partial(const float* x, int64_t n, float* part) {
     __shared__ float red[16];

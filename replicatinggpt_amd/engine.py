@@ -117,6 +117,9 @@ class TrainStep:
         def grab(j):
             def hook(mod, args):
                 leaf = args[0].detach().requires_grad_(True)
+                link = getattr(args[0], "_charpt_link", None)
+                if link is not None:   # the fused gradient hand-off (functional.GradLink) spans the cut
+                    leaf._charpt_link = link
                 xs[j] = (args[0], leaf)
                 return (leaf,) + tuple(args[1:])
             return hook

@@ -222,16 +222,56 @@ def layernorm(x2, w, b, out_dtype, eps=1e-5):
     return y, mean, rstd
 
 
-def layernorm_bwd(dy2, x2, w_reg, b_reg, mean, rstd, dres=None, want_lp=False):
-    """dx (fp32) = dres + LN'(dy); LN weight/bias grads into their regions."""
+class GradLink:
+    """What a sublayer's backward wants for its incoming residual-stream gradient (GPT1.py:163-164:
+    the gradient of x + f(x) arrives at f as-is): a bf16 copy with the sublayer's output dropout
+    applied (FeedForward, GPT1.py:146) or plain (the attention projection), plus that tensor's
+    column sums as the sublayer's output-bias gradient.  Created in the sublayer's forward and
+    attached to its output tensor; the NEXT sublayer's forward picks it up from its input and its
+    LayerNorm backward -- the kernel that produces the gradient -- fills it (cg_layernorm_bwd_ex),
+    so the consumer skips its dropout / cast and column-sum passes.  The consumer uses the copy only
+    if its gradient is the exact buffer the producer wrote (data_ptr check), else recomputes."""
+    __slots__ = ("p", "seed", "rng_call", "site", "bias", "act", "lp", "dx_ptr", "bias_done")
+
+    def __init__(self, p, seed, rng_call, site, bias, act):
+        self.p, self.seed, self.rng_call, self.site, self.bias, self.act = p, seed, rng_call, site, bias, act
+        self.lp, self.dx_ptr, self.bias_done = None, None, False
+
+    def take(self, d32):
+        ok = self.lp is not None and self.dx_ptr == d32.data_ptr()
+        lp, done = (self.lp, self.bias_done) if ok else (None, False)
+        self.lp, self.dx_ptr, self.bias_done = None, None, False
+        return lp, done
+
+
+def _link_of(x):
+    return getattr(x, "_charpt_link", None)
+
+
+def layernorm_bwd(dy2, x2, w_reg, b_reg, mean, rstd, dres=None, want_lp=False, link=None):
+    """dx (fp32) = dres + LN'(dy); LN weight/bias grads into their regions.  ``link``: the
+    consumer of dx (GradLink) -- its bf16 (dropout-applied) copy and bias column sums are produced
+    in the same kernel."""
     rows, C = x2.shape
-    dx = torch.empty((rows, C), dtype=torch.float32, device=x2.device)
-    dx_lp = torch.empty((rows, C), dtype=torch.bfloat16, device=x2.device) if want_lp else None
+    dev = x2.device
+    dx = torch.empty((rows, C), dtype=torch.float32, device=dev)
+    use_link = link is not None and link.act == torch.bfloat16
+    lp = torch.empty((rows, C), dtype=torch.bfloat16, device=dev) if (want_lp or use_link) else None
     gw, bw, fw = w_reg.grad_target()
     gb, bb, fb = b_reg.grad_target()
-    ws = torch.empty(ops.layernorm_bwd_workspace(rows, C) // 4 + 1, dtype=torch.float32, device=x2.device)
-    ops.layernorm_bwd(dy2, x2, w_reg.master, mean, rstd, dres, dx, dx_lp, gw, gb, bool(bw or bb), ws)
-    return dx, dx_lp, fw() + fb()
+    gcs, bcs, fcs = None, 0.0, None
+    if use_link and link.bias is not None and link.bias.slot is not None:
+        gcs, bcs, fcs = link.bias.grad_target()
+    ws = torch.empty(ops.layernorm_bwd_workspace(rows, C) // 4 + 1, dtype=torch.float32, device=dev)
+    p = float(link.p) if use_link else 0.0
+    ops.layernorm_bwd(dy2, x2, w_reg.master, mean, rstd, dres, dx, lp, gw, gb, bool(bw or bb), ws, gcs, bool(bcs), p,
+                      int(link.seed) if use_link else 0, link.rng_call if (use_link and p > 0) else None,
+                      int(link.site) if use_link else 0)
+    if use_link:
+        link.lp, link.dx_ptr, link.bias_done = lp, dx.data_ptr(), gcs is not None
+        if fcs is not None:
+            fcs()
+    return dx, (lp if want_lp and not use_link else None), fw() + fb()
 
 
 def attention_fwd(qkv, B, T, H, D, out, scale, p, seed, rng_call, site, premask=None):
@@ -348,7 +388,11 @@ class AttnSublayerFn(torch.autograd.Function):
         linear_fwd(o, proj_w.operand(act), out, "bias_resid", bias=proj_b.master, resid=x2)
         ctx.save_for_backward(x2, a, mean, rstd, qkv, o, lse)
         ctx.lc, ctx.regs, ctx.shape = lc, (ln_w, ln_b, qkv_w, proj_w, proj_b), (B, T, C)
-        return out.view(B, T, C)
+        ctx.in_link = _link_of(x)
+        ctx.link = GradLink(0.0, 0, None, 0, proj_b, act)
+        out_v = out.view(B, T, C)
+        out_v._charpt_link = ctx.link
+        return out_v
 
     @staticmethod
     def backward(ctx, dout):
@@ -358,15 +402,17 @@ class AttnSublayerFn(torch.autograd.Function):
         B, T, C = ctx.shape
         act = lc.act
         d32 = dout.reshape(B * T, C).contiguous()
-        dy = to_act(d32, act)
+        dy, bias_done = ctx.link.take(d32)
+        if dy is None:
+            dy = to_act(d32, act)
         dev = x2.device
-        # proj: dW = dy^T o, db = colsum(dy) (side stream), do = dy W (critical path)
+        # proj: dW = dy^T o, db = colsum(dy) (side stream, unless fused upstream), do = dy W
         g_pw, beta_pw, f_pw = proj_w.grad_target()
         g_pb, beta_pb, f_pb = proj_b.grad_target()
         with SIDE.run(dev, dy, o):
             if g_pw is not None:
                 linear_wgrad(dy, o, g_pw, beta_pw)
-            if g_pb is not None:
+            if g_pb is not None and not bias_done:
                 colsum_into(dy, g_pb, beta_pb)
         do = torch.empty((B * T, C), dtype=act, device=x2.device)
         linear_dgrad(dy, proj_w.operand(act), do)
@@ -378,7 +424,7 @@ class AttnSublayerFn(torch.autograd.Function):
                 linear_wgrad(dqkv, a, g, beta)
         da = torch.empty((B * T, C), dtype=act, device=x2.device)
         linear_dgrad(dqkv, qkv_w.operand(act), da)
-        dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd, dres=d32)
+        dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd, dres=d32, link=ctx.in_link)
         return (dx.view(B, T, C), None, None, None, None, None, None, *f_ln, *f_qkv(), *f_pw(), *f_pb())
 
 
@@ -399,7 +445,11 @@ class FFNSublayerFn(torch.autograd.Function):
                    seed=lc.seed, rng_call=lc.rng_call, site=lc.site)
         ctx.save_for_backward(x2, a, mean, rstd, h)
         ctx.lc, ctx.regs, ctx.shape = lc, (ln_w, ln_b, w1, b1, w2, b2), (B, T, C)
-        return out.view(B, T, C)
+        ctx.in_link = _link_of(x)
+        ctx.link = GradLink(lc.p, lc.seed, lc.rng_call, lc.site, b2, act)
+        out_v = out.view(B, T, C)
+        out_v._charpt_link = ctx.link
+        return out_v
 
     @staticmethod
     def backward(ctx, dout):
@@ -409,15 +459,17 @@ class FFNSublayerFn(torch.autograd.Function):
         B, T, C = ctx.shape
         act = lc.act
         d32 = dout.reshape(B * T, C).contiguous()
-        dz2 = torch.empty((B * T, C), dtype=act, device=x2.device)
-        ops.dropout_apply(d32, dz2, float(lc.p), int(lc.seed), lc.rng_call, int(lc.site))
+        dz2, bias_done = ctx.link.take(d32)
+        if dz2 is None:
+            dz2 = torch.empty((B * T, C), dtype=act, device=x2.device)
+            ops.dropout_apply(d32, dz2, float(lc.p), int(lc.seed), lc.rng_call, int(lc.site))
         dev = x2.device
         g_w2, beta_w2, f_w2 = w2.grad_target()
         g_b2, beta_b2, f_b2 = b2.grad_target()
         with SIDE.run(dev, dz2, h):
             if g_w2 is not None:
                 linear_wgrad(dz2, h, g_w2, beta_w2)
-            if g_b2 is not None:
+            if g_b2 is not None and not bias_done:
                 colsum_into(dz2, g_b2, beta_b2)
         dz1 = torch.empty_like(h)
         linear_dgrad(dz2, w2.operand(act), dz1, "relu_bwd", aux=h)
@@ -430,7 +482,7 @@ class FFNSublayerFn(torch.autograd.Function):
                 colsum_into(dz1, g_b1, beta_b1)
         da = torch.empty((B * T, C), dtype=act, device=x2.device)
         linear_dgrad(dz1, w1.operand(act), da)
-        dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd, dres=d32)
+        dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd, dres=d32, link=ctx.in_link)
         return (dx.view(B, T, C), None, None, None, None, None, None, None, *f_ln, *f_w1(), *f_b1(), *f_w2(),
                 *f_b2())
 
@@ -446,6 +498,7 @@ class HeadLossFn(torch.autograd.Function):
         a, mean, rstd = layernorm(x2, ln_w.master, ln_b.master, act)
         V = lm_w.master.shape[0]
         ctx.fused = _head_fused_ok(act, lm_w, M, C, V)
+        ctx.in_link = _link_of(x)
         if ctx.fused:
             return HeadLossFn._fused_forward(ctx, x, x2, targets, act, a, mean, rstd, (ln_w, ln_b, lm_w, lm_b))
         logits = torch.empty((M, V), dtype=torch.float32, device=x.device)
@@ -499,7 +552,7 @@ class HeadLossFn(torch.autograd.Function):
             colsum_into(dl, g, beta)
         da = torch.empty((M, C), dtype=act, device=x2.device)
         linear_dgrad(dl_op, lm_w.operand(act), da)
-        dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd)
+        dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd, link=ctx.in_link)
         return (dx.view(B, T, C), None, None, None, None, None, None, *f_ln, *f_lw(), *f_lb())
 
     # -- bf16 fast path: cg_head_fwd/bwd + K-padded MFMA GEMMs (csrc/head.hip) -------------
@@ -555,7 +608,7 @@ class HeadLossFn(torch.autograd.Function):
                     g.copy_(tmp[:V])
         da = torch.empty((M, C), dtype=torch.bfloat16, device=x2.device)
         linear_dgrad(dl, wpad, da)
-        dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd)
+        dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd, link=ctx.in_link)
         return (dx.view(B, T, C), None, None, None, None, None, None, *f_ln, *f_lw(), *f_lb())
 
 

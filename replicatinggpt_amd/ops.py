@@ -96,15 +96,20 @@ def layernorm_fwd(x: Tensor, w: Tensor, b: Tensor, y: Tensor, mean: Tensor, rstd
                                       L.ptr(rstd), rows, C, eps, _s(x)), "layernorm_fwd")
 
 
-@_op("layernorm_bwd", ("dx", "dx_lp", "dw", "db", "ws"))
+@_op("layernorm_bwd", ("dx", "dx_lp", "dw", "db", "ws", "lp_colsum"))
 def layernorm_bwd(dy: Tensor, x: Tensor, w: Tensor, mean: Tensor, rstd: Tensor, dres: Optional[Tensor], dx: Tensor,
                   dx_lp: Optional[Tensor], dw: Optional[Tensor], db: Optional[Tensor], accumulate: bool,
-                  ws: Tensor) -> None:
+                  ws: Tensor, lp_colsum: Optional[Tensor], colsum_accumulate: bool, lp_p: float, lp_seed: int,
+                  lp_rng_call: Optional[Tensor], lp_site: int) -> None:
+    # (no defaults: torch.library drops trailing default-valued arguments from the boxed call, which
+    #  would hide a mutated argument from its version-counter bookkeeping)
     C = x.shape[-1]
     rows = x.numel() // C
-    L.check(L.load().cg_layernorm_bwd(L.ptr(dy), L.dtype_code(dy.dtype), L.ptr(x), L.ptr(w), L.ptr(mean), L.ptr(rstd),
-                                      L.ptr(dres), L.ptr(dx), L.ptr(dx_lp), L.ptr(dw), L.ptr(db), int(accumulate),
-                                      L.ptr(ws), rows, C, _s(x)), "layernorm_bwd")
+    L.check(L.load().cg_layernorm_bwd_ex(L.ptr(dy), L.dtype_code(dy.dtype), L.ptr(x), L.ptr(w), L.ptr(mean),
+                                         L.ptr(rstd), L.ptr(dres), L.ptr(dx), L.ptr(dx_lp), lp_p, lp_seed,
+                                         L.ptr(lp_rng_call), lp_site, L.ptr(dw), L.ptr(db), L.ptr(lp_colsum),
+                                         int(accumulate), int(colsum_accumulate), L.ptr(ws), rows, C, _s(x)),
+            "layernorm_bwd")
 
 
 def layernorm_bwd_workspace(rows, C):
