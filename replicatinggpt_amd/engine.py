@@ -153,9 +153,47 @@ class TrainStep:
         return loss
 
     # -- capture ------------------------------------------------------------------------------
-    def capture(self, warmup=2):
+    def capture(self, warmup=2, restore=False):
+        """Run ``warmup`` eager steps (allocator, kernels) and capture the step graph(s).
+        restore=True rolls the warm-up steps back afterwards -- weights, AdamW moments and step,
+        the dropout-call counter and the CPU generator get_batch draws from -- so the first replayed
+        step is the step an eager loop would take next (the GPT1 driver needs this: its loss curve
+        starts from the reference's state)."""
         if not self.use_graph:
             return
+        saved = self._save_state() if restore else None
+        try:
+            self._capture(warmup)
+        finally:
+            if saved is not None:
+                self._restore_state(saved)
+
+    def _save_state(self):
+        st, opt = self.model.flat, self.opt
+        opt._ensure()
+        gen = self.sampler.generator
+        return {"master": st.master.detach().clone(), "m": opt._m.clone(), "v": opt._v.clone(),
+                "step": opt._step_t.clone(), "counter": self.model._rng_counter.clone(),
+                "rng": gen.get_state() if gen is not None else torch.get_rng_state()}
+
+    def _restore_state(self, s):
+        torch.cuda.synchronize()
+        st, opt = self.model.flat, self.opt
+        with torch.no_grad():
+            st.master.copy_(s["master"])
+            opt._m.copy_(s["m"])
+            opt._v.copy_(s["v"])
+            opt._step_t.copy_(s["step"])
+            self.model._rng_counter.copy_(s["counter"])
+        st.refresh_shadow()
+        gen = self.sampler.generator
+        if gen is not None:
+            gen.set_state(s["rng"])
+        else:
+            torch.set_rng_state(s["rng"])
+        torch.cuda.synchronize()
+
+    def _capture(self, warmup):
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -222,3 +260,42 @@ class TrainStep:
             self.reducer.all_reduce()
             self.g_opt.replay()
         return self.loss
+
+
+class Evaluator:
+    """The forward of estimate_loss (GPT1.py:92-93) replayed from one hipGraph: get_batch writes
+    the batch into static buffers, the replay computes the mean loss into a static scalar.  Built
+    on first use, in whatever mode the model is in then -- estimate_loss calls it in eval mode with
+    autograd off (GPT1.py:85,88)."""
+
+    def __init__(self, model, sampler, use_graph=True):
+        self.model, self.sampler = model, sampler
+        dev = model.flat.master.device
+        self.x = torch.empty((sampler.B, sampler.T), dtype=torch.int64, device=dev)
+        self.y = torch.empty_like(self.x)
+        self.use_graph = use_graph and dev.type == "cuda"
+        self.graph = None
+        self.out = None
+
+    def _forward(self):
+        _, loss = self.model(self.x, self.y)
+        return loss
+
+    @torch.no_grad()
+    def loss(self, split):
+        """Draw a batch of ``split`` (one get_batch, as GPT1.py:92) and return its mean loss as a
+        device scalar (valid until the next call)."""
+        self.sampler.get_batch(split, out=(self.x, self.y))
+        if not self.use_graph:
+            return self._forward()
+        if self.graph is None:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                self._forward()                 # warm-up on this batch; the replay recomputes it
+            torch.cuda.current_stream().wait_stream(s)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.out = self._forward()
+        self.graph.replay()
+        return self.out

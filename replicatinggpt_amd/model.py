@@ -280,6 +280,8 @@ class FlatStore:
                         m._parameters[a] = newp
                 else:
                     newp = old
+                if isinstance(newp, nn.Parameter):
+                    newp._charpt_store = self   # lets optim.AdamW find the flat buffers
                 parts.append((newp, po))
                 po += old.numel()
             padded = None
@@ -487,8 +489,11 @@ class BigramLanguageModel(nn.Module):
         (decode.DecodeEngine: K/V-cached prefix phase, sliding-window phase, device sampling, one
         hipGraph per phase); ``greedy=True`` takes the argmax (the parity mode).  Sampled draws use
         a seed taken from ``generator`` (torch's CPU multinomial stream is not reproducible on a
-        GPU).  ``engine=False`` runs the reference's loop literally (one full forward per token)."""
-        if engine and idx.device.type == "cuda" and max_new_tokens > 0:
+        GPU).  ``engine=False`` runs the reference's loop literally (one full forward per token); so
+        does a model in train mode with dropout on, as GPT1.py:235-236 calls it: the
+        engine computes the eval-mode forward only."""
+        dropout_on = self.training and self.config.dropout > 0
+        if engine and not dropout_on and idx.device.type == "cuda" and max_new_tokens > 0:
             from .decode import DecodeEngine
             B, L0 = idx.shape
             key = (B, L0 + max_new_tokens, bool(greedy), idx.device)

@@ -19,21 +19,22 @@ class AdamW(torch.optim.Optimizer):
         self._m = self._v = None
         self._step_t = None
 
-    # the model whose flat store holds these parameters is discovered lazily (after .to())
+    # the model whose flat store holds these parameters is found from the parameters, so
+    # ``AdamW(m.parameters(), lr=5e-1)`` works exactly as GPT1.py:218 writes it
     def _find_store(self):
-        from .model import BigramLanguageModel  # noqa: F401  (type only)
-        ps = [p for g in self.param_groups for p in g["params"]]
-        root = None
-        for p in ps:
-            st = getattr(p, "_charpt_store", None)
-            if st is not None:
-                root = st
-                break
-        return root, ps
+        for g in self.param_groups:
+            for p in g["params"]:
+                st = getattr(p, "_charpt_store", None)
+                if st is not None:
+                    return st
+        return None
 
-    def attach(self, model):
-        """Bind to a BigramLanguageModel's flat storage (call once after model.to(device))."""
-        st = model.flat
+    def attach(self, model=None):
+        """Bind to a BigramLanguageModel's flat storage (found from the parameters when ``model``
+        is None).  The optimizer must own exactly that model's parameters, in one group."""
+        st = model.flat if model is not None else self._find_store()
+        if st is None:
+            raise RuntimeError("charpt AdamW: the parameters do not belong to a charpt BigramLanguageModel")
         ids = {id(p) for g in self.param_groups for p in g["params"]}
         if {id(p) for p in st.params()} != ids or len(self.param_groups) != 1:
             raise ValueError("charpt AdamW: the optimizer must own exactly the model's parameters in one group")
@@ -45,7 +46,7 @@ class AdamW(torch.optim.Optimizer):
 
     def _ensure(self):
         if self._store is None:
-            raise RuntimeError("charpt AdamW: call .attach(model) before step()")
+            self.attach()
         st = self._store
         if self._m.device != st.master.device:
             self._m = self._m.to(st.master.device)
@@ -87,18 +88,57 @@ class AdamW(torch.optim.Optimizer):
         st._shadow_version = st.version()
         return loss
 
-    def state_dict(self):
-        sd = super().state_dict()
-        sd["charpt"] = {"m": self._m, "v": self._v, "step": self._step_t}
-        return sd
+    # -- checkpoints: torch.optim.AdamW's own state-dict layout ------------------------------
+    def _param_slices(self):
+        """(index in the group, parameter, element offset in the flat buffers) per parameter."""
+        st = self._store
+        base = st.master.data_ptr()
+        for i, p in enumerate(self.param_groups[0]["params"]):
+            yield i, p, (p.data_ptr() - base) // st.master.element_size()
 
-    def load_state_dict(self, sd):
-        extra = sd.get("charpt") if isinstance(sd, dict) else None
-        if extra is not None:
-            sd = {k: v for k, v in sd.items() if k != "charpt"}
-        super().load_state_dict(sd)
-        if extra is not None:
-            self._ensure()
-            self._m.copy_(extra["m"])
-            self._v.copy_(extra["v"])
-            self._step_t.copy_(extra["step"])
+    def state_dict(self):
+        """``{"state": {i: {step, exp_avg, exp_avg_sq}}, "param_groups": [...]}`` exactly as
+        torch.optim.AdamW writes it, so optimizer state moves between the two in either direction.
+        Like torch, no per-parameter entries exist before the first step."""
+        self._ensure()
+        grp = self.param_groups[0]
+        groups = [{"lr": grp["lr"], "betas": tuple(grp["betas"]), "eps": grp["eps"],
+                   "weight_decay": grp["weight_decay"], "amsgrad": False, "maximize": False, "foreach": None,
+                   "capturable": False, "differentiable": False, "fused": None, "decoupled_weight_decay": True,
+                   "params": list(range(len(grp["params"])))}]
+        state = {}
+        step = int(self._step_t.item())
+        if step > 0:
+            for i, p, off in self._param_slices():
+                n = p.numel()
+                state[i] = {"step": torch.tensor(float(step)),
+                            "exp_avg": self._m[off:off + n].view(p.shape).clone(),
+                            "exp_avg_sq": self._v[off:off + n].view(p.shape).clone()}
+        return {"state": state, "param_groups": groups}
+
+    def load_state_dict(self, state_dict):
+        grp = self.param_groups[0]
+        groups = state_dict["param_groups"]
+        if len(groups) != 1 or len(groups[0]["params"]) != len(grp["params"]):
+            raise ValueError("charpt AdamW: the state dict does not match this optimizer's parameter group")
+        for k in ("lr", "betas", "eps", "weight_decay"):
+            grp[k] = groups[0][k]
+        if groups[0].get("amsgrad") or groups[0].get("maximize"):
+            raise ValueError("charpt AdamW: amsgrad / maximize state cannot be resumed by the fused kernel")
+        self._ensure()
+        ids = groups[0]["params"]
+        steps = set()
+        with torch.no_grad():
+            self._m.zero_()
+            self._v.zero_()
+            for i, p, off in self._param_slices():
+                s = state_dict["state"].get(ids[i])
+                if s is None:
+                    continue
+                n = p.numel()
+                self._m[off:off + n].copy_(s["exp_avg"].reshape(-1))
+                self._v[off:off + n].copy_(s["exp_avg_sq"].reshape(-1))
+                steps.add(int(float(s["step"])))
+        if len(steps) > 1:
+            raise ValueError(f"charpt AdamW: one step count for all parameters is required, got {sorted(steps)}")
+        self._step_t.fill_(steps.pop() if steps else 0)

@@ -97,3 +97,76 @@ def test_tokenizer_and_sampler_match_reference():
     BigramLanguageModel()
     s2 = BatchSampler(ts, 256, 64, world_size=8, rank=3)
     assert torch.equal(s2.draw_ix("train"), b["ix_one_draw_512"][3 * 64:4 * 64])
+
+
+def _torch_adamw_stepped(model, lr=3e-3, steps=2, seed=5):
+    """torch.optim.AdamW after ``steps`` steps on synthetic gradients (CPU)."""
+    ref = torch.optim.AdamW(model.parameters(), lr=lr)
+    g = torch.Generator().manual_seed(seed)
+    for _ in range(steps):
+        for p in model.parameters():
+            p.grad = torch.randn(p.shape, generator=g)
+        ref.step()
+    return ref
+
+
+def test_adamw_state_dict_is_torch_format():
+    """optim.AdamW finds the flat buffers from the parameters (GPT1.py:218 as written), and its
+    state dict is torch.optim.AdamW's: state moves from torch to charpt and back unchanged."""
+    from replicatinggpt_amd import AdamW, BigramLanguageModel, GPTConfig
+    cfg = GPTConfig(block_size=16, n_embd=24, n_head=4, n_layers=2)
+    torch.manual_seed(0)
+    m = BigramLanguageModel(cfg)
+    ref = _torch_adamw_stepped(m)
+    ours = AdamW(m.parameters(), lr=5e-1)
+    assert ours.state_dict()["state"] == {}            # never stepped: no per-parameter state
+    ours.load_state_dict(ref.state_dict())
+    sd, rsd = ours.state_dict(), ref.state_dict()
+    assert sd["param_groups"][0]["lr"] == 3e-3 and sd["param_groups"][0]["params"] == rsd["param_groups"][0]["params"]
+    assert set(sd["state"]) == set(rsd["state"])
+    for i, s in rsd["state"].items():
+        assert float(sd["state"][i]["step"]) == float(s["step"]) == 2.0
+        assert torch.equal(sd["state"][i]["exp_avg"], s["exp_avg"])
+        assert torch.equal(sd["state"][i]["exp_avg_sq"], s["exp_avg_sq"])
+    back = torch.optim.AdamW(m.parameters(), lr=1.0)
+    back.load_state_dict(sd)
+    for p in m.parameters():
+        assert torch.equal(back.state[p]["exp_avg"], ref.state[p]["exp_avg"])
+    assert back.param_groups[0]["lr"] == 3e-3 and back.param_groups[0]["decoupled_weight_decay"]
+
+
+def test_checkpoint_roundtrip_cpu(tmp_path):
+    """checkpoint.save_checkpoint / load_checkpoint restore weights, optimizer moments, the
+    iteration, the CPU generator (get_batch's offsets) and the dropout counter; save_model writes
+    the reference's 210-key model.pth."""
+    from replicatinggpt_amd import AdamW, BigramLanguageModel, GPTConfig
+    from replicatinggpt_amd import checkpoint as ck
+    cfg = GPTConfig(block_size=16, n_embd=24, n_head=4, n_layers=2)
+    torch.manual_seed(0)
+    a = BigramLanguageModel(cfg)
+    opt = AdamW(a.parameters(), lr=1e-3)
+    opt.load_state_dict(_torch_adamw_stepped(a).state_dict())
+    with torch.no_grad():
+        a._rng_counter.fill_(7)
+    torch.manual_seed(42)
+    path = tmp_path / "ck.pt"
+    ck.save_checkpoint(path, a, opt, 123)
+    want_draw = torch.randint(1000, (5,))
+    torch.manual_seed(1)
+    b = BigramLanguageModel(cfg)
+    opt_b = AdamW(b.parameters(), lr=9.0)
+    assert ck.load_checkpoint(path, b, opt_b) == 123
+    assert torch.equal(torch.randint(1000, (5,)), want_draw)
+    assert int(b._rng_counter) == 7
+    for (ka, va), (kb, vb) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert ka == kb and torch.equal(va, vb)
+    sa, sb = opt.state_dict(), opt_b.state_dict()
+    assert sb["param_groups"][0]["lr"] == 3e-3   # from the torch state loaded into opt
+    for i in sa["state"]:
+        assert torch.equal(sa["state"][i]["exp_avg_sq"], sb["state"][i]["exp_avg_sq"])
+    mp = tmp_path / "model.pth"
+    ck.save_model(b, mp)
+    sd = torch.load(mp, weights_only=True)
+    assert len(sd) == len(b.state_dict()) and sum(k.endswith("tril") for k in sd) == 2 * 4
+    with pytest.raises(ValueError):
+        ck.load_checkpoint(mp, b)
