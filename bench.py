@@ -90,11 +90,11 @@ def time_gemm(M, N, K, at, bt, epi, dev, reps=30):
     return s.elapsed_time(e) / reps
 
 
-def gemm_census(cfg, Bsz, T, dev):
-    """Every GEMM launch of one training step: (name, M, N, K, a_trans, b_trans, kind, launches/step)."""
+def census_shapes(cfg, Bsz, T):
+    """Every bf16 GEMM of one training step: (name, M, N, K, a_trans, b_trans, kind, launches/step)."""
     M, d, L = Bsz * T, cfg.n_embd, cfg.n_layers
     F4 = 4 * d
-    shapes = [
+    return [
         ("qkv_fwd", M, 3 * d, d, 0, 0, "fwd", L), ("proj_fwd", M, d, d, 0, 0, "fwd", L),
         ("ffn1_fwd", M, F4, d, 0, 0, "fwd", L), ("ffn2_fwd", M, d, F4, 0, 0, "fwd", L),
         ("proj_dgrad", M, d, d, 0, 1, "fwd", L), ("qkv_dgrad", M, d, 3 * d, 0, 1, "fwd", L),
@@ -102,11 +102,39 @@ def gemm_census(cfg, Bsz, T, dev):
         ("proj_wgrad", d, d, M, 1, 1, "wgrad", L), ("qkv_wgrad", 3 * d, d, M, 1, 1, "wgrad", L),
         ("ffn2_wgrad", d, F4, M, 1, 1, "wgrad", L), ("ffn1_wgrad", F4, d, M, 1, 1, "wgrad", L),
     ]
+
+
+def gemm_census(cfg, Bsz, T, dev):
+    """Average launch time of every GEMM shape of one training step (HIP events, time_gemm)."""
+    from replicatinggpt_amd import functional as Fn
     out = []
-    for name, m, n, k, at, bt, epi, cnt in shapes:
+    for name, m, n, k, at, bt, epi, cnt in census_shapes(cfg, Bsz, T):
         ms = time_gemm(m, n, k, at, bt, epi, dev)
-        out.append({"name": name, "M": m, "N": n, "K": k, "ms": ms, "launches": cnt, "flops": 2.0 * m * n * k})
+        out.append({"name": name, "M": m, "N": n, "K": k, "ms": ms, "launches": cnt, "flops": 2.0 * m * n * k,
+                    "split": Fn._wgrad_split(m, n, k, True) if epi == "wgrad" else 1})
     return out
+
+
+def gemm_family(census):
+    """All GEMM launches of one step together: algorithmic FLOPs / summed launch time."""
+    fl = sum(c["flops"] * c["launches"] for c in census)
+    ms = sum(c["ms"] * c["launches"] for c in census)
+    return {"launches_per_step": sum(c["launches"] for c in census), "ms_per_step": round(ms, 4),
+            "achieved": round(fl / (ms * 1e-3) / 1e12, 1), "frac": round(fl / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4)}
+
+
+def pmc_traffic(config, dom):
+    """HBM bytes per launch of the dominant op from the committed rocprofv3 PMC passes
+    (tools/pmc_gemm.py -> profiles/r1_pmc_gemm_traffic_<config>.json); None when that file does not
+    cover this exact shape and split."""
+    path = os.path.join(ROOT, "profiles", f"r1_pmc_gemm_traffic_{config}.json")
+    try:
+        op = json.load(open(path))["ops"][dom["name"]]
+    except (OSError, KeyError, ValueError):
+        return None
+    if (op["M"], op["N"], op["K"], op["split"]) != (dom["M"], dom["N"], dom["K"], dom["split"]):
+        return None
+    return op["hbm_bytes"]
 
 
 def bench_generate(dev, B=256, new=500):
@@ -210,10 +238,13 @@ def main():
             census = gemm_census(cfg, Bsz, T, dev)
             dom = max(census, key=lambda c: c["ms"] * c["launches"])
             achieved = dom["flops"] / (dom["ms"] * 1e-3) / 1e12
-            roofline = {"bound": "mfma", "kernel": f"k_gemm_bf16 {dom['name']} M={dom['M']} N={dom['N']} K={dom['K']}",
+            roofline = {"bound": "mfma", "kernel": f"cg_gemm bf16 {dom['name']} M={dom['M']} N={dom['N']} K={dom['K']}"
+                                                  f" (k_gemm_pk{' + k_splitk_reduce' if dom['split'] > 1 else ''},"
+                                                  f" split {dom['split']})",
                         "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                        "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                        "avg_launch_ms": round(dom["ms"], 5)}
+                        "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                        "traffic": pmc_traffic(args.config, dom), "avg_launch_ms": round(dom["ms"], 5),
+                        "gemm_family": gemm_family(census)}
         result = {
             "metric": "train tokens/sec at 1/2/4/8 MI355X + MFMA util, char-GPT block 256",
             "value": round(value, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,

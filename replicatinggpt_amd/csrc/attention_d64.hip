@@ -111,21 +111,23 @@ __global__ __launch_bounds__(256, QW == 16 ? 3 : 2) void k_attn_fwd_d64(
             float alpha[QT];
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt) {
-                const int64_t qa = qw0 + 16 * qt + li;
+                // raw scores; the scale is applied inside the exponent's fma (max commutes with
+                // the positive scale, and the rounding is monotone: same max as scaling first)
+                const int qa = (int)(qw0 + 16 * qt) + li, kb = (int)k0 + 4 * g;
                 float mx = -INFINITY;
 #pragma unroll
                 for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        float x = sacc[kt][qt][r] * scale_log2;
-                        if (diag && k0 + 16 * kt + 4 * g + r > qa) x = -INFINITY;
+                        float x = sacc[kt][qt][r];
+                        if (diag && kb + 16 * kt + r > qa) x = -INFINITY;
                         sacc[kt][qt][r] = x;
                         mx = fmaxf(mx, x);
                     }
                 mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
                 mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-                const float m_new = fmaxf(m_run[qt], mx);
-                alpha[qt] = exp2f(m_run[qt] - m_new);
+                const float m_new = fmaxf(m_run[qt], mx * scale_log2);
+                alpha[qt] = __builtin_amdgcn_exp2f(m_run[qt] - m_new);
                 float ls = 0.f;
 #pragma unroll
                 for (int kt = 0; kt < 4; ++kt) {
@@ -133,9 +135,12 @@ __global__ __launch_bounds__(256, QW == 16 ? 3 : 2) void k_attn_fwd_d64(
                     if (mask) mw = lds_words(S + 2 * TILE + ((wave * QT + qt) * 4 + kt) * 32);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const float p = exp2f(sacc[kt][qt][r] - m_new);
+                        // exp2 of the raw hardware instruction: results below 2^-126 (weights that
+                        // vanish against the row max) flush to 0 instead of going denormal
+                        const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kt][qt][r], scale_log2, -m_new));
                         ls += p;
-                        sacc[kt][qt][r] = (!mask || ((mw.w[r] >> lane) & 1ull)) ? p * dscale : 0.f;
+                        // 1/(1-p) of the kept weights is applied once, in the epilogue
+                        sacc[kt][qt][r] = (!mask || ((mw.w[r] >> lane) & 1ull)) ? p : 0.f;
                     }
                 }
                 ls += __shfl_xor(ls, 16, 64);
@@ -170,7 +175,7 @@ __global__ __launch_bounds__(256, QW == 16 ? 3 : 2) void k_attn_fwd_d64(
     for (int qt = 0; qt < QT; ++qt) {
         const int64_t qa = qw0 + 16 * qt + li;
         if (qa >= T_) continue;
-        const float inv = 1.f / l_run[qt];
+        const float inv = dscale / l_run[qt];
         bf16_t* orow = o + (boff + qa) * ldo + h * 64;
 #pragma unroll
         for (int et = 0; et < 4; ++et) {
@@ -281,15 +286,16 @@ __global__ __launch_bounds__(256, QW == 16 ? 3 : 2) void k_attn_dq_d64(
             }
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt) {
-                const int64_t qa = qw0 + 16 * qt + li;
+                const int qa = (int)(qw0 + 16 * qt) + li, kb = (int)k0 + 4 * g;
 #pragma unroll
                 for (int kt = 0; kt < 4; ++kt) {
                     Words4 mw;
                     if (mask) mw = lds_words(S + 2 * TILE + ((wave * QT + qt) * 4 + kt) * 32);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const int64_t key = k0 + 16 * kt + 4 * g + r;
-                        const float p = key > qa ? 0.f : exp2f(sa[kt][qt][r] * scale_log2 - lq[qt]);
+                        const float p = kb + 16 * kt + r > qa
+                                            ? 0.f
+                                            : __builtin_amdgcn_exp2f(fmaf(sa[kt][qt][r], scale_log2, -lq[qt]));
                         float dp = pa[kt][qt][r];
                         if (mask) dp = ((mw.w[r] >> lane) & 1ull) ? dp * dscale : 0.f;
                         sa[kt][qt][r] = p * (dp - dl[qt]);
@@ -419,7 +425,7 @@ __global__ __launch_bounds__(256, KW == 16 ? 2 : 1) void k_attn_dkdv_d64(
                 sv8 zf[KT], dsf[KT];
 #pragma unroll
                 for (int kt = 0; kt < KT; ++kt) {
-                    const int64_t key = kw0 + 16 * kt + li;
+                    const int key = (int)kw0 + 16 * kt + li;
                     fv4 z[2], ds[2];
 #pragma unroll
                     for (int qt = 0; qt < 2; ++qt) {
@@ -441,14 +447,18 @@ __global__ __launch_bounds__(256, KW == 16 ? 2 : 1) void k_attn_dkdv_d64(
 #pragma unroll
                             for (int r = 0; r < 4; ++r) keepbits |= ((bw >> ((4 * g + r) + 16 * (li >> 2))) & 1ull) << r;
                         }
+                        const int qb = (int)q0 + qr0 + 16 * qt + 4 * g;
+                        const float4 lse4 = *(const float4*)(st_lse + qr0 + 16 * qt + 4 * g);
+                        const float4 del4 = *(const float4*)(st_del + qr0 + 16 * qt + 4 * g);
+                        const float lsev[4] = {lse4.x, lse4.y, lse4.z, lse4.w};
+                        const float delv[4] = {del4.x, del4.y, del4.z, del4.w};
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
-                            const int qrel = qr0 + 16 * qt + 4 * g + r;
-                            const float p = key > q0 + qrel ? 0.f : exp2f(sa[r] * scale_log2 - st_lse[qrel]);
+                            const float p = key > qb + r ? 0.f : __builtin_amdgcn_exp2f(fmaf(sa[r], scale_log2, -lsev[r]));
                             const bool kp = (keepbits >> r) & 1ull;
                             const float dp = kp ? pa[r] * dscale : 0.f;
-                            z[qt][r] = kp ? p * dscale : 0.f;
-                            ds[qt][r] = p * (dp - st_del[qrel]);
+                            z[qt][r] = kp ? p : 0.f;   // 1/(1-p) of dV applied in the epilogue
+                            ds[qt][r] = p * (dp - delv[r]);
                         }
                     }
                     zf[kt] = pack8(z[0], z[1]);
@@ -479,7 +489,7 @@ __global__ __launch_bounds__(256, KW == 16 ? 2 : 1) void k_attn_dkdv_d64(
 #pragma unroll
         for (int et = 0; et < 4; ++et) {
             const fv4 x = dka[et][kt] * scale;
-            const fv4 y = dva[et][kt];
+            const fv4 y = dva[et][kt] * dscale;
             *(uint2*)(krow + 16 * et + 4 * g) = make_uint2(pack_bf2(x[0], x[1]), pack_bf2(x[2], x[3]));
             *(uint2*)(vrow + 16 * et + 4 * g) = make_uint2(pack_bf2(y[0], y[1]), pack_bf2(y[2], y[3]));
         }

@@ -49,16 +49,15 @@ typedef __bf16 bfv8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
-// round-to-nearest-even f32 -> bf16 (NaN kept NaN)
-__device__ __forceinline__ bf16_t f2bf(float f) {
-    uint32_t u = __float_as_uint(f);
-    if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return (bf16_t)(u >> 16);
-}
+// round-to-nearest-even f32 -> bf16: a plain __bf16 conversion compiles to gfx950's
+// v_cvt_pk_bf16_f32 (one instruction for two values; the integer RNE sequence it replaces cost
+// ~5 VALU per value in every bf16-writing epilogue).  NaN stays NaN.
+typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
 
 __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
-    return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+    const bf2v v = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(uint32_t, v);
 }
 
 template <typename T>
@@ -87,6 +86,25 @@ __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
     return v;
+}
+
+// wave64 sum through DPP (no LDS round trips): quad butterflies, row rotations, then the
+// row_bcast:15 / row_bcast:31 steps carry the row sums into row 3; lane 63 holds the total and
+// is broadcast with readlane.  Fixed association order (deterministic).  Every lane of the wave
+// must be active.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xf,
+                                                                 false));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+    v += dpp_f<0xB1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v += dpp_f<0x4E, 0xf>(v);   // quad_perm [2,3,0,1]
+    v += dpp_f<0x124, 0xf>(v);  // row_ror:4
+    v += dpp_f<0x128, 0xf>(v);  // row_ror:8   -> every lane holds its row's sum
+    v += dpp_f<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3 add rows 0, 2
+    v += dpp_f<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3 add row 1 (= rows 0 + 1)
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 
 // ---------------------------------------------------------------------------------------

@@ -32,7 +32,42 @@ extern "C" int cg_embed_fwd(const int64_t* idx, const float* wte, const float* w
 }
 
 // ---- backward -------------------------------------------------------------------------
-// dwpe[t,c] = sum_b dx[b,t,c]   (fixed b order)
+// dwpe[t,c] = sum_b dx[b,t,c]   (fixed b order).  4 columns per thread, 8 batch rows of loads in
+// flight (the sum order is still b = 0, 1, 2, ...); 64-thread blocks so a T*C = 98K-element
+// table still spreads over every CU.
+__global__ __launch_bounds__(64) void k_embed_bwd_pos4(const float* __restrict__ dx, float* __restrict__ dwpe,
+                                                     int64_t B, int64_t TC, int accumulate) {
+    const int64_t i = ((int64_t)blockIdx.x * 64 + threadIdx.x) * 4;
+    if (i >= TC) return;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    int64_t b = 0;
+    for (; b + 8 <= B; b += 8) {
+        float4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = *(const float4*)(dx + (b + j) * TC + i);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            s.x += v[j].x;
+            s.y += v[j].y;
+            s.z += v[j].z;
+            s.w += v[j].w;
+        }
+    }
+    for (; b < B; ++b) {
+        const float4 v = *(const float4*)(dx + b * TC + i);
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
+    }
+    float4* o = (float4*)(dwpe + i);
+    if (accumulate) {
+        const float4 p = *o;
+        s = make_float4(p.x + s.x, p.y + s.y, p.z + s.z, p.w + s.w);
+    }
+    *o = s;
+}
+
 __global__ void k_embed_bwd_pos(const float* __restrict__ dx, float* __restrict__ dwpe, int64_t B, int64_t T,
                                 int64_t C, int accumulate) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -44,7 +79,7 @@ __global__ void k_embed_bwd_pos(const float* __restrict__ dx, float* __restrict_
 
 // per row-chunk partial histogram-sum: part[chunk][v][c] = sum_{rows in chunk, idx=v} dx[row][c].
 // Each thread owns one column and walks the chunk's rows in order (deterministic, no atomics).
-constexpr int EMB_CHUNK = 256;
+constexpr int EMB_CHUNK = 128;
 
 __global__ void k_embed_bwd_tok_partial(const int64_t* __restrict__ idx, const float* __restrict__ dx,
                                         float* __restrict__ part, int64_t rows, int64_t C, int64_t V) {
@@ -55,7 +90,20 @@ __global__ void k_embed_bwd_tok_partial(const int64_t* __restrict__ idx, const f
     const int64_t r0 = chunk * EMB_CHUNK;
     const int64_t r1 = r0 + EMB_CHUNK < rows ? r0 + EMB_CHUNK : rows;
     if (c < C) {
-        for (int64_t r = r0; r < r1; ++r) {
+        int64_t r = r0;
+        for (; r + 8 <= r1; r += 8) {   // 8 rows of loads in flight; accumulation stays in row order
+            int64_t tk[8];
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int64_t t = idx[r + j];
+                tk[j] = t < 0 ? 0 : (t >= V ? V - 1 : t);
+                v[j] = dx[(r + j) * C + c];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[tk[j] * blockDim.x + threadIdx.x] += v[j];
+        }
+        for (; r < r1; ++r) {
             int64_t tok = idx[r];
             tok = tok < 0 ? 0 : (tok >= V ? V - 1 : tok);
             acc[tok * blockDim.x + threadIdx.x] += dx[r * C + c];
@@ -70,7 +118,15 @@ __global__ void k_embed_bwd_tok_reduce(const float* __restrict__ part, float* __
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= VC) return;
     float s = 0.f;
-    for (int64_t k = 0; k < nchunk; ++k) s += part[k * VC + i];
+    int64_t k = 0;
+    for (; k + 8 <= nchunk; k += 8) {   // 8 partials in flight, summed in chunk order
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = part[(k + j) * VC + i];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; k < nchunk; ++k) s += part[k * VC + i];
     dwte[i] = accumulate ? dwte[i] + s : s;
 }
 
@@ -85,15 +141,20 @@ extern "C" int cg_embed_bwd(const int64_t* idx, const float* dx, float* dwte, fl
     CG_REQUIRE(V * 128 * 4 <= 160 * 1024, "cg_embed_bwd: vocab %lld too large for the LDS histogram", (long long)V);
     hipStream_t st = (hipStream_t)stream;
     const int64_t rows = B * T;
-    if (dwpe) k_embed_bwd_pos<<<ceil_div(T * C, 256), 256, 0, st>>>(dx, dwpe, B, T, C, accumulate);
+    if (dwpe) {
+        if ((T * C) % 4 == 0 && ((((uintptr_t)dx) | ((uintptr_t)dwpe)) & 15) == 0)
+            k_embed_bwd_pos4<<<ceil_div(T * C / 4, 64), 64, 0, st>>>(dx, dwpe, B, T * C, accumulate);
+        else
+            k_embed_bwd_pos<<<ceil_div(T * C, 256), 256, 0, st>>>(dx, dwpe, B, T, C, accumulate);
+    }
     if (dwte) {
         const int64_t nchunk = (rows + EMB_CHUNK - 1) / EMB_CHUNK;
         const int threads = 128;
         dim3 grid(ceil_div(C, threads), (unsigned)nchunk);
         size_t lds = (size_t)V * threads * sizeof(float);
         k_embed_bwd_tok_partial<<<grid, threads, lds, st>>>(idx, dx, (float*)workspace, rows, C, V);
-        k_embed_bwd_tok_reduce<<<ceil_div(V * C, 256), 256, 0, st>>>((const float*)workspace, dwte, nchunk, V * C,
-                                                                      accumulate);
+        k_embed_bwd_tok_reduce<<<ceil_div(V * C, 64), 64, 0, st>>>((const float*)workspace, dwte, nchunk, V * C,
+                                                                    accumulate);
     }
     CG_LAUNCH_CHECK("cg_embed_bwd");
     return CG_OK;

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ x, con
 #pragma unroll
             for (int q = 0; q < VEC; ++q) s += v[j][q];
         }
-        const float mu = wave_sum(s) * invC;
+        const float mu = wave_sum_dpp(s) * invC;
         float ss = 0.f;
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
@@ -95,7 +95,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ x, con
                 }
             }
         }
-        const float var = wave_sum(ss) * invC;
+        const float var = wave_sum_dpp(ss) * invC;
         const float rs = 1.0f / sqrtf(var + eps);
         TY* yr = y + r * C;
 #pragma unroll
@@ -202,8 +202,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
                 }
             }
         }
-        const float c1 = wave_sum(s1) * invC;
-        const float c2 = wave_sum(s2) * invC;
+        const float c1 = wave_sum_dpp(s1) * invC;
+        const float c2 = wave_sum_dpp(s2) * invC;
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int e = (j * 64 + lane) * VEC;

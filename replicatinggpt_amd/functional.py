@@ -186,8 +186,35 @@ def linear_dgrad(dy2, w, out, epi="store", aux=None):
     return out
 
 
+_SLOTS = {}
+
+
+def _gemm_slots():
+    """Resident blocks of the persistent bf16 GEMM (csrc/gemm_pk.hip: 2 per CU)."""
+    dev = torch.cuda.current_device() if torch.cuda.is_available() else -1
+    if dev not in _SLOTS:
+        _SLOTS[dev] = 2 * (torch.cuda.get_device_properties(dev).multi_processor_count if dev >= 0 else 256)
+    return _SLOTS[dev]
+
+
 def _wgrad_split(M, N, K, fast):
-    tiles = (-(-M // 128) * -(-N // 128)) if fast else (-(-M // 64) * -(-N // 64))
+    """Split-K factor of a weight-gradient GEMM (K = tokens).  bf16 path: the persistent kernel
+    hands each resident block ceil(items / slots) items of K/split reduction depth, and every
+    split adds an fp32 slab to write and reduce, so minimise
+        ceil(tiles * split / slots) * (K / split) * (1 + split / 50)
+    -- this picks the measured best split of every C2 / C4 weight-gradient shape
+    (tools/gemm_scan2.py, profiles/r1_gemm_scan_wgrad.txt)."""
+    if fast:
+        tiles, slots = -(-M // 128) * -(-N // 128), _gemm_slots()
+        best, best_cost = 1, None
+        for split in (1, 2, 4, 8, 16, 32):
+            if K % (64 * split) or K // split < 256:
+                break
+            cost = -(-tiles * split // slots) * (K / split) * (1 + split / 50)
+            if best_cost is None or cost < best_cost:
+                best, best_cost = split, cost
+        return best
+    tiles = -(-M // 64) * -(-N // 64)
     split = 1
     while tiles * split * 2 <= 1024 and split < 32 and K % (64 * split * 2) == 0 and K // (split * 2) >= 256:
         split *= 2

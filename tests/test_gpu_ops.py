@@ -458,3 +458,25 @@ def test_adamw_matches_torch():
         ops().adamw(pd, g.to(DEV), m, v, sh, 2e-4, 0.9, 0.999, 1e-8, 1e-2, step)
     assert relerr(pd, ref.detach()) < 1e-6
     assert torch.equal(sh.cpu(), pd.cpu().to(torch.bfloat16))
+
+
+def test_bf16_rounding_matches_torch():
+    """Every bf16 the kernels write goes through gfx950's v_cvt_pk_bf16_f32 (csrc/common.h
+    f2bf / pack_bf2): round-to-nearest-even, bit-identical to torch's float -> bfloat16 cast,
+    including ties, denormals, overflow to inf and signed zeros."""
+    torch.manual_seed(11)
+    x = torch.randn(1 << 16) * torch.exp(torch.randn(1 << 16) * 8)
+    ties = (torch.randint(0, 0x7f00, (4096,), dtype=torch.int32) << 16 | 0x8000).view(torch.float32)  # finite
+    edge = torch.tensor([0.0, -0.0, float("inf"), -float("inf"), 3.4e38, -3.4e38, 1e-40, -1e-40, 1.17e-38,
+                         2.0 ** -133, 1.0 + 2.0 ** -8, 1.0 + 3 * 2.0 ** -8])
+    src = torch.cat([x, ties, edge]).contiguous()
+    out = torch.empty(src.numel(), dtype=torch.bfloat16, device=DEV)
+    ops().cast_bf16(src.to(DEV), out)
+    torch.cuda.synchronize()
+    got, want = out.cpu().view(torch.int16), src.to(torch.bfloat16).view(torch.int16)
+    bad = (got != want).nonzero().flatten()
+    assert bad.numel() == 0, [(float(src[i]), int(got[i]), int(want[i])) for i in bad[:8]]
+    nan = torch.full((64,), float("nan"))
+    out = torch.empty(64, dtype=torch.bfloat16, device=DEV)
+    ops().cast_bf16(nan.to(DEV), out)
+    assert torch.isnan(out.cpu().float()).all()
