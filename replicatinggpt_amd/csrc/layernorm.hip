@@ -138,13 +138,17 @@ struct LnLp {
 // One wave per row, RPW rows per wave with every load of the wave's rows issued before any
 // reduction (the previous loop waited a full load latency per row); row in registers as in the
 // forward.  Partials [block][NP*C]: dgamma, dbeta (+ consumer bias column sums).
-template <int VEC, int NJ, typename TDY, int WAVES>
+// Measured: holding 64/WAVES rows per wave (all loads issued up front) spilled 328 VGPRs at C=768
+// (436 B/lane scratch, 1.3 TB/s); now each wave walks its rows RPW at a time, so the in-flight rows
+// plus the column partials fit the 128-register budget of 4 waves/SIMD.
+template <int VEC, int NJ, typename TDY, int WAVES, int RPW>
 __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ dy, const float* __restrict__ x,
                                                 const float* __restrict__ w, const float* __restrict__ mean,
                                                 const float* __restrict__ rstd, const float* __restrict__ dres,
                                                 float* __restrict__ dx, LnLp lp, float* __restrict__ part,
                                                 int64_t rows, int C) {
-    constexpr int RPW = LN_BWD_ROWS / WAVES;
+    constexpr int ITER = LN_BWD_ROWS / (WAVES * RPW);
+    static_assert(ITER * WAVES * RPW == LN_BWD_ROWS, "rows per block must split evenly");
     extern __shared__ __attribute__((aligned(16))) float red[];  // [WAVES][NP][C]
     const int NP = lp.csum ? 3 : 2;
     const int lane = threadIdx.x & 63;
@@ -163,7 +167,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
             for (int q = 0; q < VEC; ++q) wv[j][q] = 0.f;
         }
     }
-    const int64_t r0 = (int64_t)blockIdx.x * LN_BWD_ROWS + wave * RPW;
+#pragma unroll 1
+    for (int it = 0; it < ITER; ++it) {
+    const int64_t r0 = (int64_t)blockIdx.x * LN_BWD_ROWS + (it * WAVES + wave) * RPW;
     float xv[RPW][NJ][VEC], d[RPW][NJ][VEC], rv[RPW][NJ][VEC];
     float mu[RPW], rs[RPW];
 #pragma unroll
@@ -237,6 +243,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
             }
         }
     }
+    }  // it
     // block reduction of the column partials in a fixed wave order
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -284,14 +291,14 @@ int launch_ln_bwd(const TDY* dy, const float* x, const float* w, const float* me
                       (((uintptr_t)dy) & 7) == 0 && (((uintptr_t)(lp.out ? lp.out : (bf16_t*)x)) & 7) == 0;
     const int64_t nblk = (rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
     const int NP = lp.csum ? 3 : 2;
-#define LNB(V, N, W)                                                                                         \
-    k_ln_bwd<V, N, TDY, W><<<(unsigned)nblk, 64 * W, (size_t)NP * W * C * sizeof(float), st>>>(dy, x, w, mean, rstd, \
+#define LNB(V, N, W, R)                                                                                      \
+    k_ln_bwd<V, N, TDY, W, R><<<(unsigned)nblk, 64 * W, (size_t)NP * W * C * sizeof(float), st>>>(dy, x, w, mean, rstd, \
                                                                                              dres, dx, lp, part, rows, C)
-    if (C == 384 && al16) LNB(2, 3, 16);
-    else if (C == 768 && al16) LNB(4, 3, 16);
-    else if (C == 512 && al16) LNB(4, 2, 16);
-    else if (C == 1024 && al16) LNB(4, 4, 8);
-    else LNB(1, 32, 4);
+    if (C == 384 && al16) LNB(2, 3, 16, 2);
+    else if (C == 768 && al16) LNB(4, 3, 4, 1);
+    else if (C == 512 && al16) LNB(4, 2, 4, 1);
+    else if (C == 1024 && al16) LNB(4, 4, 4, 1);
+    else LNB(1, 32, 4, 1);
 #undef LNB
     if (dw || db || dbias) launch_reduce_partials3(part, nblk, NP * C, dw, db, dbias, C, accumulate, dbias_accumulate, st);
     return CG_OK;

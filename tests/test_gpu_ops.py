@@ -56,7 +56,7 @@ def test_dropout_mask_matches_oracle(p):
     assert np.array_equal(out.cpu().numpy() > 0.5, want)
 
 
-@pytest.mark.parametrize("C", [126, 384, 768, 33])
+@pytest.mark.parametrize("C", [126, 384, 512, 768, 1024, 33])
 @pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
 def test_layernorm(C, out_dtype):
     torch.manual_seed(0)
