@@ -68,6 +68,8 @@ __device__ __forceinline__ void store_out(TC* C, int64_t off, float v, float bet
 extern int g_gemm_variant;
 // test knob (cg_set_tuning("gemm_max_grid", n)): cap on persistent-kernel blocks; 0 = resident slots
 extern int g_gemm_max_grid;
+// test knob (cg_set_tuning("pk_flags", f)) for the persistent kernel's epilogue (gemm_pk.hip)
+extern int g_pk_flags;
 
 // launches the bf16 MFMA kernel if the problem qualifies; returns false (nothing launched) if not
 bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,

@@ -176,6 +176,31 @@ def test_gemm_splitk_deterministic(split, dt):
     assert relerr(outs[0], ref) < 1e-5
 
 
+@pytest.mark.parametrize("c_dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_gemm_splitk_reduce_vec_matches_scalar(c_dt, beta):
+    """The vectorised split-K reducer (16-B rows) and the scalar one (odd ldc) give bitwise the same
+    bias + residual epilogue, and both match the fp64 reference."""
+    M, N, K, split = 96, 256, 1024, 4
+    torch.manual_seed(3)
+    A = torch.randn(M, K).to(torch.bfloat16).to(DEV)
+    B = torch.randn(N, K).to(torch.bfloat16).to(DEV)
+    bias = torch.randn(N, device=DEV)
+    resid = torch.randn(M, N, device=DEV)
+    init = torch.randn(M, N + 1, device=DEV).to(c_dt)
+    ws = torch.empty(ops().gemm_workspace(M, N, split) // 4, dtype=torch.float32, device=DEV)
+    res = []
+    for ldc in (N, N + 1):
+        out = init[:, :ldc].contiguous() if ldc == N else init.clone()
+        ops().gemm(A, B, out, True, False, False, M, N, K, K, K, ldc, 3, bias, resid, N, None, 0, 0.0, 0, None, 0,
+                   beta, split, ws)
+        res.append(out[:, :N].float().cpu())
+    assert torch.equal(res[0], res[1])
+    ref = (A.double() @ B.double().t()).cpu() + bias.double().cpu() + resid.double().cpu()
+    ref = ref + beta * init[:, :N].double().cpu()
+    assert relerr(res[0], ref) < (1e-5 if c_dt == torch.float32 else 1e-2)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N,K", [(256, 384, 128), (96, 70, 40)])
 def test_gemm_epilogues(dt, M, N, K):

@@ -44,4 +44,4 @@ if __name__ == "__main__":
         print(f"attn_variant {var}", flush=True)
         for p in (0.0, 0.2):
             bench(64, 256, 6, 64, p)
-            bench(8, 1024, 12, 64, p)
+            bench(64, 1024, 12, 64, p)

@@ -41,8 +41,16 @@ def main():
             ("ffn2_dgrad relu_bwd bf16", M, F4, d, 1, L.EPI_RELU_BWD, torch.bfloat16, 0.0),
             ("proj_fwd bias_resid f32", M, d, d, 0, L.EPI_BIAS_RESID, torch.float32, 0.0),
             ("qkv_fwd store bf16", M, 3 * d, d, 0, L.EPI_STORE, torch.bfloat16, 0.0)]
+    flags = [int(a) for a in sys.argv[1:]] or [0]
+    lib = L.load()
+    print(f"{'pk_flags':38s} " + " ".join(f"{f:9d}" for f in flags), flush=True)
     for name, m, n, k, bt, epi, dt, p in rows:
-        print(f"{name:38s} {case(m, n, k, bt, epi, dt, p):7.1f} us", flush=True)
+        ts = []
+        for f in flags:
+            L.check(lib.cg_set_tuning(b"pk_flags", f))
+            ts.append(case(m, n, k, bt, epi, dt, p))
+        L.check(lib.cg_set_tuning(b"pk_flags", 0))
+        print(f"{name:38s} " + " ".join(f"{t:6.1f} us" for t in ts), flush=True)
 
 
 if __name__ == "__main__":
