@@ -185,7 +185,12 @@ bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf1
     if (e.resid && ((((uintptr_t)e.resid) & 15) || e.ld_resid % 4)) return false;
     if (e.aux && ((((uintptr_t)e.aux) & 15) || e.ld_aux % 8)) return false;
     int v = g_gemm_variant;
-    if (v == 0) v = 9;  // persistent 128x128 LDS-DMA: measured best on the C2 shapes (profiles/r1_gemm_scan.txt)
+    if (v == 0) {
+        // persistent 128x128 LDS-DMA: measured best on the C2 shapes (profiles/r1_gemm_scan.txt); the
+        // 8-wave 256x256 tile once there are >= 2 tiles per CU (C4 forward/dgrad: profiles/r1_gemm_scan_c4_v24.txt)
+        const int64_t t256 = (M / 256) * (N / 256);
+        v = (!at && split_k == 1 && M % 256 == 0 && N % 256 == 0 && t256 >= 2 * (int64_t)gemm_cu_count()) ? 24 : 9;
+    }
     if (v >= 20 && p8_gemm_launch(v, at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st))
         return true;
     if (v >= 20) v = 2;

@@ -70,6 +70,7 @@ extern int g_gemm_variant;
 extern int g_gemm_max_grid;
 // test knob (cg_set_tuning("pk_flags", f)) for the persistent kernel's epilogue (gemm_pk.hip)
 extern int g_pk_flags;
+int gemm_cu_count();  // compute units of the current device (cached; gemm_pk.hip)
 
 // launches the bf16 MFMA kernel if the problem qualifies; returns false (nothing launched) if not
 bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,

@@ -69,11 +69,12 @@ template <int BM, int BN, int NBUF>
 struct Geo8 {
     static constexpr int IMG_A = BM * FBK * 2, IMG_B = BN * FBK * 2, STAGE = IMG_A + IMG_B;
     static constexpr int LDS = NBUF * STAGE;
+    static constexpr int OCC = LDS <= 80 * 1024 ? 2 : 1;  // resident blocks per CU (LDS-bound)
 };
 
 // WM = waves along M (8 / WM along N); per-wave tile (BM/WM) x (BN/(8/WM)) in 16x16 fragments
 template <bool AT, bool BT, int BM, int BN, int WM, int NBUF>
-__global__ __launch_bounds__(P8_THREADS, 2)
+__global__ __launch_bounds__(P8_THREADS, (Geo8<BM, BN, NBUF>::OCC))
 void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
                const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype, int64_t ldc,
                EpiArgs epi, int split_k, int64_t kchunk, float* __restrict__ ws) {
@@ -179,18 +180,39 @@ void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         }
         const char* imgA = smem + cur * G::STAGE;
         const char* imgB = imgA + G::IMG_A;
+        // LDS reads run one group ahead of the MFMAs that consume them (sched_barrier pins the order;
+        // left alone the scheduler sinks each A read next to its MFMAs and waits lgkmcnt(0) on it):
+        // [B0 A0] | [B1 A1(lo)] mfma0(lo) | [A1(hi)] mfma0(hi) | mfma1 -- A1(hi) reuses A0(lo)'s
+        // registers, so a 128x64 wave tile stays inside 256 VGPRs at two waves per SIMD
+        constexpr int FH = FM / 2;
+        sv8 af0[FM], bf0[FN], af1[FM], bf1[FN];
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            sv8 af[FM], bf[FN];
+        for (int j = 0; j < FN; ++j) bf0[j] = frag<BT, BN>(imgB, wn * (BN / WN) + j * 16, 0, lane);
 #pragma unroll
-            for (int i = 0; i < FM; ++i) af[i] = frag<AT, BM>(imgA, wm * (BM / WM) + i * 16, s, lane);
+        for (int i = 0; i < FM; ++i) af0[i] = frag<AT, BM>(imgA, wm * (BM / WM) + i * 16, 0, lane);
 #pragma unroll
-            for (int j = 0; j < FN; ++j) bf[j] = frag<BT, BN>(imgB, wn * (BN / WN) + j * 16, s, lane);
+        for (int j = 0; j < FN; ++j) bf1[j] = frag<BT, BN>(imgB, wn * (BN / WN) + j * 16, 1, lane);
 #pragma unroll
-            for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FH; ++i) af1[i] = frag<AT, BM>(imgA, wm * (BM / WM) + i * 16, 1, lane);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int j = 0; j < FN; ++j) acc[i][j] = mfma_bf16(bf[j], af[i], acc[i][j]);
-        }
+        for (int i = 0; i < FH; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[i][j] = mfma_bf16(bf0[j], af0[i], acc[i][j]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = FH; i < FM; ++i) af1[i] = frag<AT, BM>(imgA, wm * (BM / WM) + i * 16, 1, lane);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = FH; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[i][j] = mfma_bf16(bf0[j], af0[i], acc[i][j]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[i][j] = mfma_bf16(bf1[j], af1[i], acc[i][j]);
+        __builtin_amdgcn_sched_barrier(0);
         cur = cur + 1 == NBUF ? 0 : cur + 1;
         stored = false;
         if (++ckt == nk) {
@@ -235,7 +257,7 @@ void launch8(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, i
     using G = Geo8<BM, BN, NBUF>;
     const int64_t kchunk = K / split_k;
     const int64_t nitems = (M / BM) * (N / BN) * split_k;
-    const int occ = G::LDS <= 80 * 1024 ? 2 : 1;
+    const int occ = G::OCC;
     int64_t slots = (int64_t)cu_count8() * occ;
     if (g_gemm_max_grid > 0 && g_gemm_max_grid < slots) slots = g_gemm_max_grid;
     const unsigned grid = (unsigned)(nitems < slots ? nitems : slots);

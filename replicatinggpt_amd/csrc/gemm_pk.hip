@@ -188,7 +188,11 @@ struct GeoP {
 };
 
 template <bool AT, bool BT, int BM, int BN, int NBUF>
+// amdgpu_waves_per_eu: LDS caps residency at OCC blocks, so tell the scheduler the real occupancy;
+// left at its default it schedules for 8+ waves/SIMD, keeps ONE A fragment register and waits
+// lgkmcnt(0) before every 4 MFMAs (LDS latency exposed 8x per K-tile)
 __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, (GeoP<BM, BN, NBUF>::OCC))
+__attribute__((amdgpu_waves_per_eu(1, (BM / 64) * (BN / 64) * GeoP<BM, BN, NBUF>::OCC / 4)))
 void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
                const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype, int64_t ldc,
                EpiArgs epi, int split_k, int64_t kchunk, float* __restrict__ ws, int flags) {
@@ -295,17 +299,24 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         }
         const char* imgA = smem + cur * G::STAGE;
         const char* imgB = imgA + G::IMG_A;
+        // both 32-deep halves' fragments are read before the first MFMA (sched_barrier pins it):
+        // otherwise the scheduler sinks each A read next to its 4 MFMAs and waits lgkmcnt(0) on it
+        sv8 af[2][4], bf[2][4];
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-            sv8 af[4], bf[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) af[i] = frag<AT, BM>(imgA, wm * 64 + i * 16, s, lane);
+            for (int j = 0; j < 4; ++j) bf[s][j] = frag<BT, BN>(imgB, wn * 64 + j * 16, s, lane);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) bf[j] = frag<BT, BN>(imgB, wn * 64 + j * 16, s, lane);
+            for (int i = 0; i < 4; ++i) af[s][i] = frag<AT, BM>(imgA, wm * 64 + i * 16, s, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = mfma_bf16(bf[j], af[i], acc[i][j]);
+                for (int j = 0; j < 4; ++j) acc[i][j] = mfma_bf16(bf[s][j], af[s][i], acc[i][j]);
+            __builtin_amdgcn_sched_barrier(0);
         }
         cur = cur + 1 == NBUF ? 0 : cur + 1;
         if (++ckt == nk) {
@@ -376,6 +387,8 @@ void launch_p(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
 }
 
 }  // namespace
+
+int gemm_cu_count() { return cu_count(); }
 
 bool pk_gemm_launch(int v, int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda,
                     const bf16_t* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k,

@@ -157,6 +157,36 @@ def test_gemm_kernel_variants(variant, max_grid, at, bt, M, N, K):
     assert relerr(o, want) < 1e-5
 
 
+@pytest.mark.parametrize("bt", [0, 1])
+def test_gemm_default_picks_large_tile(bt):
+    """At >= 2 256x256 tiles per CU the default dispatch takes the 8-wave 256x256 kernel (C4 forward
+    and dgrad shapes): plain store, bias+ReLU and bias+dropout+residual epilogues at such a shape."""
+    M, N, K = 8192, 4096, 128
+    torch.manual_seed(11)
+    A = torch.randn(M, K).to(torch.bfloat16)
+    B = (torch.randn(K, N) if bt else torch.randn(N, K)).to(torch.bfloat16)
+    bias = torch.randn(N)
+    ref = _ref_gemm(A, B, 0, bt)
+    Ad, Bd = A.to(DEV), B.to(DEV)
+    out = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    ops().gemm(Ad, Bd, out, True, False, bool(bt), M, N, K, K, B.shape[1], N, 0, None, None, 0,
+               None, 0, 0.0, 0, None, 0, 0.0, 1, None)
+    h = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ops().gemm(Ad, Bd, h, True, False, bool(bt), M, N, K, K, B.shape[1], N, 2, bias.to(DEV), None,
+               0, None, 0, 0.0, 0, None, 0, 0.0, 1, None)
+    resid = torch.randn(M, N)
+    call = torch.tensor([4], dtype=torch.int64, device=DEV)
+    o = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    ops().gemm(Ad, Bd, o, True, False, bool(bt), M, N, K, K, B.shape[1], N, 4, bias.to(DEV),
+               resid.to(DEV), N, None, 0, 0.2, 5, call, 1, 0.0, 1, None)
+    torch.cuda.synchronize()
+    assert relerr(out, ref) < 1e-5
+    assert relerr(h, torch.relu(ref + bias.double())) < 8e-3
+    keep = philox.keep_mask(5, (4 << 8) | 1, np.arange(M * N), 0.2).reshape(M, N)
+    want = resid.double() + torch.from_numpy(keep).double() * (ref + bias.double()) * float(np.float32(1 / 0.8))
+    assert relerr(o, want) < 1e-5
+
+
 @pytest.mark.parametrize("split", [2, 4, 8])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_gemm_splitk_deterministic(split, dt):
