@@ -97,6 +97,10 @@ def load():
         fn.restype = res
         fn.argtypes = args
     _lib = lib
+    # CHARPT_TUNING="key=value,key=value": kernel-selection knobs for measurement runs (cg_set_tuning)
+    for kv in filter(None, os.environ.get("CHARPT_TUNING", "").split(",")):
+        key, _, val = kv.partition("=")
+        check(lib.cg_set_tuning(key.strip().encode(), int(val)), f"cg_set_tuning({key})")
     return lib
 
 

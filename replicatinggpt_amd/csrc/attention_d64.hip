@@ -48,9 +48,11 @@ __global__ __launch_bounds__(256, QW == 16 ? 3 : 2) void k_attn_fwd_d64(
     __shared__ __attribute__((aligned(16))) char smem[2 * STG];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, li = lane & 15;
-    const int bh = blockIdx.y, b = bh / H, h = bh % H;
+    int xblk, bh;
+    block_coords<true>(xblk, bh);
+    const int b = bh / H, h = bh % H;
     const int NT = (int)(T_ >> 4);
-    const int64_t qblk0 = (int64_t)blockIdx.x * FQ;
+    const int64_t qblk0 = (int64_t)xblk * FQ;
     const int64_t qw0 = qblk0 + wave * QW;
     const int64_t boff = (int64_t)b * T_;
     const bf16_t* kb_ = k + boff * ld + h * 64;
@@ -201,9 +203,11 @@ __global__ __launch_bounds__(256, QW == 16 ? 3 : 2) void k_attn_dq_d64(
     __shared__ __attribute__((aligned(16))) char smem[2 * STG];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, li = lane & 15;
-    const int bh = blockIdx.y, b = bh / H, h = bh % H;
+    int xblk, bh;
+    block_coords<true>(xblk, bh);
+    const int b = bh / H, h = bh % H;
     const int NT = (int)(T_ >> 4);
-    const int64_t qblk0 = (int64_t)blockIdx.x * FQ;
+    const int64_t qblk0 = (int64_t)xblk * FQ;
     const int64_t qw0 = qblk0 + wave * QW;
     const int64_t boff = (int64_t)b * T_;
     const bool wave_active = qw0 < T_;
@@ -352,9 +356,11 @@ __global__ __launch_bounds__(256, KW == 16 ? 2 : 1) void k_attn_dkdv_d64(
     __shared__ __attribute__((aligned(16))) char smem[2 * STG];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, li = lane & 15;
-    const int bh = blockIdx.y, b = bh / H, h = bh % H;
+    int xblk, bh;
+    block_coords<false>(xblk, bh);
+    const int b = bh / H, h = bh % H;
     const int NT = (int)(T_ >> 4);
-    const int64_t kblk0 = (int64_t)blockIdx.x * FK;
+    const int64_t kblk0 = (int64_t)xblk * FK;
     const int64_t kw0 = kblk0 + wave * KW;
     const int64_t boff = (int64_t)b * T_;
     const bool wave_active = kw0 < T_;

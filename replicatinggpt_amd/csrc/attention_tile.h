@@ -85,5 +85,22 @@ __device__ __forceinline__ Words4 lds_words(const char* p) {
 
 constexpr int TILE = 8192;  // [64][64] bf16
 
+// XCD-aware block order for a (row blocks, B*H) grid.  The dispatcher deals linear block ids to
+// the 8 XCDs round-robin, and each XCD has its own L2: left alone, the row blocks of one (b,h) --
+// which all stream the same K/V (or Q/dO) -- land on 8 different L2s (measured: 35 % L2 hits, the
+// C4 forward fetching 4.5x its algorithmic bytes).  The bijective remap gives every XCD a
+// contiguous run of logical ids, i.e. whole (b,h) groups; REV runs a group's blocks last-first
+// (the causal forward / dQ blocks with the longest key prefix start first).
+template <bool REV>
+__device__ __forceinline__ void block_coords(int& blk, int& bh) {
+    const int nx = (int)gridDim.x, n = nx * (int)gridDim.y;
+    const int id = (int)blockIdx.y * nx + (int)blockIdx.x;
+    const int q = n >> 3, r = n & 7, xcd = id & 7;
+    const int lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
+    bh = lid / nx;
+    blk = lid - bh * nx;
+    if (REV) blk = nx - 1 - blk;
+}
+
 }  // namespace atile
 }  // namespace cg

@@ -42,6 +42,10 @@ if __name__ == "__main__":
     for var in variants:
         L.check(lib.cg_set_tuning(b"attn_variant", var))
         print(f"attn_variant {var}", flush=True)
-        for p in (0.0, 0.2):
-            bench(64, 256, 6, 64, p)
-            bench(64, 1024, 12, 64, p)
+        cfg = os.environ.get("ATTN_CFG", "all")  # c2 | c4 | all (PMC runs: one shape per run)
+        ps = (0.2,) if cfg != "all" else (0.0, 0.2)
+        for p in ps:
+            if cfg in ("c2", "all"):
+                bench(64, 256, 6, 64, p)
+            if cfg in ("c4", "all"):
+                bench(64, 1024, 12, 64, p)
