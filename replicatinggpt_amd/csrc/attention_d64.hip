@@ -133,7 +133,7 @@ __global__ __launch_bounds__(256, QW == 16 ? 3 : 2) void k_attn_fwd_d64(
                 float ls = 0.f;
 #pragma unroll
                 for (int kt = 0; kt < 4; ++kt) {
-                    Words4 mw;
+                    Words4 mw = {{~0ull, ~0ull, ~0ull, ~0ull}};  // no dropout: keep everything, no branch
                     if (mask) mw = lds_words(S + 2 * TILE + ((wave * QT + qt) * 4 + kt) * 32);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256, QW == 16 ? 3 : 2) void k_attn_fwd_d64(
                         const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kt][qt][r], scale_log2, -m_new));
                         ls += p;
                         // 1/(1-p) of the kept weights is applied once, in the epilogue
-                        sacc[kt][qt][r] = (!mask || ((mw.w[r] >> lane) & 1ull)) ? p : 0.f;
+                        sacc[kt][qt][r] = keep_sel(mw.w[r], p);
                     }
                 }
                 ls += __shfl_xor(ls, 16, 64);
@@ -293,7 +293,7 @@ __global__ __launch_bounds__(256, QW == 16 ? 3 : 2) void k_attn_dq_d64(
                 const int qa = (int)(qw0 + 16 * qt) + li, kb = (int)k0 + 4 * g;
 #pragma unroll
                 for (int kt = 0; kt < 4; ++kt) {
-                    Words4 mw;
+                    Words4 mw = {{~0ull, ~0ull, ~0ull, ~0ull}};  // no dropout: keep everything, no branch
                     if (mask) mw = lds_words(S + 2 * TILE + ((wave * QT + qt) * 4 + kt) * 32);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
@@ -301,7 +301,7 @@ __global__ __launch_bounds__(256, QW == 16 ? 3 : 2) void k_attn_dq_d64(
                                             ? 0.f
                                             : __builtin_amdgcn_exp2f(fmaf(sa[kt][qt][r], scale_log2, -lq[qt]));
                         float dp = pa[kt][qt][r];
-                        if (mask) dp = ((mw.w[r] >> lane) & 1ull) ? dp * dscale : 0.f;
+                        dp = keep_sel(mw.w[r], dp * dscale);  // dscale is 1 without dropout
                         sa[kt][qt][r] = p * (dp - dl[qt]);
                     }
                 }

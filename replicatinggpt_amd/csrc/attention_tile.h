@@ -83,6 +83,15 @@ __device__ __forceinline__ Words4 lds_words(const char* p) {
     return o;
 }
 
+// The keep words are wave-uniform 64-bit lane masks (bit i <-> lane i, k_attn_dropmask's ballots):
+// move them to SGPRs once and select with ONE v_cndmask_b32 per element, whose condition operand
+// is exactly such a lane mask -- instead of a per-lane 64-bit shift, and, compare and select.
+__device__ __forceinline__ float keep_sel(uint64_t word, float v) {
+    const uint64_t lanemask = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(word >> 32)) << 32) |
+                              (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)word);
+    return __builtin_amdgcn_inverse_ballot_w64(lanemask) ? v : 0.f;
+}
+
 constexpr int TILE = 8192;  // [64][64] bf16
 
 // XCD-aware block order for a (row blocks, B*H) grid.  The dispatcher deals linear block ids to

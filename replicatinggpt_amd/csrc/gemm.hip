@@ -241,7 +241,9 @@ __global__ void k_splitk_reduce(const float* __restrict__ ws, int split_k, int64
 // above spent its time in 64-bit division; measured 12.8 us for the C2 FFN weight gradient, split 8).
 // Same summation order (k = 0..split-1) and epilogue arithmetic as epi_scalar, so results are
 // bitwise those of the scalar form.
-template <typename TC>
+// S > 0: compile-time split, every slab's float4 loaded before the first add (S loads in flight per
+// thread instead of 4); the adds still run k = 0..S-1 in order.
+template <typename TC, int S>
 __global__ __launch_bounds__(256) void k_splitk_reduce4(const float* __restrict__ ws, int split_k, int M, int N,
                                                         TC* __restrict__ C, int64_t ldc, EpiArgs epi) {
     const int n4 = N >> 2;
@@ -250,8 +252,24 @@ __global__ __launch_bounds__(256) void k_splitk_reduce4(const float* __restrict_
     const int m = i / n4, n = (i - m * n4) * 4;
     const int64_t slab = (int64_t)M * N;
     const float* p = ws + (int64_t)m * N + n;
-    float4 s = *(const float4*)p;
+    float4 s;
     int k = 1;
+    if constexpr (S > 0) {
+        float4 a[S];
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            const fv4 t = __builtin_nontemporal_load((const fv4*)(p + j * slab));  // slabs are read once
+            a[j] = make_float4(t[0], t[1], t[2], t[3]);
+        }
+        s = a[0];
+#pragma unroll
+        for (int j = 1; j < S; ++j) {
+            s.x += a[j].x; s.y += a[j].y; s.z += a[j].z; s.w += a[j].w;
+        }
+        k = split_k;
+    } else {
+        s = *(const float4*)p;
+    }
     for (; k + 4 <= split_k; k += 4) {
         const float4 a = *(const float4*)(p + k * slab), b = *(const float4*)(p + (k + 1) * slab);
         const float4 c = *(const float4*)(p + (k + 2) * slab), d = *(const float4*)(p + (k + 3) * slab);
@@ -417,12 +435,25 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
                       (!e.resid || e.ld_resid % 4 == 0);
     if (split_k > 1 && vec4) {
         const int n4 = (int)(M * N / 4);
-        if (c_dtype == CG_BF16)
-            k_splitk_reduce4<bf16_t><<<ceil_div(n4, 256), 256, 0, st>>>((const float*)workspace, split_k, (int)M,
-                                                                        (int)N, (bf16_t*)C, ldc, e);
-        else
-            k_splitk_reduce4<float><<<ceil_div(n4, 256), 256, 0, st>>>((const float*)workspace, split_k, (int)M,
-                                                                       (int)N, (float*)C, ldc, e);
+#define SKR(TC_, S_)                                                                                  \
+    k_splitk_reduce4<TC_, S_><<<ceil_div(n4, 256), 256, 0, st>>>((const float*)workspace, split_k, (int)M, \
+                                                                 (int)N, (TC_*)C, ldc, e)
+#define SKR_ANY(TC_)                        \
+    switch (split_k) {                      \
+        case 2: SKR(TC_, 2); break;         \
+        case 4: SKR(TC_, 4); break;         \
+        case 8: SKR(TC_, 8); break;         \
+        case 16: SKR(TC_, 16); break;       \
+        case 32: SKR(TC_, 32); break;       \
+        default: SKR(TC_, 0); break;        \
+    }
+        if (c_dtype == CG_BF16) {
+            SKR_ANY(bf16_t)
+        } else {
+            SKR_ANY(float)
+        }
+#undef SKR_ANY
+#undef SKR
     } else if (split_k > 1) {
         const int64_t n = M * N;
         if (c_dtype == CG_BF16)
