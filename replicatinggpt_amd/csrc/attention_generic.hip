@@ -34,16 +34,27 @@ __global__ __launch_bounds__(256) void k_attn_dropmask(int64_t T_, int64_t nbh, 
     const int lane = threadIdx.x & 63;
     const uint64_t stream = dropout_stream(d.rng_call, d.site);
     const int64_t t0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * DM_TPW;
+    if (t0 >= total) return;
+    // (b*H + h, query tile, key tile) of the wave's first tile -- one division and root per wave;
+    // the following tiles step through the lower triangle incrementally
+    uint64_t bh = (uint64_t)(t0 / ntri);
+    const int tri0 = (int)(t0 - (int64_t)bh * ntri);
+    int qt = (int)((sqrtf(8.f * tri0 + 1.f) - 1.f) * 0.5f);
+    while ((qt + 1) * (qt + 2) / 2 <= tri0) ++qt;
+    while (qt * (qt + 1) / 2 > tri0) --qt;
+    int kt = tri0 - qt * (qt + 1) / 2;
 #pragma unroll 1
     for (int i = 0; i < DM_TPW; ++i) {
-        const int64_t t = t0 + i;
-        if (t >= total) return;
-        const uint64_t bh = (uint64_t)(t / ntri);
-        const int tri = (int)(t - (int64_t)bh * ntri);
-        int qt = (int)((sqrtf(8.f * tri + 1.f) - 1.f) * 0.5f);
-        while ((qt + 1) * (qt + 2) / 2 <= tri) ++qt;
-        while (qt * (qt + 1) / 2 > tri) --qt;
-        const int kt = tri - qt * (qt + 1) / 2;
+        if (t0 + i >= total) return;
+        if (i) {
+            if (++kt > qt) {
+                kt = 0;
+                if (++qt == NT) {
+                    qt = 0;
+                    ++bh;
+                }
+            }
+        }
         const uint64_t q = (uint64_t)qt * 16 + (lane & 15), key0 = (uint64_t)kt * 16 + 4 * (lane >> 4);
         const u32x4 r = philox_group(d.seed, stream, ((bh * T_ + q) * T_ + key0) >> 2);
         const uint64_t b0 = __ballot(r.x >= d.thr), b1 = __ballot(r.y >= d.thr);
