@@ -110,9 +110,102 @@ def gemm_census(cfg, Bsz, T, dev):
     out = []
     for name, m, n, k, at, bt, epi, cnt in census_shapes(cfg, Bsz, T):
         ms = time_gemm(m, n, k, at, bt, epi, dev)
+        split = Fn._wgrad_split(m, n, k, True) if epi == "wgrad" else 1
         out.append({"name": name, "M": m, "N": n, "K": k, "ms": ms, "launches": cnt, "flops": 2.0 * m * n * k,
-                    "split": Fn._wgrad_split(m, n, k, True) if epi == "wgrad" else 1})
+                    "split": split, "kernel": gemm_kernel_name(m, n, at, split, dev)})
     return out
+
+
+def gemm_kernel_name(M, N, at, split, dev):
+    """The kernel cg_gemm's default dispatch picks (gemm_bf16.hip fast_gemm_launch): the 8-wave
+    256x256 tile at >= 2 such tiles per CU (no split, A not transposed), else the 128x128 one."""
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    if split == 1 and not at and M % 256 == 0 and N % 256 == 0 and (M // 256) * (N // 256) >= 2 * cus:
+        return "k_gemm_p8<256x256>"
+    return "k_gemm_pk<128x128>" + (" + k_splitk_reduce4" if split > 1 else "")
+
+
+def _time_ms(fn, reps=20):
+    """Average duration (ms) of fn() over reps back-to-back calls, HIP events on the current stream
+    (the stream every charpt op launches on)."""
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def kernel_census(cfg, Bsz, T, dev):
+    """The non-GEMM kernels of the step at the step's shapes, each against its roofline (north_star:
+    MFMA utilisation for attention, achieved HBM GB/s for the norm / optimizer kernels):
+      attention fwd (incl. the Philox keep-bit kernel) / bwd: causal algorithmic FLOPs
+        fwd 4*B*H*(T(T+1)/2)*D, bwd 2x fwd (S recompute not counted) vs the bf16 MFMA peak;
+      LayerNorm fwd: M*C*(4 read + 2 write) B; LayerNorm bwd (dy bf16, x, residual grad, dx, the
+        consumer's dropout-applied bf16 copy): M*C*(2+4+4+4+2) B; AdamW: 30 B/param (p, g, m, v
+        fp32 + bf16 shadow) -- vs HBM peak."""
+    from replicatinggpt_amd import functional as Fn, ops
+    M, C, H = Bsz * T, cfg.n_embd, cfg.n_head
+    D = C // H
+    p = float(cfg.dropout)
+    out = {}
+    qkv = (torch.randn(M, 3 * C, device=dev) * 0.5).to(torch.bfloat16)
+    o = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
+    do = torch.randn(M, C, device=dev).to(torch.bfloat16)
+    call = torch.zeros(1, dtype=torch.int64, device=dev)
+    scale = C ** -0.5
+    st = {}
+
+    def fwd():
+        st["lse"], st["mask"] = Fn.attention_fwd(qkv, Bsz, T, H, D, o, scale, p, 1, call, 0)
+    t_f = _time_ms(fwd)
+    t_b = _time_ms(lambda: Fn.attention_bwd(qkv, Bsz, T, H, D, o, do, st["lse"], scale, p, 1, call, 0, st["mask"]))
+    fl = 4.0 * Bsz * H * (T * (T + 1) / 2) * D
+    for name, t, f in (("attention_fwd", t_f, fl), ("attention_bwd", t_b, 2 * fl)):
+        tf = f / (t * 1e-3) / 1e12
+        out[name] = {"ms": round(t, 4), "achieved": round(tf, 1), "unit": "TFLOP/s", "peak": PEAK_BF16_TFLOPS,
+                     "frac": round(tf / PEAK_BF16_TFLOPS, 4)}
+    del qkv, o, do
+    x = torch.randn(M, C, device=dev)
+    w, b = torch.randn(C, device=dev), torch.randn(C, device=dev)
+    y = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
+    mean, rstd = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    t = _time_ms(lambda: ops.layernorm_fwd(x, w, b, y, mean, rstd, 1e-5))
+    dy = torch.randn(M, C, device=dev).to(torch.bfloat16)
+    dres, dx = torch.randn(M, C, device=dev), torch.empty(M, C, device=dev)
+    lp = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
+    dw, db, cs = (torch.empty(C, device=dev) for _ in range(3))
+    ws = torch.empty(ops.layernorm_bwd_workspace(M, C) // 4 + 1, device=dev)
+    t2 = _time_ms(lambda: ops.layernorm_bwd(dy, x, w, mean, rstd, dres, dx, lp, dw, db, False, ws, cs, False, p, 1,
+                                            call, 3))
+    for name, tt, byts in (("layernorm_fwd", t, M * C * 6), ("layernorm_bwd", t2, M * C * 16)):
+        gbs = byts / (tt * 1e-3) / 1e9
+        out[name] = {"ms": round(tt, 4), "bytes": byts, "achieved": round(gbs, 1), "unit": "GB/s",
+                     "peak": PEAK_HBM_GBS, "frac": round(gbs / PEAK_HBM_GBS, 4)}
+    del x, y, dy, dres, dx, lp
+    n = sum(t.numel() for t in _param_shapes(cfg))
+    n = (n + 63) // 64 * 64
+    pp, g, m, v = (torch.randn(n, device=dev) * 0.01 for _ in range(4))
+    v.abs_()
+    p16 = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    step_t = torch.ones(1, dtype=torch.int64, device=dev)
+    t = _time_ms(lambda: ops.adamw(pp, g, m, v, p16, 1e-3, 0.9, 0.999, 1e-8, 0.01, step_t))
+    gbs = 30 * n / (t * 1e-3) / 1e9
+    out["adamw"] = {"ms": round(t, 4), "params": n, "bytes": 30 * n, "achieved": round(gbs, 1), "unit": "GB/s",
+                    "peak": PEAK_HBM_GBS, "frac": round(gbs / PEAK_HBM_GBS, 4)}
+    return out
+
+
+def _param_shapes(cfg):
+    """Parameter tensors of the model (for AdamW sizing) without building it."""
+    d, L, V, T = cfg.n_embd, cfg.n_layers, 65, cfg.block_size
+    shapes = [(V, d), (T, d), (d,), (d,), (V, d), (V,)]
+    for _ in range(L):
+        shapes += [(3 * d, d), (d, d), (d,), (4 * d, d), (4 * d,), (d, 4 * d), (d,), (d,), (d,), (d,), (d,)]
+    return [torch.empty(s, device="meta") for s in shapes]
 
 
 def gemm_family(census):
@@ -239,8 +332,7 @@ def main():
             dom = max(census, key=lambda c: c["ms"] * c["launches"])
             achieved = dom["flops"] / (dom["ms"] * 1e-3) / 1e12
             roofline = {"bound": "mfma", "kernel": f"cg_gemm bf16 {dom['name']} M={dom['M']} N={dom['N']} K={dom['K']}"
-                                                  f" (k_gemm_pk{' + k_splitk_reduce' if dom['split'] > 1 else ''},"
-                                                  f" split {dom['split']})",
+                                                  f" ({dom['kernel']}, split {dom['split']})",
                         "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                         "traffic": pmc_traffic(args.config, dom), "avg_launch_ms": round(dom["ms"], 5),
@@ -261,6 +353,7 @@ def main():
         }
         if census is not None:
             result["gemm_census_ms"] = {c["name"]: round(c["ms"], 4) for c in census}
+            result["kernel_census"] = kernel_census(cfg, Bsz, T, dev)
         if world == 1 and not args.no_generate:
             result["generate_c5"] = bench_generate(dev)
         if world == 1 and not args.no_cpu_baseline:
