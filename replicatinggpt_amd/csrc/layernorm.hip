@@ -58,7 +58,10 @@ __device__ __forceinline__ void ld_vec_any<bf16_t>(const bf16_t* p, float* v, in
 
 }  // namespace
 
-template <int VEC, int NJ, typename TY>
+// One wave per row, RPW rows per wave: every load of the wave's rows is issued before the first
+// reduction, and gamma/beta are held in registers for all of them (they were re-read after each
+// row's reductions, on the critical path).
+template <int VEC, int NJ, typename TY, int RPW>
 __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ x, const float* __restrict__ w,
                                                 const float* __restrict__ b, TY* __restrict__ y,
                                                 float* __restrict__ mean_out, float* __restrict__ rstd_out,
@@ -66,53 +69,71 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ x, con
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const float invC = 1.0f / (float)C;
-    for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < rows; r += (int64_t)gridDim.x * 4) {
-        const float* xr = x + r * C;
-        float v[NJ][VEC];
-        float s = 0.f;
+    float wv[NJ][VEC], bv[NJ][VEC];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int e = (j * 64 + lane) * VEC;
-            if (e < C) {
-                VecIO<VEC>::ld(xr + e, v[j]);
-            } else {
-#pragma unroll
-                for (int q = 0; q < VEC; ++q) v[j][q] = 0.f;
-            }
-#pragma unroll
-            for (int q = 0; q < VEC; ++q) s += v[j][q];
+    for (int j = 0; j < NJ; ++j) {
+        const int e = (j * 64 + lane) * VEC;
+        if (e < C) {
+            VecIO<VEC>::ld(w + e, wv[j]);
+            VecIO<VEC>::ld(b + e, bv[j]);
         }
-        const float mu = wave_sum_dpp(s) * invC;
-        float ss = 0.f;
+    }
+    const int64_t stride = (int64_t)gridDim.x * 4;
+    for (int64_t r0 = (int64_t)blockIdx.x * 4 + wave; r0 < rows; r0 += stride * RPW) {
+        float v[RPW][NJ][VEC];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int e = (j * 64 + lane) * VEC;
-            if (e < C) {
+        for (int i = 0; i < RPW; ++i) {
+            const int64_t r = r0 + i * stride < rows ? r0 + i * stride : r0;
 #pragma unroll
-                for (int q = 0; q < VEC; ++q) {
-                    const float d = v[j][q] - mu;
-                    ss += d * d;
+            for (int j = 0; j < NJ; ++j) {
+                const int e = (j * 64 + lane) * VEC;
+                if (e < C) {
+                    VecIO<VEC>::ld(x + r * C + e, v[i][j]);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < VEC; ++q) v[i][j][q] = 0.f;
                 }
             }
         }
-        const float var = wave_sum_dpp(ss) * invC;
-        const float rs = 1.0f / sqrtf(var + eps);
-        TY* yr = y + r * C;
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int e = (j * 64 + lane) * VEC;
-            if (e < C) {
-                float wv[VEC], bv[VEC], o[VEC];
-                VecIO<VEC>::ld(w + e, wv);
-                VecIO<VEC>::ld(b + e, bv);
+        for (int i = 0; i < RPW; ++i) {
+            const int64_t r = r0 + i * stride;
+            if (r >= rows) break;
+            float s = 0.f;
 #pragma unroll
-                for (int q = 0; q < VEC; ++q) o[q] = (v[j][q] - mu) * rs * wv[q] + bv[q];
-                VecIO<VEC>::st(yr + e, o);
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) s += v[i][j][q];
+            const float mu = wave_sum_dpp(s) * invC;
+            float ss = 0.f;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int e = (j * 64 + lane) * VEC;
+                if (e < C) {
+#pragma unroll
+                    for (int q = 0; q < VEC; ++q) {
+                        const float d = v[i][j][q] - mu;
+                        ss += d * d;
+                    }
+                }
             }
-        }
-        if (lane == 0) {
-            mean_out[r] = mu;
-            rstd_out[r] = rs;
+            const float var = wave_sum_dpp(ss) * invC;
+            const float rs = 1.0f / sqrtf(var + eps);
+            TY* yr = y + r * C;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int e = (j * 64 + lane) * VEC;
+                if (e < C) {
+                    float o[VEC];
+#pragma unroll
+                    for (int q = 0; q < VEC; ++q) o[q] = (v[i][j][q] - mu) * rs * wv[j][q] + bv[j][q];
+                    VecIO<VEC>::st(yr + e, o);
+                }
+            }
+            if (lane == 0) {
+                mean_out[r] = mu;
+                rstd_out[r] = rs;
+            }
         }
     }
 }
@@ -271,9 +292,10 @@ template <typename TY>
 int launch_ln_fwd(const float* x, const float* w, const float* b, TY* y, float* mean, float* rstd, int64_t rows,
                   int C, float eps, hipStream_t st) {
     const bool al16 = (((uintptr_t)x | (uintptr_t)w | (uintptr_t)b) & 15) == 0;
-    int grid = ceil_div(rows, 4);
+    constexpr int RPW = 2;
+    int grid = ceil_div(rows, 4 * RPW);
     grid = grid > 4096 ? 4096 : grid;
-#define LNF(V, N) k_ln_fwd<V, N, TY><<<grid, 256, 0, st>>>(x, w, b, y, mean, rstd, rows, C, eps)
+#define LNF(V, N) k_ln_fwd<V, N, TY, RPW><<<grid, 256, 0, st>>>(x, w, b, y, mean, rstd, rows, C, eps)
     if (C == 384 && al16) LNF(2, 3);
     else if (C == 768 && al16) LNF(4, 3);
     else if (C == 512 && al16) LNF(4, 2);
