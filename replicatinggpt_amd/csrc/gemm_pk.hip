@@ -51,6 +51,11 @@ struct DmaP {
         }
         kstep = TR ? (int64_t)FBK * ld : (int64_t)FBK;
     }
+    // instruction i (0..PER_WAVE-1) of one K-tile, from that K-tile's base address
+    __device__ __forceinline__ void issue1(const bf16_t* base, int i, char* img, int wave) const {
+        __builtin_amdgcn_global_load_lds((const void*)(base + off[i]), (lds_void*)(img + (wave * PER_WAVE + i) * 1024),
+                                         16, 0, 0);
+    }
     __device__ __forceinline__ void issue(const bf16_t* origin, int kt, char* img, int wave) const {
         const bf16_t* base = origin + kt * kstep;
 #pragma unroll
@@ -230,21 +235,30 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     int ij = 0, ikt = 0;
     const bf16_t* oa = A;
     const bf16_t* ob = B;
-    auto issue_next = [&](int buf) {
-        if (ikt == 0) {
-            int64_t m0, n0;
-            int sp;
-            decode(ij, m0, n0, sp);
-            const int64_t kb = sp * kchunk;
-            oa = AT ? A + kb * lda + m0 : A + m0 * lda + kb;
-            ob = BT ? B + kb * ldb + n0 : B + n0 * ldb + kb;
-        }
-        char* img = smem + buf * G::STAGE;
-        da.issue(oa, ikt, img, wave);
-        db.issue(ob, ikt, img + G::IMG_A, wave);
-        if (++ikt == nk) {
-            ikt = 0;
-            ++ij;
+    // The in-loop DMA is split from its address bookkeeping: prep_next() (branchy: item decode at
+    // item boundaries) runs before the fragment reads and yields the K-tile's base addresses; the
+    // LPT wave-instructions themselves are then issued one per 4 MFMAs (each costs ~60 issue
+    // cycles -- MI355X_MICROARCH.md -- which now overlap the MFMAs instead of preceding them).
+    // Past the last K-tile the same (valid) addresses are loaded again into the free stage, which
+    // nothing reads; the loop drains them before the wave exits.
+    const bf16_t* na = A;
+    const bf16_t* nbp = B;
+    auto prep_next = [&](bool real) {
+        if (real) {
+            if (ikt == 0) {
+                int64_t m0, n0;
+                int sp;
+                decode(ij, m0, n0, sp);
+                const int64_t kb = sp * kchunk;
+                oa = AT ? A + kb * lda + m0 : A + m0 * lda + kb;
+                ob = BT ? B + kb * ldb + n0 : B + n0 * ldb + kb;
+            }
+            na = oa + ikt * da.kstep;
+            nbp = ob + ikt * db.kstep;
+            if (++ikt == nk) {
+                ikt = 0;
+                ++ij;
+            }
         }
     };
 
@@ -256,7 +270,14 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
 
 #pragma unroll
     for (int s = 0; s < NBUF - 1; ++s)
-        if (s < total) issue_next(s);
+        if (s < total) {
+            prep_next(true);
+            char* img = smem + s * G::STAGE;
+#pragma unroll
+            for (int i = 0; i < DA::PER_WAVE; ++i) da.issue1(na, i, img, wave);
+#pragma unroll
+            for (int i = 0; i < DB::PER_WAVE; ++i) db.issue1(nbp, i, img + G::IMG_A, wave);
+        }
 
     // An item's epilogue issues exactly EPI_OPS vector stores (one per 16x16 fragment: dwordx2 bf16,
     // dwordx4 fp32 or split-K slab; checked in the ISA).  They are the youngest VMEM operations at
@@ -292,11 +313,10 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         stored = false;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (g + NBUF - 1 < total) {
-            int nb = cur + NBUF - 1;
-            if (nb >= NBUF) nb -= NBUF;
-            issue_next(nb);
-        }
+        int nb = cur + NBUF - 1;
+        if (nb >= NBUF) nb -= NBUF;
+        prep_next(g + NBUF - 1 < total);
+        char* dimg = smem + nb * G::STAGE;
         const char* imgA = smem + cur * G::STAGE;
         const char* imgB = imgA + G::IMG_A;
         // both 32-deep halves' fragments are read before the first MFMA (sched_barrier pins it):
@@ -310,14 +330,28 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
             for (int i = 0; i < 4; ++i) af[s][i] = frag<AT, BM>(imgA, wm * 64 + i * 16, s, lane);
         }
         __builtin_amdgcn_sched_barrier(0);
+        // 8 groups of 4 MFMAs (half s, A fragment i); the next stage's DMA instructions in between
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int t = 0; t < 8; ++t) {
+            const int s = t >> 2, i = t & 3;
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = mfma_bf16(bf[s][j], af[s][i], acc[i][j]);
-            __builtin_amdgcn_sched_barrier(0);
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma_bf16(bf[s][j], af[s][i], acc[i][j]);
+            if (t < LPT) {
+                if (t < DA::PER_WAVE) da.issue1(na, t, dimg, wave);
+                else db.issue1(nbp, t - DA::PER_WAVE, dimg + G::IMG_A, wave);
+            }
         }
+#pragma unroll
+        for (int t = 8; t < LPT; ++t) {
+            if (t < DA::PER_WAVE) da.issue1(na, t, dimg, wave);
+            else db.issue1(nbp, t - DA::PER_WAVE, dimg + G::IMG_A, wave);
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+            if (t < LPT) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
         cur = cur + 1 == NBUF ? 0 : cur + 1;
         if (++ckt == nk) {
             // item done: acc[i][j][r] = C[mw + 16i + (lane&15)][nw + 16j + 4(lane>>4) + r]
@@ -348,6 +382,7 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
             stored = true;
         }
     }
+    wait_vm<0>();  // the dummy DMAs past the last K-tile land before the workgroup's LDS is released
 }
 
 int cu_count() {
