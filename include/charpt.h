@@ -110,6 +110,16 @@ int cg_layernorm_bwd_ex(const void* dy, int dy_dtype, const float* x, const floa
                         uint64_t lp_seed, const uint64_t* lp_rng_call, int lp_site, float* dw, float* db,
                         float* lp_colsum, int accumulate, int colsum_accumulate, void* workspace, int64_t rows,
                         int64_t C, void* stream);
+/* cg_layernorm_bwd_ex in two launches, so the column-sum reduce can run off the critical path:
+   _rows writes dx / lp_out and leaves the per-block column partials (dw, db, and with lp_colsum=1
+   the lp_out column sums) in the workspace; _reduce (any stream ordered after _rows) folds them
+   into dw / db / lp_colsum exactly as cg_layernorm_bwd_ex does (same order, same bits).       */
+int cg_layernorm_bwd_rows(const void* dy, int dy_dtype, const float* x, const float* w, const float* mean,
+                          const float* rstd, const float* dres, float* dx, uint16_t* lp_out, double lp_dropout_p,
+                          uint64_t lp_seed, const uint64_t* lp_rng_call, int lp_site, int lp_colsum,
+                          void* workspace, int64_t rows, int64_t C, void* stream);
+int cg_layernorm_bwd_reduce(const void* workspace, int64_t rows, int64_t C, int lp_colsum_partials, float* dw,
+                            float* db, float* lp_colsum, int accumulate, int colsum_accumulate, void* stream);
 
 /* ---- GEMM (nn.Linear fwd/dgrad/wgrad: GPT1.py:111-112,121,136,143,145,184) -------------
    C[m,n] = epilogue( sum_k A(m,k) * B(n,k) )

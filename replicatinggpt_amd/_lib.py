@@ -45,6 +45,9 @@ _SIGS = {
     "cg_layernorm_bwd": (c_int, [P, c_int, P, P, P, P, P, P, P, P, P, c_int, P, c_i64, c_i64, P]),
     "cg_layernorm_bwd_ex": (c_int, [P, c_int, P, P, P, P, P, P, P, c_dbl, c_u64, P, c_int, P, P, P, c_int, c_int, P,
                                     c_i64, c_i64, P]),
+    "cg_layernorm_bwd_rows": (c_int, [P, c_int, P, P, P, P, P, P, P, c_dbl, c_u64, P, c_int, c_int, P, c_i64, c_i64,
+                                      P]),
+    "cg_layernorm_bwd_reduce": (c_int, [P, c_i64, c_i64, c_int, P, P, P, c_int, c_int, P]),
     "cg_gemm_workspace": (c_i64, [c_i64, c_i64, c_int]),
     "cg_gemm": (c_int, [c_int, c_int, c_int, c_i64, c_i64, c_i64, P, c_i64, P, c_i64, P, c_int, c_i64,
                         ctypes.POINTER(Epilogue), c_int, P, P]),

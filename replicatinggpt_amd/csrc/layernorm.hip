@@ -308,7 +308,7 @@ int launch_ln_fwd(const float* x, const float* w, const float* b, TY* y, float* 
 template <typename TDY>
 int launch_ln_bwd(const TDY* dy, const float* x, const float* w, const float* mean, const float* rstd,
                   const float* dres, float* dx, const LnLp& lp, float* dw, float* db, float* dbias, int accumulate,
-                  int dbias_accumulate, float* part, int64_t rows, int C, hipStream_t st) {
+                  int dbias_accumulate, float* part, int64_t rows, int C, int defer, hipStream_t st) {
     const bool al16 = (((uintptr_t)x | (uintptr_t)w | (uintptr_t)dx | (uintptr_t)(dres ? dres : x)) & 15) == 0 &&
                       (((uintptr_t)dy) & 7) == 0 && (((uintptr_t)(lp.out ? lp.out : (bf16_t*)x)) & 7) == 0;
     const int64_t nblk = (rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
@@ -322,7 +322,8 @@ int launch_ln_bwd(const TDY* dy, const float* x, const float* w, const float* me
     else if (C == 1024 && al16) LNB(4, 4, 4, 1);
     else LNB(1, 32, 4, 1);
 #undef LNB
-    if (dw || db || dbias) launch_reduce_partials3(part, nblk, NP * C, dw, db, dbias, C, accumulate, dbias_accumulate, st);
+    if (!defer && (dw || db || dbias))
+        launch_reduce_partials3(part, nblk, NP * C, dw, db, dbias, C, accumulate, dbias_accumulate, st);
     return CG_OK;
 }
 }  // namespace
@@ -341,11 +342,11 @@ extern "C" int64_t cg_layernorm_bwd_workspace(int64_t rows, int64_t C) {
     return ((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS) * 3 * C * (int64_t)sizeof(float);
 }
 
-extern "C" int cg_layernorm_bwd_ex(const void* dy, int dy_dtype, const float* x, const float* w, const float* mean,
+static int layernorm_bwd_impl(const void* dy, int dy_dtype, const float* x, const float* w, const float* mean,
                                    const float* rstd, const float* dres, float* dx, uint16_t* lp_out,
                                    double lp_dropout_p, uint64_t lp_seed, const uint64_t* lp_rng_call, int lp_site,
                                    float* dw, float* db, float* lp_colsum, int accumulate, int colsum_accumulate,
-                                   void* workspace, int64_t rows, int64_t C, void* stream) {
+                                   void* workspace, int64_t rows, int64_t C, int defer, void* stream) {
     CG_REQUIRE(rows > 0 && C > 0 && C <= 1024, "cg_layernorm_bwd: need 0 < C <= 1024");
     CG_REQUIRE(lp_dropout_p >= 0 && lp_dropout_p < 1, "cg_layernorm_bwd_ex: dropout p must be in [0, 1)");
     CG_REQUIRE(!lp_colsum || lp_out, "cg_layernorm_bwd_ex: lp_colsum needs lp_out");
@@ -360,11 +361,46 @@ extern "C" int cg_layernorm_bwd_ex(const void* dy, int dy_dtype, const float* x,
     lp.csum = lp_colsum != nullptr;
     if (dy_dtype == CG_BF16)
         launch_ln_bwd<bf16_t>((const bf16_t*)dy, x, w, mean, rstd, dres, dx, lp, dw, db, lp_colsum, accumulate,
-                              colsum_accumulate, (float*)workspace, rows, (int)C, st);
+                              colsum_accumulate, (float*)workspace, rows, (int)C, defer, st);
     else
         launch_ln_bwd<float>((const float*)dy, x, w, mean, rstd, dres, dx, lp, dw, db, lp_colsum, accumulate,
-                             colsum_accumulate, (float*)workspace, rows, (int)C, st);
+                             colsum_accumulate, (float*)workspace, rows, (int)C, defer, st);
     CG_LAUNCH_CHECK("cg_layernorm_bwd");
+    return CG_OK;
+}
+
+extern "C" int cg_layernorm_bwd_ex(const void* dy, int dy_dtype, const float* x, const float* w, const float* mean,
+                                   const float* rstd, const float* dres, float* dx, uint16_t* lp_out,
+                                   double lp_dropout_p, uint64_t lp_seed, const uint64_t* lp_rng_call, int lp_site,
+                                   float* dw, float* db, float* lp_colsum, int accumulate, int colsum_accumulate,
+                                   void* workspace, int64_t rows, int64_t C, void* stream) {
+    return layernorm_bwd_impl(dy, dy_dtype, x, w, mean, rstd, dres, dx, lp_out, lp_dropout_p, lp_seed, lp_rng_call,
+                              lp_site, dw, db, lp_colsum, accumulate, colsum_accumulate, workspace, rows, C, 0, stream);
+}
+
+// The row kernel alone: its per-block column partials stay in the workspace for
+// cg_layernorm_bwd_reduce (which the caller may launch on another stream, after this one).
+extern "C" int cg_layernorm_bwd_rows(const void* dy, int dy_dtype, const float* x, const float* w, const float* mean,
+                                     const float* rstd, const float* dres, float* dx, uint16_t* lp_out,
+                                     double lp_dropout_p, uint64_t lp_seed, const uint64_t* lp_rng_call, int lp_site,
+                                     int lp_colsum, void* workspace, int64_t rows, int64_t C, void* stream) {
+    // dw/db only gate the (deferred) reduce; lp_colsum needs a non-null marker to select 3 partials
+    float* marker = lp_colsum ? (float*)workspace : nullptr;
+    return layernorm_bwd_impl(dy, dy_dtype, x, w, mean, rstd, dres, dx, lp_out, lp_dropout_p, lp_seed, lp_rng_call,
+                              lp_site, nullptr, nullptr, marker, 0, 0, workspace, rows, C, 1, stream);
+}
+
+extern "C" int cg_layernorm_bwd_reduce(const void* workspace, int64_t rows, int64_t C, int lp_colsum_partials,
+                                       float* dw, float* db, float* lp_colsum, int accumulate, int colsum_accumulate,
+                                       void* stream) {
+    CG_REQUIRE(rows > 0 && C > 0 && C <= 1024, "cg_layernorm_bwd_reduce: need 0 < C <= 1024");
+    CG_REQUIRE(!lp_colsum || lp_colsum_partials, "cg_layernorm_bwd_reduce: lp_colsum needs the colsum partials");
+    if (!dw && !db && !lp_colsum) return CG_OK;
+    const int64_t nblk = (rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
+    const int NP = lp_colsum_partials ? 3 : 2;
+    launch_reduce_partials3((const float*)workspace, nblk, NP * C, dw, db, lp_colsum, C, accumulate,
+                            colsum_accumulate, (hipStream_t)stream);
+    CG_LAUNCH_CHECK("cg_layernorm_bwd_reduce");
     return CG_OK;
 }
 

@@ -14,6 +14,7 @@ buffer ("grad slots"), see ``Region``; the residual-stream gradient is fp32, act
 GEMM operands are bf16 (or fp32 in exact mode).
 """
 import contextlib
+import os
 import math
 
 import torch
@@ -69,6 +70,8 @@ class SideStream:
 
 
 SIDE = SideStream()
+# LayerNorm backward column-sum reduce on the side stream (CHARPT_LN_REDUCE_SIDE=0: in line, for A/B runs)
+LN_REDUCE_SIDE = os.environ.get("CHARPT_LN_REDUCE_SIDE", "1") != "0"
 
 
 def site_stream(call, site):
@@ -291,9 +294,22 @@ def layernorm_bwd(dy2, x2, w_reg, b_reg, mean, rstd, dres=None, want_lp=False, l
         gcs, bcs, fcs = link.bias.grad_target()
     ws = torch.empty(ops.layernorm_bwd_workspace(rows, C) // 4 + 1, dtype=torch.float32, device=dev)
     p = float(link.p) if use_link else 0.0
-    ops.layernorm_bwd(dy2, x2, w_reg.master, mean, rstd, dres, dx, lp, gw, gb, bool(bw or bb), ws, gcs, bool(bcs), p,
-                      int(link.seed) if use_link else 0, link.rng_call if (use_link and p > 0) else None,
-                      int(link.site) if use_link else 0)
+    seed, rng, site = (int(link.seed) if use_link else 0), (link.rng_call if (use_link and p > 0) else None), \
+        (int(link.site) if use_link else 0)
+    # the column-sum reduce (LN weight/bias grads, the consumer's bias grad) only feeds the optimizer:
+    # when every target is a flat gradient slot (read after SIDE.join) it runs on the side stream,
+    # off the dgrad chain; otherwise (tensors handed back to autograd) in line
+    side = LN_REDUCE_SIDE and SIDE.enabled and dev.type == "cuda" and (gw is not None or gb is not None or gcs is not None) and \
+        (gw is None or gw is w_reg.slot) and (gb is None or gb is b_reg.slot) and \
+        (gcs is None or gcs is link.bias.slot)
+    if side:
+        ops.layernorm_bwd_rows(dy2, x2, w_reg.master, mean, rstd, dres, dx, lp, ws, gcs is not None, p, seed, rng,
+                               site)
+        with SIDE.run(dev, ws):
+            ops.layernorm_bwd_reduce(ws, rows, C, gcs is not None, gw, gb, gcs, bool(bw or bb), bool(bcs))
+    else:
+        ops.layernorm_bwd(dy2, x2, w_reg.master, mean, rstd, dres, dx, lp, gw, gb, bool(bw or bb), ws, gcs, bool(bcs),
+                          p, seed, rng, site)
     if use_link:
         link.lp, link.dx_ptr, link.bias_done = lp, dx.data_ptr(), gcs is not None
         if fcs is not None:

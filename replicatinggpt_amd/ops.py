@@ -112,6 +112,29 @@ def layernorm_bwd(dy: Tensor, x: Tensor, w: Tensor, mean: Tensor, rstd: Tensor, 
             "layernorm_bwd")
 
 
+@_op("layernorm_bwd_rows", ("dx", "dx_lp", "ws"))
+def layernorm_bwd_rows(dy: Tensor, x: Tensor, w: Tensor, mean: Tensor, rstd: Tensor, dres: Optional[Tensor],
+                       dx: Tensor, dx_lp: Optional[Tensor], ws: Tensor, lp_colsum: bool, lp_p: float, lp_seed: int,
+                       lp_rng_call: Optional[Tensor], lp_site: int) -> None:
+    """layernorm_bwd without its column-sum reduce: the partials stay in ``ws`` for
+    layernorm_bwd_reduce (launched on any stream ordered after this one)."""
+    C = x.shape[-1]
+    rows = x.numel() // C
+    L.check(L.load().cg_layernorm_bwd_rows(L.ptr(dy), L.dtype_code(dy.dtype), L.ptr(x), L.ptr(w), L.ptr(mean),
+                                           L.ptr(rstd), L.ptr(dres), L.ptr(dx), L.ptr(dx_lp), lp_p, lp_seed,
+                                           L.ptr(lp_rng_call), lp_site, int(lp_colsum), L.ptr(ws), rows, C, _s(x)),
+            "layernorm_bwd_rows")
+
+
+@_op("layernorm_bwd_reduce", ("dw", "db", "lp_colsum"))
+def layernorm_bwd_reduce(ws: Tensor, rows: int, C: int, colsum_partials: bool, dw: Optional[Tensor],
+                         db: Optional[Tensor], lp_colsum: Optional[Tensor], accumulate: bool,
+                         colsum_accumulate: bool) -> None:
+    L.check(L.load().cg_layernorm_bwd_reduce(L.ptr(ws), rows, C, int(colsum_partials), L.ptr(dw), L.ptr(db),
+                                             L.ptr(lp_colsum), int(accumulate), int(colsum_accumulate), _s(ws)),
+            "layernorm_bwd_reduce")
+
+
 def layernorm_bwd_workspace(rows, C):
     return L.load().cg_layernorm_bwd_workspace(rows, C)
 

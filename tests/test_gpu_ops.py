@@ -86,6 +86,45 @@ def test_layernorm(C, out_dtype):
     assert relerr(grads[1], br2.grad) < 1e-5
 
 
+@pytest.mark.parametrize("C", [384, 768, 126])
+@pytest.mark.parametrize("with_link", [False, True])
+def test_layernorm_bwd_rows_then_reduce_is_bitwise_ex(C, with_link):
+    """cg_layernorm_bwd_rows + cg_layernorm_bwd_reduce on a second stream (the training path's
+    side-stream split) == cg_layernorm_bwd_ex bit for bit: dx, the consumer's dropout-applied bf16
+    copy, dgamma / dbeta (accumulated) and the copy's column sums."""
+    torch.manual_seed(3)
+    O = ops()
+    rows = 1000
+    x = (torch.randn(rows, C) * 2 + 0.5).to(DEV)
+    w = (torch.randn(C) * 0.1 + 1).to(DEV)
+    mean, rstd = x.mean(1), x.var(1, unbiased=False).add(1e-5).rsqrt()
+    dy = torch.randn(rows, C, device=DEV).to(torch.bfloat16)
+    dres = torch.randn(rows, C, device=DEV)
+    call = torch.tensor([9], dtype=torch.int64, device=DEV)
+    p = 0.2 if with_link else 0.0
+    outs = []
+    for split in (False, True):
+        dx = torch.empty(rows, C, device=DEV)
+        lp = torch.empty(rows, C, dtype=torch.bfloat16, device=DEV) if with_link else None
+        dw, db = torch.ones(C, device=DEV), torch.ones(C, device=DEV)
+        cs = torch.ones(C, device=DEV) if with_link else None
+        ws = torch.full((O.layernorm_bwd_workspace(rows, C) // 4 + 1,), float("nan"), device=DEV)
+        if split:
+            O.layernorm_bwd_rows(dy, x, w, mean, rstd, dres, dx, lp, ws, with_link, p, 11, call if p else None, 4)
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                O.layernorm_bwd_reduce(ws, rows, C, with_link, dw, db, cs, True, True)
+            torch.cuda.current_stream().wait_stream(side)
+        else:
+            O.layernorm_bwd(dy, x, w, mean, rstd, dres, dx, lp, dw, db, True, ws, cs, True, p, 11,
+                            call if p else None, 4)
+        torch.cuda.synchronize()
+        outs.append([t.cpu() for t in (dx, lp, dw, db, cs) if t is not None])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def _ref_gemm(A, B, at, bt):
     a = A.double().t() if at else A.double()
     b = B.double().t() if bt else B.double()
