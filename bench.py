@@ -64,8 +64,8 @@ def cpu_baseline(cfg, seconds=12.0):
 
 
 def time_gemm(M, N, K, at, bt, epi, dev, reps=30):
-    """Average duration (ms) of one charpt bf16 GEMM launch of this shape, HIP events on the
-    launch stream."""
+    """Average duration (ms) of one charpt bf16 GEMM launch of this shape: reps back-to-back
+    launches replayed from one hipGraph, HIP events on the replay stream."""
     from replicatinggpt_amd import functional as Fn, ops
     A = torch.randn((K, M) if at else (M, K), device=dev).to(torch.bfloat16)
     B = torch.randn((K, N) if bt else (N, K), device=dev).to(torch.bfloat16)
@@ -81,10 +81,18 @@ def time_gemm(M, N, K, at, bt, epi, dev, reps=30):
                  0.0, 0, None, 0, 0.0, split, ws)
     for _ in range(3):
         run()
+    # the reps launches replayed from a hipGraph, as in the training step: eagerly, the smallest
+    # products (C2 proj fwd / dgrad, 15 us kernels) are host-launch-bound at ~27 us per call
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        for _ in range(reps):
+            run()
+    g.replay()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(reps):
-        run()
+    g.replay()
     e.record()
     e.synchronize()
     return s.elapsed_time(e) / reps

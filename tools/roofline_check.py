@@ -26,7 +26,7 @@ def main():
     i, bursts = 0, []
     while i < len(rows):
         found = False
-        for period in (2, 1):
+        for period in (1, 2):
             j = i
             while j + period < len(rows) and names[j + period] == names[j] and \
                     ("gemm" in names[j] or "splitk" in names[j]):
