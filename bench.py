@@ -134,14 +134,21 @@ def gemm_kernel_name(M, N, at, split, dev):
 
 
 def _time_ms(fn, reps=20):
-    """Average duration (ms) of fn() over reps back-to-back calls, HIP events on the current stream
-    (the stream every charpt op launches on)."""
+    """Average duration (ms) of fn() over reps back-to-back calls replayed from one hipGraph (as in
+    the training step; eagerly the small LayerNorm launches are host-bound), HIP events on the
+    replay stream (the stream every charpt op launches on)."""
     for _ in range(3):
         fn()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        for _ in range(reps):
+            fn()
+    g.replay()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(reps):
-        fn()
+    g.replay()
     e.record()
     e.synchronize()
     return s.elapsed_time(e) / reps
