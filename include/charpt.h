@@ -52,6 +52,11 @@ typedef struct {
     const uint64_t* rng_call; /* device scalar                                               */
     int site;
     float beta;               /* out = epi(acc) + beta * out   (beta in {0,1}: grad accumulate) */
+    float* colpart;           /* CG_EPI_RELU_BWD, bf16, beta 0, split 1 only, and only where the
+                                 dispatch takes the 128x128 persistent kernel (else CG_EINVAL):
+                                 column sums of each 64-row block of the (fp32, pre-rounding)
+                                 output, [M/64][N] -- the consumer's bias-gradient partials,
+                                 folded by cg_reduce_rows.  NULL: none.                     */
 } cg_epilogue_t;
 
 const char* cg_last_error_string(void);
@@ -128,6 +133,8 @@ int cg_layernorm_bwd_reduce(const void* workspace, int64_t rows, int64_t C, int 
    c_dtype: output dtype.  split_k > 1 (CG_EPI_STORE/BIAS only) needs workspace of
    cg_gemm_workspace(M,N,split_k) bytes; results are deterministic for any split_k.            */
 int64_t cg_gemm_workspace(int64_t M, int64_t N, int split_k);
+/* out[n] (=|+=) sum_r part[r*N + n] over rows r in order (fixed order: deterministic)          */
+int cg_reduce_rows(const float* part, int64_t rows, int64_t N, float* out, int accumulate, void* stream);
 int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
             const void* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const cg_epilogue_t* epi, int split_k,
             void* workspace, void* stream);

@@ -22,7 +22,7 @@ c_i64, c_int, c_dbl, c_flt, c_u64, P = ctypes.c_int64, ctypes.c_int, ctypes.c_do
 class Epilogue(ctypes.Structure):
     _fields_ = [("kind", c_int), ("bias", P), ("resid", P), ("ld_resid", c_i64), ("aux", P), ("aux_dtype", c_int),
                 ("ld_aux", c_i64), ("dropout_p", c_dbl), ("seed", c_u64), ("rng_call", P), ("site", c_int),
-                ("beta", c_flt)]
+                ("beta", c_flt), ("colpart", P)]
 
 
 _SIGS = {
@@ -49,6 +49,7 @@ _SIGS = {
                                       P]),
     "cg_layernorm_bwd_reduce": (c_int, [P, c_i64, c_i64, c_int, P, P, P, c_int, c_int, P]),
     "cg_gemm_workspace": (c_i64, [c_i64, c_i64, c_int]),
+    "cg_reduce_rows": (c_int, [P, c_i64, c_i64, P, c_int, P]),
     "cg_gemm": (c_int, [c_int, c_int, c_int, c_i64, c_i64, c_i64, P, c_i64, P, c_i64, P, c_int, c_i64,
                         ctypes.POINTER(Epilogue), c_int, P, P]),
     "cg_colsum_workspace": (c_i64, [c_i64, c_i64]),

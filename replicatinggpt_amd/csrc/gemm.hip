@@ -348,6 +348,7 @@ EpiArgs make_epi(const cg_epilogue_t* e) {
     a.rng_call = e->rng_call;
     a.site = e->site;
     a.beta = e->beta;
+    a.colpart = e->colpart;
     return a;
 }
 
@@ -419,6 +420,10 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
     if (op_dtype == CG_BF16 && fast_gemm_launch(a_trans, b_trans, M, N, K, (const bf16_t*)A, lda,
                                                 (const bf16_t*)B, ldb, C, c_dtype, ldc, e, split_k,
                                                 (float*)workspace, st)) {
+    } else if (e.colpart) {
+        set_error("cg_gemm: colpart needs the 128x128 persistent bf16 kernel (bf16, NT/NN, beta 0, split 1, "
+                  "M %% 128 == 0, default dispatch)");
+        return CG_EINVAL;
     } else if (op_dtype == CG_BF16) {
         launch_generic<bf16_t, bf16_t>(a_trans, b_trans, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k,
                                        workspace, st);
@@ -464,6 +469,13 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
                                                                      (float*)C, ldc, e);
     }
     CG_LAUNCH_CHECK("cg_gemm");
+    return CG_OK;
+}
+
+extern "C" int cg_reduce_rows(const float* part, int64_t rows, int64_t N, float* out, int accumulate, void* stream) {
+    CG_REQUIRE(part && out && rows > 0 && N > 0, "cg_reduce_rows: bad arguments");
+    launch_reduce_partials(part, rows, N, out, nullptr, N, accumulate, (hipStream_t)stream);
+    CG_LAUNCH_CHECK("cg_reduce_rows");
     return CG_OK;
 }
 

@@ -191,6 +191,9 @@ bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf1
         const int64_t t256 = (M / 256) * (N / 256);
         v = (!at && split_k == 1 && M % 256 == 0 && N % 256 == 0 && t256 >= 2 * (int64_t)gemm_cu_count()) ? 24 : 9;
     }
+    // only the 128x128 persistent kernel's ReLU-backward epilogue writes column partials
+    if (e.colpart && (v != 9 || e.kind != CG_EPI_RELU_BWD || e.aux_dtype != CG_BF16 || e.beta != 0.f || split_k != 1 || at))
+        return false;
     if (v >= 20 && p8_gemm_launch(v, at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st))
         return true;
     if (v >= 20) v = 2;

@@ -18,6 +18,7 @@ struct EpiArgs {
     const uint64_t* rng_call;
     int site;
     float beta;
+    float* colpart;  // RELU_BWD: per-64-row-block column sums (k_gemm_pk only)
 };
 
 __device__ __forceinline__ float aux_at(const EpiArgs& e, int64_t m, int64_t n) {

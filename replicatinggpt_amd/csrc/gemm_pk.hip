@@ -99,13 +99,40 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    fv4 v = acc[i][j];
+                    fv4& v = acc[i][j];
                     v[0] = __uint_as_float(h[i][j].x << 16) > 0.f ? v[0] : 0.f;
                     v[1] = __uint_as_float(h[i][j].x & 0xffff0000u) > 0.f ? v[1] : 0.f;
                     v[2] = __uint_as_float(h[i][j].y << 16) > 0.f ? v[2] : 0.f;
                     v[3] = __uint_as_float(h[i][j].y & 0xffff0000u) > 0.f ? v[3] : 0.f;
-                    store4_plain(v, mr + 16 * i, nc + 16 * j, Cv, c_dtype, ldc);
                 }
+            if (epi.colpart) {
+                // the consumer's bias gradient, fused: column sums of this wave's 64 rows (rows
+                // 16i + lane&15 of each column 16j + 4(lane>>4) + q: 4 rows per lane, then a
+                // butterfly over the 16 lanes of the column group), lane r = 0 of each group writes.
+                // These stores precede the item's 16 output stores, which stay the youngest
+                // EPI_OPS vector-memory operations the main loop's wait counts assume.
+                const int lane = threadIdx.x & 63;
+                float* cp = epi.colpart + ((mr - (lane & 15)) >> 6) * N + nc;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    fv4 t;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        float s = ((acc[0][j][q] + acc[1][j][q]) + acc[2][j][q]) + acc[3][j][q];
+                        s += __shfl_xor(s, 1);
+                        s += __shfl_xor(s, 2);
+                        s += __shfl_xor(s, 4);
+                        s += __shfl_xor(s, 8);
+                        t[q] = s;
+                    }
+                    if ((lane & 15) == 0) *(fv4*)(cp + 16 * j) = t;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) store4_plain(acc[i][j], mr + 16 * i, nc + 16 * j, Cv, c_dtype, ldc);
         } else {
             float4 h[4][4];
 #pragma unroll

@@ -72,6 +72,8 @@ class SideStream:
 SIDE = SideStream()
 # LayerNorm backward column-sum reduce on the side stream (CHARPT_LN_REDUCE_SIDE=0: in line, for A/B runs)
 LN_REDUCE_SIDE = os.environ.get("CHARPT_LN_REDUCE_SIDE", "1") != "0"
+# FFN b1 gradient fused into the ReLU-backward dgrad epilogue (CHARPT_FUSE_COLPART=0: separate colsum)
+FUSE_COLPART = os.environ.get("CHARPT_FUSE_COLPART", "1") != "0"
 
 
 def site_stream(call, site):
@@ -236,6 +238,23 @@ def linear_wgrad(dy2, x2, out, beta):
     ops.gemm(dy2, x2, out, _is_bf16(dy2.dtype), True, True, N, K, M, N, K, out.stride(0), L.EPI_STORE, None, None, 0,
              None, 0, 0.0, 0, None, 0, float(beta), split, ws)
     return out
+
+
+def _colpart_ok(dy2, w, aux):
+    """Whether cg_gemm's default dispatch runs the ReLU-backward dgrad out[M,F] = relu_bwd(dy2 @ w)
+    on the 128x128 persistent kernel, whose epilogue can also write the output's column partials
+    (csrc/gemm_bf16.hip fast_gemm_launch: the 8-wave 256x256 tile takes over at >= 2 such tiles per
+    CU, e.g. every C4 product; an explicit gemm_variant tuning disables the fusion)."""
+    if not (FUSE_COLPART and _is_bf16(dy2.dtype) and _is_bf16(aux.dtype) and dy2.is_cuda):
+        return False
+    M, K = dy2.shape
+    F = w.shape[1]
+    if M % 128 or F % 128 or K % 64 or "gemm_variant" in os.environ.get("CHARPT_TUNING", ""):
+        return False
+    if dy2.stride(0) % 8 or w.stride(0) % 8 or aux.stride(0) % 8 or dy2.stride(1) != 1 or w.stride(1) != 1:
+        return False
+    cus = _gemm_slots() // 2
+    return not (M % 256 == 0 and F % 256 == 0 and (M // 256) * (F // 256) >= 2 * cus)
 
 
 def colsum_into(x2, out, beta):
@@ -515,14 +534,27 @@ class FFNSublayerFn(torch.autograd.Function):
             if g_b2 is not None and not bias_done:
                 colsum_into(dz2, g_b2, beta_b2)
         dz1 = torch.empty_like(h)
-        linear_dgrad(dz2, w2.operand(act), dz1, "relu_bwd", aux=h)
         g_w1, beta_w1, f_w1 = w1.grad_target()
         g_b1, beta_b1, f_b1 = b1.grad_target()
-        with SIDE.run(dev, dz1, a):
+        part = None
+        if g_b1 is not None and _colpart_ok(dz2, w2.operand(act), h):
+            # b1's gradient (column sums of dz1) fused into the ReLU-backward dgrad's epilogue as
+            # per-64-row partials; only their fold runs on the side stream
+            M, F4 = h.shape
+            part = torch.empty((M // 64, F4), dtype=torch.float32, device=dev)
+            wt = w2.operand(act)
+            ops.gemm_relu_bwd_colpart(dz2, wt, dz1, M, F4, dz2.shape[1], dz2.stride(0), wt.stride(0), dz1.stride(0),
+                                      h, h.stride(0), part)
+        else:
+            linear_dgrad(dz2, w2.operand(act), dz1, "relu_bwd", aux=h)
+        with SIDE.run(dev, dz1, a, part):
             if g_w1 is not None:
                 linear_wgrad(dz1, a, g_w1, beta_w1)
             if g_b1 is not None:
-                colsum_into(dz1, g_b1, beta_b1)
+                if part is not None:
+                    ops.reduce_rows(part, part.shape[0], part.shape[1], g_b1, bool(beta_b1))
+                else:
+                    colsum_into(dz1, g_b1, beta_b1)
         da = torch.empty((B * T, C), dtype=act, device=x2.device)
         linear_dgrad(dz1, w1.operand(act), da)
         dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd, dres=d32, link=ctx.in_link)

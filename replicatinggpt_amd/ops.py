@@ -153,6 +153,23 @@ def gemm(a: Tensor, b: Tensor, out: Tensor, op_bf16: bool, a_trans: bool, b_tran
             "gemm")
 
 
+@_op("gemm_relu_bwd_colpart", ("out", "colpart"))
+def gemm_relu_bwd_colpart(a: Tensor, b: Tensor, out: Tensor, M: int, N: int, K: int, lda: int, ldb: int, ldc: int,
+                          aux: Tensor, ld_aux: int, colpart: Tensor) -> None:
+    """out = relu_bwd(a[M,K] @ b[N,K]^T, aux) in bf16 with the column sums of every 64-row block of
+    the output into colpart [M/64, N] (the consumer's bias-gradient partials; cg_reduce_rows folds
+    them).  Fails (CG_EINVAL) unless the dispatch takes the 128x128 persistent kernel."""
+    e = L.Epilogue(L.EPI_RELU_BWD, None, None, 0, L.ptr(aux), L.dtype_code(aux.dtype), ld_aux, 0.0, 0, None, 0, 0.0,
+                   L.ptr(colpart))
+    L.check(L.load().cg_gemm(L.CG_BF16, 0, 1, M, N, K, L.ptr(a), lda, L.ptr(b), ldb, L.ptr(out),
+                             L.dtype_code(out.dtype), ldc, e, 1, None, _s(out)), "gemm_relu_bwd_colpart")
+
+
+@_op("reduce_rows", ("out",))
+def reduce_rows(part: Tensor, rows: int, N: int, out: Tensor, accumulate: bool) -> None:
+    L.check(L.load().cg_reduce_rows(L.ptr(part), rows, N, L.ptr(out), int(accumulate), _s(out)), "reduce_rows")
+
+
 def gemm_workspace(M, N, split_k):
     return L.load().cg_gemm_workspace(M, N, split_k)
 

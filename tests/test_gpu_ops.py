@@ -125,6 +125,29 @@ def test_layernorm_bwd_rows_then_reduce_is_bitwise_ex(C, with_link):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("M,F,K", [(512, 384, 128), (1024, 1536, 384), (16384, 1536, 384)])
+def test_relu_bwd_colpart_matches_colsum(M, F, K):
+    """The ReLU-backward dgrad with fused column partials (cg_epilogue_t.colpart): the output is
+    bitwise the plain relu_bwd GEMM's, and the folded partials equal the column sums of the fp32
+    (pre-rounding) output to 1e-5 relative."""
+    O = ops()
+    torch.manual_seed(5)
+    dy = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(K, F, device=DEV) * 0.05).to(torch.bfloat16)
+    h = torch.relu(torch.randn(M, F, device=DEV)).to(torch.bfloat16)
+    ref = torch.empty(M, F, dtype=torch.bfloat16, device=DEV)
+    O.gemm(dy, w, ref, True, False, True, M, F, K, K, F, F, 5, None, None, 0, h, F, 0.0, 0, None, 0, 0.0, 1, None)
+    out = torch.empty_like(ref)
+    part = torch.full((M // 64, F), float("nan"), device=DEV)
+    O.gemm_relu_bwd_colpart(dy, w, out, M, F, K, K, F, F, h, F, part)
+    cs = torch.empty(F, device=DEV)
+    O.reduce_rows(part, M // 64, F, cs, False)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    want = ((dy.double() @ w.double()) * (h.double() > 0)).sum(0)
+    assert relerr(cs, want) < 1e-5
+
+
 def _ref_gemm(A, B, at, bt):
     a = A.double().t() if at else A.double()
     b = B.double().t() if bt else B.double()
