@@ -33,34 +33,56 @@ def flops_per_token(cfg, T):
     return 6 * (L * 12 * d * d + d * V) + 6 * L * (T + 1) * d
 
 
-def cpu_baseline(cfg, seconds=12.0):
-    """The oracle (CPU fp32 restatement of GPT1.py, 'port') timed on this host, bounded sample:
-    batch 4 x block 256 of the same model, fwd+bwd+AdamW per step."""
+def _cpu_info():
+    """Host CPU model (lscpu 'Model name') and the cores this process may run on."""
+    model = None
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    return model, cores
+
+
+def cpu_baseline(cfg, seconds=12.0, batch=16):
+    """The oracle (CPU fp32 restatement of GPT1.py, 'port') timed on this host on the benchmarked
+    workload: the same model shape and block size, dropout ON through torch's own CPU dropout op
+    (nn.Dropout's bernoulli_, the reference's dominant CPU cost -- SURVEY §6), fwd + bwd + AdamW,
+    all cores this process may use.  Bounded sample: ``batch`` sequences per step (the bench's 64 at
+    C2 take ~4 s per CPU step; per-token throughput is batch-independent at B >= 16) for ~``seconds``."""
     from oracle import gpt1_oracle as O
-    torch.set_num_threads(min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+    model_name, cores = _cpu_info()
+    torch.set_num_threads(cores)
     ocfg = O.OracleConfig(vocab_size=cfg.vocab_size, block_size=cfg.block_size, n_embd=cfg.n_embd,
-                          n_head=cfg.n_head, n_layers=cfg.n_layers, dropout=0.0)
+                          n_head=cfg.n_head, n_layers=cfg.n_layers, dropout=cfg.dropout, torch_dropout=True)
     torch.manual_seed(1337)
     P = O.init_params(ocfg)
     opt = O.AdamWOracle(P, lr=2e-4)
-    Bc = 4
     g = torch.Generator().manual_seed(1)
-    x = torch.randint(0, 65, (Bc, cfg.block_size), generator=g)
-    y = torch.randint(0, 65, (Bc, cfg.block_size), generator=g)
-    _, _, gr = O.loss_and_grads(P, x, y, ocfg)   # warm-up
+    x = torch.randint(0, 65, (batch, cfg.block_size), generator=g)
+    y = torch.randint(0, 65, (batch, cfg.block_size), generator=g)
+    _, _, gr = O.loss_and_grads(P, x, y, ocfg, train=True)   # warm-up
     opt.step(gr)
     n, t0 = 0, time.perf_counter()
     while True:
-        _, _, gr = O.loss_and_grads(P, x, y, ocfg)
+        _, _, gr = O.loss_and_grads(P, x, y, ocfg, train=True)
         opt.step(gr)
         n += 1
         if time.perf_counter() - t0 > seconds and n >= 2:
             break
     dt = time.perf_counter() - t0
-    return {"value": round(n * Bc * cfg.block_size / dt, 1), "unit": "tokens/s", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": f"oracle fp32 fwd+bwd+AdamW, {n} steps of batch {Bc} x block {cfg.block_size}, "
-                      f"{cfg.n_layers}L/{cfg.n_head}H/{cfg.n_embd}d, dropout 0 (CPU cost of dropout excluded)"}
+    return {"value": round(n * batch * cfg.block_size / dt, 1), "unit": "tokens/s", "cores": torch.get_num_threads(),
+            "kind": "port", "cpu_model": model_name,
+            "sample": f"oracle fp32 train step (fwd+bwd+AdamW, dropout {cfg.dropout} via torch CPU bernoulli_ as "
+                      f"GPT1.py:117,146), {n} steps of batch {batch} x block {cfg.block_size}, "
+                      f"{cfg.n_layers}L/{cfg.n_head}H/{cfg.n_embd}d (the bench workload's shape)"}
 
 
 def time_gemm(M, N, K, at, bt, epi, dev, reps=30):
@@ -245,11 +267,33 @@ def pmc_traffic(config, dom):
     return op["hbm_bytes"]
 
 
+PEAK_FP32_TFLOPS = 157.3     # MI355X f32 MFMA / vector peak (MI355X_MICROARCH.md)
+
+
+def generate_flops(cfg, B, L0, new):
+    """Algorithmic forward FLOPs of GPT1.py's generate(): while the context fits the
+    block, one new token per sequence per step against the cached prefix,
+    2 (L 12 d^2 + d V) + 4 L t d (t = current length); once it slides (Q7: positions re-indexed, no
+    K/V reuse), the full block_size-token window forward per step -- GEMMs 2 T (L 12 d^2), causal
+    attention 4 L d T (T+1)/2, lm_head on the last row 2 d V."""
+    L, d, V, T = cfg.n_layers, cfg.n_embd, cfg.vocab_size, cfg.block_size
+    total = 0.0
+    for i in range(new):
+        t = L0 + i + 1
+        if t <= T:
+            total += 2 * (L * 12 * d * d + d * V) + 4 * L * t * d
+        else:
+            total += 2 * T * (L * 12 * d * d) + 4 * L * d * T * (T + 1) / 2 + 2 * d * V
+    return B * total
+
+
 def bench_generate(dev, B=256, new=500):
     """BASELINE configs[4] (C5): generate() batched decode, 256 sequences x 500 new tokens from
     the reference-trained C1-shape weights (tests/golden/model_c1_trained.safetensors -- the
-    model.pth of GPT1.py:239-241 as produced by the reference), fp32, greedy, through the
-    decode engine (K/V-cached prefix phase + sliding-window phase, one hipGraph per phase)."""
+    model.pth of GPT1.py:239-241 as produced by the reference), fp32, through the decode engine
+    (K/V-cached prefix phase + sliding-window phase, one hipGraph per phase): greedy (the parity
+    mode) and sampled (GPT1.py:206-208's multinomial, device inverse-CDF draw).  ``frac`` =
+    algorithmic forward FLOPs (generate_flops) / time against the fp32 peak (the model runs fp32)."""
     from safetensors.torch import load_file
     from replicatinggpt_amd import BigramLanguageModel, GPTConfig
     sd = load_file(os.path.join(ROOT, "tests", "golden", "model_c1_trained.safetensors"))
@@ -257,18 +301,28 @@ def bench_generate(dev, B=256, new=500):
     m.load_state_dict(sd, strict=False)
     m = m.to(dev).eval()
     idx = torch.zeros((B, 1), dtype=torch.long, device=dev)
+    res = {}
     with torch.no_grad():
-        m.generate(idx, new, greedy=True)              # capture + warm-up
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        out = m.generate(idx, new, greedy=True)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
+        for mode, greedy in (("greedy", True), ("sampled", False)):
+            gen = torch.Generator().manual_seed(1337)
+            m.generate(idx, new, greedy=greedy, generator=gen)       # capture + warm-up
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = m.generate(idx, new, greedy=greedy, generator=gen)
+            torch.cuda.synchronize()
+            res[mode] = (time.perf_counter() - t0, int(out.sum()))
     T = m.config.block_size
+    fl = generate_flops(m.config, B, 1, new)
+    dt, ck = res["greedy"]
+    ach = fl / dt / 1e12
     return {"metric": "generate tokens/sec (C5: 256 seqs x 500 new tokens, model.pth C1 shape, fp32 greedy)",
             "value": round(B * new / dt, 1), "unit": "tokens/s", "seconds": round(dt, 4),
             "phases": {"kv_cached_steps": T, "sliding_window_steps": new - T},
-            "checksum": int(out.sum())}
+            "roofline": {"bound": "mfma_f32", "achieved": round(ach, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(ach / PEAK_FP32_TFLOPS, 4), "flops": fl},
+            "sampled": {"value": round(B * new / res["sampled"][0], 1), "unit": "tokens/s",
+                        "seconds": round(res["sampled"][0], 4)},
+            "checksum": ck}
 
 
 def main():
@@ -305,7 +359,6 @@ def main():
     T = cfg.block_size
     torch.manual_seed(cfg.seed)
     model = BigramLanguageModel(cfg).to(dev)
-    model.config.dropout_seed = cfg.dropout_seed + 7919 * rank
     opt = AdamW(model.parameters(), lr=cfg.learning_rate).attach(model)
     stream = TokenStream.synthetic(device=dev)
     sampler = BatchSampler(stream, T, Bsz, world_size=world, rank=rank,

@@ -54,8 +54,8 @@ typedef struct {
     float beta;               /* out = epi(acc) + beta * out   (beta in {0,1}: grad accumulate) */
     float* colpart;           /* CG_EPI_RELU_BWD, bf16, beta 0, split 1 only, and only where the
                                  dispatch takes the 128x128 persistent kernel (else CG_EINVAL):
-                                 column sums of each 64-row block of the (fp32, pre-rounding)
-                                 output, [M/64][N] -- the consumer's bias-gradient partials,
+                                 column sums of each 64-row block of the output (of its bf16-
+                                 rounded values, as cg_colsum would see them), [M/64][N] -- the consumer's bias-gradient partials,
                                  folded by cg_reduce_rows.  NULL: none.                     */
 } cg_epilogue_t;
 
@@ -133,6 +133,11 @@ int cg_layernorm_bwd_reduce(const void* workspace, int64_t rows, int64_t C, int 
    c_dtype: output dtype.  split_k > 1 (CG_EPI_STORE/BIAS only) needs workspace of
    cg_gemm_workspace(M,N,split_k) bytes; results are deterministic for any split_k.            */
 int64_t cg_gemm_workspace(int64_t M, int64_t N, int split_k);
+/* 1 if cg_gemm (bf16, split_k 1, CG_EPI_RELU_BWD with bf16 aux, beta 0) can fill epi->colpart for
+   this problem under the current dispatch and tuning knobs (16-B aligned operands assumed), else 0
+   -- the caller then computes the bias gradient with cg_colsum instead.                          */
+int cg_gemm_colpart_supported(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
+                              int64_t ldc);
 /* out[n] (=|+=) sum_r part[r*N + n] over rows r in order (fixed order: deterministic)          */
 int cg_reduce_rows(const float* part, int64_t rows, int64_t N, float* out, int accumulate, void* stream);
 int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
@@ -205,8 +210,9 @@ int cg_decode_embed(const int64_t* idx, int64_t ld, const float* wte, const floa
 int cg_decode_kv_append(const float* qkv, int64_t ld, int64_t k_off, int64_t v_off, int64_t B, int64_t H,
                         int64_t D, int64_t Tmax, const int64_t* len_dev, float* kcache, float* vcache,
                         void* stream);
-/* one query per (b, h) against keys 0..n-1 (n = *len_dev, or nkeys when len_dev is NULL);
-   K/V element (b, h, j, e) at base + b*sb + h*sh + j*sj + e; o[b, h*D + e]; D <= 64            */
+/* one query per (b, h) against keys 0..n-1 (n = *len_dev, or nkeys when len_dev is NULL; any n
+   >= 1: online softmax over 16-key chunks); K/V element (b, h, j, e) at base + b*sb + h*sh + j*sj
+   + e; o[b, h*D + e]; D <= 64                                                                    */
 int cg_decode_attn(const float* q, int64_t ldq, const float* k, const float* v, int64_t sb, int64_t sh, int64_t sj,
                    int64_t B, int64_t H, int64_t D, const int64_t* len_dev, int64_t nkeys, float scale, float* o,
                    int64_t ldo, void* stream);

@@ -26,6 +26,10 @@ class OracleConfig:
     n_head: int = 6               # GPT1.py:21
     n_layers: int = 6             # GPT1.py:22
     dropout: float = 0.2          # GPT1.py:23
+    # timing mode for the CPU baseline (bench.py): dropout through torch's own CPU op, as
+    # nn.Dropout does it in the reference (bernoulli_ on the CPU generator, GPT1.py:117,146) --
+    # the cost the reference pays; masks are then not the Philox ones, so never for parity
+    torch_dropout: bool = False
 
     @property
     def head_size(self):          # n_embd // n_head, GPT1.py:156
@@ -151,7 +155,9 @@ def attention(xn, P, prefix, cfg, train, seed, stream, scale_dim=None):
         s = (q @ k.transpose(-2, -1)) * scale             # GPT1.py:114
         s = s.masked_fill(~causal, float("-inf"))         # GPT1.py:115
         p = torch.softmax(s, dim=-1)                      # GPT1.py:116
-        if train and cfg.dropout > 0:                     # GPT1.py:117
+        if train and cfg.dropout > 0 and cfg.torch_dropout:
+            p = F.dropout(p, cfg.dropout, training=True)  # GPT1.py:117 as the reference runs it
+        elif train and cfg.dropout > 0:                   # GPT1.py:117
             bi = torch.arange(B)[:, None, None]
             qi = torch.arange(T)[None, :, None]
             ki = torch.arange(T)[None, None, :]
@@ -167,7 +173,9 @@ def feed_forward(xn, P, prefix, cfg, train, seed, stream):
     """FeedForward.net (GPT1.py:142-147): Linear -> ReLU -> Linear -> Dropout."""
     h = torch.relu(xn @ P[prefix + "ffwd.net.0.weight"].t() + P[prefix + "ffwd.net.0.bias"])
     y = h @ P[prefix + "ffwd.net.2.weight"].t() + P[prefix + "ffwd.net.2.bias"]
-    if train and cfg.dropout > 0:
+    if train and cfg.dropout > 0 and cfg.torch_dropout:
+        y = F.dropout(y, cfg.dropout, training=True)      # GPT1.py:146 as the reference runs it
+    elif train and cfg.dropout > 0:
         idx = np.arange(y.numel(), dtype=np.uint64).reshape(y.shape)
         y = _dropout(y, cfg.dropout, seed, stream, idx)
     return y

@@ -7,12 +7,14 @@ replaces them with Philox4x32-10 (Salmon et al., SC'11; Random123) keyed by a pe
 and addressed by (stream, element index), so that forward and backward regenerate the same
 mask and so that this oracle can apply the *identical* mask on the CPU.
 
-Mask spec (shared with csrc/philox.h):
-  group = idx >> 2, word = idx & 3
+Mask spec (shared with csrc/common.h): 16-bit decisions, 8 consecutive elements per Philox call
+  group = idx >> 3, word = (idx >> 1) & 3, half = idx & 1
   ctr   = (group & 0xffffffff, group >> 32, stream & 0xffffffff, stream >> 32)
   key   = (seed & 0xffffffff, seed >> 32)
-  keep  = philox4x32_10(ctr, key)[word] >= threshold(p),  threshold = min(round(p*2^32), 2^32-1)
-  kept values are scaled by float32(1/(1-p)).
+  u16   = (philox4x32_10(ctr, key)[word] >> (16 * half)) & 0xffff
+  keep  = u16 >= threshold(p),  threshold = clamp(round(p * 2^16), 1, 2^16 - 1) for p > 0
+  kept values are scaled by float32(1/(1-p)).  (p = 0.2: threshold 13107, keep probability
+  52429/65536 = 0.7999878.)
 """
 import numpy as np
 
@@ -41,17 +43,21 @@ def philox4x32_10(c0, c1, c2, c3, k0, k1):
 
 
 def threshold(p):
-    return min(int(round(p * 4294967296.0)), 0xFFFFFFFF)
+    if not p > 0:
+        return 0
+    return min(max(int(round(p * 65536.0)), 1), 0xFFFF)
 
 
 def keep_mask(seed, stream, idx, p):
     """Boolean keep-mask for element indices ``idx`` (any int array)."""
     idx = np.asarray(idx, dtype=np.uint64)
-    group = idx >> np.uint64(2)
-    word = (idx & np.uint64(3)).astype(np.int64)
+    group = idx >> np.uint64(3)
+    word = ((idx >> np.uint64(1)) & np.uint64(3)).astype(np.int64)
+    half = idx & np.uint64(1)
     seed = np.uint64(seed)
     stream = np.uint64(stream)
     out = philox4x32_10(group & MASK32, group >> np.uint64(32), stream & MASK32, stream >> np.uint64(32),
                         seed & MASK32, seed >> np.uint64(32))
     r = np.choose(word, out)
-    return r >= np.uint64(threshold(p))
+    u16 = (r >> (np.uint64(16) * half)) & np.uint64(0xFFFF)
+    return u16 >= np.uint64(threshold(p))

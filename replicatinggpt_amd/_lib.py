@@ -49,6 +49,7 @@ _SIGS = {
                                       P]),
     "cg_layernorm_bwd_reduce": (c_int, [P, c_i64, c_i64, c_int, P, P, P, c_int, c_int, P]),
     "cg_gemm_workspace": (c_i64, [c_i64, c_i64, c_int]),
+    "cg_gemm_colpart_supported": (c_int, [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64]),
     "cg_reduce_rows": (c_int, [P, c_i64, c_i64, P, c_int, P]),
     "cg_gemm": (c_int, [c_int, c_int, c_int, c_i64, c_i64, c_i64, P, c_i64, P, c_i64, P, c_int, c_i64,
                         ctypes.POINTER(Epilogue), c_int, P, P]),

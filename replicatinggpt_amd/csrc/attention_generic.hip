@@ -22,54 +22,69 @@ using namespace cg;
 namespace {
 
 
-// one wave per 16x16 (query tile, key tile) on or below the diagonal, DM_TPW tiles per wave over
-// the flattened (b*H + h, lower-triangle tile) sequence: no idle waves above the diagonal and
-// enough work per wave that the launch is not dispatch-bound (B*H*NT(NT+1)/2 tiles in all).
-constexpr int DM_TPW = 8;
+// Keep bits of the MFMA kernels (attention_common.h mask_tile), for the 16x16 (query tile, key
+// tile) blocks on or below the diagonal, flattened over (b*H + h, lower-triangle tile).  One wave
+// handles a PAIR of consecutive tiles per step: lane l takes tile l>>5, query row l&15 and keys
+// 8((l>>4)&1) .. +7 -- one Philox call gives those 8 decisions (16 bits each).  The ballot words
+// (bit l' <-> query l'&15, key 4(l'>>4) + w) then need, per tile, one cross-lane fetch of the
+// source lane's 8 bits: lane l' reads lane 32*tile + 16(l'>>5) + (l'&15), bits 4((l'>>4)&1) + w.
+// DM_PPW pairs per wave (no idle waves above the diagonal; enough work per wave that the launch
+// is not dispatch-bound).
+constexpr int DM_PPW = 8;
+__device__ __forceinline__ void tri_next(uint64_t& bh, int& qt, int& kt, int NT) {
+    if (++kt > qt) {
+        kt = 0;
+        if (++qt == NT) {
+            qt = 0;
+            ++bh;
+        }
+    }
+}
 __global__ __launch_bounds__(256) void k_attn_dropmask(int64_t T_, int64_t nbh, uint64_t* __restrict__ mask,
                                                        DropArgs d) {
     const int NT = (int)(T_ >> 4);
     const int64_t ntri = (int64_t)NT * (NT + 1) / 2;
     const int64_t total = nbh * ntri;
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, t = lane >> 5;
     const uint64_t stream = dropout_stream(d.rng_call, d.site);
-    const int64_t t0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * DM_TPW;
-    if (t0 >= total) return;
-    // (b*H + h, query tile, key tile) of the wave's first tile -- one division and root per wave;
-    // the following tiles step through the lower triangle incrementally
-    uint64_t bh = (uint64_t)(t0 / ntri);
-    const int tri0 = (int)(t0 - (int64_t)bh * ntri);
+    const int64_t first = (((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * DM_PPW) * 2;  // first tile of the wave
+    if (first >= total) return;
+    // (b*H + h, query tile, key tile) of this lane's tile first + t: one division and root per
+    // wave, then incremental steps through the lower triangle
+    uint64_t bh = (uint64_t)(first / ntri);
+    const int tri0 = (int)(first - (int64_t)bh * ntri);
     int qt = (int)((sqrtf(8.f * tri0 + 1.f) - 1.f) * 0.5f);
     while ((qt + 1) * (qt + 2) / 2 <= tri0) ++qt;
     while (qt * (qt + 1) / 2 > tri0) --qt;
     int kt = tri0 - qt * (qt + 1) / 2;
+    if (t) tri_next(bh, qt, kt, NT);
+    const int src_lo = 16 * (lane >> 5) + (lane & 15), sub = 4 * ((lane >> 4) & 1);
 #pragma unroll 1
-    for (int i = 0; i < DM_TPW; ++i) {
-        if (t0 + i >= total) return;
+    for (int i = 0; i < DM_PPW; ++i) {
+        const int64_t tile0 = first + 2 * i;
+        if (tile0 >= total) return;
         if (i) {
-            if (++kt > qt) {
-                kt = 0;
-                if (++qt == NT) {
-                    qt = 0;
-                    ++bh;
-                }
-            }
+            tri_next(bh, qt, kt, NT);
+            tri_next(bh, qt, kt, NT);
         }
-        const uint64_t q = (uint64_t)qt * 16 + (lane & 15), key0 = (uint64_t)kt * 16 + 4 * (lane >> 4);
-        const u32x4 r = philox_group(d.seed, stream, ((bh * T_ + q) * T_ + key0) >> 2);
-        const uint64_t b0 = __ballot(r.x >= d.thr), b1 = __ballot(r.y >= d.thr);
-        const uint64_t b2 = __ballot(r.z >= d.thr), b3 = __ballot(r.w >= d.thr);
-        if (lane == 0) {
-            uint64_t* o = mask + (((bh * NT + qt) * NT + kt) << 2);
-            *(uint4*)o = make_uint4((uint32_t)b0, (uint32_t)(b0 >> 32), (uint32_t)b1, (uint32_t)(b1 >> 32));
-            *(uint4*)(o + 2) = make_uint4((uint32_t)b2, (uint32_t)(b2 >> 32), (uint32_t)b3, (uint32_t)(b3 >> 32));
+        const uint64_t q = (uint64_t)qt * 16 + (lane & 15), key0 = (uint64_t)kt * 16 + 8 * ((lane >> 4) & 1);
+        const uint32_t bits = keep8_bits(philox_group(d.seed, stream, ((bh * T_ + q) * T_ + key0) >> 3), d.thr);
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+            const uint32_t v = (uint32_t)__shfl((int)bits, 32 * tt + src_lo, 64);
+            const uint64_t b0 = __ballot((v >> sub) & 1u), b1 = __ballot((v >> (sub + 1)) & 1u);
+            const uint64_t b2 = __ballot((v >> (sub + 2)) & 1u), b3 = __ballot((v >> (sub + 3)) & 1u);
+            if (lane == 32 * tt && tile0 + tt < total) {
+                uint64_t* o = mask + (((bh * NT + qt) * NT + kt) << 2);
+                *(uint4*)o = make_uint4((uint32_t)b0, (uint32_t)(b0 >> 32), (uint32_t)b1, (uint32_t)(b1 >> 32));
+                *(uint4*)(o + 2) = make_uint4((uint32_t)b2, (uint32_t)(b2 >> 32), (uint32_t)b3, (uint32_t)(b3 >> 32));
+            }
         }
     }
 }
 
 __device__ __forceinline__ bool keep_elem(const DropArgs& d, uint64_t stream, uint64_t idx) {
-    const u32x4 r = philox_group(d.seed, stream, idx >> 2);
-    return philox_word(r, (int)(idx & 3)) >= d.thr;
+    return keep_of(philox_of(d.seed, stream, idx), idx, d.thr);
 }
 
 // =====================================================================================
@@ -504,7 +519,7 @@ int64_t mask_bytes(int64_t B, int64_t H, int64_t T) { return B * H * (T / 16) * 
 void launch_dropmask(int64_t B, int64_t H, int64_t T, uint64_t* mask, const DropArgs& d, hipStream_t st) {
     const int64_t NT = T / 16;
     const int64_t tiles = B * H * NT * (NT + 1) / 2;
-    k_attn_dropmask<<<ceil_div(tiles, 4 * DM_TPW), 256, 0, st>>>(T, B * H, mask, d);
+    k_attn_dropmask<<<ceil_div(tiles, 4 * 2 * DM_PPW), 256, 0, st>>>(T, B * H, mask, d);
 }
 
 bool fast_attn_ok(int dtype, int64_t T, int64_t D, const void* a, const void* b, const void* c, int64_t ld1,

@@ -24,9 +24,10 @@ __global__ __launch_bounds__(256) void k_ce_fwd(const float* __restrict__ logits
     if (lane == 0) {
         lse[r] = l;
         if (targets && loss_rows) {
-            int64_t t = targets[r];
-            t = t < 0 ? 0 : (t >= V ? V - 1 : t);
-            loss_rows[r] = l - x[t];
+            // F.cross_entropy raises on a target outside [0, V) (ignore_index is never produced by
+            // GPT1.py): the row loss turns NaN instead, so a bad label cannot pass silently
+            const int64_t t = targets[r];
+            loss_rows[r] = (t < 0 || t >= V) ? __builtin_nanf("") : l - x[t];
         }
     }
 }
@@ -48,10 +49,9 @@ __global__ void k_ce_bwd(const float* __restrict__ logits, int64_t rows, int V, 
     const int64_t r = i / V;
     const int v = (int)(i % V);
     const float g = *gp * g_mult;
-    int64_t t = targets[r];
-    t = t < 0 ? 0 : (t >= V ? V - 1 : t);
+    const int64_t t = targets[r];
     const float p = expf(logits[r * ld + v] - lse[r]);
-    const float d = g * (p - (v == t ? 1.f : 0.f));
+    const float d = (t < 0 || t >= V) ? __builtin_nanf("") : g * (p - (v == t ? 1.f : 0.f));
     if (dlogits) dlogits[r * ldd + v] = d;
     if (dlp) dlp[r * ldd + v] = f2bf(d);
 }
@@ -83,6 +83,7 @@ __device__ __forceinline__ float adam_one(float p, float g, float& m, float& v, 
     return __fadd_rn(p, __fdiv_rn(__fmul_rn(s.neg_step, m), denom));
 }
 
+template <bool VEC>
 __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const float* __restrict__ g,
                                                float* __restrict__ m, float* __restrict__ v, bf16_t* __restrict__ pb,
                                                int64_t n, double lr, double beta1, double beta2, double eps,
@@ -101,7 +102,7 @@ __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const floa
     const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
     for (int64_t i = i0; i < n; i += stride) {
-        if (i + 3 < n) {
+        if (VEC && i + 3 < n) {
             float4 pv = *(float4*)(p + i), gv = *(const float4*)(g + i), mv = *(float4*)(m + i), vv = *(float4*)(v + i);
             pv.x = adam_one(pv.x, gv.x, mv.x, vv.x, s);
             pv.y = adam_one(pv.y, gv.y, mv.y, vv.y, s);
@@ -112,7 +113,7 @@ __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const floa
             *(float4*)(v + i) = vv;
             if (pb) *(uint2*)(pb + i) = make_uint2(pack_bf2(pv.x, pv.y), pack_bf2(pv.z, pv.w));
         } else {
-            for (int64_t j = i; j < n; ++j) {
+            for (int64_t j = i; j < n && j < i + 4; ++j) {
                 float mm = m[j], vv = v[j];
                 const float np = adam_one(p[j], g[j], mm, vv, s);
                 p[j] = np;
@@ -129,13 +130,18 @@ extern "C" int cg_adamw(float* p, const float* g, float* m, float* v, uint16_t* 
                         void* stream) {
     CG_REQUIRE(n >= 0, "cg_adamw: n < 0");
     if (n == 0) return CG_OK;
-    CG_REQUIRE((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0 &&
-                   (((uintptr_t)p_bf16) & 7) == 0,
-               "cg_adamw: buffers must be 16-B aligned");
+    // the flat buffers are 16-B aligned; a single parameter's slice (torch-AdamW-style skipping of
+    // grad-None parameters, optim.py) may not be: element-wise path
+    const bool vec = (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0 &&
+                     (((uintptr_t)p_bf16) & 7) == 0;
     int grid = ceil_div((n + 3) / 4, 256);
     grid = grid > 8192 ? 8192 : grid;
-    k_adamw<<<grid, 256, 0, (hipStream_t)stream>>>(p, g, m, v, (bf16_t*)p_bf16, n, lr, beta1, beta2, eps,
-                                                   weight_decay, step_ptr);
+    if (vec)
+        k_adamw<true><<<grid, 256, 0, (hipStream_t)stream>>>(p, g, m, v, (bf16_t*)p_bf16, n, lr, beta1, beta2, eps,
+                                                             weight_decay, step_ptr);
+    else
+        k_adamw<false><<<grid, 256, 0, (hipStream_t)stream>>>(p, g, m, v, (bf16_t*)p_bf16, n, lr, beta1, beta2, eps,
+                                                              weight_decay, step_ptr);
     CG_LAUNCH_CHECK("cg_adamw");
     return CG_OK;
 }

@@ -109,7 +109,9 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
 
 // ---------------------------------------------------------------------------------------
 // Philox4x32-10 counter-based dropout RNG (spec: oracle/philox.py; DESIGN.md "Dropout").
-//   element idx -> ctr = (idx>>2 lo, idx>>2 hi, stream lo, stream hi), key = seed, word idx&3
+// 16-bit keep decisions, 8 consecutive elements per Philox call:
+//   element idx -> ctr = (idx>>3 lo, idx>>3 hi, stream lo, stream hi), key = seed,
+//   u16 = half (idx&1) of word ((idx>>1)&3);  keep = u16 >= thr (thr = round(p * 2^16))
 // ---------------------------------------------------------------------------------------
 struct u32x4 {
     uint32_t x, y, z, w;
@@ -134,7 +136,7 @@ __device__ __forceinline__ u32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_
     return {c0, c1, c2, c3};
 }
 
-// the four consecutive elements [4*group, 4*group+4)
+// Philox output of one counter group (elements [8*group, 8*group+8) of a dropout stream)
 __device__ __forceinline__ u32x4 philox_group(uint64_t seed, uint64_t stream, uint64_t group) {
     return philox4x32_10((uint32_t)group, (uint32_t)(group >> 32), (uint32_t)stream, (uint32_t)(stream >> 32),
                          (uint32_t)seed, (uint32_t)(seed >> 32));
@@ -144,15 +146,48 @@ __device__ __forceinline__ uint32_t philox_word(const u32x4& r, int w) {
     return w == 0 ? r.x : (w == 1 ? r.y : (w == 2 ? r.z : r.w));
 }
 
+// Philox of the group holding element idx
+__device__ __forceinline__ u32x4 philox_of(uint64_t seed, uint64_t stream, uint64_t idx) {
+    return philox_group(seed, stream, idx >> 3);
+}
+
+// keep decision of element idx from its group's Philox output r
+__device__ __forceinline__ bool keep_of(const u32x4& r, uint64_t idx, uint32_t thr) {
+    const uint32_t w = philox_word(r, (int)((idx >> 1) & 3));
+    return ((idx & 1) ? (w >> 16) : (w & 0xffffu)) >= thr;
+}
+
+// keep bits (bit q <-> element idx + q) of the 4 consecutive elements idx..idx+3, idx % 4 == 0:
+// one Philox call, half of its output
+__device__ __forceinline__ uint32_t keep4_bits(uint64_t seed, uint64_t stream, uint64_t idx, uint32_t thr) {
+    const u32x4 r = philox_group(seed, stream, idx >> 3);
+    const bool hi = (idx >> 2) & 1;
+    const uint32_t a = hi ? r.z : r.x, b = hi ? r.w : r.y;
+    return (uint32_t)((a & 0xffffu) >= thr) | ((uint32_t)((a >> 16) >= thr) << 1) |
+           ((uint32_t)((b & 0xffffu) >= thr) << 2) | ((uint32_t)((b >> 16) >= thr) << 3);
+}
+
+// keep bits of 8 consecutive elements 8*group .. 8*group+7 (bit e <-> element 8*group + e)
+__device__ __forceinline__ uint32_t keep8_bits(const u32x4& r, uint32_t thr) {
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+    uint32_t bits = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const uint32_t u = (e & 1) ? (w[e >> 1] >> 16) : (w[e >> 1] & 0xffffu);
+        bits |= (uint32_t)(u >= thr) << e;
+    }
+    return bits;
+}
+
 __device__ __forceinline__ uint64_t dropout_stream(const uint64_t* rng_call, int site) {
     return (rng_call ? (*rng_call << 8) : 0ull) | (uint64_t)(site & 0xff);
 }
 
+// 16-bit threshold: drop iff u16 < thr.  Any p > 0 gives thr >= 1, so thr != 0 <=> dropout on.
 inline uint32_t dropout_threshold(double p) {
-    double t = p * 4294967296.0;
-    t = t < 0 ? 0 : t;
-    double r = __builtin_nearbyint(t);
-    return r >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)r;
+    if (!(p > 0)) return 0u;
+    const double r = __builtin_nearbyint(p * 65536.0);
+    return r < 1.0 ? 1u : (r >= 65535.0 ? 65535u : (uint32_t)r);
 }
 
 inline float dropout_scale(double p) { return (float)(1.0 / (1.0 - p)); }

@@ -51,9 +51,12 @@ __global__ void k_decode_kv_append(const float* __restrict__ qkv, int64_t ld, in
     vc[dst] = qkv[b * ld + v_off + h * D + e];
 }
 
-// one wave per (b, h): the newest query against cached keys 0..pos (causal by construction).
-// Scores in fp32 (scale = n_embd^-0.5), exact softmax (max + sum over the wave), then
-// o[e] = sum_j p_j v_j[e] reduced across lanes.  D <= 64.
+// one wave per (b, h): the newest query against cached keys 0..n-1 (causal by construction),
+// scale = n_embd^-0.5.  Online softmax over chunks of 16 keys, so any key count works
+// (no LDS score buffer): a chunk is read by the whole wave -- 4 lanes per key, each a contiguous
+// 16-float quarter of the row (float4 loads, coalesced 64-B pieces) -- the 4 partial dots meet in
+// two shuffles, then lane e < D accumulates o[e] += p_j v_j[e] over the chunk (rows of V read
+// contiguously across lanes).  D <= 64.
 // K/V element (b, h, key j, e) at base + b*sb + h*sh + j*sj + e: the [B, H, Tmax, D] cache
 // (sb = H*Tmax*D, sh = Tmax*D, sj = D) or the rows of a window's qkv buffer (sb = T*ld, sh = D, sj = ld).
 __global__ __launch_bounds__(256) void k_decode_attn(const float* __restrict__ q, int64_t ldq,
@@ -61,40 +64,55 @@ __global__ __launch_bounds__(256) void k_decode_attn(const float* __restrict__ q
                                                      int64_t sb, int64_t sh, int64_t sj, int64_t B, int64_t H,
                                                      int64_t D, const int64_t* __restrict__ len_dev, int64_t nfix,
                                                      float scale, float* __restrict__ o, int64_t ldo) {
-    __shared__ float sq[4][64];
-    __shared__ float sp[4][1024];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t bh = (int64_t)blockIdx.x * 4 + w;
     if (bh >= B * H) return;
     const int64_t b = bh / H, h = bh % H;
     const int64_t n = len_dev ? *len_dev : nfix;  // keys 0..n-1
-    if (lane < D) sq[w][lane] = q[b * ldq + h * D + lane];
-    __builtin_amdgcn_wave_barrier();
     const float* K = kc + b * sb + h * sh;
     const float* V = vc + b * sb + h * sh;
-    float mx = -INFINITY;
-    for (int64_t j = lane; j < n; j += 64) {
+    const int part = lane & 3, e0 = 16 * part;     // this lane's quarter of the head dimension
+    const bool vec = (D == 64) && ((sj & 3) == 0) && ((((uintptr_t)K) & 15) == 0);
+    float qv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) qv[i] = e0 + i < D ? q[b * ldq + h * D + e0 + i] : 0.f;
+    float m = -INFINITY, l = 0.f, acc = 0.f;
+    for (int64_t j0 = 0; j0 < n; j0 += 16) {
+        const int64_t j = j0 + (lane >> 2);
         float s = 0.f;
-        for (int e = 0; e < D; ++e) s = fmaf(sq[w][e], K[j * sj + e], s);
-        s *= scale;
-        sp[w][j] = s;
-        mx = fmaxf(mx, s);
+        if (j < n) {
+            const float* kr = K + j * sj + e0;
+            if (vec) {
+#pragma unroll
+                for (int i = 0; i < 16; i += 4) {
+                    const float4 k4 = *(const float4*)(kr + i);
+                    s = fmaf(qv[i], k4.x, s);
+                    s = fmaf(qv[i + 1], k4.y, s);
+                    s = fmaf(qv[i + 2], k4.z, s);
+                    s = fmaf(qv[i + 3], k4.w, s);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    if (e0 + i < D) s = fmaf(qv[i], kr[i], s);
+            }
+        }
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        s = j < n ? s * scale : -INFINITY;
+        const float m_new = fmaxf(m, wave_max(s));
+        const float alpha = __expf(m - m_new);
+        const float p = j < n ? __expf(s - m_new) : 0.f;
+        l = l * alpha + wave_sum(p) * 0.25f;   // every key's p is held by its 4 lanes
+        m = m_new;
+        acc *= alpha;
+        const int jn = (int)(n - j0 < 16 ? n - j0 : 16);
+        for (int jj = 0; jj < jn; ++jj) {
+            const float pj = __shfl(p, 4 * jj, 64);
+            if (lane < D) acc = fmaf(pj, V[(j0 + jj) * sj + lane], acc);
+        }
     }
-    mx = wave_max(mx);
-    float sum = 0.f;
-    for (int64_t j = lane; j < n; j += 64) {
-        const float p = __expf(sp[w][j] - mx);
-        sp[w][j] = p;
-        sum += p;
-    }
-    sum = wave_sum(sum);
-    __builtin_amdgcn_wave_barrier();
-    // lane e accumulates output element e over all keys (probabilities from LDS)
-    if (lane < D) {
-        float acc = 0.f;
-        for (int64_t j = 0; j < n; ++j) acc = fmaf(sp[w][j], V[j * sj + lane], acc);
-        o[b * ldo + h * D + lane] = acc / sum;
-    }
+    if (lane < D) o[b * ldo + h * D + lane] = acc / l;
 }
 
 // next token per row from logits [B, V]: greedy = first argmax (torch.argmax tie rule); else
@@ -173,7 +191,7 @@ extern "C" int cg_decode_attn(const float* q, int64_t ldq, const float* k, const
                               int64_t sj, int64_t B, int64_t H, int64_t D, const int64_t* len_dev, int64_t nkeys,
                               float scale, float* o, int64_t ldo, void* stream) {
     CG_REQUIRE(B > 0 && H > 0 && D > 0 && D <= 64, "cg_decode_attn: needs D <= 64");
-    CG_REQUIRE(len_dev || (nkeys > 0 && nkeys <= 1024), "cg_decode_attn: 1..1024 keys");
+    CG_REQUIRE(len_dev || nkeys > 0, "cg_decode_attn: needs at least one key");
     k_decode_attn<<<ceil_div(B * H, 4), 256, 0, (hipStream_t)stream>>>(q, ldq, k, v, sb, sh, sj, B, H, D, len_dev,
                                                                        nkeys, scale, o, ldo);
     CG_LAUNCH_CHECK("cg_decode_attn");

@@ -401,6 +401,11 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     return CG_EINVAL;
 }
 
+extern "C" int cg_gemm_colpart_supported(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, int64_t lda,
+                                         int64_t ldb, int64_t ldc) {
+    return gemm_colpart_supported(a_trans, b_trans, M, N, K, lda, ldb, ldc) ? 1 : 0;
+}
+
 extern "C" int64_t cg_gemm_workspace(int64_t M, int64_t N, int split_k) {
     return split_k > 1 ? (int64_t)split_k * M * N * (int64_t)sizeof(float) : 0;
 }

@@ -175,15 +175,8 @@ void launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, in
 
 }  // namespace
 
-bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
-                      int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, float* ws,
-                      hipStream_t st) {
-    if (N % 128 || K % (FBK * split_k) || M % 128) return false;
-    if (lda % 8 || ldb % 8 || ldc % 8) return false;
-    if ((((uintptr_t)A) | ((uintptr_t)B) | ((uintptr_t)C)) & 15) return false;
-    if (e.bias && (((uintptr_t)e.bias) & 15)) return false;
-    if (e.resid && ((((uintptr_t)e.resid) & 15) || e.ld_resid % 4)) return false;
-    if (e.aux && ((((uintptr_t)e.aux) & 15) || e.ld_aux % 8)) return false;
+// the kernel variant cg_gemm's bf16 dispatch runs for this problem (before any fallback)
+static int pick_variant(int at, int64_t M, int64_t N, int split_k) {
     int v = g_gemm_variant;
     if (v == 0) {
         // persistent 128x128 LDS-DMA: measured best on the C2 shapes (profiles/r1_gemm_scan.txt); the
@@ -191,8 +184,32 @@ bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf1
         const int64_t t256 = (M / 256) * (N / 256);
         v = (!at && split_k == 1 && M % 256 == 0 && N % 256 == 0 && t256 >= 2 * (int64_t)gemm_cu_count()) ? 24 : 9;
     }
-    // only the 128x128 persistent kernel's ReLU-backward epilogue writes column partials
-    if (e.colpart && (v != 9 || e.kind != CG_EPI_RELU_BWD || e.aux_dtype != CG_BF16 || e.beta != 0.f || split_k != 1 || at))
+    return v;
+}
+
+static bool fast_shape_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int split_k) {
+    return N % 128 == 0 && K % (FBK * split_k) == 0 && M % 128 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0;
+}
+
+// only the 128x128 persistent kernel's per-item ReLU-backward epilogue (not its pk_flags bit-1
+// per-fragment form) writes column partials
+static bool colpart_ok(int v, int at, int split_k) { return v == 9 && !(g_pk_flags & 2) && split_k == 1 && !at; }
+
+bool gemm_colpart_supported(int at, int bt, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc) {
+    (void)bt;
+    return fast_shape_ok(M, N, K, lda, ldb, ldc, 1) && colpart_ok(pick_variant(at, M, N, 1), at, 1);
+}
+
+bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
+                      int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, float* ws,
+                      hipStream_t st) {
+    if (!fast_shape_ok(M, N, K, lda, ldb, ldc, split_k)) return false;
+    if ((((uintptr_t)A) | ((uintptr_t)B) | ((uintptr_t)C)) & 15) return false;
+    if (e.bias && (((uintptr_t)e.bias) & 15)) return false;
+    if (e.resid && ((((uintptr_t)e.resid) & 15) || e.ld_resid % 4)) return false;
+    if (e.aux && ((((uintptr_t)e.aux) & 15) || e.ld_aux % 8)) return false;
+    int v = pick_variant(at, M, N, split_k);
+    if (e.colpart && (!colpart_ok(v, at, split_k) || e.kind != CG_EPI_RELU_BWD || e.aux_dtype != CG_BF16 || e.beta != 0.f))
         return false;
     if (v >= 20 && p8_gemm_launch(v, at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st))
         return true;

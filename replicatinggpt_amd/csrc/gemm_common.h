@@ -44,8 +44,7 @@ __device__ __forceinline__ float epi_scalar(const EpiArgs& e, float v, int64_t m
         case CG_EPI_BIAS_DROP_RESID: {
             if (e.bias) v += e.bias[n];
             const uint64_t idx = (uint64_t)m * (uint64_t)N + (uint64_t)n;
-            const u32x4 r = philox_group(e.seed, stream, idx >> 2);
-            if (e.thr) v = philox_word(r, (int)(idx & 3)) >= e.thr ? v * e.dscale : 0.f;
+            if (e.thr) v = keep_of(philox_of(e.seed, stream, idx), idx, e.thr) ? v * e.dscale : 0.f;
             if (e.resid) v = e.resid[m * e.ld_resid + n] + v;
             break;
         }
@@ -77,6 +76,8 @@ int gemm_cu_count();  // compute units of the current device (cached; gemm_pk.hi
 bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
                       int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, float* ws,
                       hipStream_t st);
+// whether cg_gemm (bf16, split 1, CG_EPI_RELU_BWD with bf16 aux, beta 0) can write column partials
+bool gemm_colpart_supported(int at, int bt, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
 // LDS-DMA (global_load_lds) kernels, variant >= 5 (gemm_glds.hip); false if the variant/shape does not apply
 bool glds_gemm_launch(int variant, int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda,
                       const bf16_t* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k,

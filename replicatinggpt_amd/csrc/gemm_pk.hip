@@ -65,6 +65,8 @@ struct DmaP {
     }
 };
 
+__device__ __forceinline__ float rbf(float x) { return bf2f(f2bf(x)); }
+
 __device__ __forceinline__ void store4_plain(const fv4& v, int64_t m, int64_t n, void* Cv, int c_dtype, int64_t ldc) {
     if (c_dtype == CG_BF16)
         *(uint2*)((bf16_t*)Cv + m * ldc + n) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
@@ -118,7 +120,9 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
                     fv4 t;
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        float s = ((acc[0][j][q] + acc[1][j][q]) + acc[2][j][q]) + acc[3][j][q];
+                        // the bf16-rounded values the stores below write (the precision cg_colsum
+                        // and the W1 weight gradient see), summed in fp32
+                        float s = ((rbf(acc[0][j][q]) + rbf(acc[1][j][q])) + rbf(acc[2][j][q])) + rbf(acc[3][j][q]);
                         s += __shfl_xor(s, 1);
                         s += __shfl_xor(s, 2);
                         s += __shfl_xor(s, 4);
@@ -176,11 +180,9 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
                     v[0] += bv[j].x; v[1] += bv[j].y; v[2] += bv[j].z; v[3] += bv[j].w;
                 }
                 if (drop) {
-                    const u32x4 q = philox_group(epi.seed, stream, ((uint64_t)m * (uint64_t)N + (uint64_t)n) >> 2);
-                    v[0] = q.x >= epi.thr ? v[0] * epi.dscale : 0.f;
-                    v[1] = q.y >= epi.thr ? v[1] * epi.dscale : 0.f;
-                    v[2] = q.z >= epi.thr ? v[2] * epi.dscale : 0.f;
-                    v[3] = q.w >= epi.thr ? v[3] * epi.dscale : 0.f;
+                    const uint32_t kb = keep4_bits(epi.seed, stream, (uint64_t)m * (uint64_t)N + (uint64_t)n, epi.thr);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) v[q] = ((kb >> q) & 1u) ? v[q] * epi.dscale : 0.f;
                 }
                 v[0] = r[i][j].x + v[0]; v[1] = r[i][j].y + v[1]; v[2] = r[i][j].z + v[2]; v[3] = r[i][j].w + v[3];
                 store4_plain(v, m, n, Cv, c_dtype, ldc);
@@ -200,11 +202,9 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
             } else if (kind == CG_EPI_BIAS_DROP_RESID && epi.thr) {
-                const u32x4 q = philox_group(epi.seed, stream, ((uint64_t)m * (uint64_t)N + (uint64_t)n) >> 2);
-                v[0] = q.x >= epi.thr ? v[0] * epi.dscale : 0.f;
-                v[1] = q.y >= epi.thr ? v[1] * epi.dscale : 0.f;
-                v[2] = q.z >= epi.thr ? v[2] * epi.dscale : 0.f;
-                v[3] = q.w >= epi.thr ? v[3] * epi.dscale : 0.f;
+                const uint32_t kb = keep4_bits(epi.seed, stream, (uint64_t)m * (uint64_t)N + (uint64_t)n, epi.thr);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = ((kb >> q) & 1u) ? v[q] * epi.dscale : 0.f;
             }
             store4_plain(v, m, n, Cv, c_dtype, ldc);
         }

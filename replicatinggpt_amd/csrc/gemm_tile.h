@@ -64,12 +64,10 @@ __device__ __forceinline__ void epi_store8(float (&v)[8], int64_t m, int64_t n, 
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
     } else if (kind == CG_EPI_BIAS_DROP_RESID && epi.thr) {
-        const uint64_t idx = (uint64_t)m * (uint64_t)N + (uint64_t)n;
-        const u32x4 r0 = philox_group(epi.seed, stream, idx >> 2);
-        const u32x4 r1 = philox_group(epi.seed, stream, (idx >> 2) + 1);
-        const uint32_t w[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+        const uint64_t idx = (uint64_t)m * (uint64_t)N + (uint64_t)n;  // n % 8 == 0, N % 8 == 0
+        const uint32_t kb = keep4_bits(epi.seed, stream, idx, epi.thr) | (keep4_bits(epi.seed, stream, idx + 4, epi.thr) << 4);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = w[q] >= epi.thr ? v[q] * epi.dscale : 0.f;
+        for (int q = 0; q < 8; ++q) v[q] = ((kb >> q) & 1u) ? v[q] * epi.dscale : 0.f;
     } else if (kind == CG_EPI_RELU_BWD) {
         if (epi.aux_dtype == CG_BF16) {
             const uint4 h = *(const uint4*)((const bf16_t*)epi.aux + m * epi.ld_aux + n);
@@ -129,11 +127,9 @@ __device__ __forceinline__ void epi_store4(fv4 v, int64_t m, int64_t n, int64_t 
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
     } else if (kind == CG_EPI_BIAS_DROP_RESID && epi.thr) {
-        const u32x4 r = philox_group(epi.seed, stream, ((uint64_t)m * (uint64_t)N + (uint64_t)n) >> 2);
-        v[0] = r.x >= epi.thr ? v[0] * epi.dscale : 0.f;
-        v[1] = r.y >= epi.thr ? v[1] * epi.dscale : 0.f;
-        v[2] = r.z >= epi.thr ? v[2] * epi.dscale : 0.f;
-        v[3] = r.w >= epi.thr ? v[3] * epi.dscale : 0.f;
+        const uint32_t kb = keep4_bits(epi.seed, stream, (uint64_t)m * (uint64_t)N + (uint64_t)n, epi.thr);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = ((kb >> q) & 1u) ? v[q] * epi.dscale : 0.f;
     } else if (kind == CG_EPI_RELU_BWD) {
         if (epi.aux_dtype == CG_BF16) {
             const uint2 h = *(const uint2*)((const bf16_t*)epi.aux + m * epi.ld_aux + n);

@@ -97,7 +97,8 @@ __global__ __launch_bounds__(256) void k_head_fwd(const bf16_t* __restrict__ a, 
         const float l = mx + __logf(s);
         if (lane < 16) {
             lse[row] = l;
-            my_loss = l - xt;
+            // F.cross_entropy raises on a target outside [0, V): here the loss turns NaN instead
+            my_loss = (tgt && (tr < 0 || tr >= V)) ? __builtin_nanf("") : l - xt;
         }
     }
     // block partial of the loss sum (fixed order: lanes 0-15 of each wave, then waves)
@@ -144,7 +145,7 @@ __global__ __launch_bounds__(256) void k_head_bwd(const float* __restrict__ logi
             float d = 0.f;
             if (c < V) {
                 const float x = logits[m * V + c];
-                if (tgt) d = gs * (__expf(x - l) - (c == t ? 1.f : 0.f));
+                if (tgt) d = (t < 0 || t >= V) ? __builtin_nanf("") : gs * (__expf(x - l) - (c == t ? 1.f : 0.f));
                 if (g_logits) d += g_logits[m * V + c];
             }
             v[q] = d;

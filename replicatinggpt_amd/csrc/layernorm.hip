@@ -246,12 +246,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
                     float z[VEC];
                     if (lp.thr) {
                         const uint64_t idx = (uint64_t)r * (uint64_t)C + (uint64_t)e;
-                        u32x4 ph = philox_group(lp.seed, stream, idx >> 2);
+                        u32x4 ph = philox_of(lp.seed, stream, idx);
 #pragma unroll
                         for (int q = 0; q < VEC; ++q) {
                             const uint64_t iq = idx + q;
-                            if (q > 0 && (iq & 3) == 0) ph = philox_group(lp.seed, stream, iq >> 2);
-                            z[q] = philox_word(ph, (int)(iq & 3)) >= lp.thr ? o[q] * lp.dscale : 0.f;
+                            if (q > 0 && (iq & 7) == 0) ph = philox_of(lp.seed, stream, iq);
+                            z[q] = keep_of(ph, iq, lp.thr) ? o[q] * lp.dscale : 0.f;
                         }
                     } else {
 #pragma unroll

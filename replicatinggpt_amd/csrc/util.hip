@@ -54,19 +54,18 @@ extern "C" int cg_rng_snapshot(uint64_t* counter, uint64_t* snap, void* stream) 
 __global__ void k_dropout_mask(float* dst, int64_t n, uint32_t thr, uint64_t seed, const uint64_t* rng_call,
                                int site) {
     const uint64_t stream = dropout_stream(rng_call, site);
-    int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    int64_t i0 = g * 4;
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // group of 8 consecutive elements
+    const int64_t i0 = g * 8;
     if (i0 >= n) return;
-    u32x4 r = philox_group(seed, stream, (uint64_t)g);
-    uint32_t w[4] = {r.x, r.y, r.z, r.w};
-    for (int j = 0; j < 4 && i0 + j < n; ++j) dst[i0 + j] = w[j] >= thr ? 1.f : 0.f;
+    const uint32_t kb = keep8_bits(philox_group(seed, stream, (uint64_t)g), thr);
+    for (int j = 0; j < 8 && i0 + j < n; ++j) dst[i0 + j] = ((kb >> j) & 1u) ? 1.f : 0.f;
 }
 
 extern "C" int cg_dropout_mask(float* dst, int64_t n, double p, uint64_t seed, const uint64_t* rng_call, int site,
                                void* stream) {
     CG_REQUIRE(n >= 0, "cg_dropout_mask: n < 0");
     if (n == 0) return CG_OK;
-    int64_t groups = (n + 3) / 4;
+    const int64_t groups = (n + 7) / 8;
     k_dropout_mask<<<ceil_div(groups, 256), 256, 0, (hipStream_t)stream>>>(dst, n, dropout_threshold(p),
                                                                                  seed, rng_call, site);
     CG_LAUNCH_CHECK("cg_dropout_mask");
@@ -78,20 +77,18 @@ template <typename TY>
 __global__ void k_dropout_apply(const float* __restrict__ x, int64_t rows, int64_t C, int64_t ldx, TY* __restrict__ y,
                                 uint32_t thr, float dscale, uint64_t seed, const uint64_t* rng_call, int site) {
     const uint64_t stream = thr ? dropout_stream(rng_call, site) : 0;
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // group of 4 consecutive elements
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // group of 8 consecutive elements
     const int64_t n = rows * C;
-    const int64_t i0 = g * 4;
+    const int64_t i0 = g * 8;
     if (i0 >= n) return;
-    u32x4 r = {0, 0, 0, 0};
-    if (thr) r = philox_group(seed, stream, (uint64_t)g);
-    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+    const uint32_t kb = thr ? keep8_bits(philox_group(seed, stream, (uint64_t)g), thr) : 0xffu;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < 8; ++j) {
         const int64_t i = i0 + j;
         if (i < n) {
             const int64_t row = i / C, col = i % C;
             float v = x[row * ldx + col];
-            if (thr) v = w[j] >= thr ? v * dscale : 0.f;
+            if (thr) v = ((kb >> j) & 1u) ? v * dscale : 0.f;
             st_from_f32<TY>(y + i, v);
         }
     }
@@ -104,7 +101,7 @@ extern "C" int cg_dropout_apply(const float* x, int64_t rows, int64_t C, int64_t
     if (n == 0) return CG_OK;
     const uint32_t thr = p > 0 ? dropout_threshold(p) : 0u;
     const float ds = p > 0 ? dropout_scale(p) : 1.f;
-    const int grid = ceil_div((n + 3) / 4, 256);
+    const int grid = ceil_div((n + 7) / 8, 256);
     if (y_dtype == CG_BF16)
         k_dropout_apply<bf16_t><<<grid, 256, 0, (hipStream_t)stream>>>(x, rows, C, ldx, (bf16_t*)y, thr, ds, seed,
                                                                         rng_call, site);

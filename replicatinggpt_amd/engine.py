@@ -90,6 +90,9 @@ class TrainStep:
         self.g_seg = []
         self.loss = None
         self.overlap = (reducer is not None and reducer.world > 1) if overlap is None else bool(overlap)
+        # per-rank dropout key: the replicas must not draw identical masks
+        if reducer is not None and reducer.world > 1:
+            model.set_dropout_rank(dist.get_rank(reducer.group))
         self.cuts, self.ranges = segment_plan(model, seg_layers) if self.overlap else ([], [])
 
     # -- eager ----------------------------------------------------------------------------

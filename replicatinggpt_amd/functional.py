@@ -240,21 +240,19 @@ def linear_wgrad(dy2, x2, out, beta):
     return out
 
 
-def _colpart_ok(dy2, w, aux):
-    """Whether cg_gemm's default dispatch runs the ReLU-backward dgrad out[M,F] = relu_bwd(dy2 @ w)
-    on the 128x128 persistent kernel, whose epilogue can also write the output's column partials
-    (csrc/gemm_bf16.hip fast_gemm_launch: the 8-wave 256x256 tile takes over at >= 2 such tiles per
-    CU, e.g. every C4 product; an explicit gemm_variant tuning disables the fusion)."""
+def _colpart_ok(dy2, w, aux, out_ld):
+    """Whether cg_gemm's dispatch can write the ReLU-backward dgrad out[M,F] = relu_bwd(dy2 @ w)
+    together with its column partials (the b1 gradient) -- asked from the library itself
+    (cg_gemm_colpart_supported: same predicate as the dispatch, current tuning knobs included)."""
     if not (FUSE_COLPART and _is_bf16(dy2.dtype) and _is_bf16(aux.dtype) and dy2.is_cuda):
+        return False
+    if dy2.stride(1) != 1 or w.stride(1) != 1 or aux.stride(1) != 1 or aux.stride(0) % 8:
+        return False
+    if any(t.data_ptr() % 16 for t in (dy2, w, aux)):
         return False
     M, K = dy2.shape
     F = w.shape[1]
-    if M % 128 or F % 128 or K % 64 or "gemm_variant" in os.environ.get("CHARPT_TUNING", ""):
-        return False
-    if dy2.stride(0) % 8 or w.stride(0) % 8 or aux.stride(0) % 8 or dy2.stride(1) != 1 or w.stride(1) != 1:
-        return False
-    cus = _gemm_slots() // 2
-    return not (M % 256 == 0 and F % 256 == 0 and (M // 256) * (F // 256) >= 2 * cus)
+    return bool(L.load().cg_gemm_colpart_supported(0, 1, M, F, K, dy2.stride(0), w.stride(0), out_ld))
 
 
 def colsum_into(x2, out, beta):
@@ -537,7 +535,7 @@ class FFNSublayerFn(torch.autograd.Function):
         g_w1, beta_w1, f_w1 = w1.grad_target()
         g_b1, beta_b1, f_b1 = b1.grad_target()
         part = None
-        if g_b1 is not None and _colpart_ok(dz2, w2.operand(act), h):
+        if g_b1 is not None and _colpart_ok(dz2, w2.operand(act), h, dz1.stride(0)):
             # b1's gradient (column sums of dz1) fused into the ReLU-backward dgrad's epilogue as
             # per-64-row partials; only their fold runs on the side stream
             M, F4 = h.shape

@@ -398,6 +398,18 @@ class BigramLanguageModel(nn.Module):
     def flat(self):
         return self._store
 
+    def set_dropout_rank(self, rank):
+        """Data parallel: give rank ``rank`` its own Philox dropout key (base seed + 7919 * rank),
+        so the W replicas draw independent masks (GPT1.py:117,146) -- rank 0 keeps the base seed,
+        i.e. the single-GPU stream.  Idempotent; the engine (engine.TrainStep) calls it."""
+        base = self.__dict__.setdefault("_dropout_seed_base", self.config.dropout_seed)
+        old = self.config
+        new = old.with_(dropout_seed=base + 7919 * int(rank))   # never mutate a (possibly shared) config
+        for m in self.modules():
+            if getattr(m, "config", None) is old:
+                m.config = new
+        return new.dropout_seed
+
     def _apply(self, fn, recurse=True):
         store = self._store
         if store is None:

@@ -312,3 +312,193 @@ def adamw(p: Tensor, g: Tensor, m: Tensor, v: Tensor, p_bf16: Optional[Tensor], 
           eps: float, weight_decay: float, step: Tensor) -> None:
     L.check(L.load().cg_adamw(L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), L.ptr(p_bf16), p.numel(), lr, beta1, beta2, eps,
                               weight_decay, L.ptr(step), _s(p)), "adamw")
+
+
+# ---------------------------------------------------------------------------------------
+# Fake (meta) implementations of the out-style ops above: each returns None and only writes
+# buffers it declares as mutated, so FakeTensor / torch.compile tracing treats it as a no-op on
+# shapes.
+for _name, _obj in list(globals().items()):
+    if isinstance(_obj, torch._library.custom_ops.CustomOpDef):
+        _obj.register_fake(lambda *a, **k: None)
+
+
+# ---------------------------------------------------------------------------------------
+# Functional ops with fake + autograd registrations (torch.library.register_fake /
+# register_autograd): the traceable seam of the GPT1.py module surface outside the fused model
+# path -- nn.LayerNorm (GPT1.py:159-160,173), nn.Linear (:103-105,131,143,145,174) and the causal
+# softmax-attention of Head / MultiHeadAttention (:109-123,134-135), all heads at once.  The
+# fused training nodes (functional.AttnSublayerFn / FFNSublayerFn / HeadLossFn) stay
+# autograd.Functions: they write parameter gradients straight into the model's flat gradient
+# buffer, hand bf16 gradient copies between sublayers (GradLink) and fork side-stream work --
+# effects a functional custom op cannot express.  Forward and backward are each ONE custom op, so a
+# tracer only ever sees their fakes; all host-side kernel selection stays inside the real bodies.
+def _flat_rows(x):
+    return x.reshape(-1, x.shape[-1])
+
+
+@torch.library.custom_op(f"{_NS}::layer_norm", mutates_args=(), device_types="cuda")
+def layer_norm(x: Tensor, weight: Tensor, bias: Tensor, eps: float) -> tuple[Tensor, Tensor, Tensor]:
+    """y = (x - mean) * rstd * weight + bias over the last dim (fp32); also returns mean, rstd."""
+    x2 = _flat_rows(x).contiguous()
+    rows = x2.shape[0]
+    y = torch.empty_like(x2)
+    mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+    layernorm_fwd(x2, weight, bias, y, mean, rstd, eps)
+    return y.view(x.shape), mean, rstd
+
+
+@layer_norm.register_fake
+def _(x, weight, bias, eps):
+    rows = x.numel() // x.shape[-1]
+    return torch.empty_like(x), x.new_empty(rows), x.new_empty(rows)
+
+
+@torch.library.custom_op(f"{_NS}::layer_norm_backward", mutates_args=(), device_types="cuda")
+def layer_norm_backward(dy: Tensor, x: Tensor, weight: Tensor, mean: Tensor, rstd: Tensor) -> tuple[Tensor, Tensor, Tensor]:
+    x2 = _flat_rows(x).contiguous()
+    rows, C = x2.shape
+    dx = torch.empty_like(x2)
+    dw = torch.empty(C, dtype=torch.float32, device=x.device)
+    db = torch.empty(C, dtype=torch.float32, device=x.device)
+    ws = torch.empty(layernorm_bwd_workspace(rows, C) // 4 + 1, dtype=torch.float32, device=x.device)
+    layernorm_bwd(_flat_rows(dy).float().contiguous(), x2, weight, mean, rstd, None, dx, None, dw, db, False, ws, None,
+                  False, 0.0, 0, None, 0)
+    return dx.view(x.shape), dw, db
+
+
+@layer_norm_backward.register_fake
+def _(dy, x, weight, mean, rstd):
+    C = x.shape[-1]
+    return torch.empty_like(x), x.new_empty(C), x.new_empty(C)
+
+
+def _ln_setup(ctx, inputs, output):
+    x, weight, _, _ = inputs
+    _, mean, rstd = output
+    ctx.save_for_backward(x, weight, mean, rstd)
+
+
+def _ln_backward(ctx, dy, _dmean, _drstd):
+    x, weight, mean, rstd = ctx.saved_tensors
+    dx, dw, db = layer_norm_backward(dy, x, weight, mean, rstd)
+    return dx, dw, db, None
+
+
+layer_norm.register_autograd(_ln_backward, setup_context=_ln_setup)
+
+
+@torch.library.custom_op(f"{_NS}::linear", mutates_args=(), device_types="cuda")
+def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor]) -> Tensor:
+    """y = x weight^T (+ bias): fp32 (exact f32 MFMA) or bf16 (bf16 MFMA, fp32 accumulate) operands,
+    bias fp32, output in x's dtype."""
+    from . import functional as Fn
+    x2 = _flat_rows(x).contiguous()
+    out = torch.empty((x2.shape[0], weight.shape[0]), dtype=x.dtype, device=x.device)
+    Fn.linear_fwd(x2, weight.contiguous(), out, "bias" if bias is not None else "store", bias=bias)
+    return out.view(*x.shape[:-1], weight.shape[0])
+
+
+@linear.register_fake
+def _(x, weight, bias):
+    return x.new_empty((*x.shape[:-1], weight.shape[0]))
+
+
+@torch.library.custom_op(f"{_NS}::linear_backward", mutates_args=(), device_types="cuda")
+def linear_backward(dy: Tensor, x: Tensor, weight: Tensor, with_bias: bool) -> tuple[Tensor, Tensor, Tensor]:
+    """(dx, dweight, dbias): dy weight, dy^T x (fp32 accumulation, deterministic split-K), colsum(dy);
+    dbias is empty when with_bias is False."""
+    from . import functional as Fn
+    dy2 = _flat_rows(dy).to(x.dtype).contiguous()
+    x2 = _flat_rows(x).contiguous()
+    w = weight.contiguous()
+    dx = torch.empty_like(x2)
+    Fn.linear_dgrad(dy2, w, dx)
+    dw32 = torch.empty(w.shape, dtype=torch.float32, device=x.device)
+    Fn.linear_wgrad(dy2, x2, dw32, 0.0)
+    dw = dw32 if w.dtype == torch.float32 else Fn.to_act(dw32, w.dtype)
+    db = torch.empty(w.shape[0] if with_bias else 0, dtype=torch.float32, device=x.device)
+    if with_bias:
+        Fn.colsum_into(dy2, db, 0.0)
+    return dx.view(x.shape), dw, db
+
+
+@linear_backward.register_fake
+def _(dy, x, weight, with_bias):
+    return torch.empty_like(x), torch.empty_like(weight), x.new_empty(weight.shape[0] if with_bias else 0,
+                                                                      dtype=torch.float32)
+
+
+def _lin_setup(ctx, inputs, output):
+    x, weight, bias = inputs
+    ctx.save_for_backward(x, weight)
+    ctx.with_bias = bias is not None
+
+
+def _lin_backward(ctx, dy):
+    x, weight = ctx.saved_tensors
+    dx, dw, db = linear_backward(dy, x, weight, ctx.with_bias)
+    return dx, dw, (db if ctx.with_bias else None)
+
+
+linear.register_autograd(_lin_backward, setup_context=_lin_setup)
+
+
+@torch.library.custom_op(f"{_NS}::causal_attention", mutates_args=(), device_types="cuda")
+def causal_attention(qkv: Tensor, n_head: int, head_size: int, scale: float, dropout_p: float, seed: int,
+                     rng_call: Optional[Tensor], site: int) -> tuple[Tensor, Tensor]:
+    """All heads of GPT1.py's Head.forward at once: qkv [B, T, 3*H*D] (queries of every head, then
+    keys, then values; head-major inside each) -> (out [B, T, H*D] = the torch.cat of GPT1.py:135,
+    logsumexp [B, H, T]).  Causal mask, softmax with scale (n_embd^-0.5), Philox dropout on
+    the probabilities (dropout stream (rng_call, site), key seed)."""
+    from . import functional as Fn
+    B, T, _ = qkv.shape
+    d = n_head * head_size
+    q2 = qkv.reshape(B * T, 3 * d).contiguous()
+    o = torch.empty((B * T, d), dtype=qkv.dtype, device=qkv.device)
+    lse, _mask = Fn.attention_fwd(q2, B, T, n_head, head_size, o, scale, dropout_p, seed, rng_call, site)
+    return o.view(B, T, d), lse
+
+
+@causal_attention.register_fake
+def _(qkv, n_head, head_size, scale, dropout_p, seed, rng_call, site):
+    B, T, _ = qkv.shape
+    return qkv.new_empty((B, T, n_head * head_size)), qkv.new_empty((B, n_head, T), dtype=torch.float32)
+
+
+@torch.library.custom_op(f"{_NS}::causal_attention_backward", mutates_args=(), device_types="cuda")
+def causal_attention_backward(dout: Tensor, qkv: Tensor, out: Tensor, lse: Tensor, n_head: int, head_size: int,
+                              scale: float, dropout_p: float, seed: int, rng_call: Optional[Tensor],
+                              site: int) -> Tensor:
+    """d qkv of causal_attention (the forward's dropout keep bits are regenerated from the stream)."""
+    from . import functional as Fn
+    B, T, _ = qkv.shape
+    d = n_head * head_size
+    q2 = qkv.reshape(B * T, 3 * d).contiguous()
+    dq = Fn.attention_bwd(q2, B, T, n_head, head_size, out.reshape(B * T, d).contiguous(),
+                          dout.reshape(B * T, d).to(qkv.dtype).contiguous(), lse.contiguous(), scale, dropout_p, seed,
+                          rng_call, site, None)
+    return dq.view(qkv.shape)
+
+
+@causal_attention_backward.register_fake
+def _(dout, qkv, out, lse, n_head, head_size, scale, dropout_p, seed, rng_call, site):
+    return torch.empty_like(qkv)
+
+
+def _attn_setup(ctx, inputs, output):
+    qkv, n_head, head_size, scale, p, seed, rng_call, site = inputs
+    o, lse = output
+    ctx.save_for_backward(qkv, o, lse, rng_call)
+    ctx.args = (n_head, head_size, scale, p, seed, site)
+
+
+def _attn_backward(ctx, dout, _dlse):
+    qkv, o, lse, rng_call = ctx.saved_tensors
+    n_head, head_size, scale, p, seed, site = ctx.args
+    dq = causal_attention_backward(dout, qkv, o, lse, n_head, head_size, scale, p, seed, rng_call, site)
+    return dq, None, None, None, None, None, None, None
+
+
+causal_attention.register_autograd(_attn_backward, setup_context=_attn_setup)

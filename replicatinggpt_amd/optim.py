@@ -18,6 +18,7 @@ class AdamW(torch.optim.Optimizer):
         self._store = None
         self._m = self._v = None
         self._step_t = None
+        self._psteps = None   # per-parameter step counts, once a step skipped some parameter
 
     # the model whose flat store holds these parameters is found from the parameters, so
     # ``AdamW(m.parameters(), lr=5e-1)`` works exactly as GPT1.py:218 writes it
@@ -42,6 +43,7 @@ class AdamW(torch.optim.Optimizer):
         self._m = torch.zeros_like(st.master)
         self._v = torch.zeros_like(st.master)
         self._step_t = torch.zeros(1, dtype=torch.int64, device=st.master.device)
+        self._psteps = None
         return self
 
     def _ensure(self):
@@ -52,6 +54,8 @@ class AdamW(torch.optim.Optimizer):
             self._m = self._m.to(st.master.device)
             self._v = self._v.to(st.master.device)
             self._step_t = self._step_t.to(st.master.device)
+            if self._psteps is not None:
+                self._psteps = self._psteps.to(st.master.device)
 
     def zero_grad(self, set_to_none=True):
         for g in self.param_groups:
@@ -72,21 +76,42 @@ class AdamW(torch.optim.Optimizer):
         st = self._store
         grp = self.param_groups[0]
         b1, b2 = grp["betas"]
-        ops.counter_add(self._step_t, 1)
         # gradients must sit in the flat slots; copy strays in (rare: user-assigned grads)
-        all_in_slots = True
+        missing = []
         for r in st.regions.values():
             for p, off in r.parts:
-                slot = r.slot.view(-1)[off:off + p.numel()].view(p.shape)
                 if p.grad is None:
-                    slot.zero_()
-                    all_in_slots = False
-                elif p.grad.data_ptr() != slot.data_ptr():
+                    missing.append(p)
+                    continue
+                slot = r.slot.view(-1)[off:off + p.numel()].view(p.shape)
+                if p.grad.data_ptr() != slot.data_ptr():
                     slot.copy_(p.grad)
-        ops.adamw(st.master, st.grad, self._m, self._v, st.shadow, float(grp["lr"]), float(b1), float(b2),
-                  float(grp["eps"]), float(grp["weight_decay"]), self._step_t)
+        args = (float(grp["lr"]), float(b1), float(b2), float(grp["eps"]), float(grp["weight_decay"]))
+        if not missing and self._psteps is None:
+            # the training path: every parameter has a gradient, one launch over the flat buffers
+            ops.counter_add(self._step_t, 1)
+            ops.adamw(st.master, st.grad, self._m, self._v, st.shadow, *args, self._step_t)
+        else:
+            # torch.optim.AdamW skips parameters whose .grad is None (no decay, no moment update,
+            # no step count): per-parameter launches over the flat slices, per-parameter step counts
+            self._split_steps()
+            skip = {id(p) for p in missing}
+            for i, p, off in self._param_slices():
+                if id(p) in skip:
+                    continue
+                n = p.numel()
+                step = self._psteps[i:i + 1]
+                ops.counter_add(step, 1)
+                ops.adamw(st.master[off:off + n], st.grad[off:off + n], self._m[off:off + n], self._v[off:off + n],
+                          st.shadow[off:off + n], *args, step)
         st._shadow_version = st.version()
         return loss
+
+    def _split_steps(self):
+        """Switch to per-parameter step counts (first step on which some parameter had no grad)."""
+        if self._psteps is None:
+            n = len(self.param_groups[0]["params"])
+            self._psteps = self._step_t.repeat(n).contiguous()
 
     # -- checkpoints: torch.optim.AdamW's own state-dict layout ------------------------------
     def _param_slices(self):
@@ -107,9 +132,11 @@ class AdamW(torch.optim.Optimizer):
                    "capturable": False, "differentiable": False, "fused": None, "decoupled_weight_decay": True,
                    "params": list(range(len(grp["params"])))}]
         state = {}
-        step = int(self._step_t.item())
-        if step > 0:
-            for i, p, off in self._param_slices():
+        steps = self._psteps.tolist() if self._psteps is not None else None
+        step_all = int(self._step_t.item())
+        for i, p, off in self._param_slices():
+            step = steps[i] if steps is not None else step_all
+            if step > 0:
                 n = p.numel()
                 state[i] = {"step": torch.tensor(float(step)),
                             "exp_avg": self._m[off:off + n].view(p.shape).clone(),
@@ -127,18 +154,21 @@ class AdamW(torch.optim.Optimizer):
             raise ValueError("charpt AdamW: amsgrad / maximize state cannot be resumed by the fused kernel")
         self._ensure()
         ids = groups[0]["params"]
-        steps = set()
+        steps = []
         with torch.no_grad():
             self._m.zero_()
             self._v.zero_()
             for i, p, off in self._param_slices():
                 s = state_dict["state"].get(ids[i])
                 if s is None:
+                    steps.append(0)
                     continue
                 n = p.numel()
                 self._m[off:off + n].copy_(s["exp_avg"].reshape(-1))
                 self._v[off:off + n].copy_(s["exp_avg_sq"].reshape(-1))
-                steps.add(int(float(s["step"])))
-        if len(steps) > 1:
-            raise ValueError(f"charpt AdamW: one step count for all parameters is required, got {sorted(steps)}")
-        self._step_t.fill_(steps.pop() if steps else 0)
+                steps.append(int(float(s["step"])))
+        if len(set(steps)) <= 1:
+            self._psteps = None
+            self._step_t.fill_(steps[0] if steps else 0)
+        else:   # parameters that skipped steps (grad None) resume with their own counts
+            self._psteps = torch.tensor(steps, dtype=torch.int64, device=self._step_t.device)

@@ -27,13 +27,22 @@ import torch
 
 REF = "/root/reference"
 OUT = os.path.dirname(os.path.abspath(__file__))
+# the GPT1.py these fixtures were generated from; a different file is refused (it is untrusted
+# public content and is executed below)
+GPT1_SHA256 = "38818880dff1983cea405e926b8e5ac06fad4cad4dac850dbdc0d58011c13a92"
+# top-level statement kinds allowed to run (GPT1.py:1-216): imports of torch, the seed call, the
+# hyper-parameter globals, the input read, the encoder branch, function and class definitions
+_ALLOWED = (ast.Import, ast.ImportFrom, ast.Assign, ast.With, ast.If, ast.FunctionDef, ast.ClassDef)
 
 
 def load_reference(overrides=None, build_model=True):
     """Exec GPT1.py up to (and optionally including) model construction (GPT1.py:215-216)."""
     ov = {"encoder": "base", "device": "cpu"}
     ov.update(overrides or {})
-    tree = ast.parse(open(os.path.join(REF, "GPT1.py")).read())
+    raw = open(os.path.join(REF, "GPT1.py"), "rb").read()
+    if hashlib.sha256(raw).hexdigest() != GPT1_SHA256:
+        raise SystemExit("make_golden: /root/reference/GPT1.py differs from the pinned file; refusing to execute it")
+    tree = ast.parse(raw.decode())
     body = []
     for node in tree.body:
         if node.lineno >= 218:  # optimizer (lr literal), train loop, sample, save
@@ -42,6 +51,15 @@ def load_reference(overrides=None, build_model=True):
             continue
         if isinstance(node, ast.Expr) and ast.unparse(node).startswith("print("):
             continue
+        if isinstance(node, ast.Expr) and ast.unparse(node) == "torch.manual_seed(1337)":
+            body.append(node)
+            continue
+        if not isinstance(node, _ALLOWED):
+            raise SystemExit(f"make_golden: unexpected statement at GPT1.py:{node.lineno}: {type(node).__name__}")
+        if isinstance(node, (ast.Import, ast.ImportFrom)):
+            mods = [node.module] if isinstance(node, ast.ImportFrom) else [a.name for a in node.names]
+            if not all(m == "torch" or m.startswith("torch.") for m in mods):
+                raise SystemExit(f"make_golden: unexpected import at GPT1.py:{node.lineno}: {mods}")
         if isinstance(node, ast.Assign) and len(node.targets) == 1 and isinstance(node.targets[0], ast.Name):
             name = node.targets[0].id
             if name in ("model", "m") and not build_model:
@@ -290,6 +308,25 @@ def fx_trained_and_greedy(steps=200, eval_every=50, eval_iters=20):
                os.path.join(OUT, "trained_c1.pt"))
 
 
+def fx_model_pth():
+    """A model.pth in the reference's own format (GPT1.py:239-241: torch.save of the full state_dict,
+    tril buffers included) at a small shape, plus the reference's logits/loss for a fixed batch:
+    the GPU suite loads it with load_state_dict(strict=True)."""
+    cfg = dict(block_size=32, n_embd=48, n_head=3, n_layers=2, batch_size=2)
+    ns = load_reference(dict(cfg, Dropout=0.0))
+    model = ns["model"]
+    gen = torch.Generator().manual_seed(21)
+    _perturb_ln(model, gen)
+    torch.save(model.state_dict(), os.path.join(OUT, "model_small_ref.pth"))
+    idx = torch.randint(0, 65, (2, 32), generator=gen)
+    tgt = torch.randint(0, 65, (2, 32), generator=gen)
+    with torch.no_grad():
+        logits, loss = model(idx, tgt)
+    torch.save({"config": cfg, "idx": idx, "targets": tgt, "logits": logits.clone(), "loss": loss.clone(),
+                "n_keys": len(model.state_dict())}, os.path.join(OUT, "model_small_ref_io.pt"))
+    print("model_small_ref.pth", len(model.state_dict()), "keys, loss", float(loss))
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-train", action="store_true")
@@ -297,7 +334,7 @@ if __name__ == "__main__":
     a = ap.parse_args()
     torch.set_num_threads(8)
     jobs = {"tokenizer": fx_tokenizer, "batches": fx_batches, "ops": fx_ops_small, "c1grads": fx_model_c1_grads,
-            "train": fx_train_deterministic, "trained": fx_trained_and_greedy}
+            "train": fx_train_deterministic, "trained": fx_trained_and_greedy, "modelpth": fx_model_pth}
     for name, fn in jobs.items():
         if a.only and name not in a.only.split(","):
             continue

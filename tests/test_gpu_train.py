@@ -85,19 +85,22 @@ def test_checkpoint_resume_is_bit_identical(tmp_path):
     assert torch.equal(m2.flat.master.detach().cpu(), w_master)
 
 
-def test_gpt1_driver_loss_curve_matches_reference(tmp_path, capsys):
+@pytest.mark.parametrize("dtype,tol0", [("fp32", 2e-4), ("bf16", 5e-3)])
+def test_gpt1_driver_loss_curve_matches_reference(tmp_path, capsys, dtype, tol0):
     """GPT1.py's loop (python -m replicatinggpt_amd.gpt1) on input.txt against the eval-loss curve the
     reference itself produced (tests/golden/trained_c1.pt: C1 shape, Dropout 0.2, lr 2e-4, 200
     steps, estimate_loss every 50 steps over 20 batches; fp32 here).  Step 0 evaluates the seeded
     init on the reference's own batch offsets (dropout is off in eval mode), so it must agree to
     fp32 rounding.  Later points follow different dropout masks and, because the reference's CPU
     dropout shares the generator with get_batch, different batches: they must agree
-    within 0.05 nats (2% of the loss)."""
+    within 0.05 nats (2% of the loss).  The bf16 path (the benchmarked one, GPT1.py:85-98,221-233 in
+    bf16 GEMM operands / activations with fp32 master weights) is held to the same curve; its step-0
+    point is the seeded init evaluated with bf16 operands, so it gets 5e-3 instead of fp32 rounding."""
     from replicatinggpt_amd import gpt1
     gold = torch.load(golden_path("trained_c1.pt"), weights_only=True)
     out = tmp_path / "model.pth"
     gpt1.main(["--lr", "2e-4", "--max-iters", "201", "--eval-interval", "50", "--eval-iters", "20",
-               "--max-new-tokens", "40", "--out", str(out)])
+               "--max-new-tokens", "40", "--out", str(out), "--dtype", dtype])
     text = capsys.readouterr().out
     lines = text.splitlines()
     assert lines[0] == "True"
@@ -105,7 +108,7 @@ def test_gpt1_driver_loss_curve_matches_reference(tmp_path, capsys):
     curve = [tuple(float(v) for v in mt.groups()) for mt in map(pat.match, lines) if mt]
     assert [c[0] for c in curve] == [0, 50, 100, 150, 200]
     for (it, tr, va), ref in zip(curve, gold["curve"].tolist()):
-        tol = 2e-4 if it == 0 else 0.05
+        tol = tol0 if it == 0 else 0.05
         assert abs(tr - ref[1]) <= tol and abs(va - ref[2]) <= tol, (it, tr, va, ref)
     sample = lines[len(curve) + 1:]
     assert sum(len(s) for s in sample) + len(sample) - 1 == 41    # decode of 1 + 40 tokens

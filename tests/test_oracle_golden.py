@@ -33,6 +33,25 @@ def test_philox_known_answers():
 def test_philox_keep_rate():
     keep = philox.keep_mask(1234, 7, np.arange(1 << 18), 0.2)
     assert abs(keep.mean() - 0.8) < 0.004
+    assert philox.threshold(0.2) == 13107 and philox.threshold(1e-9) == 1 and philox.threshold(0.0) == 0
+
+
+def test_philox_keep_spec_16bit():
+    """keep(idx) = half (idx & 1) of word ((idx >> 1) & 3) of Philox(group idx >> 3) >= round(p 2^16),
+    restated element by element from the KAT-pinned philox4x32_10, plus a regression pin of the packed
+    bits (csrc/common.h keep_of / keep4_bits / keep8_bits follow the same spec)."""
+    seed, stream, p = 0x1337, (5 << 8) | 3, 0.5
+    idx = np.arange(64, dtype=np.uint64) + np.uint64(1 << 33)
+    got = philox.keep_mask(seed, stream, idx, p)
+    for i, e in enumerate(idx.tolist()):
+        g = e >> 3
+        out = philox.philox4x32_10(g & 0xFFFFFFFF, g >> 32, stream & 0xFFFFFFFF, stream >> 32, seed, 0)
+        w = int(out[(e >> 1) & 3])
+        u = (w >> 16) if (e & 1) else (w & 0xFFFF)
+        assert bool(got[i]) == (u >= 32768), e
+    pack = lambda k: sum(int(b) << i for i, b in enumerate(k))
+    assert pack(got) == 0xb8ff66c6338a74a9
+    assert pack(philox.keep_mask(1234, 7, np.arange(64), 0.2)) == 0x7fff7d76dbf72d66
 
 
 def test_tokenizer_matches_reference():
