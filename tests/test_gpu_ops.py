@@ -128,8 +128,8 @@ def test_layernorm_bwd_rows_then_reduce_is_bitwise_ex(C, with_link):
 @pytest.mark.parametrize("M,F,K", [(512, 384, 128), (1024, 1536, 384), (16384, 1536, 384)])
 def test_relu_bwd_colpart_matches_colsum(M, F, K):
     """The ReLU-backward dgrad with fused column partials (cg_epilogue_t.colpart): the output is
-    bitwise the plain relu_bwd GEMM's, and the folded partials equal the column sums of the fp32
-    (pre-rounding) output to 1e-5 relative."""
+    bitwise the plain relu_bwd GEMM's, and the folded partials equal the column sums of that bf16
+    output (the values cg_colsum and the W1 weight gradient see) to 1e-5 relative."""
     O = ops()
     torch.manual_seed(5)
     dy = torch.randn(M, K, device=DEV).to(torch.bfloat16)
@@ -144,8 +144,10 @@ def test_relu_bwd_colpart_matches_colsum(M, F, K):
     O.reduce_rows(part, M // 64, F, cs, False)
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
+    assert relerr(cs, out.double().sum(0)) < 1e-5
+    # and they are the exact product's column sums up to the bf16 rounding of the output
     want = ((dy.double() @ w.double()) * (h.double() > 0)).sum(0)
-    assert relerr(cs, want) < 1e-5
+    assert relerr(cs, want) < 1e-2
 
 
 def _ref_gemm(A, B, at, bt):
