@@ -14,17 +14,27 @@ struct DropArgs {
     uint64_t seed;
     const uint64_t* rng_call;
     int site;
-    const uint64_t* mask;  // fast kernels: precomputed keep bits (k_attn_dropmask), NULL = no dropout
+    const uint64_t* mask;      // fast kernels: precomputed keep bits, FWD orientation; NULL = no dropout
+    const uint64_t* mask_bwd;  // the same bits, BWD orientation (mask + B*H*mask_tri_blocks(T)*16)
 };
 
-// Keep-bit image for the MFMA kernels, per (b*H + h) and 16x16 (query tile, key tile):
-// 4 uint64 words, bit l of word w = keep(query = 16*qt + (l & 15), key = 16*kt + 4*(l >> 4) + w).
-// Generated once per forward from the canonical Philox stream (same bits as keep_elem), read by
-// the forward, dQ and dK/dV kernels instead of re-running Philox in their inner loops.
-__device__ __forceinline__ const uint64_t* mask_tile(const uint64_t* mask, int bh, int NT, int qt, int kt) {
-    return mask + ((((int64_t)bh * NT + qt) * NT + kt) << 2);
+// Keep-bit image of the MFMA kernels, generated once per forward (k_attn_dropmask) from the
+// canonical Philox stream (same bits as keep_of on element ((b*H + h)*T + q)*T + k) and read by the
+// forward, dQ and dK/dV kernels.  Per (b*H + h) and per 32x32 block (query block qb, key block
+// kb <= qb, lower-triangle order), 16 uint64 words in each of two orientations -- exactly the
+// 32x32x16 MFMA accumulator layout (column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+// for register r), so word r is the lane mask of accumulator register r (one v_cndmask each):
+//   FWD (forward, dQ: swapped products, lane = query):
+//        bit l of word r = keep(q = 32 qb + (l & 31), k = 32 kb + (r & 3) + 8 (r >> 2) + 4 (l >> 5))
+//   BWD (dK/dV: lane = key):
+//        bit l of word r = keep(q = 32 qb + (r & 3) + 8 (r >> 2) + 4 (l >> 5), k = 32 kb + (l & 31))
+__host__ __device__ __forceinline__ int64_t mask_tri_blocks(int64_t T) {
+    const int64_t n = T / 32;
+    return n * (n + 1) / 2;
 }
-
+__device__ __forceinline__ const uint64_t* mask_block(const uint64_t* mask, int64_t bh, int64_t ntri, int qb, int kb) {
+    return mask + (bh * ntri + (int64_t)qb * (qb + 1) / 2 + kb) * 16;
+}
 
 namespace attn {
 // bf16 MFMA kernels, head_size 64, T % 64 == 0 (attention_d64.hip)
@@ -37,14 +47,6 @@ void launch_dq_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k
 void launch_dkdv_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                      const bf16_t* dout, int64_t ldd, const float* lse, const float* delta, bf16_t* dk, bf16_t* dv,
                      int64_t lddkv, float scale, const DropArgs& d, hipStream_t st);
-// whole-(b, h)-resident kernels for T % 64 == 0, T <= 256 (attention_res.hip), opt-in with
-// attn_variant bit 8
-bool res_ok(int64_t T);
-void launch_fwd_res(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
-                    bf16_t* o, int64_t ldo, float* lse, float scale, const DropArgs& d, hipStream_t st);
-void launch_bwd_res(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
-                    const bf16_t* o, int64_t ldo, const bf16_t* dout, int64_t ldd, const float* lse, bf16_t* dq,
-                    bf16_t* dk, bf16_t* dv, int64_t lddqkv, float scale, const DropArgs& d, hipStream_t st);
 }  // namespace attn
 extern int g_attn_variant;
 

@@ -1,546 +1,504 @@
 // charpt: bf16 MFMA causal attention for head_size 64 (the C2/C4 perf path of Head.forward x
-// n_head, GPT1.py:109-123,134-135) -- forward, dQ and dK/dV kernels.
+// n_head, GPT1.py:109-123,134-135) -- forward, dQ and dK/dV kernels on v_mfma_f32_32x32x16_bf16.
 //
-// All three kernels stream 64-row tiles (K/V for the query-block kernels, Q/dO for dK/dV)
-// through a double-buffered LDS ring: the next tile's global loads are issued into registers
-// before the current tile's MFMAs and written to the other LDS stage after them (one barrier per
-// tile), so load latency hides under compute.  Dropout keep bits (k_attn_dropmask) are staged
-// with each tile and read from LDS with uniform-address loads.
-//
-// Layouts (16x16x32 bf16 MFMA, lane l: A/B fragment rows l&15, k = 8(l>>4)..+7; C col = l&15,
-// row = 4(l>>4) + r):
-//  * forward / dQ: swapped S^T = K Q^T -- the query is the C column, so softmax statistics are
-//    lane-local; P^T (bf16) is directly the B operand of O^T = V^T P^T, and dS^T of dQ^T = K^T dS^T
-//    (V / K read with ds_read_b64_tr_b16 in the matching key order).
-//  * dK/dV: S = Q K^T -- the key is the C column; Z (= dropped P) and dS are the B operands of
-//    dV^T = dO^T Z and dK^T = Q^T dS.
-// QW / KW (queries / keys per wave, 16 or 32) trade registers (occupancy) for reuse.
-#include "attention_tile.h"
+// Structure (CDNA4: 64-wide waves, 32x32 MFMA tiles):
+//  * forward / dQ: a block of 4 waves owns 256 queries; each wave two 32-query groups, g and 7-g
+//    of the block, so every wave walks the same number of causal key tiles (1+4, 1+4, 2+3, 2+3 at
+//    the first block: the causal triangle is balanced inside the block).  Products are swapped --
+//    S^T = K Q^T, dP^T = V dO^T -- so the query is the accumulator column (lane & 31): softmax
+//    statistics are lane-local plus one lane^32 exchange, and the accumulator, packed to bf16, is
+//    directly the B operand of O^T = V^T P^T / dQ^T = K^T dS^T (V / K read transposed).
+//  * dK/dV: a block of 4 waves owns 128 keys (32 per wave); S = Q K^T, dP = dO V^T with the key
+//    as the column, Z = dropped P and dS feed dV^T = dO^T Z and dK^T = Q^T dS as B operands.
+//  * 64-row K/V (or Q/dO) tiles, register-staged into a double-buffered LDS ring (next tile's
+//    global loads issued before the current tile's MFMAs, written after them, one barrier per
+//    tile).  One XOR swizzle serves both the row reads (ds_read_b128) and the transposed reads
+//    (ds_read_b64_tr_b16) conflict-free.
+//  * Forward: lazy rescaling -- the running max is only moved (and O, l rescaled) when a tile's max
+//    exceeds it by 2^8, so the O-wide multiply is off the common path; probabilities stay <= 256.
+//  * Dropout keep bits (k_attn_dropmask, attention_common.h) are read as 64-bit lane masks by
+//    scalar loads and applied with one v_cndmask per element; the 1/(1-p) is applied once at the end.
+#include "attention_common.h"
 
 namespace cg {
 int g_attn_variant = 0;
 
 namespace {
-using namespace atile;
 
-// keep-bit rows for a (QROWS*16)-query block x 64-key tile: [QROWS q16][4 k16][32 B], 16 B per thread
-template <int QROWS>
-__device__ __forceinline__ uint4 qmask_load(const uint64_t* mask, int bh, int NT, int q16_0, int k16_0, int tid) {
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (mask && tid < QROWS * 8) {
-        const int row = tid >> 3, c = tid & 7;
-        if (q16_0 + row < NT) v = *(const uint4*)((const char*)mask_tile(mask, bh, NT, q16_0 + row, k16_0) + c * 16);
-    }
-    return v;
+typedef float fv16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) sv4 lds_sv4;
+
+constexpr int TILE = 8192;             // [64 rows][64 bf16] image
+constexpr float RESCALE_THR = 8.0f;    // log2 units (forward lazy rescale)
+
+__device__ __forceinline__ fv16 mfma32(sv8 a, sv8 b, fv16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bfv8, a), __builtin_bit_cast(bfv8, b), c, 0, 0,
+                                                   0);
+}
+
+// [64][64] bf16 image, 128-B rows; 16-B chunk c of row r at r*128 + ((c ^ X(r)) << 4) with
+// X(r) = ((r>>1)&1)<<2 | (r>>2)&3.  Row reads of the 32x32x16 operand (16-lane groups of
+// ds_read_b128 over rows {0-3,12-15,20-27} / {4-11,16-19,28-31}) land on 16 distinct 16-B slots;
+// transposed reads (a 32-lane half reads rows r0..r0+3, 64 bytes each) on 64 distinct banks.
+__device__ __forceinline__ int aoff(int r, int c) { return r * 128 + ((c ^ ((((r >> 1) & 1) << 2) | ((r >> 2) & 3))) << 4); }
+
+// A operand, tile rows rb..rb+31: lane l holds X(rb + (l&31), 16 ks + 8 (l>>5) + j), j = 0..7
+__device__ __forceinline__ sv8 frag_row(const char* img, int rb, int ks, int lane) {
+    return *(const sv8*)(img + aoff(rb + (lane & 31), 2 * ks + (lane >> 5)));
+}
+
+// A operand = tile^T, tile columns cb..cb+31 as rows: lane l, element j <-> tile row
+// rb + 16 ks + 8 (j>>2) + 4 (l>>5) + (j&3), column cb + (l&31) -- the k order of an accumulator
+// packed as the B operand (pack16 below).  Two ds_read_b64_tr_b16: each 16-lane group reads a
+// 4-row x 16-column block, lane 4q+p addressing row q, columns 4p..4p+3.
+__device__ __forceinline__ sv8 frag_tr(const char* img, int rb, int ks, int cb, int lane) {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int col = cb + 16 * (g & 1) + 4 * p;
+    const int r0 = rb + 16 * ks + 4 * (g >> 1) + q;
+    const int chunk = col >> 3, byte = (col & 7) * 2;
+    const sv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_sv4*)(img + aoff(r0, chunk) + byte));
+    const sv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_sv4*)(img + aoff(r0 + 8, chunk) + byte));
+    return sv8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// accumulator registers 8s..8s+7 -> bf16 B-operand fragment of k-step s
+__device__ __forceinline__ sv8 pack16(const fv16& x, int s) {
+    const uint32_t w0 = pack_bf2(x[8 * s + 0], x[8 * s + 1]), w1 = pack_bf2(x[8 * s + 2], x[8 * s + 3]);
+    const uint32_t w2 = pack_bf2(x[8 * s + 4], x[8 * s + 5]), w3 = pack_bf2(x[8 * s + 6], x[8 * s + 7]);
+    sv8 r;
+    r[0] = (short)(w0 & 0xffff); r[1] = (short)(w0 >> 16);
+    r[2] = (short)(w1 & 0xffff); r[3] = (short)(w1 >> 16);
+    r[4] = (short)(w2 & 0xffff); r[5] = (short)(w2 >> 16);
+    r[6] = (short)(w3 & 0xffff); r[7] = (short)(w3 >> 16);
+    return r;
+}
+
+// accumulator row of register r (column = lane & 31)
+__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+__device__ __forceinline__ bool keep_bit(uint64_t word) { return __builtin_amdgcn_inverse_ballot_w64(word); }
+
+// two [64][64] bf16 tiles (rows row0..row0+63 of X and Y) staged through registers: 4 x 16 B per thread
+struct Stage2 {
+    uint4 a0, a1, b0, b1;
+};
+__device__ __forceinline__ Stage2 stage_load(const bf16_t* X, int64_t ldx, const bf16_t* Y, int64_t ldy, int64_t row0,
+                                             int tid) {
+    const int r = tid >> 3, c = tid & 7;
+    Stage2 s;
+    s.a0 = *(const uint4*)(X + (row0 + r) * ldx + c * 8);
+    s.a1 = *(const uint4*)(X + (row0 + r + 32) * ldx + c * 8);
+    s.b0 = *(const uint4*)(Y + (row0 + r) * ldy + c * 8);
+    s.b1 = *(const uint4*)(Y + (row0 + r + 32) * ldy + c * 8);
+    return s;
+}
+__device__ __forceinline__ void stage_store(const Stage2& s, char* img, int tid) {
+    const int r = tid >> 3, c = tid & 7;
+    *(uint4*)(img + aoff(r, c)) = s.a0;
+    *(uint4*)(img + aoff(r + 32, c)) = s.a1;
+    *(uint4*)(img + TILE + aoff(r, c)) = s.b0;
+    *(uint4*)(img + TILE + aoff(r + 32, c)) = s.b1;
+}
+
+// XCD-aware block order for a (row blocks, B*H) grid: the dispatcher deals linear block ids to the
+// 8 XCDs round-robin and each XCD has its own L2; the bijective remap hands every XCD a contiguous
+// run of logical ids (whole (b, h) groups, which stream the same K/V or Q/dO), measured 35 -> 81 %
+// L2 hits at C4.  REV runs a group's blocks last-first (longest causal prefix first).
+template <bool REV>
+__device__ __forceinline__ void block_coords(int& blk, int& bh) {
+    const int nx = (int)gridDim.x, n = nx * (int)gridDim.y;
+    const int id = (int)blockIdx.y * nx + (int)blockIdx.x;
+    const int q = n >> 3, r = n & 7, xcd = id & 7;
+    const int lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
+    bh = lid / nx;
+    blk = lid - bh * nx;
+    if (REV) blk = nx - 1 - blk;
+}
+
+// 16-B fragment of row `row` of a row-major bf16 matrix, columns 16 ks + 8 (lane>>5) .. +7
+__device__ __forceinline__ sv8 ld_frag(const bf16_t* base, int64_t ld, int64_t row, int ks, int lane) {
+    return *(const sv8*)(base + row * ld + 16 * ks + 8 * (lane >> 5));
+}
+
+// store an O^T-layout accumulator pair (dims 32 dt + acc_row, one row per lane) as bf16, x mult
+__device__ __forceinline__ void store_rows(bf16_t* row, const fv16 (&acc)[2], float mult, int lane) {
+    const int h = lane >> 5;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float* x = &((const float*)&acc[dt])[4 * i];
+            *(uint2*)(row + 32 * dt + 8 * i + 4 * h) =
+                make_uint2(pack_bf2(x[0] * mult, x[1] * mult), pack_bf2(x[2] * mult, x[3] * mult));
+        }
 }
 
 // =====================================================================================
-// forward: block = 4 waves x QW queries, KV tiles of 64 keys
+// forward
 // =====================================================================================
-template <int QW>
-__global__ __launch_bounds__(256, QW == 16 ? 3 : 2) void k_attn_fwd_d64(
-    int64_t T_, int H, const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-    int64_t ld, bf16_t* __restrict__ o, int64_t ldo, float* __restrict__ lse, float scale_log2,
-    const uint64_t* __restrict__ mask, float dscale) {
-    constexpr int QT = QW / 16, FQ = 4 * QW, QROWS = FQ / 16;
-    constexpr int MB = QROWS * 128;  // keep-bit bytes per stage
-    constexpr int STG = 2 * TILE + MB;
-    __shared__ __attribute__((aligned(16))) char smem[2 * STG];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int g = lane >> 4, li = lane & 15;
-    int xblk, bh;
-    block_coords<true>(xblk, bh);
-    const int b = bh / H, h = bh % H;
-    const int NT = (int)(T_ >> 4);
-    const int64_t qblk0 = (int64_t)xblk * FQ;
-    const int64_t qw0 = qblk0 + wave * QW;
-    const int64_t boff = (int64_t)b * T_;
-    const bf16_t* kb_ = k + boff * ld + h * 64;
-    const bf16_t* vb_ = v + boff * ld + h * 64;
-    const bool wave_active = qw0 < T_;
-
-    sv8 qf[QT][2];  // Q^T as B operand: lane holds Q[qw0 + 16qt + li][32s + 8g ..]
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, const bf16_t* __restrict__ q,
+                                                         const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                                                         int64_t ld, bf16_t* __restrict__ o, int64_t ldo,
+                                                         float* __restrict__ lse, float scale_log2,
+                                                         const uint64_t* __restrict__ mask, float dscale) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int qblk, bh;
+    block_coords<true>(qblk, bh);
+    const int T = (int)T_, b = bh / H, hh = bh % H;
+    const int Q0 = qblk * 256;
+    const int64_t boff = (int64_t)b * T_, ntri = mask_tri_blocks(T_);
+    const bf16_t* kb_ = k + boff * ld + hh * 64;
+    const bf16_t* vb_ = v + boff * ld + hh * 64;
+    const int qg[2] = {Q0 + 32 * (7 - wave), Q0 + 32 * wave};   // g = 0: the longer causal prefix
+    const bool act[2] = {qg[0] < T, qg[1] < T};
+    sv8 qf[2][4];
 #pragma unroll
-    for (int qt = 0; qt < QT; ++qt)
+    for (int g = 0; g < 2; ++g)
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
-            qf[qt][s] = wave_active ? *(const sv8*)(q + (boff + qw0 + 16 * qt + li) * ld + h * 64 + 32 * s + 8 * g) : sv8{};
-
-    fv4 oacc[4][QT];
+        for (int ks = 0; ks < 4; ++ks)
+            qf[g][ks] = act[g] ? ld_frag(q + boff * ld + hh * 64, ld, qg[g] + (lane & 31), ks, lane) : sv8{};
+    fv16 oacc[2][2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < QT; ++j) oacc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
-    float m_run[QT], l_run[QT];
-#pragma unroll
-    for (int j = 0; j < QT; ++j) {
-        m_run[j] = -INFINITY;
-        l_run[j] = 0.f;
-    }
-
-    const int64_t qlast = (qblk0 + FQ - 1) < (T_ - 1) ? (qblk0 + FQ - 1) : (T_ - 1);
-    const int nkv = (int)(qlast / 64) + 1;
-    const int q16_0 = (int)(qblk0 >> 4);
-    {
-        const Tile2 kt = tile_load(kb_, ld, 0, tid), vt = tile_load(vb_, ld, 0, tid);
-        const uint4 mt = qmask_load<QROWS>(mask, bh, NT, q16_0, 0, tid);
-        tile_store<false>(kt, smem, tid);
-        tile_store<true>(vt, smem + TILE, tid);
-        if (tid < QROWS * 8) *(uint4*)(smem + 2 * TILE + tid * 16) = mt;
-    }
+    for (int g = 0; g < 2; ++g) oacc[g][0] = oacc[g][1] = fv16{};
+    float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+    const int qlast = (Q0 + 255 < T - 1) ? Q0 + 255 : T - 1;
+    const int nkv = qlast / 64 + 1;
+    stage_store(stage_load(kb_, ld, vb_, ld, 0, tid), smem, tid);
     __syncthreads();
     for (int kv = 0; kv < nkv; ++kv) {
         const int nxt = kv + 1 < nkv ? kv + 1 : kv;
-        const Tile2 kn = tile_load(kb_, ld, (int64_t)nxt * 64, tid), vn = tile_load(vb_, ld, (int64_t)nxt * 64, tid);
-        const uint4 mn = qmask_load<QROWS>(mask, bh, NT, q16_0, nxt * 4, tid);
-        const char* S = smem + (kv & 1) * STG;
-        const int64_t k0 = (int64_t)kv * 64;
-        if (wave_active && k0 <= qw0 + QW - 1) {
-            const char* Ki = S;
-            const char* Vi = S + TILE;
-            fv4 sacc[4][QT];
+        const Stage2 st = stage_load(kb_, ld, vb_, ld, (int64_t)nxt * 64, tid);
+        const char* Ki = smem + (kv & 1) * 2 * TILE;
+        const char* Vi = Ki + TILE;
+        const int k0 = kv * 64;
 #pragma unroll
-            for (int kt = 0; kt < 4; ++kt) {
-                const sv8 a0 = frag_rows<false>(Ki, 16 * kt, 0, lane), a1 = frag_rows<false>(Ki, 16 * kt, 1, lane);
+        for (int g = 0; g < 2; ++g) {
+            if (!act[g] || k0 > qg[g] + 31) continue;
+            const bool live1 = k0 + 32 <= qg[g] + 31;   // second 32-key subtile not fully masked
+            fv16 s[2] = {fv16{}, fv16{}};
 #pragma unroll
-                for (int qt = 0; qt < QT; ++qt) {
-                    fv4 c = {0.f, 0.f, 0.f, 0.f};
-                    c = mfma16(a0, qf[qt][0], c);
-                    sacc[kt][qt] = mfma16(a1, qf[qt][1], c);
-                }
+            for (int kt = 0; kt < 2; ++kt) {
+                if (kt == 1 && !live1) break;
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) s[kt] = mfma32(frag_row(Ki, 32 * kt, ks, lane), qf[g][ks], s[kt]);
             }
-            const bool diag = k0 + 63 > qw0;
-            float alpha[QT];
+            const int qa = qg[g] + (lane & 31);
+            const bool diag = k0 + 63 > qg[g];
+            float mx = -INFINITY;
 #pragma unroll
-            for (int qt = 0; qt < QT; ++qt) {
-                // raw scores; the scale is applied inside the exponent's fma (max commutes with
-                // the positive scale, and the rounding is monotone: same max as scaling first)
-                const int qa = (int)(qw0 + 16 * qt) + li, kb = (int)k0 + 4 * g;
-                float mx = -INFINITY;
+            for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-                for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        float x = sacc[kt][qt][r];
-                        if (diag && kb + 16 * kt + r > qa) x = -INFINITY;
-                        sacc[kt][qt][r] = x;
-                        mx = fmaxf(mx, x);
-                    }
-                mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-                mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-                const float m_new = fmaxf(m_run[qt], mx * scale_log2);
-                alpha[qt] = __builtin_amdgcn_exp2f(m_run[qt] - m_new);
-                float ls = 0.f;
-#pragma unroll
-                for (int kt = 0; kt < 4; ++kt) {
-                    Words4 mw = {{~0ull, ~0ull, ~0ull, ~0ull}};  // no dropout: keep everything, no branch
-                    if (mask) mw = lds_words(S + 2 * TILE + ((wave * QT + qt) * 4 + kt) * 32);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        // exp2 of the raw hardware instruction: results below 2^-126 (weights that
-                        // vanish against the row max) flush to 0 instead of going denormal
-                        const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kt][qt][r], scale_log2, -m_new));
-                        ls += p;
-                        // 1/(1-p) of the kept weights is applied once, in the epilogue
-                        sacc[kt][qt][r] = keep_sel(mw.w[r], p);
-                    }
+                for (int r = 0; r < 16; ++r) {
+                    float x = s[kt][r];
+                    if (diag && k0 + 32 * kt + acc_row(r, lane) > qa) x = -INFINITY;
+                    s[kt][r] = x;
+                    mx = fmaxf(mx, x);
                 }
-                ls += __shfl_xor(ls, 16, 64);
-                ls += __shfl_xor(ls, 32, 64);
-                l_run[qt] = l_run[qt] * alpha[qt] + ls;
-                m_run[qt] = m_new;
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            const float mt = mx * scale_log2;
+            if (__any(mt > m_run[g] + RESCALE_THR)) {   // rare after the first tiles
+                const float mn = fmaxf(m_run[g], mt);
+                const float alpha = __builtin_amdgcn_exp2f(m_run[g] - mn);
+                oacc[g][0] *= alpha;
+                oacc[g][1] *= alpha;
+                l_run[g] *= alpha;
+                m_run[g] = mn;
             }
-            sv8 pf[2][QT];
+            const float mneg = -m_run[g];
+            float ls = 0.f;
+            sv8 pf[2][2];
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int qt = 0; qt < QT; ++qt) pf[u][qt] = pack8(sacc[2 * u][qt], sacc[2 * u + 1][qt]);
-#pragma unroll
-            for (int et = 0; et < 4; ++et) {
-                const sv8 v0 = frag_tr<true>(Vi, 0, 16 * et, lane), v1 = frag_tr<true>(Vi, 32, 16 * et, lane);
-#pragma unroll
-                for (int qt = 0; qt < QT; ++qt) {
-                    fv4 c = oacc[et][qt] * alpha[qt];
-                    c = mfma16(v0, pf[0][qt], c);
-                    oacc[et][qt] = mfma16(v1, pf[1][qt], c);
+            for (int kt = 0; kt < 2; ++kt) {
+                if (kt == 1 && !live1) {
+                    pf[1][0] = pf[1][1] = sv8{};
+                    break;
                 }
+                const uint64_t* mw = DROP ? mask_block(mask, bh, ntri, qg[g] >> 5, (k0 >> 5) + kt) : nullptr;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    // raw v_exp_f32: weights below 2^-126 of the stale max flush to 0
+                    const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][r], scale_log2, mneg));
+                    ls += p;
+                    s[kt][r] = DROP ? (keep_bit(mw[r]) ? p : 0.f) : p;
+                }
+                pf[kt][0] = pack16(s[kt], 0);
+                pf[kt][1] = pack16(s[kt], 1);
             }
+            l_run[g] += ls;
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                for (int kt = 0; kt < 2; ++kt) {
+                    if (kt == 1 && !live1) break;
+#pragma unroll
+                    for (int sk = 0; sk < 2; ++sk)
+                        oacc[g][dt] = mfma32(frag_tr(Vi, 32 * kt, sk, 32 * dt, lane), pf[kt][sk], oacc[g][dt]);
+                }
         }
-        char* D = smem + ((kv + 1) & 1) * STG;
-        tile_store<false>(kn, D, tid);
-        tile_store<true>(vn, D + TILE, tid);
-        if (tid < QROWS * 8) *(uint4*)(D + 2 * TILE + tid * 16) = mn;
+        stage_store(st, smem + ((kv + 1) & 1) * 2 * TILE, tid);
         __syncthreads();
     }
-    if (!wave_active) return;
 #pragma unroll
-    for (int qt = 0; qt < QT; ++qt) {
-        const int64_t qa = qw0 + 16 * qt + li;
-        if (qa >= T_) continue;
-        const float inv = dscale / l_run[qt];
-        bf16_t* orow = o + (boff + qa) * ldo + h * 64;
-#pragma unroll
-        for (int et = 0; et < 4; ++et) {
-            const fv4 x = oacc[et][qt] * inv;
-            *(uint2*)(orow + 16 * et + 4 * g) = make_uint2(pack_bf2(x[0], x[1]), pack_bf2(x[2], x[3]));
-        }
-        if (g == 0) lse[(int64_t)bh * T_ + qa] = (m_run[qt] + log2f(l_run[qt])) * LN2;
+    for (int g = 0; g < 2; ++g) {
+        if (!act[g]) continue;
+        const float lt = l_run[g] + __shfl_xor(l_run[g], 32, 64);
+        const int64_t qa = qg[g] + (lane & 31);
+        store_rows(o + (boff + qa) * ldo + hh * 64, oacc[g], dscale / lt, lane);
+        if (lane < 32) lse[(int64_t)bh * T_ + qa] = (m_run[g] + __log2f(lt)) * LN2;
     }
 }
 
 // =====================================================================================
 // dQ: S^T = K Q^T, dP^T = V dO^T, dS^T = P^T (keep/(1-p) dP^T - delta), dQ^T += K^T dS^T
 // =====================================================================================
-template <int QW>
-__global__ __launch_bounds__(256, QW == 16 ? 3 : 2) void k_attn_dq_d64(
-    int64_t T_, int H, const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-    int64_t ld, const bf16_t* __restrict__ o, int64_t ldo, const bf16_t* __restrict__ dout, int64_t ldd,
-    const float* __restrict__ lse, float* __restrict__ delta, bf16_t* __restrict__ dq, int64_t lddq, float scale,
-    const uint64_t* __restrict__ mask, float dscale) {
-    constexpr int QT = QW / 16, FQ = 4 * QW, QROWS = FQ / 16;
-    constexpr int MB = QROWS * 128;
-    constexpr int STG = 2 * TILE + MB;
-    __shared__ __attribute__((aligned(16))) char smem[2 * STG];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int g = lane >> 4, li = lane & 15;
-    int xblk, bh;
-    block_coords<true>(xblk, bh);
-    const int b = bh / H, h = bh % H;
-    const int NT = (int)(T_ >> 4);
-    const int64_t qblk0 = (int64_t)xblk * FQ;
-    const int64_t qw0 = qblk0 + wave * QW;
-    const int64_t boff = (int64_t)b * T_;
-    const bool wave_active = qw0 < T_;
-    const float scale_log2 = scale * LOG2E;
-
-    sv8 qf[QT][2], of[QT][2];
-    float lq[QT], dl[QT];
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void k_attn_dq_d64(int64_t T_, int H, const bf16_t* __restrict__ q,
+                                                        const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                                                        int64_t ld, const bf16_t* __restrict__ o, int64_t ldo,
+                                                        const bf16_t* __restrict__ dout, int64_t ldd,
+                                                        const float* __restrict__ lse, float* __restrict__ delta,
+                                                        bf16_t* __restrict__ dq, int64_t lddq, float scale,
+                                                        const uint64_t* __restrict__ mask, float dscale) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int qblk, bh;
+    block_coords<true>(qblk, bh);
+    const int T = (int)T_, b = bh / H, hh = bh % H;
+    const int Q0 = qblk * 256;
+    const int64_t boff = (int64_t)b * T_, ntri = mask_tri_blocks(T_);
+    const float c2 = scale * LOG2E;
+    const bf16_t* kb_ = k + boff * ld + hh * 64;
+    const bf16_t* vb_ = v + boff * ld + hh * 64;
+    const int qg[2] = {Q0 + 32 * (7 - wave), Q0 + 32 * wave};
+    const bool act[2] = {qg[0] < T, qg[1] < T};
+    sv8 qf[2][4], df[2][4];
+    float lse2[2], dl[2];
 #pragma unroll
-    for (int qt = 0; qt < QT; ++qt) {
-        const int64_t qrow = qw0 + 16 * qt + li;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            qf[qt][s] = wave_active ? *(const sv8*)(q + (boff + qrow) * ld + h * 64 + 32 * s + 8 * g) : sv8{};
-            of[qt][s] = wave_active ? *(const sv8*)(dout + (boff + qrow) * ldd + h * 64 + 32 * s + 8 * g) : sv8{};
-        }
-        lq[qt] = wave_active ? lse[(int64_t)bh * T_ + qrow] * LOG2E : 0.f;
-        // delta = rowsum(dO * O) (dropout-invariant: O already holds the dropped P); lane group g
-        // holds elements 32s + 8g .. +7 of the row: reduce over s in-lane, then across g
+    for (int g = 0; g < 2; ++g) {
+        const int64_t qa = qg[g] + (lane & 31);
         float dsum = 0.f;
-        if (wave_active) {
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const uint4 ov = *(const uint4*)(o + (boff + qrow) * ldo + h * 64 + 32 * s + 8 * g);
-                const sv8 dv8 = of[qt][s];
-                const uint32_t ow[4] = {ov.x, ov.y, ov.z, ov.w};
+        for (int ks = 0; ks < 4; ++ks) {
+            qf[g][ks] = act[g] ? ld_frag(q + boff * ld + hh * 64, ld, qa, ks, lane) : sv8{};
+            df[g][ks] = act[g] ? ld_frag(dout + boff * ldd + hh * 64, ldd, qa, ks, lane) : sv8{};
+            if (act[g]) {
+                // delta = rowsum(dO * O) (dropout-invariant: O already holds the dropped P)
+                const sv8 of = ld_frag(o + boff * ldo + hh * 64, ldo, qa, ks, lane);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    dsum += __uint_as_float(ow[e] << 16) * __uint_as_float(((uint32_t)(uint16_t)dv8[2 * e]) << 16);
-                    dsum += __uint_as_float(ow[e] & 0xffff0000u) *
-                            __uint_as_float(((uint32_t)(uint16_t)dv8[2 * e + 1]) << 16);
-                }
+                for (int j = 0; j < 8; ++j) dsum += bf2f((bf16_t)of[j]) * bf2f((bf16_t)df[g][ks][j]);
             }
         }
-        dsum += __shfl_xor(dsum, 16, 64);
         dsum += __shfl_xor(dsum, 32, 64);
-        dl[qt] = dsum;
-        if (wave_active && g == 0) delta[(int64_t)bh * T_ + qrow] = dsum;
+        dl[g] = dsum;
+        lse2[g] = act[g] ? lse[(int64_t)bh * T_ + qa] * LOG2E : 0.f;
+        if (act[g] && lane < 32) delta[(int64_t)bh * T_ + qa] = dsum;
     }
-    fv4 dqacc[4][QT];
+    fv16 dqa[2][2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < QT; ++j) dqacc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
-    const bf16_t* kb_ = k + boff * ld + h * 64;
-    const bf16_t* vb_ = v + boff * ld + h * 64;
-    const int64_t qlast = (qblk0 + FQ - 1) < (T_ - 1) ? (qblk0 + FQ - 1) : (T_ - 1);
-    const int nkv = (int)(qlast / 64) + 1;
-    const int q16_0 = (int)(qblk0 >> 4);
-    {
-        const Tile2 kt = tile_load(kb_, ld, 0, tid), vt = tile_load(vb_, ld, 0, tid);
-        const uint4 mt = qmask_load<QROWS>(mask, bh, NT, q16_0, 0, tid);
-        tile_store<false>(kt, smem, tid);
-        tile_store<false>(vt, smem + TILE, tid);
-        if (tid < QROWS * 8) *(uint4*)(smem + 2 * TILE + tid * 16) = mt;
-    }
+    for (int g = 0; g < 2; ++g) dqa[g][0] = dqa[g][1] = fv16{};
+    const int qlast = (Q0 + 255 < T - 1) ? Q0 + 255 : T - 1;
+    const int nkv = qlast / 64 + 1;
+    stage_store(stage_load(kb_, ld, vb_, ld, 0, tid), smem, tid);
     __syncthreads();
     for (int kv = 0; kv < nkv; ++kv) {
         const int nxt = kv + 1 < nkv ? kv + 1 : kv;
-        const Tile2 kn = tile_load(kb_, ld, (int64_t)nxt * 64, tid), vn = tile_load(vb_, ld, (int64_t)nxt * 64, tid);
-        const uint4 mn = qmask_load<QROWS>(mask, bh, NT, q16_0, nxt * 4, tid);
-        const char* S = smem + (kv & 1) * STG;
-        const int64_t k0 = (int64_t)kv * 64;
-        if (wave_active && k0 <= qw0 + QW - 1) {
-            const char* Ki = S;
-            const char* Vi = S + TILE;
-            fv4 sa[4][QT], pa[4][QT];
+        const Stage2 st = stage_load(kb_, ld, vb_, ld, (int64_t)nxt * 64, tid);
+        const char* Ki = smem + (kv & 1) * 2 * TILE;
+        const char* Vi = Ki + TILE;
+        const int k0 = kv * 64;
 #pragma unroll
-            for (int kt = 0; kt < 4; ++kt) {
-                const sv8 k0f = frag_rows<false>(Ki, 16 * kt, 0, lane), k1f = frag_rows<false>(Ki, 16 * kt, 1, lane);
-                const sv8 v0f = frag_rows<false>(Vi, 16 * kt, 0, lane), v1f = frag_rows<false>(Vi, 16 * kt, 1, lane);
+        for (int g = 0; g < 2; ++g) {
+            if (!act[g] || k0 > qg[g] + 31) continue;
+            const int qa = qg[g] + (lane & 31);
+            const bool diag = k0 + 63 > qg[g];
 #pragma unroll
-                for (int qt = 0; qt < QT; ++qt) {
-                    fv4 c = {0.f, 0.f, 0.f, 0.f};
-                    c = mfma16(k0f, qf[qt][0], c);
-                    sa[kt][qt] = mfma16(k1f, qf[qt][1], c);
-                    fv4 d = {0.f, 0.f, 0.f, 0.f};
-                    d = mfma16(v0f, of[qt][0], d);
-                    pa[kt][qt] = mfma16(v1f, of[qt][1], d);
+            for (int kt = 0; kt < 2; ++kt) {
+                if (k0 + 32 * kt > qg[g] + 31) break;   // subtile fully masked
+                fv16 s = fv16{}, dp = fv16{};
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) {
+                    s = mfma32(frag_row(Ki, 32 * kt, ks, lane), qf[g][ks], s);
+                    dp = mfma32(frag_row(Vi, 32 * kt, ks, lane), df[g][ks], dp);
                 }
-            }
+                const uint64_t* mw = DROP ? mask_block(mask, bh, ntri, qg[g] >> 5, (k0 >> 5) + kt) : nullptr;
 #pragma unroll
-            for (int qt = 0; qt < QT; ++qt) {
-                const int qa = (int)(qw0 + 16 * qt) + li, kb = (int)k0 + 4 * g;
-#pragma unroll
-                for (int kt = 0; kt < 4; ++kt) {
-                    Words4 mw = {{~0ull, ~0ull, ~0ull, ~0ull}};  // no dropout: keep everything, no branch
-                    if (mask) mw = lds_words(S + 2 * TILE + ((wave * QT + qt) * 4 + kt) * 32);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const float p = kb + 16 * kt + r > qa
-                                            ? 0.f
-                                            : __builtin_amdgcn_exp2f(fmaf(sa[kt][qt][r], scale_log2, -lq[qt]));
-                        float dp = pa[kt][qt][r];
-                        dp = keep_sel(mw.w[r], dp * dscale);  // dscale is 1 without dropout
-                        sa[kt][qt][r] = p * (dp - dl[qt]);
-                    }
+                for (int r = 0; r < 16; ++r) {
+                    float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lse2[g]));
+                    if (diag && k0 + 32 * kt + acc_row(r, lane) > qa) p = 0.f;
+                    float d = dp[r];
+                    if (DROP) d = keep_bit(mw[r]) ? d * dscale : 0.f;
+                    s[r] = p * (d - dl[g]);
                 }
-            }
+                const sv8 d0 = pack16(s, 0), d1 = pack16(s, 1);
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                sv8 dsf[QT];
-#pragma unroll
-                for (int qt = 0; qt < QT; ++qt) dsf[qt] = pack8(sa[2 * u][qt], sa[2 * u + 1][qt]);
-#pragma unroll
-                for (int et = 0; et < 4; ++et) {
-                    const sv8 kf = frag_tr<false>(Ki, 32 * u, 16 * et, lane);
-#pragma unroll
-                    for (int qt = 0; qt < QT; ++qt) dqacc[et][qt] = mfma16(kf, dsf[qt], dqacc[et][qt]);
+                for (int dt = 0; dt < 2; ++dt) {
+                    dqa[g][dt] = mfma32(frag_tr(Ki, 32 * kt, 0, 32 * dt, lane), d0, dqa[g][dt]);
+                    dqa[g][dt] = mfma32(frag_tr(Ki, 32 * kt, 1, 32 * dt, lane), d1, dqa[g][dt]);
                 }
             }
         }
-        char* D = smem + ((kv + 1) & 1) * STG;
-        tile_store<false>(kn, D, tid);
-        tile_store<false>(vn, D + TILE, tid);
-        if (tid < QROWS * 8) *(uint4*)(D + 2 * TILE + tid * 16) = mn;
+        stage_store(st, smem + ((kv + 1) & 1) * 2 * TILE, tid);
         __syncthreads();
     }
-    if (!wave_active) return;
 #pragma unroll
-    for (int qt = 0; qt < QT; ++qt) {
-        const int64_t qa = qw0 + 16 * qt + li;
-        if (qa >= T_) continue;
-        bf16_t* row = dq + (boff + qa) * lddq + h * 64;
-#pragma unroll
-        for (int et = 0; et < 4; ++et) {
-            const fv4 x = dqacc[et][qt] * scale;
-            *(uint2*)(row + 16 * et + 4 * g) = make_uint2(pack_bf2(x[0], x[1]), pack_bf2(x[2], x[3]));
-        }
+    for (int g = 0; g < 2; ++g) {
+        if (!act[g]) continue;
+        const int64_t qa = qg[g] + (lane & 31);
+        store_rows(dq + (boff + qa) * lddq + hh * 64, dqa[g], scale, lane);
     }
 }
 
 // =====================================================================================
-// dK / dV: block = 4 waves x KW keys; stream 64-query tiles (Q, dO, lse, delta, keep bits)
+// dK / dV: block = 4 waves x 32 keys; stream 64-query tiles (Q, dO, lse, delta)
 // =====================================================================================
-template <int KW>
-__global__ __launch_bounds__(256, KW == 16 ? 2 : 1) void k_attn_dkdv_d64(
-    int64_t T_, int H, const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-    int64_t ld, const bf16_t* __restrict__ dout, int64_t ldd, const float* __restrict__ lse,
-    const float* __restrict__ delta, bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int64_t lddkv, float scale,
-    const uint64_t* __restrict__ mask, float dscale) {
-    constexpr int KT = KW / 16, FK = 4 * KW, K16 = FK / 16;  // key tiles per block
-    constexpr int CPR = K16 * 2;                             // 16-B keep-bit chunks per q16 row
-    constexpr int STAT = 2 * TILE;                           // lse*log2e [64] then delta [64]
-    constexpr int MSK = 2 * TILE + 512;                      // keep bits [4 q16][K16][32 B]
-    constexpr int STG = MSK + 4 * K16 * 32;
-    __shared__ __attribute__((aligned(16))) char smem[2 * STG];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int g = lane >> 4, li = lane & 15;
-    int xblk, bh;
-    block_coords<false>(xblk, bh);
-    const int b = bh / H, h = bh % H;
-    const int NT = (int)(T_ >> 4);
-    const int64_t kblk0 = (int64_t)xblk * FK;
-    const int64_t kw0 = kblk0 + wave * KW;
-    const int64_t boff = (int64_t)b * T_;
-    const bool wave_active = kw0 < T_;
-    const float scale_log2 = scale * LOG2E;
-    const int k16_0 = (int)(kblk0 >> 4);
+constexpr int KV_STAGE = 2 * TILE + 512;   // Q image, dO image, lse*log2e [64], delta [64]
 
-    sv8 kf[KT][2], vf[KT][2];
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, const bf16_t* __restrict__ q,
+                                                          const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                                                          int64_t ld, const bf16_t* __restrict__ dout, int64_t ldd,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ delta, bf16_t* __restrict__ dk,
+                                                          bf16_t* __restrict__ dv, int64_t lddkv, float scale,
+                                                          const uint64_t* __restrict__ mask, float dscale) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * KV_STAGE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int kblk, bh;
+    block_coords<false>(kblk, bh);
+    const int T = (int)T_, b = bh / H, hh = bh % H;
+    const int K0 = kblk * 128, kq = K0 + 32 * wave;
+    const bool act = kq < T;
+    const int64_t boff = (int64_t)b * T_, ntri = mask_tri_blocks(T_);
+    const float c2 = scale * LOG2E;
+    const int key = kq + (lane & 31);
+    sv8 kf[4], vf[4];
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int64_t krow = kw0 + 16 * kt + li;
-            kf[kt][s] = wave_active ? *(const sv8*)(k + (boff + krow) * ld + h * 64 + 32 * s + 8 * g) : sv8{};
-            vf[kt][s] = wave_active ? *(const sv8*)(v + (boff + krow) * ld + h * 64 + 32 * s + 8 * g) : sv8{};
-        }
-    fv4 dka[4][KT], dva[4][KT];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < KT; ++j) dka[i][j] = dva[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
-    const bf16_t* qb_ = q + boff * ld + h * 64;
-    const bf16_t* ob_ = dout + boff * ldd + h * 64;
-    const int nq = (int)(T_ / 64);
-    const int q_start = (int)(kblk0 / 64);
-
-    struct QStage {
-        Tile2 qt, ot;
-        float stat;
-        uint4 msk;
-    };
-    auto qload = [&](int qtile) {
-        QStage s;
-        s.qt = tile_load(qb_, ld, (int64_t)qtile * 64, tid);
-        s.ot = tile_load(ob_, ldd, (int64_t)qtile * 64, tid);
-        s.stat = 0.f;
-        if (tid < 64) s.stat = lse[(int64_t)bh * T_ + (int64_t)qtile * 64 + tid] * LOG2E;
-        else if (tid < 128) s.stat = delta[(int64_t)bh * T_ + (int64_t)qtile * 64 + tid - 64];
-        s.msk = make_uint4(0, 0, 0, 0);
-        if (mask && tid >= 128 && tid < 128 + 4 * CPR) {
-            const int row = (tid - 128) / CPR, c = (tid - 128) % CPR;
-            if (k16_0 + (c >> 1) < NT)
-                s.msk = *(const uint4*)((const char*)mask_tile(mask, bh, NT, qtile * 4 + row, k16_0) + c * 16);
-        }
+    for (int ks = 0; ks < 4; ++ks) {
+        kf[ks] = act ? ld_frag(k + boff * ld + hh * 64, ld, key, ks, lane) : sv8{};
+        vf[ks] = act ? ld_frag(v + boff * ld + hh * 64, ld, key, ks, lane) : sv8{};
+    }
+    fv16 dka[2] = {fv16{}, fv16{}}, dva[2] = {fv16{}, fv16{}};
+    const bf16_t* qb_ = q + boff * ld + hh * 64;
+    const bf16_t* ob_ = dout + boff * ldd + hh * 64;
+    const float* lse_b = lse + (int64_t)bh * T_;
+    const float* del_b = delta + (int64_t)bh * T_;
+    const int nq = T / 64, qt0 = K0 / 64;
+    auto stat_load = [&](int qt) {
+        float s = 0.f;
+        if (tid < 64) s = lse_b[qt * 64 + tid] * LOG2E;
+        else if (tid < 128) s = del_b[qt * 64 + tid - 64];
         return s;
     };
-    auto qstore = [&](const QStage& s, char* D) {
-        tile_store<false>(s.qt, D, tid);
-        tile_store<false>(s.ot, D + TILE, tid);
-        if (tid < 128) ((float*)(D + STAT))[tid] = s.stat;
-        else if (tid < 128 + 4 * CPR) *(uint4*)(D + MSK + (tid - 128) * 16) = s.msk;
-    };
-    qstore(qload(q_start), smem);
+    {
+        stage_store(stage_load(qb_, ld, ob_, ldd, (int64_t)qt0 * 64, tid), smem, tid);
+        const float s = stat_load(qt0);
+        if (tid < 128) ((float*)(smem + 2 * TILE))[tid] = s;
+    }
     __syncthreads();
-    for (int qtile = q_start; qtile < nq; ++qtile) {
-        const int it = qtile - q_start;
-        const QStage nxt = qload(qtile + 1 < nq ? qtile + 1 : qtile);
-        const char* S = smem + (it & 1) * STG;
-        const int64_t q0 = (int64_t)qtile * 64;
-        if (wave_active && q0 + 63 >= kw0) {
-            const char* Qi = S;
-            const char* Oi = S + TILE;
-            const float* st_lse = (const float*)(S + STAT);
-            const float* st_del = st_lse + 64;
+    for (int qt = qt0; qt < nq; ++qt) {
+        const int it = qt - qt0;
+        const int nxt = qt + 1 < nq ? qt + 1 : qt;
+        const Stage2 st = stage_load(qb_, ld, ob_, ldd, (int64_t)nxt * 64, tid);
+        const float sn = stat_load(nxt);
+        const char* S0 = smem + (it & 1) * KV_STAGE;
+        const char* Qi = S0;
+        const char* Oi = S0 + TILE;
+        const float* st_lse = (const float*)(S0 + 2 * TILE);
+        const float* st_del = st_lse + 64;
+        const int q0 = qt * 64;
+        if (act && q0 + 63 >= kq) {
 #pragma unroll
-            for (int half = 0; half < 2; ++half) {
-                const int qr0 = 32 * half;
-                if (q0 + qr0 + 31 < kw0) continue;
-                sv8 zf[KT], dsf[KT];
+            for (int qs = 0; qs < 2; ++qs) {
+                const int q0s = q0 + 32 * qs;
+                if (q0s + 31 < kq) continue;   // every query of the subtile precedes every key
+                fv16 s = fv16{}, dp = fv16{};
 #pragma unroll
-                for (int kt = 0; kt < KT; ++kt) {
-                    const int key = (int)kw0 + 16 * kt + li;
-                    fv4 z[2], ds[2];
-#pragma unroll
-                    for (int qt = 0; qt < 2; ++qt) {
-                        const sv8 q0f = frag_rows<false>(Qi, qr0 + 16 * qt, 0, lane);
-                        const sv8 q1f = frag_rows<false>(Qi, qr0 + 16 * qt, 1, lane);
-                        const sv8 o0f = frag_rows<false>(Oi, qr0 + 16 * qt, 0, lane);
-                        const sv8 o1f = frag_rows<false>(Oi, qr0 + 16 * qt, 1, lane);
-                        fv4 sa = {0.f, 0.f, 0.f, 0.f}, pa = {0.f, 0.f, 0.f, 0.f};
-                        sa = mfma16(q0f, kf[kt][0], sa);
-                        sa = mfma16(q1f, kf[kt][1], sa);
-                        pa = mfma16(o0f, vf[kt][0], pa);
-                        pa = mfma16(o1f, vf[kt][1], pa);
-                        uint64_t keepbits = 0xFull;  // bit r -> keep(query 4g + r, key li)
-                        if (mask) {
-                            const Words4 mw = lds_words(S + MSK + ((half * 2 + qt) * K16 + wave * KT + kt) * 32);
-                            const int w = li & 3;
-                            const uint64_t bw = w == 0 ? mw.w[0] : (w == 1 ? mw.w[1] : (w == 2 ? mw.w[2] : mw.w[3]));
-                            keepbits = 0;
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) keepbits |= ((bw >> ((4 * g + r) + 16 * (li >> 2))) & 1ull) << r;
-                        }
-                        const int qb = (int)q0 + qr0 + 16 * qt + 4 * g;
-                        const float4 lse4 = *(const float4*)(st_lse + qr0 + 16 * qt + 4 * g);
-                        const float4 del4 = *(const float4*)(st_del + qr0 + 16 * qt + 4 * g);
-                        const float lsev[4] = {lse4.x, lse4.y, lse4.z, lse4.w};
-                        const float delv[4] = {del4.x, del4.y, del4.z, del4.w};
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const float p = key > qb + r ? 0.f : __builtin_amdgcn_exp2f(fmaf(sa[r], scale_log2, -lsev[r]));
-                            const bool kp = (keepbits >> r) & 1ull;
-                            const float dp = kp ? pa[r] * dscale : 0.f;
-                            z[qt][r] = kp ? p : 0.f;   // 1/(1-p) of dV applied in the epilogue
-                            ds[qt][r] = p * (dp - delv[r]);
-                        }
-                    }
-                    zf[kt] = pack8(z[0], z[1]);
-                    dsf[kt] = pack8(ds[0], ds[1]);
+                for (int ks = 0; ks < 4; ++ks) {
+                    s = mfma32(frag_row(Qi, 32 * qs, ks, lane), kf[ks], s);
+                    dp = mfma32(frag_row(Oi, 32 * qs, ks, lane), vf[ks], dp);
                 }
+                const bool diag = q0s < kq + 31;
+                const uint64_t* mw = DROP ? mask_block(mask, bh, ntri, q0s >> 5, kq >> 5) : nullptr;
+                fv16 z;
 #pragma unroll
-                for (int et = 0; et < 4; ++et) {
-                    const sv8 oft = frag_tr<false>(Oi, qr0, 16 * et, lane);
-                    const sv8 qft = frag_tr<false>(Qi, qr0, 16 * et, lane);
+                for (int i = 0; i < 4; ++i) {
+                    // rows 8i + 4(lane>>5) + 0..3 of the subtile: one 16-B LDS read each (broadcast)
+                    const int row = 32 * qs + 8 * i + 4 * (lane >> 5);
+                    const float4 l4 = *(const float4*)(st_lse + row);
+                    const float4 d4 = *(const float4*)(st_del + row);
+                    const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dvv[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
-                    for (int kt = 0; kt < KT; ++kt) {
-                        dva[et][kt] = mfma16(oft, zf[kt], dva[et][kt]);
-                        dka[et][kt] = mfma16(qft, dsf[kt], dka[et][kt]);
+                    for (int e = 0; e < 4; ++e) {
+                        const int r = 4 * i + e;
+                        float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lv[e]));
+                        if (diag && q0 + row + e < key) p = 0.f;
+                        float zz = p, d = dp[r];
+                        if (DROP) {
+                            const bool kp = keep_bit(mw[r]);
+                            zz = kp ? p : 0.f;   // 1/(1-p) of dV applied in the epilogue
+                            d = kp ? d * dscale : 0.f;
+                        }
+                        z[r] = zz;
+                        s[r] = p * (d - dvv[e]);
                     }
+                }
+                const sv8 z0 = pack16(z, 0), z1 = pack16(z, 1), s0 = pack16(s, 0), s1 = pack16(s, 1);
+#pragma unroll
+                for (int dt = 0; dt < 2; ++dt) {
+                    dva[dt] = mfma32(frag_tr(Oi, 32 * qs, 0, 32 * dt, lane), z0, dva[dt]);
+                    dva[dt] = mfma32(frag_tr(Oi, 32 * qs, 1, 32 * dt, lane), z1, dva[dt]);
+                    dka[dt] = mfma32(frag_tr(Qi, 32 * qs, 0, 32 * dt, lane), s0, dka[dt]);
+                    dka[dt] = mfma32(frag_tr(Qi, 32 * qs, 1, 32 * dt, lane), s1, dka[dt]);
                 }
             }
         }
-        qstore(nxt, smem + ((it + 1) & 1) * STG);
+        char* D = smem + ((it + 1) & 1) * KV_STAGE;
+        stage_store(st, D, tid);
+        if (tid < 128) ((float*)(D + 2 * TILE))[tid] = sn;
         __syncthreads();
     }
-    if (!wave_active) return;
-#pragma unroll
-    for (int kt = 0; kt < KT; ++kt) {
-        const int64_t key = kw0 + 16 * kt + li;
-        if (key >= T_) continue;
-        bf16_t* krow = dk + (boff + key) * lddkv + h * 64;
-        bf16_t* vrow = dv + (boff + key) * lddkv + h * 64;
-#pragma unroll
-        for (int et = 0; et < 4; ++et) {
-            const fv4 x = dka[et][kt] * scale;
-            const fv4 y = dva[et][kt] * dscale;
-            *(uint2*)(krow + 16 * et + 4 * g) = make_uint2(pack_bf2(x[0], x[1]), pack_bf2(x[2], x[3]));
-            *(uint2*)(vrow + 16 * et + 4 * g) = make_uint2(pack_bf2(y[0], y[1]), pack_bf2(y[2], y[3]));
-        }
-    }
+    if (!act) return;
+    store_rows(dk + (boff + key) * lddkv + hh * 64, dka, scale, lane);
+    store_rows(dv + (boff + key) * lddkv + hh * 64, dva, DROP ? dscale : 1.f, lane);
 }
-
-// variant bits: 1 -> forward/dQ with 32 queries per wave; 2 -> dK/dV with 32 keys per wave;
-// 8 -> the whole-(b, h)-resident kernels where they apply (attention_res.hip)
-inline int qw_of() { return (g_attn_variant & 1) ? 32 : 16; }
-inline int kw_of() { return (g_attn_variant & 2) ? 32 : 16; }
 
 }  // namespace
 
 namespace attn {
 void launch_fwd_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                     bf16_t* o, int64_t ldo, float* lse, float scale, const DropArgs& d, hipStream_t st) {
-    const float ds = d.mask ? d.dscale : 1.f;
-    if (qw_of() == 32)
-        k_attn_fwd_d64<32><<<dim3(ceil_div(T, 128), (unsigned)(B * H)), 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, lse,
-                                                                                     scale * LOG2E, d.mask, ds);
+    const dim3 grid(ceil_div(T, 256), (unsigned)(B * H));
+    if (d.mask)
+        k_attn_fwd_d64<true><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, lse, scale * LOG2E, d.mask, d.dscale);
     else
-        k_attn_fwd_d64<16><<<dim3(ceil_div(T, 64), (unsigned)(B * H)), 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, lse,
-                                                                                    scale * LOG2E, d.mask, ds);
+        k_attn_fwd_d64<false><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, lse, scale * LOG2E, nullptr, 1.f);
 }
 void launch_dq_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                    const bf16_t* o, int64_t ldo, const bf16_t* dout, int64_t ldd, const float* lse, float* delta,
                    bf16_t* dq, int64_t lddq, float scale, const DropArgs& d, hipStream_t st) {
-    const float ds = d.mask ? d.dscale : 1.f;
-    if (qw_of() == 32)
-        k_attn_dq_d64<32><<<dim3(ceil_div(T, 128), (unsigned)(B * H)), 256, 0, st>>>(
-            T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale, d.mask, ds);
+    const dim3 grid(ceil_div(T, 256), (unsigned)(B * H));
+    if (d.mask)
+        k_attn_dq_d64<true><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
+                                                  d.mask, d.dscale);
     else
-        k_attn_dq_d64<16><<<dim3(ceil_div(T, 64), (unsigned)(B * H)), 256, 0, st>>>(
-            T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale, d.mask, ds);
+        k_attn_dq_d64<false><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
+                                                   nullptr, 1.f);
 }
 void launch_dkdv_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                      const bf16_t* dout, int64_t ldd, const float* lse, const float* delta, bf16_t* dk, bf16_t* dv,
                      int64_t lddkv, float scale, const DropArgs& d, hipStream_t st) {
-    const float ds = d.mask ? d.dscale : 1.f;
-    if (kw_of() == 32)
-        k_attn_dkdv_d64<32><<<dim3(ceil_div(T, 128), (unsigned)(B * H)), 256, 0, st>>>(
-            T, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale, d.mask, ds);
+    const dim3 grid(ceil_div(T, 128), (unsigned)(B * H));
+    if (d.mask)
+        k_attn_dkdv_d64<true><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
+                                                    d.mask_bwd, d.dscale);
     else
-        k_attn_dkdv_d64<16><<<dim3(ceil_div(T, 64), (unsigned)(B * H)), 256, 0, st>>>(
-            T, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale, d.mask, ds);
+        k_attn_dkdv_d64<false><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
+                                                     nullptr, 1.f);
 }
 }  // namespace attn
 

@@ -22,62 +22,63 @@ using namespace cg;
 namespace {
 
 
-// Keep bits of the MFMA kernels (attention_common.h mask_tile), for the 16x16 (query tile, key
-// tile) blocks on or below the diagonal, flattened over (b*H + h, lower-triangle tile).  One wave
-// handles a PAIR of consecutive tiles per step: lane l takes tile l>>5, query row l&15 and keys
-// 8((l>>4)&1) .. +7 -- one Philox call gives those 8 decisions (16 bits each).  The ballot words
-// (bit l' <-> query l'&15, key 4(l'>>4) + w) then need, per tile, one cross-lane fetch of the
-// source lane's 8 bits: lane l' reads lane 32*tile + 16(l'>>5) + (l'&15), bits 4((l'>>4)&1) + w.
-// DM_PPW pairs per wave (no idle waves above the diagonal; enough work per wave that the launch
-// is not dispatch-bound).
-constexpr int DM_PPW = 8;
-__device__ __forceinline__ void tri_next(uint64_t& bh, int& qt, int& kt, int NT) {
-    if (++kt > qt) {
-        kt = 0;
-        if (++qt == NT) {
-            qt = 0;
+// Keep bits of the MFMA kernels (attention_common.h: both orientations) for the 32x32 (query
+// block, key block) pairs on or below the diagonal, flattened over (b*H + h, lower-triangle block).
+// One wave per block per step, DM_BPW blocks per wave: lane l takes query 32 qb + (l & 31) and keys
+// 32 kb + 16 (l >> 5) .. +15 -- two Philox calls, 16 decisions (bit e <-> key 16 (l >> 5) + e).  The
+// 32 ballot words need, per FWD word, the bits of lane (l & 31) + 32 (r >> 3) (two cross-lane
+// fetches in all) and, per BWD word, those of lane (query row of r) + 32 ((l >> 4) & 1).
+constexpr int DM_BPW = 4;
+__device__ __forceinline__ void tri_next(uint64_t& bh, int& qb, int& kb, int NB) {
+    if (++kb > qb) {
+        kb = 0;
+        if (++qb == NB) {
+            qb = 0;
             ++bh;
         }
     }
 }
-__global__ __launch_bounds__(256) void k_attn_dropmask(int64_t T_, int64_t nbh, uint64_t* __restrict__ mask,
-                                                       DropArgs d) {
-    const int NT = (int)(T_ >> 4);
-    const int64_t ntri = (int64_t)NT * (NT + 1) / 2;
+__global__ __launch_bounds__(256) void k_attn_dropmask(int64_t T_, int64_t nbh, uint64_t* __restrict__ mask_f,
+                                                       uint64_t* __restrict__ mask_b, DropArgs d) {
+    const int NB = (int)(T_ >> 5);
+    const int64_t ntri = (int64_t)NB * (NB + 1) / 2;
     const int64_t total = nbh * ntri;
-    const int lane = threadIdx.x & 63, t = lane >> 5;
+    const int lane = threadIdx.x & 63, h = lane >> 5, lq = lane & 31;
     const uint64_t stream = dropout_stream(d.rng_call, d.site);
-    const int64_t first = (((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * DM_PPW) * 2;  // first tile of the wave
+    const int64_t first = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * DM_BPW;
     if (first >= total) return;
-    // (b*H + h, query tile, key tile) of this lane's tile first + t: one division and root per
-    // wave, then incremental steps through the lower triangle
+    // (b*H + h, query block, key block) of the wave's first block: one division and root per wave,
+    // then incremental steps through the lower triangle
     uint64_t bh = (uint64_t)(first / ntri);
     const int tri0 = (int)(first - (int64_t)bh * ntri);
-    int qt = (int)((sqrtf(8.f * tri0 + 1.f) - 1.f) * 0.5f);
-    while ((qt + 1) * (qt + 2) / 2 <= tri0) ++qt;
-    while (qt * (qt + 1) / 2 > tri0) --qt;
-    int kt = tri0 - qt * (qt + 1) / 2;
-    if (t) tri_next(bh, qt, kt, NT);
-    const int src_lo = 16 * (lane >> 5) + (lane & 15), sub = 4 * ((lane >> 4) & 1);
+    int qb = (int)((sqrtf(8.f * tri0 + 1.f) - 1.f) * 0.5f);
+    while ((qb + 1) * (qb + 2) / 2 <= tri0) ++qb;
+    while (qb * (qb + 1) / 2 > tri0) --qb;
+    int kb = tri0 - qb * (qb + 1) / 2;
 #pragma unroll 1
-    for (int i = 0; i < DM_PPW; ++i) {
-        const int64_t tile0 = first + 2 * i;
-        if (tile0 >= total) return;
-        if (i) {
-            tri_next(bh, qt, kt, NT);
-            tri_next(bh, qt, kt, NT);
-        }
-        const uint64_t q = (uint64_t)qt * 16 + (lane & 15), key0 = (uint64_t)kt * 16 + 8 * ((lane >> 4) & 1);
-        const uint32_t bits = keep8_bits(philox_group(d.seed, stream, ((bh * T_ + q) * T_ + key0) >> 3), d.thr);
+    for (int i = 0; i < DM_BPW; ++i) {
+        if (first + i >= total) return;
+        if (i) tri_next(bh, qb, kb, NB);
+        const uint64_t q = (uint64_t)qb * 32 + lq, key0 = (uint64_t)kb * 32 + 16 * h;
+        const uint64_t grp = ((bh * T_ + q) * T_ + key0) >> 3;
+        const uint32_t bits = keep8_bits(philox_group(d.seed, stream, grp), d.thr) |
+                              (keep8_bits(philox_group(d.seed, stream, grp + 1), d.thr) << 8);
+        const uint32_t v0 = (uint32_t)__shfl((int)bits, lq, 64) >> (4 * h);
+        const uint32_t v1 = (uint32_t)__shfl((int)bits, lq + 32, 64) >> (4 * h);
+        uint64_t fw[16], bw[16];
 #pragma unroll
-        for (int tt = 0; tt < 2; ++tt) {
-            const uint32_t v = (uint32_t)__shfl((int)bits, 32 * tt + src_lo, 64);
-            const uint64_t b0 = __ballot((v >> sub) & 1u), b1 = __ballot((v >> (sub + 1)) & 1u);
-            const uint64_t b2 = __ballot((v >> (sub + 2)) & 1u), b3 = __ballot((v >> (sub + 3)) & 1u);
-            if (lane == 32 * tt && tile0 + tt < total) {
-                uint64_t* o = mask + (((bh * NT + qt) * NT + kt) << 2);
-                *(uint4*)o = make_uint4((uint32_t)b0, (uint32_t)(b0 >> 32), (uint32_t)b1, (uint32_t)(b1 >> 32));
-                *(uint4*)(o + 2) = make_uint4((uint32_t)b2, (uint32_t)(b2 >> 32), (uint32_t)b3, (uint32_t)(b3 >> 32));
+        for (int r = 0; r < 16; ++r) {
+            fw[r] = __ballot(((r < 8 ? v0 : v1) >> ((r & 3) + 8 * ((r >> 2) & 1))) & 1u);
+            const int src = (r & 3) + 8 * (r >> 2) + 4 * h + 32 * ((lane >> 4) & 1);
+            bw[r] = __ballot(((uint32_t)__shfl((int)bits, src, 64) >> (lane & 15)) & 1u);
+        }
+        if (lane < 2) {
+            const int64_t off = ((int64_t)bh * ntri + (int64_t)qb * (qb + 1) / 2 + kb) * 16;
+            uint64_t* dst = (lane ? mask_b : mask_f) + off;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint64_t a = lane ? bw[2 * j] : fw[2 * j], c = lane ? bw[2 * j + 1] : fw[2 * j + 1];
+                *(uint4*)(dst + 2 * j) = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)c, (uint32_t)(c >> 32));
             }
         }
     }
@@ -511,15 +512,22 @@ DropArgs make_drop(double p, uint64_t seed, const uint64_t* rng_call, int site) 
     d.rng_call = rng_call;
     d.site = site;
     d.mask = nullptr;
+    d.mask_bwd = nullptr;
     return d;
 }
 
-int64_t mask_bytes(int64_t B, int64_t H, int64_t T) { return B * H * (T / 16) * (T / 16) * 32; }
+// both orientations, lower-triangle 32x32 blocks, 128 B each
+int64_t mask_bytes(int64_t B, int64_t H, int64_t T) { return 2 * B * H * mask_tri_blocks(T) * 128; }
+
+void set_masks(DropArgs& d, uint64_t* mask, int64_t B, int64_t H, int64_t T) {
+    d.mask = mask;
+    d.mask_bwd = mask + B * H * mask_tri_blocks(T) * 16;
+}
 
 void launch_dropmask(int64_t B, int64_t H, int64_t T, uint64_t* mask, const DropArgs& d, hipStream_t st) {
-    const int64_t NT = T / 16;
-    const int64_t tiles = B * H * NT * (NT + 1) / 2;
-    k_attn_dropmask<<<ceil_div(tiles, 4 * 2 * DM_PPW), 256, 0, st>>>(T, B * H, mask, d);
+    const int64_t blocks = B * H * mask_tri_blocks(T);
+    k_attn_dropmask<<<ceil_div(blocks, 4 * DM_BPW), 256, 0, st>>>(T, B * H, mask, mask + B * H * mask_tri_blocks(T) * 16,
+                                                                   d);
 }
 
 bool fast_attn_ok(int dtype, int64_t T, int64_t D, const void* a, const void* b, const void* c, int64_t ld1,
@@ -579,18 +587,14 @@ int attn_fwd_impl(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const v
         if (d.thr) {
             CG_REQUIRE(mask, "cg_attn_fwd: dropout on the MFMA path needs a mask buffer (cg_attn_mask_bytes)");
             if (!mask_ready) launch_dropmask(B, H, T, mask, d, st);
-            d.mask = mask;
+            set_masks(d, mask, B, H, T);
         }
-        if (attn::res_ok(T))
-            attn::launch_fwd_res(B, T, (int)H, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ld_qkv,
-                                 (bf16_t*)o, ld_o, lse, scale, d, st);
-        else
-            attn::launch_fwd_d64(B, T, (int)H, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ld_qkv,
-                                 (bf16_t*)o, ld_o, lse, scale, d, st);
+        attn::launch_fwd_d64(B, T, (int)H, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ld_qkv, (bf16_t*)o,
+                             ld_o, lse, scale, d, st);
     } else {
         dim3 grid(ceil_div(T, GB), (unsigned)(B * H));
         const size_t lds = generic_lds<float>((int)D, 3, 1);
-        if (dtype == CG_F32 && !d.thr && D <= 32 && g_attn_variant != 8) {
+        if (dtype == CG_F32 && !d.thr && D <= 32) {
             dim3 g2(ceil_div(T, 64), (unsigned)(B * H));
 #define AF(dp)                                                                                                  \
     k_attn_fwd_f32mfma<dp><<<g2, 256, 0, st>>>(T, (int)H, (int)D, (const float*)q, (const float*)k, (const float*)v, \
@@ -649,18 +653,13 @@ extern "C" int cg_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D
                 launch_dropmask(B, H, T, m, d, st);
                 mask = m;
             }
-            d.mask = mask;
+            set_masks(d, (uint64_t*)mask, B, H, T);
         }
         const bf16_t *Q = (const bf16_t*)q, *K = (const bf16_t*)k, *V = (const bf16_t*)v, *DO = (const bf16_t*)dout;
-        if (attn::res_ok(T)) {
-            attn::launch_bwd_res(B, T, (int)H, Q, K, V, ld_qkv, (const bf16_t*)o, ld_o, DO, ld_do, lse, (bf16_t*)dq,
-                                 (bf16_t*)dk, (bf16_t*)dv, ld_dqkv, scale, d, st);
-        } else {
-            attn::launch_dq_d64(B, T, (int)H, Q, K, V, ld_qkv, (const bf16_t*)o, ld_o, DO, ld_do, lse, delta,
-                                (bf16_t*)dq, ld_dqkv, scale, d, st);
-            attn::launch_dkdv_d64(B, T, (int)H, Q, K, V, ld_qkv, DO, ld_do, lse, delta, (bf16_t*)dk, (bf16_t*)dv,
-                                  ld_dqkv, scale, d, st);
-        }
+        attn::launch_dq_d64(B, T, (int)H, Q, K, V, ld_qkv, (const bf16_t*)o, ld_o, DO, ld_do, lse, delta, (bf16_t*)dq,
+                            ld_dqkv, scale, d, st);
+        attn::launch_dkdv_d64(B, T, (int)H, Q, K, V, ld_qkv, DO, ld_do, lse, delta, (bf16_t*)dk, (bf16_t*)dv, ld_dqkv,
+                              scale, d, st);
     } else {
         dim3 grid(ceil_div(T, GB), (unsigned)(B * H));
         const size_t lds_dq = generic_lds<float>((int)D, 4, 1);

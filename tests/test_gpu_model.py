@@ -362,3 +362,36 @@ def test_decode_attn_any_key_count(n):
     s = (qq @ kc[:, :, :n].double().transpose(-1, -2)) * scale
     ref = (torch.softmax(s, -1) @ vc[:, :, :n].double()).view(B, H * D)
     assert relerr(o, ref) < 1e-5
+
+
+def test_fused_b1_gradient_training_parity():
+    """CHARPT_FUSE_COLPART (FFN b1 gradient fused into the ReLU-backward dgrad epilogue) on vs off:
+    both sum the same bf16-rounded dz1, so a few bf16 training steps agree to summation-order
+    rounding (losses within 1e-4 relative, weights within 1e-3 relative)."""
+    from replicatinggpt_amd import AdamW, BigramLanguageModel, GPTConfig
+    from replicatinggpt_amd import functional as Fn
+    cfg = GPTConfig(block_size=128, n_embd=128, n_head=2, n_layers=2, dropout=0.0, dtype="bf16")
+    g = torch.Generator().manual_seed(12)
+    batches = [(torch.randint(0, 65, (8, 128), generator=g).to(DEV), torch.randint(0, 65, (8, 128), generator=g).to(DEV))
+               for _ in range(4)]
+    runs = []
+    saved = Fn.FUSE_COLPART
+    try:
+        for fuse in (False, True):
+            Fn.FUSE_COLPART = fuse
+            torch.manual_seed(1337)
+            m = BigramLanguageModel(cfg).to(DEV)
+            opt = AdamW(m.parameters(), lr=1e-3).attach(m)
+            losses = []
+            for x, y in batches:
+                _, loss = m(x, y)
+                opt.zero_grad(set_to_none=True)
+                loss.backward()
+                opt.step()
+                losses.append(float(loss))
+            runs.append((losses, m.flat.master.detach().clone()))
+    finally:
+        Fn.FUSE_COLPART = saved
+    for a, b in zip(runs[0][0], runs[1][0]):
+        assert abs(a - b) < 1e-4 * abs(b)
+    assert relerr(runs[1][1], runs[0][1]) < 1e-3

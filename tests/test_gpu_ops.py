@@ -393,15 +393,14 @@ def test_attention_fast_matches_generic_bf16():
     assert relerr(lse_fast[0], lse) < 1e-4
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 8])
-def test_attention_fast_variants(variant):
-    """Every per-wave width of the streaming MFMA kernels (16/32 queries, 16/32 keys) and the
-    resident-(b, h) kernels (variant 8) against the fp64 reference, at a T that leaves the
-    128-wide blocks partially filled."""
-    from replicatinggpt_amd import _lib as L
+@pytest.mark.parametrize("T", [64, 128, 192, 320, 512])
+def test_attention_fast_block_shapes(T):
+    """The 32x32x16 MFMA kernels at sequence lengths that leave the 256-query (forward / dQ) and
+    128-key (dK/dV) blocks partially filled, several 64-key tiles per block, and the causal group
+    pairing (g, 7-g), with dropout, against the fp64 reference with the oracle's keep mask."""
     Fn = F()
-    B, T, H, D, p = 2, 192, 3, 64, 0.2
-    torch.manual_seed(6)
+    B, H, D, p = 2, 3, 64, 0.2
+    torch.manual_seed(6 + T)
     d = H * D
     qkv = (torch.randn(B * T, 3 * d) * 0.7).to(torch.bfloat16)
     q = qkv[:, :d].double().view(B, T, H, D).requires_grad_(True)
@@ -411,21 +410,42 @@ def test_attention_fast_variants(variant):
     ref = _attn_ref(q, k, v, scale, p, 21, (3 << 8) | 4)
     dout = torch.randn(B, T, H, D).to(torch.bfloat16)
     ref.backward(dout.double())
-    lib = L.load()
-    L.check(lib.cg_set_tuning(b"attn_variant", variant))
-    try:
-        call = torch.tensor([3], dtype=torch.int64, device=DEV)
-        qkv_d = qkv.to(DEV)
-        o = torch.empty(B * T, d, dtype=torch.bfloat16, device=DEV)
-        lse, mask = Fn.attention_fwd(qkv_d, B, T, H, D, o, scale, p, 21, call, 4)
-        dqkv = Fn.attention_bwd(qkv_d, B, T, H, D, o, dout.reshape(B * T, d).to(DEV), lse, scale, p, 21, call, 4,
-                                mask)
-        torch.cuda.synchronize()
-    finally:
-        L.check(lib.cg_set_tuning(b"attn_variant", 0))
+    call = torch.tensor([3], dtype=torch.int64, device=DEV)
+    qkv_d = qkv.to(DEV)
+    o = torch.empty(B * T, d, dtype=torch.bfloat16, device=DEV)
+    lse, mask = Fn.attention_fwd(qkv_d, B, T, H, D, o, scale, p, 21, call, 4)
+    dqkv = Fn.attention_bwd(qkv_d, B, T, H, D, o, dout.reshape(B * T, d).to(DEV), lse, scale, p, 21, call, 4, mask)
+    torch.cuda.synchronize()
     assert relerr(o, ref.reshape(B * T, d)) < 2e-2
     for i, t in enumerate((q, k, v)):
         assert relerr(dqkv[:, i * d:(i + 1) * d], t.grad.reshape(B * T, d)) < 3e-2
+
+
+def test_attention_forward_rescale_branch():
+    """The forward's lazy rescale (running max moved only when a tile's max exceeds it by 2^8) with
+    inputs that force it: one key row spiked against every query so that the max jumps at a late
+    tile, plus a query row whose scores all collapse to a huge common value.  fp64 reference."""
+    Fn = F()
+    B, T, H, D = 1, 512, 2, 64
+    torch.manual_seed(31)
+    d = H * D
+    qkv = torch.randn(B * T, 3 * d) * 0.5
+    qkv[:, :d] += 2.0                    # queries share a direction ...
+    qkv[300, d:2 * d] = 8.0              # ... that key 300 (tile 4) matches strongly
+    qkv[:, d:2 * d][:, :D] *= torch.linspace(0.1, 3.0, T)[:, None]   # growing key norms: the max climbs tile by tile
+    qkv = qkv.to(torch.bfloat16)
+    q = qkv[:, :d].double().view(B, T, H, D)
+    k = qkv[:, d:2 * d].double().view(B, T, H, D)
+    v = qkv[:, 2 * d:].double().view(B, T, H, D)
+    scale = D ** -0.5
+    ref = _attn_ref(q, k, v, scale)
+    o = torch.empty(B * T, d, dtype=torch.bfloat16, device=DEV)
+    lse, _ = Fn.attention_fwd(qkv.to(DEV), B, T, H, D, o, scale, 0.0, 0, None, 0)
+    torch.cuda.synchronize()
+    assert relerr(o, ref.reshape(B * T, d)) < 2e-2
+    s = torch.einsum("bthd,bshd->bhts", q, k) * scale
+    s = s.masked_fill(~torch.tril(torch.ones(T, T, dtype=torch.bool)), float("-inf"))
+    assert relerr(lse, torch.logsumexp(s, -1)) < 1e-4
 
 
 def test_attention_bwd_regenerates_mask():
