@@ -19,7 +19,8 @@ def test_library_exports_header_symbols():
         assert s in _lib._SIGS, f"{s} has no ctypes signature"
     assert lib.cg_version() >= 1
     assert lib.cg_gemm_workspace(128, 256, 4) == 4 * 128 * 256 * 4
-    assert lib.cg_attn_mask_bytes(2, 6, 256) == 2 * 6 * 16 * 16 * 32
+    # two orientations x lower-triangle 32x32 blocks (8 * 9 / 2 at T = 256) x 128 B
+    assert lib.cg_attn_mask_bytes(2, 6, 256) == 2 * (2 * 6 * 36 * 128)
     assert lib.cg_attn_bwd_workspace(2, 256, 6, 64) == 2 * 6 * 256 * 4 + lib.cg_attn_mask_bytes(2, 6, 256)
 
 
