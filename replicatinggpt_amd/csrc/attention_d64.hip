@@ -76,7 +76,24 @@ __device__ __forceinline__ sv8 pack16(const fv16& x, int s) {
 // accumulator row of register r (column = lane & 31)
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
-__device__ __forceinline__ bool keep_bit(uint64_t word) { return __builtin_amdgcn_inverse_ballot_w64(word); }
+// x where this lane's bit of the (wave-uniform, SGPR) keep word is set, else 0: ONE v_cndmask with
+// the word as its lane mask.  In asm so that hipcc cannot sink the select past the bf16 packing
+// (it otherwise converts each value alone, selects the 16-bit result and re-packs with v_perm:
+// 2.5 instructions per element instead of 1.5).
+__device__ __forceinline__ float keep_sel(uint64_t word, float x) {
+    float r;
+    asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(x), "s"(word));
+    return r;
+}
+
+// causal mask of one 32x32 accumulator tile whose key rows start at key0 (column = query qa):
+// rows acc_row(r) > qa - key0 become -inf.  Called under a wave-uniform branch (diagonal tiles only).
+__device__ __forceinline__ void mask_upper(fv16& x, int qa, int key0, int lane, float fill) {
+    const int rel = qa - key0 - 4 * (lane >> 5);
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+        if ((r & 3) + 8 * (r >> 2) > rel) x[r] = fill;
+}
 
 // two [64][64] bf16 tiles (rows row0..row0+63 of X and Y) staged through registers: 4 x 16 B per thread
 struct Stage2 {
@@ -186,17 +203,15 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, cons
                 for (int ks = 0; ks < 4; ++ks) s[kt] = mfma32(frag_row(Ki, 32 * kt, ks, lane), qf[g][ks], s[kt]);
             }
             const int qa = qg[g] + (lane & 31);
-            const bool diag = k0 + 63 > qg[g];
+            if (__builtin_amdgcn_readfirstlane(k0 + 63 > qg[g])) {   // diagonal tile: causal mask
+                mask_upper(s[0], qa, k0, lane, -INFINITY);
+                mask_upper(s[1], qa, k0 + 32, lane, -INFINITY);
+            }
             float mx = -INFINITY;
 #pragma unroll
             for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    float x = s[kt][r];
-                    if (diag && k0 + 32 * kt + acc_row(r, lane) > qa) x = -INFINITY;
-                    s[kt][r] = x;
-                    mx = fmaxf(mx, x);
-                }
+                for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
             mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
             const float mt = mx * scale_log2;
             if (__any(mt > m_run[g] + RESCALE_THR)) {   // rare after the first tiles
@@ -222,7 +237,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, cons
                     // raw v_exp_f32: weights below 2^-126 of the stale max flush to 0
                     const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][r], scale_log2, mneg));
                     ls += p;
-                    s[kt][r] = DROP ? (keep_bit(mw[r]) ? p : 0.f) : p;
+                    s[kt][r] = DROP ? keep_sel(mw[r], p) : p;
                 }
                 pf[kt][0] = pack16(s[kt], 0);
                 pf[kt][1] = pack16(s[kt], 1);
@@ -314,7 +329,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_dq_d64(int64_t T_, int H, const
         for (int g = 0; g < 2; ++g) {
             if (!act[g] || k0 > qg[g] + 31) continue;
             const int qa = qg[g] + (lane & 31);
-            const bool diag = k0 + 63 > qg[g];
+            const bool diag = __builtin_amdgcn_readfirstlane(k0 + 63 > qg[g]);
 #pragma unroll
             for (int kt = 0; kt < 2; ++kt) {
                 if (k0 + 32 * kt > qg[g] + 31) break;   // subtile fully masked
@@ -325,12 +340,12 @@ __global__ __launch_bounds__(256, 2) void k_attn_dq_d64(int64_t T_, int H, const
                     dp = mfma32(frag_row(Vi, 32 * kt, ks, lane), df[g][ks], dp);
                 }
                 const uint64_t* mw = DROP ? mask_block(mask, bh, ntri, qg[g] >> 5, (k0 >> 5) + kt) : nullptr;
+                if (diag) mask_upper(s, qa, k0 + 32 * kt, lane, -INFINITY);
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lse2[g]));
-                    if (diag && k0 + 32 * kt + acc_row(r, lane) > qa) p = 0.f;
+                    const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lse2[g]));
                     float d = dp[r];
-                    if (DROP) d = keep_bit(mw[r]) ? d * dscale : 0.f;
+                    if (DROP) d = keep_sel(mw[r], d * dscale);
                     s[r] = p * (d - dl[g]);
                 }
                 const sv8 d0 = pack16(s, 0), d1 = pack16(s, 1);
@@ -422,7 +437,13 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, con
                     s = mfma32(frag_row(Qi, 32 * qs, ks, lane), kf[ks], s);
                     dp = mfma32(frag_row(Oi, 32 * qs, ks, lane), vf[ks], dp);
                 }
-                const bool diag = q0s < kq + 31;
+                if (__builtin_amdgcn_readfirstlane(q0s < kq + 31)) {
+                    // diagonal subtile: queries (rows) before the key (column) are masked
+                    const int rel = key - q0s - 4 * (lane >> 5);
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        if ((r & 3) + 8 * (r >> 2) < rel) s[r] = -INFINITY;
+                }
                 const uint64_t* mw = DROP ? mask_block(mask, bh, ntri, q0s >> 5, kq >> 5) : nullptr;
                 fv16 z;
 #pragma unroll
@@ -435,15 +456,14 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, con
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const int r = 4 * i + e;
-                        float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lv[e]));
-                        if (diag && q0 + row + e < key) p = 0.f;
-                        float zz = p, d = dp[r];
+                        const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lv[e]));
+                        float d = dp[r];
                         if (DROP) {
-                            const bool kp = keep_bit(mw[r]);
-                            zz = kp ? p : 0.f;   // 1/(1-p) of dV applied in the epilogue
-                            d = kp ? d * dscale : 0.f;
+                            z[r] = keep_sel(mw[r], p);   // 1/(1-p) of dV applied in the epilogue
+                            d = keep_sel(mw[r], d * dscale);
+                        } else {
+                            z[r] = p;
                         }
-                        z[r] = zz;
                         s[r] = p * (d - dvv[e]);
                     }
                 }
