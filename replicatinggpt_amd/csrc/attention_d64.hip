@@ -77,12 +77,13 @@ __device__ __forceinline__ sv8 pack16(const fv16& x, int s) {
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
 // x where this lane's bit of the (wave-uniform, SGPR) keep word is set, else 0: ONE v_cndmask with
-// the word as its lane mask.  In asm so that hipcc cannot sink the select past the bf16 packing
-// (it otherwise converts each value alone, selects the 16-bit result and re-packs with v_perm:
-// 2.5 instructions per element instead of 1.5).
+// the word as its lane mask.  The empty asm makes the selected value opaque, so hipcc cannot sink
+// the select past the bf16 packing (it otherwise converts each value alone, selects the 16-bit
+// result and re-packs with v_perm: 2.5 instructions per element instead of 1.5).  The select
+// itself stays compiler-generated, so the SGPR-write -> lane-mask-read hazards are padded for us.
 __device__ __forceinline__ float keep_sel(uint64_t word, float x) {
-    float r;
-    asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(x), "s"(word));
+    float r = __builtin_amdgcn_inverse_ballot_w64(word) ? x : 0.f;
+    asm("" : "+v"(r));
     return r;
 }
 
