@@ -160,12 +160,14 @@ int cg_attn_fwd_premasked(int dtype, int64_t B, int64_t T, int64_t H, int64_t D,
                           const void* v, int64_t ld_qkv, void* o, int64_t ld_o, float* lse, float scale,
                           double dropout_p, uint64_t seed, const uint64_t* rng_call, int site, uint64_t* mask,
                           void* stream);
-/* fill the MFMA path's keep-bit buffer for one attention call (0 < p < 1, T % 16 == 0)          */
+/* fill the MFMA path's keep-bit buffer for one attention call (0 < p < 1, T % 64 == 0)          */
 int cg_attn_dropmask(int64_t B, int64_t H, int64_t T, double dropout_p, uint64_t seed, const uint64_t* rng_call,
                      int site, uint64_t* mask, void* stream);
 /* keep-bit buffer for dropout on the MFMA (bf16, head_size 64) path: the forward fills it from the
    Philox stream (cg_attn_fwd `mask`, may be NULL on the generic path or with p = 0) and the
-   backward reads it (cg_attn_bwd `mask`; NULL -> regenerated inside the workspace).            */
+   backward reads it (cg_attn_bwd `mask`; NULL -> regenerated inside the workspace).  Layout
+   (attention_common.h): per (b*H + h), T/32 + (T/32 - 1)^2/4 tiles of 64 x 32-bit lane words in
+   each of two orientations (query-major for the forward / dQ, key-major for dK/dV).            */
 int64_t cg_attn_mask_bytes(int64_t B, int64_t H, int64_t T);
 /* dq/dk/dv written (not accumulated) with stride ld_dqkv; workspace cg_attn_bwd_workspace. */
 int64_t cg_attn_bwd_workspace(int64_t B, int64_t T, int64_t H, int64_t D);

@@ -14,27 +14,34 @@ struct DropArgs {
     uint64_t seed;
     const uint64_t* rng_call;
     int site;
-    const uint64_t* mask;      // fast kernels: precomputed keep bits, FWD orientation; NULL = no dropout
-    const uint64_t* mask_bwd;  // the same bits, BWD orientation (mask + B*H*mask_tri_blocks(T)*16)
+    const uint32_t* mask;      // fast kernels: precomputed keep bits, FWD tiles; NULL = no dropout
+    const uint32_t* mask_bwd;  // the same bits, BWD tiles (mask + B*H*mask_tiles(T)*64)
 };
 
 // Keep-bit image of the MFMA kernels, generated once per forward (k_attn_dropmask) from the
 // canonical Philox stream (same bits as keep_of on element ((b*H + h)*T + q)*T + k) and read by the
-// forward, dQ and dK/dV kernels.  Per (b*H + h) and per 32x32 block (query block qb, key block
-// kb <= qb, lower-triangle order), 16 uint64 words in each of two orientations -- exactly the
-// 32x32x16 MFMA accumulator layout (column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
-// for register r), so word r is the lane mask of accumulator register r (one v_cndmask each):
-//   FWD (forward, dQ: swapped products, lane = query):
-//        bit l of word r = keep(q = 32 qb + (l & 31), k = 32 kb + (r & 3) + 8 (r >> 2) + 4 (l >> 5))
-//   BWD (dK/dV: lane = key):
-//        bit l of word r = keep(q = 32 qb + (r & 3) + 8 (r >> 2) + 4 (l >> 5), k = 32 kb + (l & 31))
-__host__ __device__ __forceinline__ int64_t mask_tri_blocks(int64_t T) {
-    const int64_t n = T / 32;
-    return n * (n + 1) / 2;
+// forward, dQ and dK/dV kernels with one coalesced 32-bit load per lane per 64-row tile, prefetched
+// a tile ahead (a VGPR: no scalar-load latency in the inner loop, one v_bfe_i32 + v_and per use).
+// T % 64 == 0; NB = T/32 blocks of 32, NP = T/64 tiles of 64.  Bit 16 s + r of a lane's word is
+// accumulator register r of 32x32 sub-block s (32x32x16 MFMA layout: column = lane & 31,
+// row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5) =: row(r, l)):
+//   FWD (forward, dQ: swapped products, lane = query), tile (qb, kt) for kt <= qb/2:
+//        bit 16 s + r of lane l = keep(q = 32 qb + (l & 31), k = 64 kt + 32 s + row(r, l))
+//   BWD (dK/dV: lane = key), tile (kb, qt) for qt >= kb/2:
+//        bit 16 s + r of lane l = keep(q = 64 qt + 32 s + row(r, l), k = 32 kb + (l & 31))
+// Sub-blocks wholly above the diagonal are 0; diagonal sub-blocks are stored whole (the kernels
+// apply the causal mask themselves).  Per (b*H + h): mask_tiles(T) tiles of 64 words each, FWD
+// row-major over qb, BWD column-major over kb.
+__host__ __device__ __forceinline__ int64_t mask_tiles(int64_t T) {
+    const int64_t nb = T / 32;
+    return nb + (nb - 1) * (nb - 1) / 4;
 }
-__device__ __forceinline__ const uint64_t* mask_block(const uint64_t* mask, int64_t bh, int64_t ntri, int qb, int kb) {
-    return mask + (bh * ntri + (int64_t)qb * (qb + 1) / 2 + kb) * 16;
+__device__ __forceinline__ int64_t mask_fwd_tile(int qb, int kt) { return qb + (qb ? (qb - 1) * (qb - 1) / 4 : 0) + kt; }
+__device__ __forceinline__ int64_t mask_bwd_tile(int kb, int qt, int np) {
+    return (int64_t)kb * np - (kb ? (kb - 1) * (kb - 1) / 4 : 0) + qt - kb / 2;
 }
+// all-ones where bit `bit` of a lane's mask word is set (one v_bfe_i32)
+__device__ __forceinline__ uint32_t keep_lanes(uint32_t w, int bit) { return (uint32_t)((int32_t)(w << (31 - bit)) >> 31); }
 
 namespace attn {
 // bf16 MFMA kernels, head_size 64, T % 64 == 0 (attention_d64.hip)

@@ -16,8 +16,9 @@
 //    (ds_read_b64_tr_b16) conflict-free.
 //  * Forward: lazy rescaling -- the running max is only moved (and O, l rescaled) when a tile's max
 //    exceeds it by 2^8, so the O-wide multiply is off the common path; probabilities stay <= 256.
-//  * Dropout keep bits (k_attn_dropmask, attention_common.h) are read as 64-bit lane masks by
-//    scalar loads and applied with one v_cndmask per element; the 1/(1-p) is applied once at the end.
+//  * Dropout keep bits (k_attn_dropmask, attention_common.h): one 32-bit word per lane per 64-row
+//    tile, loaded a tile ahead with the K/V (or Q/dO) staging loads and applied as v_bfe_i32 +
+//    v_and_b32 per element; the 1/(1-p) is applied once at the end.
 #include "attention_common.h"
 
 namespace cg {
@@ -76,15 +77,18 @@ __device__ __forceinline__ sv8 pack16(const fv16& x, int s) {
 // accumulator row of register r (column = lane & 31)
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
-// x where this lane's bit of the (wave-uniform, SGPR) keep word is set, else 0: ONE v_cndmask with
-// the word as its lane mask.  The empty asm makes the selected value opaque, so hipcc cannot sink
-// the select past the bf16 packing (it otherwise converts each value alone, selects the 16-bit
-// result and re-packs with v_perm: 2.5 instructions per element instead of 1.5).  The select
-// itself stays compiler-generated, so the SGPR-write -> lane-mask-read hazards are padded for us.
-__device__ __forceinline__ float keep_sel(uint64_t word, float x) {
-    float r = __builtin_amdgcn_inverse_ballot_w64(word) ? x : 0.f;
-    asm("" : "+v"(r));
-    return r;
+// all-ones / zero lane mask from bit `bit` of this lane's keep word (one v_bfe_i32).  The empty asm
+// hides that the value is a sign-extended bit: hipcc otherwise rewrites `x & mask` as a select,
+// v_and + v_cmp + v_cndmask, sunk past the bf16 packing (+v_lshr / v_perm): 4-5 instructions per
+// element instead of v_bfe_i32 + v_and_b32.  (No real instruction in asm here: an asm consumer of a
+// v_exp result would bypass the transcendental-use hazard padding.)
+__device__ __forceinline__ uint32_t keep_mask(uint32_t w, int bit) {
+    uint32_t m = keep_lanes(w, bit);
+    asm("" : "+v"(m));
+    return m;
+}
+__device__ __forceinline__ float keep_and(uint32_t w, int bit, float x) {
+    return __uint_as_float(__float_as_uint(x) & keep_mask(w, bit));
 }
 
 // causal mask of one 32x32 accumulator tile whose key rows start at key0 (column = query qa):
@@ -159,7 +163,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, cons
                                                          const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
                                                          int64_t ld, bf16_t* __restrict__ o, int64_t ldo,
                                                          float* __restrict__ lse, float scale_log2,
-                                                         const uint64_t* __restrict__ mask, float dscale) {
+                                                         const uint32_t* __restrict__ mask, float dscale) {
     __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -167,11 +171,19 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, cons
     block_coords<true>(qblk, bh);
     const int T = (int)T_, b = bh / H, hh = bh % H;
     const int Q0 = qblk * 256;
-    const int64_t boff = (int64_t)b * T_, ntri = mask_tri_blocks(T_);
+    const int64_t boff = (int64_t)b * T_, ntile = mask_tiles(T_);
     const bf16_t* kb_ = k + boff * ld + hh * 64;
     const bf16_t* vb_ = v + boff * ld + hh * 64;
     const int qg[2] = {Q0 + 32 * (7 - wave), Q0 + 32 * wave};   // g = 0: the longer causal prefix
     const bool act[2] = {qg[0] < T, qg[1] < T};
+    // keep words: FWD tile (query block, key tile kv) of each group, prefetched one tile ahead
+    const uint32_t* mrow[2];
+    uint32_t mw[2] = {0u, 0u};
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        mrow[g] = DROP ? mask + ((int64_t)bh * ntile + mask_fwd_tile(qg[g] >> 5, 0)) * 64 + lane : nullptr;
+        if (DROP && act[g]) mw[g] = mrow[g][0];
+    }
     sv8 qf[2][4];
 #pragma unroll
     for (int g = 0; g < 2; ++g)
@@ -189,6 +201,10 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, cons
     for (int kv = 0; kv < nkv; ++kv) {
         const int nxt = kv + 1 < nkv ? kv + 1 : kv;
         const Stage2 st = stage_load(kb_, ld, vb_, ld, (int64_t)nxt * 64, tid);
+        uint32_t mn[2] = {0u, 0u};
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+            if (DROP && act[g] && nxt * 64 <= qg[g] + 31) mn[g] = mrow[g][nxt * 64];
         const char* Ki = smem + (kv & 1) * 2 * TILE;
         const char* Vi = Ki + TILE;
         const int k0 = kv * 64;
@@ -232,13 +248,12 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, cons
                     pf[1][0] = pf[1][1] = sv8{};
                     break;
                 }
-                const uint64_t* mw = DROP ? mask_block(mask, bh, ntri, qg[g] >> 5, (k0 >> 5) + kt) : nullptr;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     // raw v_exp_f32: weights below 2^-126 of the stale max flush to 0
                     const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][r], scale_log2, mneg));
                     ls += p;
-                    s[kt][r] = DROP ? keep_sel(mw[r], p) : p;
+                    s[kt][r] = DROP ? keep_and(mw[g], 16 * kt + r, p) : p;
                 }
                 pf[kt][0] = pack16(s[kt], 0);
                 pf[kt][1] = pack16(s[kt], 1);
@@ -255,6 +270,8 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, cons
                 }
         }
         stage_store(st, smem + ((kv + 1) & 1) * 2 * TILE, tid);
+        mw[0] = mn[0];
+        mw[1] = mn[1];
         __syncthreads();
     }
 #pragma unroll
@@ -277,7 +294,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_dq_d64(int64_t T_, int H, const
                                                         const bf16_t* __restrict__ dout, int64_t ldd,
                                                         const float* __restrict__ lse, float* __restrict__ delta,
                                                         bf16_t* __restrict__ dq, int64_t lddq, float scale,
-                                                        const uint64_t* __restrict__ mask, float dscale) {
+                                                        const uint32_t* __restrict__ mask, float dscale) {
     __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -285,12 +302,19 @@ __global__ __launch_bounds__(256, 2) void k_attn_dq_d64(int64_t T_, int H, const
     block_coords<true>(qblk, bh);
     const int T = (int)T_, b = bh / H, hh = bh % H;
     const int Q0 = qblk * 256;
-    const int64_t boff = (int64_t)b * T_, ntri = mask_tri_blocks(T_);
+    const int64_t boff = (int64_t)b * T_, ntile = mask_tiles(T_);
     const float c2 = scale * LOG2E;
     const bf16_t* kb_ = k + boff * ld + hh * 64;
     const bf16_t* vb_ = v + boff * ld + hh * 64;
     const int qg[2] = {Q0 + 32 * (7 - wave), Q0 + 32 * wave};
     const bool act[2] = {qg[0] < T, qg[1] < T};
+    const uint32_t* mrow[2];
+    uint32_t mw[2] = {0u, 0u};
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        mrow[g] = DROP ? mask + ((int64_t)bh * ntile + mask_fwd_tile(qg[g] >> 5, 0)) * 64 + lane : nullptr;
+        if (DROP && act[g]) mw[g] = mrow[g][0];
+    }
     sv8 qf[2][4], df[2][4];
     float lse2[2], dl[2];
 #pragma unroll
@@ -323,6 +347,10 @@ __global__ __launch_bounds__(256, 2) void k_attn_dq_d64(int64_t T_, int H, const
     for (int kv = 0; kv < nkv; ++kv) {
         const int nxt = kv + 1 < nkv ? kv + 1 : kv;
         const Stage2 st = stage_load(kb_, ld, vb_, ld, (int64_t)nxt * 64, tid);
+        uint32_t mn[2] = {0u, 0u};
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+            if (DROP && act[g] && nxt * 64 <= qg[g] + 31) mn[g] = mrow[g][nxt * 64];
         const char* Ki = smem + (kv & 1) * 2 * TILE;
         const char* Vi = Ki + TILE;
         const int k0 = kv * 64;
@@ -340,13 +368,12 @@ __global__ __launch_bounds__(256, 2) void k_attn_dq_d64(int64_t T_, int H, const
                     s = mfma32(frag_row(Ki, 32 * kt, ks, lane), qf[g][ks], s);
                     dp = mfma32(frag_row(Vi, 32 * kt, ks, lane), df[g][ks], dp);
                 }
-                const uint64_t* mw = DROP ? mask_block(mask, bh, ntri, qg[g] >> 5, (k0 >> 5) + kt) : nullptr;
                 if (diag) mask_upper(s, qa, k0 + 32 * kt, lane, -INFINITY);
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lse2[g]));
                     float d = dp[r];
-                    if (DROP) d = keep_sel(mw[r], d * dscale);
+                    if (DROP) d = keep_and(mw[g], 16 * kt + r, d * dscale);
                     s[r] = p * (d - dl[g]);
                 }
                 const sv8 d0 = pack16(s, 0), d1 = pack16(s, 1);
@@ -358,6 +385,8 @@ __global__ __launch_bounds__(256, 2) void k_attn_dq_d64(int64_t T_, int H, const
             }
         }
         stage_store(st, smem + ((kv + 1) & 1) * 2 * TILE, tid);
+        mw[0] = mn[0];
+        mw[1] = mn[1];
         __syncthreads();
     }
 #pragma unroll
@@ -380,7 +409,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, con
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta, bf16_t* __restrict__ dk,
                                                           bf16_t* __restrict__ dv, int64_t lddkv, float scale,
-                                                          const uint64_t* __restrict__ mask, float dscale) {
+                                                          const uint32_t* __restrict__ mask, float dscale) {
     __shared__ __attribute__((aligned(16))) char smem[2 * KV_STAGE];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -389,7 +418,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, con
     const int T = (int)T_, b = bh / H, hh = bh % H;
     const int K0 = kblk * 128, kq = K0 + 32 * wave;
     const bool act = kq < T;
-    const int64_t boff = (int64_t)b * T_, ntri = mask_tri_blocks(T_);
+    const int64_t boff = (int64_t)b * T_, ntile = mask_tiles(T_);
     const float c2 = scale * LOG2E;
     const int key = kq + (lane & 31);
     sv8 kf[4], vf[4];
@@ -404,6 +433,11 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, con
     const float* lse_b = lse + (int64_t)bh * T_;
     const float* del_b = delta + (int64_t)bh * T_;
     const int nq = T / 64, qt0 = K0 / 64;
+    // keep words: BWD tiles (key block kq/32, query tile qt >= kq/64), prefetched one tile ahead
+    const int kbw = kq >> 5, qtm = kbw >> 1;
+    const uint32_t* mcol =
+        DROP && act ? mask + ((int64_t)bh * ntile + mask_bwd_tile(kbw, qtm, nq)) * 64 + lane : nullptr;
+    uint32_t mw = (DROP && act && qt0 >= qtm) ? mcol[(qt0 - qtm) * 64] : 0u;
     auto stat_load = [&](int qt) {
         float s = 0.f;
         if (tid < 64) s = lse_b[qt * 64 + tid] * LOG2E;
@@ -421,6 +455,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, con
         const int nxt = qt + 1 < nq ? qt + 1 : qt;
         const Stage2 st = stage_load(qb_, ld, ob_, ldd, (int64_t)nxt * 64, tid);
         const float sn = stat_load(nxt);
+        const uint32_t mn = (DROP && act && nxt >= qtm) ? mcol[(nxt - qtm) * 64] : 0u;
         const char* S0 = smem + (it & 1) * KV_STAGE;
         const char* Qi = S0;
         const char* Oi = S0 + TILE;
@@ -445,7 +480,6 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, con
                     for (int r = 0; r < 16; ++r)
                         if ((r & 3) + 8 * (r >> 2) < rel) s[r] = -INFINITY;
                 }
-                const uint64_t* mw = DROP ? mask_block(mask, bh, ntri, q0s >> 5, kq >> 5) : nullptr;
                 fv16 z;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
@@ -460,8 +494,9 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, con
                         const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lv[e]));
                         float d = dp[r];
                         if (DROP) {
-                            z[r] = keep_sel(mw[r], p);   // 1/(1-p) of dV applied in the epilogue
-                            d = keep_sel(mw[r], d * dscale);
+                            const uint32_t kp = keep_mask(mw, 16 * qs + r);   // 1/(1-p) of dV: epilogue
+                            z[r] = __uint_as_float(__float_as_uint(p) & kp);
+                            d = __uint_as_float(__float_as_uint(d * dscale) & kp);
                         } else {
                             z[r] = p;
                         }
@@ -481,6 +516,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, con
         char* D = smem + ((it + 1) & 1) * KV_STAGE;
         stage_store(st, D, tid);
         if (tid < 128) ((float*)(D + 2 * TILE))[tid] = sn;
+        mw = mn;
         __syncthreads();
     }
     if (!act) return;

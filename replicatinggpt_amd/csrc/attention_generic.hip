@@ -22,64 +22,77 @@ using namespace cg;
 namespace {
 
 
-// Keep bits of the MFMA kernels (attention_common.h: both orientations) for the 32x32 (query
-// block, key block) pairs on or below the diagonal, flattened over (b*H + h, lower-triangle block).
-// One wave per block per step, DM_BPW blocks per wave: lane l takes query 32 qb + (l & 31) and keys
-// 32 kb + 16 (l >> 5) .. +15 -- two Philox calls, 16 decisions (bit e <-> key 16 (l >> 5) + e).  The
-// 32 ballot words need, per FWD word, the bits of lane (l & 31) + 32 (r >> 3) (two cross-lane
-// fetches in all) and, per BWD word, those of lane (query row of r) + 32 ((l >> 4) & 1).
-constexpr int DM_BPW = 4;
-__device__ __forceinline__ void tri_next(uint64_t& bh, int& qb, int& kb, int NB) {
-    if (++kb > qb) {
-        kb = 0;
-        if (++qb == NB) {
-            qb = 0;
-            ++bh;
-        }
-    }
-}
-__global__ __launch_bounds__(256) void k_attn_dropmask(int64_t T_, int64_t nbh, uint64_t* __restrict__ mask_f,
-                                                       uint64_t* __restrict__ mask_b, DropArgs d) {
-    const int NB = (int)(T_ >> 5);
-    const int64_t ntri = (int64_t)NB * (NB + 1) / 2;
-    const int64_t total = nbh * ntri;
-    const int lane = threadIdx.x & 63, h = lane >> 5, lq = lane & 31;
+// Keep bits of the MFMA kernels (attention_common.h: FWD and BWD tiles).  One wave per 64x64
+// (query tile QT, key tile KT <= QT) region, TPW regions per wave: its four 32x32 sub-blocks
+// (qs, ks) give FWD tiles (2 QT + qs, KT) and BWD tiles (2 KT + ks, QT) whole.  Per sub-block, lane l
+// takes query 32 qb + (l & 31) and keys 32 kb + 16 (l >> 5) .. +15 -- two Philox calls, 16 decisions.
+// FWD word: the lane's register keys 4h + {0-3, 8-11, 16-19, 24-27} (h = l >> 5) are nibbles of its
+// own and its lane^32 partner's decisions; BWD word: bit (key & 15) of the 16 query rows the lane's
+// registers hold, read back from a wave-private LDS copy of the 64 lanes' decisions.
+constexpr int DM_TPW = 2;
+__global__ __launch_bounds__(256) void k_attn_dropmask(int64_t T_, int64_t nbh, uint32_t* __restrict__ mask_f,
+                                                       uint32_t* __restrict__ mask_b, DropArgs d) {
+    __shared__ __attribute__((aligned(16))) uint16_t sbits[4][64];
+    const int NB = (int)(T_ >> 5), NP = NB >> 1;
+    const int64_t nreg = (int64_t)NP * (NP + 1) / 2, ntile = mask_tiles(T_);
+    const int64_t total = nbh * nreg;
+    const int lane = threadIdx.x & 63, h = lane >> 5, lq = lane & 31, w = threadIdx.x >> 6;
+    const int kk = lq, e = kk & 15, hh = kk >> 4;
     const uint64_t stream = dropout_stream(d.rng_call, d.site);
-    const int64_t first = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * DM_BPW;
+    const int64_t first = ((int64_t)blockIdx.x * 4 + w) * DM_TPW;
     if (first >= total) return;
-    // (b*H + h, query block, key block) of the wave's first block: one division and root per wave,
-    // then incremental steps through the lower triangle
-    uint64_t bh = (uint64_t)(first / ntri);
-    const int tri0 = (int)(first - (int64_t)bh * ntri);
-    int qb = (int)((sqrtf(8.f * tri0 + 1.f) - 1.f) * 0.5f);
-    while ((qb + 1) * (qb + 2) / 2 <= tri0) ++qb;
-    while (qb * (qb + 1) / 2 > tri0) --qb;
-    int kb = tri0 - qb * (qb + 1) / 2;
+    uint64_t bh = (uint64_t)(first / nreg);
+    const int r0 = (int)(first - (int64_t)bh * nreg);
+    int QT = (int)((sqrtf(8.f * r0 + 1.f) - 1.f) * 0.5f);
+    while ((QT + 1) * (QT + 2) / 2 <= r0) ++QT;
+    while (QT * (QT + 1) / 2 > r0) --QT;
+    int KT = r0 - QT * (QT + 1) / 2;
 #pragma unroll 1
-    for (int i = 0; i < DM_BPW; ++i) {
+    for (int i = 0; i < DM_TPW; ++i) {
         if (first + i >= total) return;
-        if (i) tri_next(bh, qb, kb, NB);
-        const uint64_t q = (uint64_t)qb * 32 + lq, key0 = (uint64_t)kb * 32 + 16 * h;
-        const uint64_t grp = ((bh * T_ + q) * T_ + key0) >> 3;
-        const uint32_t bits = keep8_bits(philox_group(d.seed, stream, grp), d.thr) |
-                              (keep8_bits(philox_group(d.seed, stream, grp + 1), d.thr) << 8);
-        const uint32_t v0 = (uint32_t)__shfl((int)bits, lq, 64) >> (4 * h);
-        const uint32_t v1 = (uint32_t)__shfl((int)bits, lq + 32, 64) >> (4 * h);
-        uint64_t fw[16], bw[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            fw[r] = __ballot(((r < 8 ? v0 : v1) >> ((r & 3) + 8 * ((r >> 2) & 1))) & 1u);
-            const int src = (r & 3) + 8 * (r >> 2) + 4 * h + 32 * ((lane >> 4) & 1);
-            bw[r] = __ballot(((uint32_t)__shfl((int)bits, src, 64) >> (lane & 15)) & 1u);
-        }
-        if (lane < 2) {
-            const int64_t off = ((int64_t)bh * ntri + (int64_t)qb * (qb + 1) / 2 + kb) * 16;
-            uint64_t* dst = (lane ? mask_b : mask_f) + off;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const uint64_t a = lane ? bw[2 * j] : fw[2 * j], c = lane ? bw[2 * j + 1] : fw[2 * j + 1];
-                *(uint4*)(dst + 2 * j) = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)c, (uint32_t)(c >> 32));
+        if (i && ++KT > QT) {
+            KT = 0;
+            if (++QT == NP) {
+                QT = 0;
+                ++bh;
             }
+        }
+        uint32_t fw[2] = {0u, 0u}, bw[2] = {0u, 0u};
+#pragma unroll
+        for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                if (QT == KT && ks > qs) continue;   // sub-block above the diagonal: zero bits
+                const int qb = 2 * QT + qs, kb = 2 * KT + ks;
+                const uint64_t q = (uint64_t)qb * 32 + lq, key0 = (uint64_t)kb * 32 + 16 * h;
+                const uint64_t grp = ((bh * T_ + q) * T_ + key0) >> 3;
+                const uint32_t bits = keep8_bits(philox_group(d.seed, stream, grp), d.thr) |
+                                      (keep8_bits(philox_group(d.seed, stream, grp + 1), d.thr) << 8);
+                const uint32_t part = (uint32_t)__shfl_xor((int)bits, 32, 64);
+                const uint32_t lo = h ? part : bits, hi = h ? bits : part, sh = 4 * h;
+                const uint32_t f16 = ((lo >> sh) & 0xFu) | (((lo >> (8 + sh)) & 0xFu) << 4) |
+                                     (((hi >> sh) & 0xFu) << 8) | (((hi >> (8 + sh)) & 0xFu) << 12);
+                fw[qs] |= f16 << (16 * ks);
+                sbits[w][lane] = (uint16_t)bits;          // lane q + 32 h': keys 16 h' .. +15 of query q
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                uint32_t b16 = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {   // query rows 4h + 8j + 0..3 of key kk
+                    const uint2 v = *(const uint2*)&sbits[w][32 * hh + 4 * h + 8 * j];
+                    b16 |= ((v.x >> e) & 1u) << (4 * j) | ((v.x >> (16 + e)) & 1u) << (4 * j + 1) |
+                           ((v.y >> e) & 1u) << (4 * j + 2) | ((v.y >> (16 + e)) & 1u) << (4 * j + 3);
+                }
+                bw[ks] |= b16 << (16 * qs);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            mask_f[((int64_t)bh * ntile + mask_fwd_tile(2 * QT + s, KT)) * 64 + lane] = fw[s];
+            mask_b[((int64_t)bh * ntile + mask_bwd_tile(2 * KT + s, QT, NP)) * 64 + lane] = bw[s];
         }
     }
 }
@@ -516,18 +529,18 @@ DropArgs make_drop(double p, uint64_t seed, const uint64_t* rng_call, int site) 
     return d;
 }
 
-// both orientations, lower-triangle 32x32 blocks, 128 B each
-int64_t mask_bytes(int64_t B, int64_t H, int64_t T) { return 2 * B * H * mask_tri_blocks(T) * 128; }
+// FWD and BWD tiles, 256 B each
+int64_t mask_bytes(int64_t B, int64_t H, int64_t T) { return 2 * B * H * mask_tiles(T) * 256; }
 
-void set_masks(DropArgs& d, uint64_t* mask, int64_t B, int64_t H, int64_t T) {
-    d.mask = mask;
-    d.mask_bwd = mask + B * H * mask_tri_blocks(T) * 16;
+void set_masks(DropArgs& d, const uint64_t* mask, int64_t B, int64_t H, int64_t T) {
+    d.mask = (const uint32_t*)mask;
+    d.mask_bwd = (const uint32_t*)mask + B * H * mask_tiles(T) * 64;
 }
 
 void launch_dropmask(int64_t B, int64_t H, int64_t T, uint64_t* mask, const DropArgs& d, hipStream_t st) {
-    const int64_t blocks = B * H * mask_tri_blocks(T);
-    k_attn_dropmask<<<ceil_div(blocks, 4 * DM_BPW), 256, 0, st>>>(T, B * H, mask, mask + B * H * mask_tri_blocks(T) * 16,
-                                                                   d);
+    const int64_t np = T / 64, regions = B * H * np * (np + 1) / 2;
+    uint32_t* m = (uint32_t*)mask;
+    k_attn_dropmask<<<ceil_div(regions, 4 * DM_TPW), 256, 0, st>>>(T, B * H, m, m + B * H * mask_tiles(T) * 64, d);
 }
 
 bool fast_attn_ok(int dtype, int64_t T, int64_t D, const void* a, const void* b, const void* c, int64_t ld1,
@@ -567,7 +580,7 @@ extern "C" int cg_attn_fwd_premasked(int dtype, int64_t B, int64_t T, int64_t H,
 
 extern "C" int cg_attn_dropmask(int64_t B, int64_t H, int64_t T, double dropout_p, uint64_t seed,
                                 const uint64_t* rng_call, int site, uint64_t* mask, void* stream) {
-    CG_REQUIRE(B > 0 && H > 0 && T > 0 && T % 16 == 0, "cg_attn_dropmask: bad shape (T %% 16 == 0 required)");
+    CG_REQUIRE(B > 0 && H > 0 && T > 0 && T % 64 == 0, "cg_attn_dropmask: bad shape (T %% 64 == 0 required)");
     CG_REQUIRE(dropout_p > 0 && dropout_p < 1 && mask, "cg_attn_dropmask: needs 0 < p < 1 and a mask buffer");
     DropArgs d = make_drop(dropout_p, seed, rng_call, site);
     launch_dropmask(B, H, T, mask, d, (hipStream_t)stream);
@@ -653,7 +666,7 @@ extern "C" int cg_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D
                 launch_dropmask(B, H, T, m, d, st);
                 mask = m;
             }
-            set_masks(d, (uint64_t*)mask, B, H, T);
+            set_masks(d, mask, B, H, T);
         }
         const bf16_t *Q = (const bf16_t*)q, *K = (const bf16_t*)k, *V = (const bf16_t*)v, *DO = (const bf16_t*)dout;
         attn::launch_dq_d64(B, T, (int)H, Q, K, V, ld_qkv, (const bf16_t*)o, ld_o, DO, ld_do, lse, delta, (bf16_t*)dq,

@@ -20,7 +20,7 @@ def test_library_exports_header_symbols():
     assert lib.cg_version() >= 1
     assert lib.cg_gemm_workspace(128, 256, 4) == 4 * 128 * 256 * 4
     # two orientations x lower-triangle 32x32 blocks (8 * 9 / 2 at T = 256) x 128 B
-    assert lib.cg_attn_mask_bytes(2, 6, 256) == 2 * (2 * 6 * 36 * 128)
+    assert lib.cg_attn_mask_bytes(2, 6, 256) == 2 * (2 * 6 * 20 * 256)   # NB = 8: 8 + 49 // 4 tiles
     assert lib.cg_attn_bwd_workspace(2, 256, 6, 64) == 2 * 6 * 256 * 4 + lib.cg_attn_mask_bytes(2, 6, 256)
 
 

@@ -79,28 +79,36 @@ def test_c4_attention_fwd_bwd_vs_fp64(p):
 
 def _decode_keep_bits(mask, BH, T):
     """Keep-bit buffer of the MFMA kernels (attention_common.h) -> two bool arrays [BH, T, T]
-    (FWD and BWD orientation), lower-triangle 32x32 blocks only (the rest False)."""
-    NB = T // 32
-    ntri = NB * (NB + 1) // 2
-    words = mask.cpu().numpy().view(np.uint64).reshape(2, BH, ntri, 16)
+    (FWD and BWD tiles decoded), blocks outside the stored tiles False."""
+    NB, NP = T // 32, T // 64
+    ntile = NB + (NB - 1) ** 2 // 4
+    words = mask.cpu().numpy().view(np.uint32).reshape(2, BH, ntile, 64)
     lanes = np.arange(64)
     r = np.arange(16)
     accrow = (r[:, None] & 3) + 8 * (r[:, None] >> 2) + 4 * (lanes[None, :] >> 5)     # [16, 64]
     col = np.broadcast_to(lanes[None, :] & 31, (16, 64))
     out = np.zeros((2, BH, T, T), dtype=bool)
-    t = 0
+
+    def bits(w, s):   # [BH, 64] words -> [BH, 16, 64] bits 16 s + r
+        sh = (16 * s + r).astype(np.uint32)
+        return ((w[:, None, :] >> sh[None, :, None]) & np.uint32(1)).astype(bool)
+
     for qb in range(NB):
-        for kb in range(qb + 1):
-            bits = ((words[:, :, t, :, None] >> lanes.astype(np.uint64)) & np.uint64(1)).astype(bool)  # [2,BH,16,64]
-            out[0][:, 32 * qb + col, 32 * kb + accrow] = bits[0]    # FWD: lane <-> query, register <-> key
-            out[1][:, 32 * qb + accrow, 32 * kb + col] = bits[1]    # BWD: register <-> query, lane <-> key
-            t += 1
+        for kt in range(qb // 2 + 1):
+            t = qb + (qb - 1) ** 2 // 4 + kt if qb else kt
+            for s in range(2):
+                out[0][:, 32 * qb + col, 64 * kt + 32 * s + accrow] = bits(words[0, :, t], s)
+    for kb in range(NB):
+        for qt in range(kb // 2, NP):
+            t = kb * NP - ((kb - 1) ** 2 // 4 if kb else 0) + qt - kb // 2
+            for s in range(2):
+                out[1][:, 64 * qt + 32 * s + accrow, 32 * kb + col] = bits(words[1, :, t], s)
     return out
 
 
 def test_c4_dropmask_bits_match_oracle():
-    """cg_attn_dropmask at T=1024 (528 lower-triangle 32x32 blocks per (b, h), both orientations): every
-    keep bit of the MFMA kernels' layouts equals the oracle's keep(((b H + h) T + q) T + key)."""
+    """cg_attn_dropmask at T=1024 (272 FWD and 272 BWD 64-row tiles per (b, h)): every keep bit of the
+    MFMA kernels' layouts equals the oracle's keep(((b H + h) T + q) T + key)."""
     from replicatinggpt_amd import ops
     B, H, T, p, seed, site = 1, 2, T4, 0.2, 0x5EED, 6
     call = torch.tensor([11], dtype=torch.int64, device=DEV)
