@@ -19,6 +19,8 @@
 //  * Dropout keep bits (k_attn_dropmask, attention_common.h): one 32-bit word per lane per 64-row
 //    tile, loaded a tile ahead with the K/V (or Q/dO) staging loads and applied as v_bfe_i32 +
 //    v_and_b32 per element; the 1/(1-p) is applied once at the end.
+#include <float.h>
+
 #include "attention_common.h"
 
 namespace cg {
@@ -87,7 +89,10 @@ __device__ __forceinline__ uint32_t keep_mask(uint32_t w, int bit) {
     asm("" : "+v"(m));
     return m;
 }
+// x & keep mask.  The keep word passes through an empty asm tied to x first, so the v_bfe_i32 is
+// issued beside its use, not hoisted (32 mask VGPRs live at once) to the start of the tile.
 __device__ __forceinline__ float keep_and(uint32_t w, int bit, float x) {
+    asm("" : "+v"(w) : "v"(x));
     return __uint_as_float(__float_as_uint(x) & keep_mask(w, bit));
 }
 
@@ -120,6 +125,20 @@ __device__ __forceinline__ void stage_store(const Stage2& s, char* img, int tid)
     *(uint4*)(img + aoff(r + 32, c)) = s.a1;
     *(uint4*)(img + TILE + aoff(r, c)) = s.b0;
     *(uint4*)(img + TILE + aoff(r + 32, c)) = s.b1;
+}
+
+// one [64][64] bf16 tile staged through registers: 2 x 16 B per thread
+struct Stage1 {
+    uint4 a0, a1;
+};
+__device__ __forceinline__ Stage1 stage_load1(const bf16_t* X, int64_t ldx, int64_t row0, int tid) {
+    const int r = tid >> 3, c = tid & 7;
+    return Stage1{*(const uint4*)(X + (row0 + r) * ldx + c * 8), *(const uint4*)(X + (row0 + r + 32) * ldx + c * 8)};
+}
+__device__ __forceinline__ void stage_store1(const Stage1& s, char* img, int tid) {
+    const int r = tid >> 3, c = tid & 7;
+    *(uint4*)(img + aoff(r, c)) = s.a0;
+    *(uint4*)(img + aoff(r + 32, c)) = s.a1;
 }
 
 // XCD-aware block order for a (row blocks, B*H) grid: the dispatcher deals linear block ids to the
@@ -158,13 +177,102 @@ __device__ __forceinline__ void store_rows(bf16_t* row, const fv16 (&acc)[2], fl
 // =====================================================================================
 // forward
 // =====================================================================================
+// S^T (64 keys x 32 queries) of one query group (rows qr..qr+31 of the block's Q image) against a
+// K image: two independent MFMA chains, Q fragments read from LDS (not held in registers)
+__device__ __forceinline__ void qk_tile(fv16 (&s)[2], const char* Ki, const char* Qimg, int qr, int lane) {
+    s[0] = fv16{};
+    s[1] = fv16{};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        const sv8 qf = frag_row(Qimg, qr, ks, lane);
+        s[0] = mfma32(frag_row(Ki, 0, ks, lane), qf, s[0]);
+        s[1] = mfma32(frag_row(Ki, 32, ks, lane), qf, s[1]);
+    }
+}
+
+// max over this lane's 32 scores (a v_max3 tree, not a 32-deep chain), then over the lane^32
+// partner (v_permlane32_swap: no LDS round trip)
+__device__ __forceinline__ float tile_max(const fv16 (&s)[2]) {
+    float t[11];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+        const int i0 = 3 * j, i1 = 3 * j + 1, i2 = 3 * j + 2;
+        t[j] = fmaxf(fmaxf(s[i0 >> 4][i0 & 15], s[i1 >> 4][i1 & 15]), s[i2 >> 4][i2 & 15]);
+    }
+    t[10] = fmaxf(s[1][14], s[1][15]);
+    const float u0 = fmaxf(fmaxf(t[0], t[1]), t[2]), u1 = fmaxf(fmaxf(t[3], t[4]), t[5]);
+    const float u2 = fmaxf(fmaxf(t[6], t[7]), t[8]), u3 = fmaxf(t[9], t[10]);
+    const float m = fmaxf(fmaxf(u0, u1), fmaxf(u2, u3));
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+    return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+}
+
+// lazy online-softmax rescale (threshold RESCALE_THR in log2 units): called after the group's
+// previous tiles are all in O and l, before this tile is exponentiated
+__device__ __forceinline__ void rescale_if(float mt, float& m_run, float& l_run, fv16 (&o)[2]) {
+    if (__any(mt > m_run + RESCALE_THR)) {   // rare after the first tiles
+        const float mn = fmaxf(m_run, mt);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - mn);
+        o[0] *= alpha;
+        o[1] *= alpha;
+        l_run *= alpha;
+        m_run = mn;
+    }
+}
+
+// P = exp2(S scale_log2 - m) of a full tile: row sums (four partial sums) into l_run, dropout keep
+// bits applied, packed to the bf16 B operands of O^T += V^T P^T
+template <bool DROP>
+__device__ __forceinline__ void softmax_pack(fv16 (&s)[2], float scale_log2, float m_run, float& l_run, uint32_t mw,
+                                             sv8 (&pf)[2][2]) {
+    const float mneg = -m_run;
+    float ls[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            // raw v_exp_f32: weights below 2^-126 of the stale max flush to 0
+            const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][r], scale_log2, mneg));
+            ls[r & 3] += p;
+            s[kt][r] = DROP ? keep_and(mw, 16 * kt + r, p) : p;
+        }
+        pf[kt][0] = pack16(s[kt], 0);
+        pf[kt][1] = pack16(s[kt], 1);
+    }
+    l_run += (ls[0] + ls[1]) + (ls[2] + ls[3]);
+}
+
+// O^T += V^T P^T over a full 64-key tile (two independent chains, one per 32-dim half)
+__device__ __forceinline__ void pv_tile(fv16 (&o)[2], const char* Vi, const sv8 (&pf)[2][2], int lane) {
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int sk = 0; sk < 2; ++sk) {
+            o[0] = mfma32(frag_tr(Vi, 32 * kt, sk, 0, lane), pf[kt][sk], o[0]);
+            o[1] = mfma32(frag_tr(Vi, 32 * kt, sk, 32, lane), pf[kt][sk], o[1]);
+        }
+}
+
+// Forward.  Tiles where both of a wave's query groups (A = 7 - w, B = w) are full (before B's
+// diagonal tile) run software-pipelined, B one phase behind A, so every MFMA phase has the other
+// group's softmax VALU work beside it:
+//   [1] S_A(kv)      || P_B(kv-1) = softmax of B's previous tile
+//   [2] O_B += P_B V(kv-1) || max_A(kv), A's rescale decision
+//   [3] S_B(kv)      || P_A(kv)
+//   [4] O_A += P_A V(kv)   || max_B(kv), B's rescale decision
+// (each group's decision precedes its exponentials and follows its previous P V).  K/V tiles go
+// through a 3-slot LDS ring (B still reads V(kv-1) while kv+1 is written), one barrier per tile.
+// The diagonal and later tiles run unpipelined.  The block's 256 Q rows live in LDS (32 KB, same
+// swizzle) rather than in registers: 48 + 32 KB per block, two blocks per CU.
 template <bool DROP>
 __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, const bf16_t* __restrict__ q,
                                                          const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
                                                          int64_t ld, bf16_t* __restrict__ o, int64_t ldo,
                                                          float* __restrict__ lse, float scale_log2,
                                                          const uint32_t* __restrict__ mask, float dscale) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
+    constexpr int SLOT = 2 * TILE;
+    __shared__ __attribute__((aligned(16))) char smem[3 * SLOT + 4 * TILE];
+    char* const Qimg = smem + 3 * SLOT;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int qblk, bh;
@@ -174,7 +282,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, cons
     const int64_t boff = (int64_t)b * T_, ntile = mask_tiles(T_);
     const bf16_t* kb_ = k + boff * ld + hh * 64;
     const bf16_t* vb_ = v + boff * ld + hh * 64;
-    const int qg[2] = {Q0 + 32 * (7 - wave), Q0 + 32 * wave};   // g = 0: the longer causal prefix
+    const int qg[2] = {Q0 + 32 * (7 - wave), Q0 + 32 * wave};   // g = 0 (A): the longer causal prefix
     const bool act[2] = {qg[0] < T, qg[1] < T};
     // keep words: FWD tile (query block, key tile kv) of each group, prefetched one tile ahead
     const uint32_t* mrow[2];
@@ -184,28 +292,94 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, cons
         mrow[g] = DROP ? mask + ((int64_t)bh * ntile + mask_fwd_tile(qg[g] >> 5, 0)) * 64 + lane : nullptr;
         if (DROP && act[g]) mw[g] = mrow[g][0];
     }
-    sv8 qf[2][4];
+    {   // Q image: rows Q0 .. Q0 + 255 (zero past T)
+        const bf16_t* qb_ = q + boff * ld + hh * 64;
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-            qf[g][ks] = act[g] ? ld_frag(q + boff * ld + hh * 64, ld, qg[g] + (lane & 31), ks, lane) : sv8{};
+        for (int i = 0; i < 8; ++i) {
+            const int r = (tid >> 3) + 32 * i, c = tid & 7;
+            const uint4 x = Q0 + r < T ? *(const uint4*)(qb_ + (int64_t)(Q0 + r) * ld + c * 8) : make_uint4(0, 0, 0, 0);
+            *(uint4*)(Qimg + aoff(r, c)) = x;
+        }
+    }
+    const int qr[2] = {32 * (7 - wave), 32 * wave};   // the groups' rows in the Q image
     fv16 oacc[2][2];
 #pragma unroll
     for (int g = 0; g < 2; ++g) oacc[g][0] = oacc[g][1] = fv16{};
-    float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+    // running max starts at -FLT_MAX, not -inf: a -inf score then exponentiates to 0, never NaN,
+    // and the first tile still always moves the max (its decision compares against -FLT_MAX + THR)
+    float m_run[2] = {-FLT_MAX, -FLT_MAX}, l_run[2] = {0.f, 0.f};
     const int qlast = (Q0 + 255 < T - 1) ? Q0 + 255 : T - 1;
     const int nkv = qlast / 64 + 1;
+    const int npipe = act[1] ? (qg[1] + 31) / 64 : 0;   // B's diagonal tile: first unpipelined tile
+    fv16 sA[2], sB[2] = {fv16{} - INFINITY, fv16{} - INFINITY};
+    sv8 pfA[2][2], pfB[2][2];
+    uint32_t mwBp = 0u;   // B's keep word of the previous tile
+    int cs = 0, ps = 2, ns = 1;   // ring slots of tiles kv, kv - 1, kv + 1
     stage_store(stage_load(kb_, ld, vb_, ld, 0, tid), smem, tid);
+    {   // the V half of slot 2 is tile -1 of the pipeline head: zeros
+        const int r = tid >> 3, c = tid & 7;
+        *(uint4*)(smem + 2 * SLOT + TILE + aoff(r, c)) = make_uint4(0, 0, 0, 0);
+        *(uint4*)(smem + 2 * SLOT + TILE + aoff(r + 32, c)) = make_uint4(0, 0, 0, 0);
+    }
     __syncthreads();
-    for (int kv = 0; kv < nkv; ++kv) {
+    // per tile: issue the next tile's loads first, write them to the ring after the compute
+    auto next_loads = [&](int kv, uint32_t (&mn)[2]) {
         const int nxt = kv + 1 < nkv ? kv + 1 : kv;
-        const Stage2 st = stage_load(kb_, ld, vb_, ld, (int64_t)nxt * 64, tid);
-        uint32_t mn[2] = {0u, 0u};
 #pragma unroll
         for (int g = 0; g < 2; ++g)
-            if (DROP && act[g] && nxt * 64 <= qg[g] + 31) mn[g] = mrow[g][nxt * 64];
-        const char* Ki = smem + (kv & 1) * 2 * TILE;
+            mn[g] = (DROP && act[g] && nxt * 64 <= qg[g] + 31) ? mrow[g][nxt * 64] : 0u;
+        return stage_load(kb_, ld, vb_, ld, (int64_t)nxt * 64, tid);
+    };
+    auto advance = [&](const Stage2& st, const uint32_t (&mn)[2]) {
+        stage_store(st, smem + ns * SLOT, tid);
+        mwBp = mw[1];
+        mw[0] = mn[0];
+        mw[1] = mn[1];
+        ps = cs;
+        cs = ns;
+        ns = ns == 2 ? 0 : ns + 1;
+        __syncthreads();
+    };
+    int kv = 0;
+    for (; kv < npipe; ++kv) {
+        // next K tile loaded now and written to its (free) slot mid-tile, next V tile loaded then
+        // and written at the end: 8 staging VGPRs live at a time instead of 16
+        const int nxt = kv + 1;   // < nkv: B's diagonal tile is still ahead
+        uint32_t mn[2];
+#pragma unroll
+        for (int g = 0; g < 2; ++g) mn[g] = DROP ? mrow[g][nxt * 64] : 0u;   // both groups full through nxt
+        const Stage1 stk = stage_load1(kb_, ld, (int64_t)nxt * 64, tid);
+        const char* Ki = smem + cs * SLOT;
+        const char* Vi = Ki + TILE;
+        const char* Vp = smem + ps * SLOT + TILE;
+        // at kv = 0, B's "previous tile" is sB = -inf against a zeroed V slot: it adds exactly 0
+        qk_tile(sA, Ki, Qimg, qr[0], lane);
+        softmax_pack<DROP>(sB, scale_log2, m_run[1], l_run[1], mwBp, pfB);
+        pv_tile(oacc[1], Vp, pfB, lane);
+        rescale_if(tile_max(sA) * scale_log2, m_run[0], l_run[0], oacc[0]);
+        stage_store1(stk, smem + ns * SLOT, tid);
+        const Stage1 stv = stage_load1(vb_, ld, (int64_t)nxt * 64, tid);
+        qk_tile(sB, Ki, Qimg, qr[1], lane);
+        softmax_pack<DROP>(sA, scale_log2, m_run[0], l_run[0], mw[0], pfA);
+        pv_tile(oacc[0], Vi, pfA, lane);
+        rescale_if(tile_max(sB) * scale_log2, m_run[1], l_run[1], oacc[1]);
+        stage_store1(stv, smem + ns * SLOT + TILE, tid);
+        mwBp = mw[1];
+        mw[0] = mn[0];
+        mw[1] = mn[1];
+        ps = cs;
+        cs = ns;
+        ns = ns == 2 ? 0 : ns + 1;
+        __syncthreads();
+    }
+    if (npipe > 0) {   // pipeline tail: B's pending tile npipe - 1 (its V still in the previous slot)
+        softmax_pack<DROP>(sB, scale_log2, m_run[1], l_run[1], mwBp, pfB);
+        pv_tile(oacc[1], smem + ps * SLOT + TILE, pfB, lane);
+    }
+    for (; kv < nkv; ++kv) {
+        uint32_t mn[2];
+        const Stage2 st = next_loads(kv, mn);
+        const char* Ki = smem + cs * SLOT;
         const char* Vi = Ki + TILE;
         const int k0 = kv * 64;
 #pragma unroll
@@ -217,48 +391,18 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, cons
             for (int kt = 0; kt < 2; ++kt) {
                 if (kt == 1 && !live1) break;
 #pragma unroll
-                for (int ks = 0; ks < 4; ++ks) s[kt] = mfma32(frag_row(Ki, 32 * kt, ks, lane), qf[g][ks], s[kt]);
+                for (int ks = 0; ks < 4; ++ks)
+                    s[kt] = mfma32(frag_row(Ki, 32 * kt, ks, lane), frag_row(Qimg, qr[g], ks, lane), s[kt]);
             }
             const int qa = qg[g] + (lane & 31);
             if (__builtin_amdgcn_readfirstlane(k0 + 63 > qg[g])) {   // diagonal tile: causal mask
                 mask_upper(s[0], qa, k0, lane, -INFINITY);
                 mask_upper(s[1], qa, k0 + 32, lane, -INFINITY);
             }
-            float mx = -INFINITY;
-#pragma unroll
-            for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
-            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-            const float mt = mx * scale_log2;
-            if (__any(mt > m_run[g] + RESCALE_THR)) {   // rare after the first tiles
-                const float mn = fmaxf(m_run[g], mt);
-                const float alpha = __builtin_amdgcn_exp2f(m_run[g] - mn);
-                oacc[g][0] *= alpha;
-                oacc[g][1] *= alpha;
-                l_run[g] *= alpha;
-                m_run[g] = mn;
-            }
-            const float mneg = -m_run[g];
-            float ls = 0.f;
+            if (!live1) s[1] = fv16{} - INFINITY;
+            rescale_if(tile_max(s) * scale_log2, m_run[g], l_run[g], oacc[g]);
             sv8 pf[2][2];
-#pragma unroll
-            for (int kt = 0; kt < 2; ++kt) {
-                if (kt == 1 && !live1) {
-                    pf[1][0] = pf[1][1] = sv8{};
-                    break;
-                }
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    // raw v_exp_f32: weights below 2^-126 of the stale max flush to 0
-                    const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][r], scale_log2, mneg));
-                    ls += p;
-                    s[kt][r] = DROP ? keep_and(mw[g], 16 * kt + r, p) : p;
-                }
-                pf[kt][0] = pack16(s[kt], 0);
-                pf[kt][1] = pack16(s[kt], 1);
-            }
-            l_run[g] += ls;
+            softmax_pack<DROP>(s, scale_log2, m_run[g], l_run[g], mw[g], pf);
 #pragma unroll
             for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -269,15 +413,14 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, cons
                         oacc[g][dt] = mfma32(frag_tr(Vi, 32 * kt, sk, 32 * dt, lane), pf[kt][sk], oacc[g][dt]);
                 }
         }
-        stage_store(st, smem + ((kv + 1) & 1) * 2 * TILE, tid);
-        mw[0] = mn[0];
-        mw[1] = mn[1];
-        __syncthreads();
+        advance(st, mn);
     }
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
         if (!act[g]) continue;
-        const float lt = l_run[g] + __shfl_xor(l_run[g], 32, 64);
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run[g]), __float_as_uint(l_run[g]), false,
+                                                         false);
+        const float lt = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
         const int64_t qa = qg[g] + (lane & 31);
         store_rows(o + (boff + qa) * ldo + hh * 64, oacc[g], dscale / lt, lane);
         if (lane < 32) lse[(int64_t)bh * T_ + qa] = (m_run[g] + __log2f(lt)) * LN2;
