@@ -190,21 +190,20 @@ __device__ __forceinline__ void qk_tile(fv16 (&s)[2], const char* Ki, const char
     }
 }
 
-// max over this lane's 32 scores (a v_max3 tree, not a 32-deep chain), then over the lane^32
+// max over this lane's 32 scores (two interleaved v_max3 chains: a 2-input fmaxf of raw MFMA
+// results would be preceded by canonicalising v_max x, x on each input), then over the lane^32
 // partner (v_permlane32_swap: no LDS round trip)
 __device__ __forceinline__ float tile_max(const fv16 (&s)[2]) {
-    float t[11];
+    float m0 = fmaxf(fmaxf(s[0][0], s[0][1]), s[0][2]), m1 = fmaxf(fmaxf(s[1][0], s[1][1]), s[1][2]);
 #pragma unroll
-    for (int j = 0; j < 10; ++j) {
-        const int i0 = 3 * j, i1 = 3 * j + 1, i2 = 3 * j + 2;
-        t[j] = fmaxf(fmaxf(s[i0 >> 4][i0 & 15], s[i1 >> 4][i1 & 15]), s[i2 >> 4][i2 & 15]);
+    for (int r = 3; r < 15; r += 2) {
+        m0 = fmaxf(fmaxf(m0, s[0][r]), s[0][r + 1]);
+        m1 = fmaxf(fmaxf(m1, s[1][r]), s[1][r + 1]);
     }
-    t[10] = fmaxf(s[1][14], s[1][15]);
-    const float u0 = fmaxf(fmaxf(t[0], t[1]), t[2]), u1 = fmaxf(fmaxf(t[3], t[4]), t[5]);
-    const float u2 = fmaxf(fmaxf(t[6], t[7]), t[8]), u3 = fmaxf(t[9], t[10]);
-    const float m = fmaxf(fmaxf(u0, u1), fmaxf(u2, u3));
+    m0 = fmaxf(fmaxf(m0, s[0][15]), s[1][15]);
+    const float m = fmaxf(m0, m1);
     const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
-    return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    return __builtin_amdgcn_fmed3f(__uint_as_float(sw[0]), __uint_as_float(sw[1]), INFINITY);   // max, no re-canonicalising
 }
 
 // lazy online-softmax rescale (threshold RESCALE_THR in log2 units): called after the group's
@@ -264,19 +263,18 @@ __device__ __forceinline__ void pv_tile(fv16 (&o)[2], const char* Vi, const sv8 
 // through a 3-slot LDS ring (B still reads V(kv-1) while kv+1 is written), one barrier per tile.
 // The diagonal and later tiles run unpipelined.  The block's 256 Q rows live in LDS (32 KB, same
 // swizzle) rather than in registers: 48 + 32 KB per block, two blocks per CU.
+constexpr int FWD_SLOT = 2 * TILE;
+constexpr int FWD_LDS = 3 * FWD_SLOT + 4 * TILE;   // K/V ring + Q image: 80 KB
+
 template <bool DROP>
-__global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, const bf16_t* __restrict__ q,
-                                                         const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-                                                         int64_t ld, bf16_t* __restrict__ o, int64_t ldo,
-                                                         float* __restrict__ lse, float scale_log2,
-                                                         const uint32_t* __restrict__ mask, float dscale) {
-    constexpr int SLOT = 2 * TILE;
-    __shared__ __attribute__((aligned(16))) char smem[3 * SLOT + 4 * TILE];
+__device__ __forceinline__ void fwd_qblock(int qblk, int bh, char* smem, int64_t T_, int H, const bf16_t* __restrict__ q,
+                                           const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, int64_t ld,
+                                           bf16_t* __restrict__ o, int64_t ldo, float* __restrict__ lse,
+                                           float scale_log2, const uint32_t* __restrict__ mask, float dscale) {
+    constexpr int SLOT = FWD_SLOT;
     char* const Qimg = smem + 3 * SLOT;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    int qblk, bh;
-    block_coords<true>(qblk, bh);
     const int T = (int)T_, b = bh / H, hh = bh % H;
     const int Q0 = qblk * 256;
     const int64_t boff = (int64_t)b * T_, ntile = mask_tiles(T_);
@@ -424,6 +422,27 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, cons
         const int64_t qa = qg[g] + (lane & 31);
         store_rows(o + (boff + qa) * ldo + hh * 64, oacc[g], dscale / lt, lane);
         if (lane < 32) lse[(int64_t)bh * T_ + qa] = (m_run[g] + __log2f(lt)) * LN2;
+    }
+}
+
+// One workgroup per (b, h) and PAIR of 256-query blocks (nq - 1 - x, then x): the causal work of a
+// pair is the same for every x, so the grid has no long-block tail (measured occupancy of the
+// one-block-per-workgroup grid at C4: 63 %).  K/V reuse stays inside the workgroup and its L2.
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, const bf16_t* __restrict__ q,
+                                                         const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                                                         int64_t ld, bf16_t* __restrict__ o, int64_t ldo,
+                                                         float* __restrict__ lse, float scale_log2,
+                                                         const uint32_t* __restrict__ mask, float dscale) {
+    __shared__ __attribute__((aligned(16))) char smem[FWD_LDS];
+    int x, bh;
+    block_coords<false>(x, bh);
+    const int nq = (int)((T_ + 255) / 256), first = nq - 1 - x;
+    const int npass = x == first ? 1 : 2;
+#pragma unroll 1
+    for (int pass = 0; pass < npass; ++pass) {
+        if (pass) __syncthreads();
+        fwd_qblock<DROP>(pass ? x : first, bh, smem, T_, H, q, k, v, ld, o, ldo, lse, scale_log2, mask, dscale);
     }
 }
 
@@ -672,7 +691,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, con
 namespace attn {
 void launch_fwd_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                     bf16_t* o, int64_t ldo, float* lse, float scale, const DropArgs& d, hipStream_t st) {
-    const dim3 grid(ceil_div(T, 256), (unsigned)(B * H));
+    const dim3 grid((unsigned)((ceil_div(T, 256) + 1) / 2), (unsigned)(B * H));   // pairs of query blocks
     if (d.mask)
         k_attn_fwd_d64<true><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, lse, scale * LOG2E, d.mask, d.dscale);
     else

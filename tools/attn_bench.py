@@ -1,7 +1,7 @@
 """Times the charpt attention kernels at the C2 / C4 training shapes: the keep-bit kernel alone,
 the forward on premade keep bits, the forward with its keep bits (what bench.py's kernel_census
 counts) and the backward (dQ + dK/dV).  Each figure = HIP events around one hipGraph replay of
-`reps` back-to-back calls.  GPU only.  ATTN_CFG = c2 | c4 | all."""
+`reps` back-to-back calls.  GPU only.  ATTN_CFG = c2 | c4 | all; ATTN_P = one dropout p."""
 import os
 import sys
 
@@ -62,6 +62,8 @@ if __name__ == "__main__":
     L.load()
     cfg = os.environ.get("ATTN_CFG", "all")
     ps = (0.2,) if cfg != "all" else (0.0, 0.2)
+    if "ATTN_P" in os.environ:
+        ps = (float(os.environ["ATTN_P"]),)
     for p in ps:
         if cfg in ("c2", "all"):
             bench(64, 256, 6, 64, p)
