@@ -450,18 +450,14 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, cons
 // dQ: S^T = K Q^T, dP^T = V dO^T, dS^T = P^T (keep/(1-p) dP^T - delta), dQ^T += K^T dS^T
 // =====================================================================================
 template <bool DROP>
-__global__ __launch_bounds__(256, 2) void k_attn_dq_d64(int64_t T_, int H, const bf16_t* __restrict__ q,
-                                                        const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-                                                        int64_t ld, const bf16_t* __restrict__ o, int64_t ldo,
-                                                        const bf16_t* __restrict__ dout, int64_t ldd,
-                                                        const float* __restrict__ lse, float* __restrict__ delta,
-                                                        bf16_t* __restrict__ dq, int64_t lddq, float scale,
-                                                        const uint32_t* __restrict__ mask, float dscale) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
+__device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t T_, int H, const bf16_t* __restrict__ q,
+                                          const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, int64_t ld,
+                                          const bf16_t* __restrict__ o, int64_t ldo, const bf16_t* __restrict__ dout,
+                                          int64_t ldd, const float* __restrict__ lse, float* __restrict__ delta,
+                                          bf16_t* __restrict__ dq, int64_t lddq, float scale,
+                                          const uint32_t* __restrict__ mask, float dscale) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    int qblk, bh;
-    block_coords<true>(qblk, bh);
     const int T = (int)T_, b = bh / H, hh = bh % H;
     const int Q0 = qblk * 256;
     const int64_t boff = (int64_t)b * T_, ntile = mask_tiles(T_);
@@ -559,24 +555,43 @@ __global__ __launch_bounds__(256, 2) void k_attn_dq_d64(int64_t T_, int H, const
     }
 }
 
+// pairs of query blocks per workgroup, as the forward
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void k_attn_dq_d64(int64_t T_, int H, const bf16_t* __restrict__ q,
+                                                        const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                                                        int64_t ld, const bf16_t* __restrict__ o, int64_t ldo,
+                                                        const bf16_t* __restrict__ dout, int64_t ldd,
+                                                        const float* __restrict__ lse, float* __restrict__ delta,
+                                                        bf16_t* __restrict__ dq, int64_t lddq, float scale,
+                                                        const uint32_t* __restrict__ mask, float dscale) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
+    int x, bh;
+    block_coords<false>(x, bh);
+    const int nq = (int)((T_ + 255) / 256), first = nq - 1 - x;
+    const int npass = x == first ? 1 : 2;
+#pragma unroll 1
+    for (int pass = 0; pass < npass; ++pass) {
+        if (pass) __syncthreads();
+        dq_qblock<DROP>(pass ? x : first, bh, smem, T_, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
+                        mask, dscale);
+    }
+}
+
 // =====================================================================================
 // dK / dV: block = 4 waves x 32 keys; stream 64-query tiles (Q, dO, lse, delta)
 // =====================================================================================
 constexpr int KV_STAGE = 2 * TILE + 512;   // Q image, dO image, lse*log2e [64], delta [64]
 
 template <bool DROP>
-__global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, const bf16_t* __restrict__ q,
-                                                          const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-                                                          int64_t ld, const bf16_t* __restrict__ dout, int64_t ldd,
-                                                          const float* __restrict__ lse,
-                                                          const float* __restrict__ delta, bf16_t* __restrict__ dk,
-                                                          bf16_t* __restrict__ dv, int64_t lddkv, float scale,
-                                                          const uint32_t* __restrict__ mask, float dscale) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * KV_STAGE];
+__device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_t T_, int H,
+                                            const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+                                            const bf16_t* __restrict__ v, int64_t ld, const bf16_t* __restrict__ dout,
+                                            int64_t ldd, const float* __restrict__ lse,
+                                            const float* __restrict__ delta, bf16_t* __restrict__ dk,
+                                            bf16_t* __restrict__ dv, int64_t lddkv, float scale,
+                                            const uint32_t* __restrict__ mask, float dscale) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    int kblk, bh;
-    block_coords<false>(kblk, bh);
     const int T = (int)T_, b = bh / H, hh = bh % H;
     const int K0 = kblk * 128, kq = K0 + 32 * wave;
     const bool act = kq < T;
@@ -686,6 +701,28 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, con
     store_rows(dv + (boff + key) * lddkv + hh * 64, dva, DROP ? dscale : 1.f, lane);
 }
 
+// pairs of 128-key blocks per workgroup (x, then nk - 1 - x): uniform causal work per workgroup
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, const bf16_t* __restrict__ q,
+                                                          const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                                                          int64_t ld, const bf16_t* __restrict__ dout, int64_t ldd,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ delta, bf16_t* __restrict__ dk,
+                                                          bf16_t* __restrict__ dv, int64_t lddkv, float scale,
+                                                          const uint32_t* __restrict__ mask, float dscale) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * KV_STAGE];
+    int x, bh;
+    block_coords<false>(x, bh);
+    const int nk = (int)((T_ + 127) / 128), second = nk - 1 - x;
+    const int npass = x == second ? 1 : 2;
+#pragma unroll 1
+    for (int pass = 0; pass < npass; ++pass) {
+        if (pass) __syncthreads();
+        dkdv_kblock<DROP>(pass ? second : x, bh, smem, T_, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
+                          mask, dscale);
+    }
+}
+
 }  // namespace
 
 namespace attn {
@@ -700,7 +737,7 @@ void launch_fwd_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* 
 void launch_dq_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                    const bf16_t* o, int64_t ldo, const bf16_t* dout, int64_t ldd, const float* lse, float* delta,
                    bf16_t* dq, int64_t lddq, float scale, const DropArgs& d, hipStream_t st) {
-    const dim3 grid(ceil_div(T, 256), (unsigned)(B * H));
+    const dim3 grid((unsigned)((ceil_div(T, 256) + 1) / 2), (unsigned)(B * H));
     if (d.mask)
         k_attn_dq_d64<true><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
                                                   d.mask, d.dscale);
@@ -711,7 +748,7 @@ void launch_dq_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k
 void launch_dkdv_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                      const bf16_t* dout, int64_t ldd, const float* lse, const float* delta, bf16_t* dk, bf16_t* dv,
                      int64_t lddkv, float scale, const DropArgs& d, hipStream_t st) {
-    const dim3 grid(ceil_div(T, 128), (unsigned)(B * H));
+    const dim3 grid((unsigned)((ceil_div(T, 128) + 1) / 2), (unsigned)(B * H));
     if (d.mask)
         k_attn_dkdv_d64<true><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
                                                     d.mask_bwd, d.dscale);
