@@ -138,7 +138,19 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ x, con
     }
 }
 
-constexpr int LN_BWD_ROWS = 64;   // rows per block in the backward
+// Backward rows per block: sized so the grid has ~512 blocks (2 per CU) at any token count, 8..256,
+// a multiple of the 8 waves.  The per-block column partials (dgamma, dbeta, consumer bias) are
+// [nblk][NP*C]: 512 x 2304 floats at C4.
+constexpr int LN_BWD_WAVES = 8;
+__host__ __device__ __forceinline__ int ln_bwd_rpb(int64_t rows) {
+    int64_t r = rows / 512;
+    r = r < 8 ? 8 : (r > 256 ? 256 : r);
+    return (int)((r + 7) / 8 * 8);
+}
+__host__ __device__ __forceinline__ int64_t ln_bwd_blocks(int64_t rows) {
+    const int rpb = ln_bwd_rpb(rows);
+    return (rows + rpb - 1) / rpb;
+}
 
 // The consumer-side extras of the backward (the residual-stream gradient dx feeds the previous
 // sublayer's backward, GPT1.py:163-164): a bf16 copy of it with that sublayer's dropout applied
@@ -156,26 +168,30 @@ struct LnLp {
     int csum;                // 1: column sums of the copy into part columns [2C, 3C)
 };
 
-// One wave per row, RPW rows per wave with every load of the wave's rows issued before any
-// reduction (the previous loop waited a full load latency per row); row in registers as in the
-// forward.  Partials [block][NP*C]: dgamma, dbeta (+ consumer bias column sums).
-// Measured: holding 64/WAVES rows per wave (all loads issued up front) spilled 328 VGPRs at C=768
-// (436 B/lane scratch, 1.3 TB/s); now each wave walks its rows RPW at a time, so the in-flight rows
-// plus the column partials fit the 128-register budget of 4 waves/SIMD.
-template <int VEC, int NJ, typename TDY, int WAVES, int RPW>
-__global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ dy, const float* __restrict__ x,
-                                                const float* __restrict__ w, const float* __restrict__ mean,
-                                                const float* __restrict__ rstd, const float* __restrict__ dres,
-                                                float* __restrict__ dx, LnLp lp, float* __restrict__ part,
-                                                int64_t rows, int C) {
-    constexpr int ITER = LN_BWD_ROWS / (WAVES * RPW);
-    static_assert(ITER * WAVES * RPW == LN_BWD_ROWS, "rows per block must split evenly");
-    extern __shared__ __attribute__((aligned(16))) float red[];  // [WAVES][NP][C]
+template <int VEC, int NJ>
+struct LnRow {
+    float x[NJ][VEC], d[NJ][VEC], rv[NJ][VEC];
+    float mu, rs;
+};
+
+// One wave per row, row in registers as in the forward; 8 waves per block, each walking rpb/8
+// consecutive rows.  PF: the next row's loads are issued before the current row is reduced
+// (double-buffered rows: a wave always has a row in flight while it computes -- the one-row loop
+// waited a full load latency per row and ran at 48 % of HBM at C4).  Partials [block][NP*C]:
+// dgamma, dbeta (+ consumer bias column sums), summed over the 8 waves in a fixed order.
+template <int VEC, int NJ, typename TDY, bool PF>
+__global__ __launch_bounds__(64 * LN_BWD_WAVES) void k_ln_bwd(const TDY* __restrict__ dy, const float* __restrict__ x,
+                                                           const float* __restrict__ w, const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd,
+                                                           const float* __restrict__ dres, float* __restrict__ dx,
+                                                           LnLp lp, float* __restrict__ part, int64_t rows, int C) {
+    extern __shared__ __attribute__((aligned(16))) float red[];  // [4][NP*C]
     const int NP = lp.csum ? 3 : 2;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const float invC = 1.0f / (float)C;
     const uint64_t stream = lp.thr ? dropout_stream(lp.rng_call, lp.site) : 0;
+    const int rpb = ln_bwd_rpb(rows), rpw = rpb / LN_BWD_WAVES;
     float adw[NJ][VEC], adb[NJ][VEC], acs[NJ][VEC], wv[NJ][VEC];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -188,30 +204,20 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
             for (int q = 0; q < VEC; ++q) wv[j][q] = 0.f;
         }
     }
-#pragma unroll 1
-    for (int it = 0; it < ITER; ++it) {
-    const int64_t r0 = (int64_t)blockIdx.x * LN_BWD_ROWS + (it * WAVES + wave) * RPW;
-    float xv[RPW][NJ][VEC], d[RPW][NJ][VEC], rv[RPW][NJ][VEC];
-    float mu[RPW], rs[RPW];
-#pragma unroll
-    for (int i = 0; i < RPW; ++i) {
-        const int64_t r = r0 + i < rows ? r0 + i : rows - 1;
-        mu[i] = mean[r];
-        rs[i] = rstd[r];
+    auto load = [&](int64_t r, LnRow<VEC, NJ>& b) {
+        b.mu = mean[r];
+        b.rs = rstd[r];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int e = (j * 64 + lane) * VEC;
             if (e < C) {
-                VecIO<VEC>::ld(x + r * C + e, xv[i][j]);
-                ld_vec_any<TDY>(dy + r * C + e, d[i][j], VEC);
-                if (dres) VecIO<VEC>::ld(dres + r * C + e, rv[i][j]);
+                VecIO<VEC>::ld(x + r * C + e, b.x[j]);
+                ld_vec_any<TDY>(dy + r * C + e, b.d[j], VEC);
+                if (dres) VecIO<VEC>::ld(dres + r * C + e, b.rv[j]);
             }
         }
-    }
-#pragma unroll
-    for (int i = 0; i < RPW; ++i) {
-        const int64_t r = r0 + i;
-        if (r >= rows) break;
+    };
+    auto process = [&](int64_t r, const LnRow<VEC, NJ>& b) {
         float xh[NJ][VEC], g[NJ][VEC];
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -220,12 +226,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
             if (e < C) {
 #pragma unroll
                 for (int q = 0; q < VEC; ++q) {
-                    xh[j][q] = (xv[i][j][q] - mu[i]) * rs[i];
-                    g[j][q] = d[i][j][q] * wv[j][q];
+                    xh[j][q] = (b.x[j][q] - b.mu) * b.rs;
+                    g[j][q] = b.d[j][q] * wv[j][q];
                     s1 += g[j][q];
                     s2 += g[j][q] * xh[j][q];
-                    adw[j][q] += d[i][j][q] * xh[j][q];
-                    adb[j][q] += d[i][j][q];
+                    adw[j][q] += b.d[j][q] * xh[j][q];
+                    adb[j][q] += b.d[j][q];
                 }
             }
         }
@@ -238,8 +244,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
                 float o[VEC];
 #pragma unroll
                 for (int q = 0; q < VEC; ++q) {
-                    o[q] = rs[i] * (g[j][q] - c1 - xh[j][q] * c2);
-                    if (dres) o[q] += rv[i][j][q];
+                    o[q] = b.rs * (g[j][q] - c1 - xh[j][q] * c2);
+                    if (dres) o[q] += b.rv[j][q];
                 }
                 VecIO<VEC>::st(dx + r * C + e, o);
                 if (lp.out) {
@@ -263,28 +269,51 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
                 }
             }
         }
-    }
-    }  // it
-    // block reduction of the column partials in a fixed wave order
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-        const int e = (j * 64 + lane) * VEC;
-        if (e < C) {
-#pragma unroll
-            for (int q = 0; q < VEC; ++q) {
-                red[(wave * NP + 0) * C + e + q] = adw[j][q];
-                red[(wave * NP + 1) * C + e + q] = adb[j][q];
-                if (NP == 3) red[(wave * NP + 2) * C + e + q] = acs[j][q];
-            }
+    };
+    const int64_t r0 = (int64_t)blockIdx.x * rpb + (int64_t)wave * rpw;
+    const int n = (int)(r0 < rows ? (rows - r0 < rpw ? rows - r0 : rpw) : 0);
+    if (PF) {
+        LnRow<VEC, NJ> A, B;
+        if (n > 0) load(r0, A);
+#pragma unroll 1
+        for (int i = 0; i < n; i += 2) {
+            if (i + 1 < n) load(r0 + i + 1, B);
+            process(r0 + i, A);
+            if (i + 1 >= n) break;
+            if (i + 2 < n) load(r0 + i + 2, A);
+            process(r0 + i + 1, B);
+        }
+    } else {
+#pragma unroll 1
+        for (int i = 0; i < n; ++i) {
+            LnRow<VEC, NJ> A;
+            load(r0 + i, A);
+            process(r0 + i, A);
         }
     }
+    // column partials of the block: waves w and w + 4 pairwise, then waves 0..3 in order
+    const int NC = NP * C;
+    auto put = [&](bool add) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int e = (j * 64 + lane) * VEC;
+            if (e < C) {
+                float* dst = red + (wave & 3) * NC + e;
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) {
+                    dst[q] = add ? dst[q] + adw[j][q] : adw[j][q];
+                    dst[C + q] = add ? dst[C + q] + adb[j][q] : adb[j][q];
+                    if (NP == 3) dst[2 * C + q] = add ? dst[2 * C + q] + acs[j][q] : acs[j][q];
+                }
+            }
+        }
+    };
+    if (wave >= 4) put(false);
     __syncthreads();
-    for (int c = threadIdx.x; c < NP * C; c += blockDim.x) {
-        const int which = c / C, e = c % C;
-        float s = 0.f;
-        for (int wv2 = 0; wv2 < WAVES; ++wv2) s += red[(wv2 * NP + which) * C + e];
-        part[(int64_t)blockIdx.x * NP * C + c] = s;
-    }
+    if (wave < 4) put(true);
+    __syncthreads();
+    for (int c = threadIdx.x; c < NC; c += blockDim.x)
+        part[(int64_t)blockIdx.x * NC + c] = ((red[c] + red[NC + c]) + red[2 * NC + c]) + red[3 * NC + c];
 }
 
 namespace {
@@ -311,16 +340,17 @@ int launch_ln_bwd(const TDY* dy, const float* x, const float* w, const float* me
                   int dbias_accumulate, float* part, int64_t rows, int C, int defer, hipStream_t st) {
     const bool al16 = (((uintptr_t)x | (uintptr_t)w | (uintptr_t)dx | (uintptr_t)(dres ? dres : x)) & 15) == 0 &&
                       (((uintptr_t)dy) & 7) == 0 && (((uintptr_t)(lp.out ? lp.out : (bf16_t*)x)) & 7) == 0;
-    const int64_t nblk = (rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
+    const int64_t nblk = ln_bwd_blocks(rows);
     const int NP = lp.csum ? 3 : 2;
-#define LNB(V, N, W, R)                                                                                      \
-    k_ln_bwd<V, N, TDY, W, R><<<(unsigned)nblk, 64 * W, (size_t)NP * W * C * sizeof(float), st>>>(dy, x, w, mean, rstd, \
-                                                                                             dres, dx, lp, part, rows, C)
-    if (C == 384 && al16) LNB(2, 3, 16, 2);
-    else if (C == 768 && al16) LNB(4, 3, 4, 1);
-    else if (C == 512 && al16) LNB(4, 2, 4, 1);
-    else if (C == 1024 && al16) LNB(4, 4, 4, 1);
-    else LNB(1, 32, 4, 1);
+    const size_t lds = (size_t)4 * NP * C * sizeof(float);
+#define LNB(V, N, PF)                                                                                          \
+    k_ln_bwd<V, N, TDY, PF><<<(unsigned)nblk, 64 * LN_BWD_WAVES, lds, st>>>(dy, x, w, mean, rstd, dres, dx, lp, part, \
+                                                                           rows, C)
+    if (C == 384 && al16) LNB(2, 3, true);
+    else if (C == 768 && al16) LNB(4, 3, true);
+    else if (C == 512 && al16) LNB(4, 2, true);
+    else if (C == 1024 && al16) LNB(4, 4, false);
+    else LNB(1, 16, false);   // C <= 1024
 #undef LNB
     if (!defer && (dw || db || dbias))
         launch_reduce_partials3(part, nblk, NP * C, dw, db, dbias, C, accumulate, dbias_accumulate, st);
@@ -339,7 +369,7 @@ extern "C" int cg_layernorm_fwd(const float* x, const float* w, const float* b, 
 }
 
 extern "C" int64_t cg_layernorm_bwd_workspace(int64_t rows, int64_t C) {
-    return ((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS) * 3 * C * (int64_t)sizeof(float);
+    return ln_bwd_blocks(rows) * 3 * C * (int64_t)sizeof(float);
 }
 
 static int layernorm_bwd_impl(const void* dy, int dy_dtype, const float* x, const float* w, const float* mean,
@@ -396,7 +426,7 @@ extern "C" int cg_layernorm_bwd_reduce(const void* workspace, int64_t rows, int6
     CG_REQUIRE(rows > 0 && C > 0 && C <= 1024, "cg_layernorm_bwd_reduce: need 0 < C <= 1024");
     CG_REQUIRE(!lp_colsum || lp_colsum_partials, "cg_layernorm_bwd_reduce: lp_colsum needs the colsum partials");
     if (!dw && !db && !lp_colsum) return CG_OK;
-    const int64_t nblk = (rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
+    const int64_t nblk = ln_bwd_blocks(rows);
     const int NP = lp_colsum_partials ? 3 : 2;
     launch_reduce_partials3((const float*)workspace, nblk, NP * C, dw, db, lp_colsum, C, accumulate,
                             colsum_accumulate, (hipStream_t)stream);

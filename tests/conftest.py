@@ -1,7 +1,12 @@
 import os
 import sys
 
-import pytest
+# fixed BLAS thread count: MKL's dynamic threading changes CPU float summation order under load,
+# and the lr=0.5 oracle trajectories (test_oracle_golden) amplify that past their tolerance
+os.environ.setdefault("MKL_DYNAMIC", "FALSE")
+os.environ.setdefault("OMP_DYNAMIC", "FALSE")
+
+import pytest  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
