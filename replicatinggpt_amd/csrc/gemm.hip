@@ -377,6 +377,7 @@ namespace cg {
 int g_gemm_variant = 0;
 int g_gemm_max_grid = 0;
 extern int g_attn_variant;  // attention_d64.hip
+extern int g_ln_rpb;  // layernorm.hip
 }
 
 extern "C" int cg_set_tuning(const char* key, int value) {
@@ -395,6 +396,10 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     }
     if (!strcmp(key, "attn_variant")) {
         g_attn_variant = value;
+        return CG_OK;
+    }
+    if (!strcmp(key, "ln_rpb")) {   // takes effect for workspaces sized after the call
+        g_ln_rpb = value;
         return CG_OK;
     }
     set_error("cg_set_tuning: unknown key %s", key);

@@ -142,12 +142,16 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ x, con
 // a multiple of the 8 waves.  The per-block column partials (dgamma, dbeta, consumer bias) are
 // [nblk][NP*C]: 512 x 2304 floats at C4.
 constexpr int LN_BWD_WAVES = 8;
-__host__ __device__ __forceinline__ int ln_bwd_rpb(int64_t rows) {
+namespace cg {
+int g_ln_rpb = 0;   // cg_set_tuning("ln_rpb"): rows per backward block (0 = automatic)
+}  // namespace cg
+static int ln_bwd_rpb(int64_t rows) {
+    if (g_ln_rpb > 0) return (g_ln_rpb + 7) / 8 * 8;
     int64_t r = rows / 512;
     r = r < 8 ? 8 : (r > 256 ? 256 : r);
     return (int)((r + 7) / 8 * 8);
 }
-__host__ __device__ __forceinline__ int64_t ln_bwd_blocks(int64_t rows) {
+static int64_t ln_bwd_blocks(int64_t rows) {
     const int rpb = ln_bwd_rpb(rows);
     return (rows + rpb - 1) / rpb;
 }
@@ -175,23 +179,24 @@ struct LnRow {
 };
 
 // One wave per row, row in registers as in the forward; 8 waves per block, each walking rpb/8
-// consecutive rows.  PF: the next row's loads are issued before the current row is reduced
-// (double-buffered rows: a wave always has a row in flight while it computes -- the one-row loop
-// waited a full load latency per row and ran at 48 % of HBM at C4).  Partials [block][NP*C]:
-// dgamma, dbeta (+ consumer bias column sums), summed over the 8 waves in a fixed order.
-template <int VEC, int NJ, typename TDY, bool PF>
+// consecutive rows (rpb: ln_bwd_rpb).  Partials [block][NP*C]: dgamma, dbeta (+ consumer bias
+// column sums), summed over the 8 waves in a fixed order.  Measured (tools/ln_bench.py): issuing
+// the next row's loads before reducing the current one (double-buffered rows) gained nothing at
+// C4 and lost 15-25 % at C2 (occupancy); ~4.8 TB/s at C4, 5.2 TB/s at C2 without dropout.
+template <int VEC, int NJ, typename TDY>
 __global__ __launch_bounds__(64 * LN_BWD_WAVES) void k_ln_bwd(const TDY* __restrict__ dy, const float* __restrict__ x,
                                                            const float* __restrict__ w, const float* __restrict__ mean,
                                                            const float* __restrict__ rstd,
                                                            const float* __restrict__ dres, float* __restrict__ dx,
-                                                           LnLp lp, float* __restrict__ part, int64_t rows, int C) {
+                                                           LnLp lp, float* __restrict__ part, int64_t rows, int C,
+                                                           int rpb) {
     extern __shared__ __attribute__((aligned(16))) float red[];  // [4][NP*C]
     const int NP = lp.csum ? 3 : 2;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const float invC = 1.0f / (float)C;
     const uint64_t stream = lp.thr ? dropout_stream(lp.rng_call, lp.site) : 0;
-    const int rpb = ln_bwd_rpb(rows), rpw = rpb / LN_BWD_WAVES;
+    const int rpw = rpb / LN_BWD_WAVES;
     float adw[NJ][VEC], adb[NJ][VEC], acs[NJ][VEC], wv[NJ][VEC];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -272,24 +277,11 @@ __global__ __launch_bounds__(64 * LN_BWD_WAVES) void k_ln_bwd(const TDY* __restr
     };
     const int64_t r0 = (int64_t)blockIdx.x * rpb + (int64_t)wave * rpw;
     const int n = (int)(r0 < rows ? (rows - r0 < rpw ? rows - r0 : rpw) : 0);
-    if (PF) {
-        LnRow<VEC, NJ> A, B;
-        if (n > 0) load(r0, A);
 #pragma unroll 1
-        for (int i = 0; i < n; i += 2) {
-            if (i + 1 < n) load(r0 + i + 1, B);
-            process(r0 + i, A);
-            if (i + 1 >= n) break;
-            if (i + 2 < n) load(r0 + i + 2, A);
-            process(r0 + i + 1, B);
-        }
-    } else {
-#pragma unroll 1
-        for (int i = 0; i < n; ++i) {
-            LnRow<VEC, NJ> A;
-            load(r0 + i, A);
-            process(r0 + i, A);
-        }
+    for (int i = 0; i < n; ++i) {
+        LnRow<VEC, NJ> A;
+        load(r0 + i, A);
+        process(r0 + i, A);
     }
     // column partials of the block: waves w and w + 4 pairwise, then waves 0..3 in order
     const int NC = NP * C;
@@ -343,14 +335,15 @@ int launch_ln_bwd(const TDY* dy, const float* x, const float* w, const float* me
     const int64_t nblk = ln_bwd_blocks(rows);
     const int NP = lp.csum ? 3 : 2;
     const size_t lds = (size_t)4 * NP * C * sizeof(float);
-#define LNB(V, N, PF)                                                                                          \
-    k_ln_bwd<V, N, TDY, PF><<<(unsigned)nblk, 64 * LN_BWD_WAVES, lds, st>>>(dy, x, w, mean, rstd, dres, dx, lp, part, \
-                                                                           rows, C)
-    if (C == 384 && al16) LNB(2, 3, true);
-    else if (C == 768 && al16) LNB(4, 3, true);
-    else if (C == 512 && al16) LNB(4, 2, true);
-    else if (C == 1024 && al16) LNB(4, 4, false);
-    else LNB(1, 16, false);   // C <= 1024
+    const int rpb = ln_bwd_rpb(rows);
+#define LNB(V, N)                                                                                              \
+    k_ln_bwd<V, N, TDY><<<(unsigned)nblk, 64 * LN_BWD_WAVES, lds, st>>>(dy, x, w, mean, rstd, dres, dx, lp, part, rows, \
+                                                                       C, rpb)
+    if (C == 384 && al16) LNB(2, 3);
+    else if (C == 768 && al16) LNB(4, 3);
+    else if (C == 512 && al16) LNB(4, 2);
+    else if (C == 1024 && al16) LNB(4, 4);
+    else LNB(1, 16);   // C <= 1024
 #undef LNB
     if (!defer && (dw || db || dbias))
         launch_reduce_partials3(part, nblk, NP * C, dw, db, dbias, C, accumulate, dbias_accumulate, st);
