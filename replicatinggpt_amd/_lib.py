@@ -10,7 +10,7 @@ import re
 import torch  # noqa: F401  -- load torch's HIP runtime first so the library binds to the same one
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcharpt_hip.so")
+LIB_PATH = os.environ.get("CHARPT_LIB") or os.path.join(_HERE, "libcharpt_hip.so")   # CHARPT_LIB: A/B builds
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "charpt.h")
 
 CG_F32, CG_BF16 = 0, 1

@@ -431,8 +431,8 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
                                                 (const bf16_t*)B, ldb, C, c_dtype, ldc, e, split_k,
                                                 (float*)workspace, st)) {
     } else if (e.colpart) {
-        set_error("cg_gemm: colpart needs the 128x128 persistent bf16 kernel (bf16, NT/NN, beta 0, split 1, "
-                  "M %% 128 == 0, default dispatch)");
+        set_error("cg_gemm: colpart needs a persistent bf16 kernel (bf16 operands and output, NT/NN, beta 0, "
+                  "split 1, M %% 128 == 0, default dispatch)");
         return CG_EINVAL;
     } else if (op_dtype == CG_BF16) {
         launch_generic<bf16_t, bf16_t>(a_trans, b_trans, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k,

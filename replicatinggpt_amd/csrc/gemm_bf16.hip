@@ -191,9 +191,11 @@ static bool fast_shape_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t 
     return N % 128 == 0 && K % (FBK * split_k) == 0 && M % 128 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0;
 }
 
-// only the 128x128 persistent kernel's per-item ReLU-backward epilogue (not its pk_flags bit-1
-// per-fragment form) writes column partials
-static bool colpart_ok(int v, int at, int split_k) { return v == 9 && !(g_pk_flags & 2) && split_k == 1 && !at; }
+// column partials come from the 128x128 persistent kernel's per-item ReLU-backward epilogue (not its
+// pk_flags bit-1 per-fragment form) and from the 8-wave 256x256 persistent kernel
+static bool colpart_ok(int v, int at, int split_k) {
+    return (v == 24 || (v == 9 && !(g_pk_flags & 2))) && split_k == 1 && !at;
+}
 
 bool gemm_colpart_supported(int at, int bt, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc) {
     (void)bt;
@@ -209,7 +211,8 @@ bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf1
     if (e.resid && ((((uintptr_t)e.resid) & 15) || e.ld_resid % 4)) return false;
     if (e.aux && ((((uintptr_t)e.aux) & 15) || e.ld_aux % 8)) return false;
     int v = pick_variant(at, M, N, split_k);
-    if (e.colpart && (!colpart_ok(v, at, split_k) || e.kind != CG_EPI_RELU_BWD || e.aux_dtype != CG_BF16 || e.beta != 0.f))
+    if (e.colpart && (!colpart_ok(v, at, split_k) || e.kind != CG_EPI_RELU_BWD || e.aux_dtype != CG_BF16 ||
+                      e.beta != 0.f || c_dtype != CG_BF16))
         return false;
     if (v >= 20 && p8_gemm_launch(v, at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st))
         return true;

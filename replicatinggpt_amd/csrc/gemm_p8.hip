@@ -72,8 +72,9 @@ struct Geo8 {
     static constexpr int OCC = LDS <= 80 * 1024 ? 2 : 1;  // resident blocks per CU (LDS-bound)
 };
 
-// WM = waves along M (8 / WM along N); per-wave tile (BM/WM) x (BN/(8/WM)) in 16x16 fragments
-template <bool AT, bool BT, int BM, int BN, int WM, int NBUF>
+// WM = waves along M (8 / WM along N); per-wave tile (BM/WM) x (BN/(8/WM)) in 16x16 fragments.
+// COLPART: the ReLU-backward epilogue with fused bias-gradient column partials (bf16 output)
+template <bool AT, bool BT, int BM, int BN, int WM, int NBUF, bool COLPART>
 __global__ __launch_bounds__(P8_THREADS, (Geo8<BM, BN, NBUF>::OCC))
 void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
                const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype, int64_t ldc,
@@ -221,17 +222,65 @@ void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
             int sp;
             decode(cj, m0, n0, sp);
             const int64_t mr = m0 + wm * (BM / WM) + (lane & 15), nc = n0 + wn * (BN / WN) + 4 * (lane >> 4);
+            if (COLPART) {
+                // ReLU backward (bf16 ReLU output as the mask, beta 0: checked on the host) with the
+                // consumer's bias gradient fused: column sums of the bf16-rounded outputs per 64-row
+                // block (the layout of k_gemm_pk's colpart), 4 rows per lane then a butterfly over the
+                // column group's 16 lanes.  The partial stores go before the item's FM x FN output
+                // stores, which stay the youngest EPI_OPS vector-memory operations.
 #pragma unroll
-            for (int i = 0; i < FM; ++i)
+                for (int i = 0; i < FM; ++i)
 #pragma unroll
-                for (int j = 0; j < FN; ++j) {
-                    const int64_t m = mr + 16 * i, n = nc + 16 * j;
-                    if (split_k > 1)
-                        *(fv4*)(ws + ((int64_t)sp * M + m) * N + n) = acc[i][j];
-                    else
-                        epi_store4(acc[i][j], m, n, N, Cv, c_dtype, ldc, epi, stream);
-                    acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
+                    for (int j = 0; j < FN; ++j) {
+                        const uint2 h = *(const uint2*)((const bf16_t*)epi.aux + (mr + 16 * i) * epi.ld_aux + nc + 16 * j);
+                        fv4& v = acc[i][j];
+                        v[0] = bf2f(f2bf(__uint_as_float(h.x << 16) > 0.f ? v[0] : 0.f));
+                        v[1] = bf2f(f2bf(__uint_as_float(h.x & 0xffff0000u) > 0.f ? v[1] : 0.f));
+                        v[2] = bf2f(f2bf(__uint_as_float(h.y << 16) > 0.f ? v[2] : 0.f));
+                        v[3] = bf2f(f2bf(__uint_as_float(h.y & 0xffff0000u) > 0.f ? v[3] : 0.f));
+                    }
+#pragma unroll
+                for (int ib = 0; ib < FM / 4; ++ib) {
+                    float* cp = epi.colpart + ((mr - (lane & 15) + 64 * ib) >> 6) * N + nc;
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) {
+                        fv4 t;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            float sum = ((acc[4 * ib][j][q] + acc[4 * ib + 1][j][q]) + acc[4 * ib + 2][j][q]) +
+                                        acc[4 * ib + 3][j][q];
+                            sum += __shfl_xor(sum, 1);
+                            sum += __shfl_xor(sum, 2);
+                            sum += __shfl_xor(sum, 4);
+                            sum += __shfl_xor(sum, 8);
+                            t[q] = sum;
+                        }
+                        if ((lane & 15) == 0) *(fv4*)(cp + 16 * j) = t;
+                    }
                 }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) {
+                        const fv4& v = acc[i][j];
+                        *(uint2*)((bf16_t*)Cv + (mr + 16 * i) * ldc + nc + 16 * j) =
+                            make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+                        acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
+                    }
+            } else {
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) {
+                        const int64_t m = mr + 16 * i, n = nc + 16 * j;
+                        if (split_k > 1)
+                            *(fv4*)(ws + ((int64_t)sp * M + m) * N + n) = acc[i][j];
+                        else
+                            epi_store4(acc[i][j], m, n, N, Cv, c_dtype, ldc, epi, stream);
+                        acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
+                    }
+            }
             ckt = 0;
             ++cj;
             stored = true;
@@ -261,13 +310,16 @@ void launch8(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, i
     int64_t slots = (int64_t)cu_count8() * occ;
     if (g_gemm_max_grid > 0 && g_gemm_max_grid < slots) slots = g_gemm_max_grid;
     const unsigned grid = (unsigned)(nitems < slots ? nitems : slots);
-#define FG(AT_, BT_)                                                                                     \
-    k_gemm_p8<AT_, BT_, BM, BN, WM, NBUF><<<grid, P8_THREADS, G::LDS, st>>>(M, N, K, A, lda, B, ldb, C, c_dtype, \
-                                                                            ldc, e, split_k, kchunk, ws)
-    if (!at && !bt) FG(false, false);
-    else if (!at && bt) FG(false, true);
-    else if (at && !bt) FG(true, false);
-    else FG(true, true);
+#define FG(AT_, BT_, CP_)                                                                                \
+    k_gemm_p8<AT_, BT_, BM, BN, WM, NBUF, CP_><<<grid, P8_THREADS, G::LDS, st>>>(M, N, K, A, lda, B, ldb, C,     \
+                                                                                 c_dtype, ldc, e, split_k, kchunk, ws)
+    if (e.colpart) {   // non-transposed A, split 1, RELU_BWD with bf16 aux and output (host-checked)
+        if (!bt) FG(false, false, true);
+        else FG(false, true, true);
+    } else if (!at && !bt) FG(false, false, false);
+    else if (!at && bt) FG(false, true, false);
+    else if (at && !bt) FG(true, false, false);
+    else FG(true, true, false);
 #undef FG
 }
 

@@ -125,11 +125,13 @@ def test_layernorm_bwd_rows_then_reduce_is_bitwise_ex(C, with_link):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("M,F,K", [(512, 384, 128), (1024, 1536, 384), (16384, 1536, 384)])
+@pytest.mark.parametrize("M,F,K", [(512, 384, 128), (1024, 1536, 384), (16384, 1536, 384), (32768, 3072, 768),
+                                   (65536, 3072, 768)])
 def test_relu_bwd_colpart_matches_colsum(M, F, K):
     """The ReLU-backward dgrad with fused column partials (cg_epilogue_t.colpart): the output is
     bitwise the plain relu_bwd GEMM's, and the folded partials equal the column sums of that bf16
-    output (the values cg_colsum and the W1 weight gradient see) to 1e-5 relative."""
+    output (the values cg_colsum and the W1 weight gradient see) to 1e-5 relative.  The last two
+    shapes (C4's FFN2 dgrad and half of it) run the 8-wave 256x256 kernel, the others the 128x128."""
     O = ops()
     torch.manual_seed(5)
     dy = torch.randn(M, K, device=DEV).to(torch.bfloat16)
