@@ -89,10 +89,7 @@ __device__ __forceinline__ uint32_t keep_mask(uint32_t w, int bit) {
     asm("" : "+v"(m));
     return m;
 }
-// x & keep mask.  The keep word passes through an empty asm tied to x first, so the v_bfe_i32 is
-// issued beside its use, not hoisted (32 mask VGPRs live at once) to the start of the tile.
 __device__ __forceinline__ float keep_and(uint32_t w, int bit, float x) {
-    asm("" : "+v"(w) : "v"(x));
     return __uint_as_float(__float_as_uint(x) & keep_mask(w, bit));
 }
 
@@ -193,15 +190,27 @@ __device__ __forceinline__ void qk_tile(fv16 (&s)[2], const char* Ki, const char
 // max over this lane's 32 scores (two interleaved v_max3 chains: a 2-input fmaxf of raw MFMA
 // results would be preceded by canonicalising v_max x, x on each input), then over the lane^32
 // partner (v_permlane32_swap: no LDS round trip)
+template <int NSUB = 2>
 __device__ __forceinline__ float tile_max(const fv16 (&s)[2]) {
-    float m0 = fmaxf(fmaxf(s[0][0], s[0][1]), s[0][2]), m1 = fmaxf(fmaxf(s[1][0], s[1][1]), s[1][2]);
+    float m;
+    if (NSUB == 2) {
+        float m0 = fmaxf(fmaxf(s[0][0], s[0][1]), s[0][2]), m1 = fmaxf(fmaxf(s[1][0], s[1][1]), s[1][2]);
 #pragma unroll
-    for (int r = 3; r < 15; r += 2) {
-        m0 = fmaxf(fmaxf(m0, s[0][r]), s[0][r + 1]);
-        m1 = fmaxf(fmaxf(m1, s[1][r]), s[1][r + 1]);
+        for (int r = 3; r < 15; r += 2) {
+            m0 = fmaxf(fmaxf(m0, s[0][r]), s[0][r + 1]);
+            m1 = fmaxf(fmaxf(m1, s[1][r]), s[1][r + 1]);
+        }
+        m0 = fmaxf(fmaxf(m0, s[0][15]), s[1][15]);
+        m = fmaxf(m0, m1);
+    } else {
+        float m0 = fmaxf(fmaxf(s[0][0], s[0][1]), s[0][2]), m1 = fmaxf(fmaxf(s[0][3], s[0][4]), s[0][5]);
+#pragma unroll
+        for (int r = 6; r < 14; r += 4) {
+            m0 = fmaxf(fmaxf(m0, s[0][r]), s[0][r + 1]);
+            m1 = fmaxf(fmaxf(m1, s[0][r + 2]), s[0][r + 3]);
+        }
+        m = fmaxf(fmaxf(m0, s[0][14]), fmaxf(m1, s[0][15]));
     }
-    m0 = fmaxf(fmaxf(m0, s[0][15]), s[1][15]);
-    const float m = fmaxf(m0, m1);
     const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
     return __builtin_amdgcn_fmed3f(__uint_as_float(sw[0]), __uint_as_float(sw[1]), INFINITY);   // max, no re-canonicalising
 }
@@ -221,13 +230,13 @@ __device__ __forceinline__ void rescale_if(float mt, float& m_run, float& l_run,
 
 // P = exp2(S scale_log2 - m) of a full tile: row sums (four partial sums) into l_run, dropout keep
 // bits applied, packed to the bf16 B operands of O^T += V^T P^T
-template <bool DROP>
+template <bool DROP, int NSUB = 2>
 __device__ __forceinline__ void softmax_pack(fv16 (&s)[2], float scale_log2, float m_run, float& l_run, uint32_t mw,
                                              sv8 (&pf)[2][2]) {
     const float mneg = -m_run;
     float ls[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+    for (int kt = 0; kt < NSUB; ++kt) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             // raw v_exp_f32: weights below 2^-126 of the stale max flush to 0
@@ -241,15 +250,39 @@ __device__ __forceinline__ void softmax_pack(fv16 (&s)[2], float scale_log2, flo
     l_run += (ls[0] + ls[1]) + (ls[2] + ls[3]);
 }
 
-// O^T += V^T P^T over a full 64-key tile (two independent chains, one per 32-dim half)
+// O^T += V^T P^T over a 64-key tile's NSUB live subtiles (two independent chains, one per 32-dim half)
+template <int NSUB = 2>
 __device__ __forceinline__ void pv_tile(fv16 (&o)[2], const char* Vi, const sv8 (&pf)[2][2], int lane) {
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+    for (int kt = 0; kt < NSUB; ++kt)
 #pragma unroll
         for (int sk = 0; sk < 2; ++sk) {
             o[0] = mfma32(frag_tr(Vi, 32 * kt, sk, 0, lane), pf[kt][sk], o[0]);
             o[1] = mfma32(frag_tr(Vi, 32 * kt, sk, 32, lane), pf[kt][sk], o[1]);
         }
+}
+
+// One query group's 64-key tile outside the pipeline: NSUB live 32-key subtiles (1 when the second
+// lies wholly above the diagonal); DIAG = the subtile holding the diagonal (-1: none) -- the only
+// one masked.  Straight-line code per case (the merged form copied accumulators between paths).
+template <bool DROP, int NSUB, int DIAG>
+__device__ __forceinline__ void fwd_group_tile(const char* Ki, const char* Vi, const char* Qimg, int qr, int lane,
+                                               float scale_log2, float& m_run, float& l_run, fv16 (&o)[2],
+                                               uint32_t mw) {
+    fv16 s[2];
+    s[0] = fv16{};
+    s[1] = fv16{};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        const sv8 qf = frag_row(Qimg, qr, ks, lane);
+        s[0] = mfma32(frag_row(Ki, 0, ks, lane), qf, s[0]);
+        if (NSUB == 2) s[1] = mfma32(frag_row(Ki, 32, ks, lane), qf, s[1]);
+    }
+    if (DIAG >= 0) mask_upper(s[DIAG], lane & 31, 0, lane, -INFINITY);   // key0 = the group's first query
+    rescale_if(tile_max<NSUB>(s) * scale_log2, m_run, l_run, o);
+    sv8 pf[2][2];
+    softmax_pack<DROP, NSUB>(s, scale_log2, m_run, l_run, mw, pf);
+    pv_tile<NSUB>(o, Vi, pf, lane);
 }
 
 // Forward.  Tiles where both of a wave's query groups (A = 7 - w, B = w) are full (before B's
@@ -383,33 +416,15 @@ __device__ __forceinline__ void fwd_qblock(int qblk, int bh, char* smem, int64_t
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
             if (!act[g] || k0 > qg[g] + 31) continue;
-            const bool live1 = k0 + 32 <= qg[g] + 31;   // second 32-key subtile not fully masked
-            fv16 s[2] = {fv16{}, fv16{}};
-#pragma unroll
-            for (int kt = 0; kt < 2; ++kt) {
-                if (kt == 1 && !live1) break;
-#pragma unroll
-                for (int ks = 0; ks < 4; ++ks)
-                    s[kt] = mfma32(frag_row(Ki, 32 * kt, ks, lane), frag_row(Qimg, qr[g], ks, lane), s[kt]);
-            }
-            const int qa = qg[g] + (lane & 31);
-            if (__builtin_amdgcn_readfirstlane(k0 + 63 > qg[g])) {   // diagonal tile: causal mask
-                mask_upper(s[0], qa, k0, lane, -INFINITY);
-                mask_upper(s[1], qa, k0 + 32, lane, -INFINITY);
-            }
-            if (!live1) s[1] = fv16{} - INFINITY;
-            rescale_if(tile_max(s) * scale_log2, m_run[g], l_run[g], oacc[g]);
-            sv8 pf[2][2];
-            softmax_pack<DROP>(s, scale_log2, m_run[g], l_run[g], mw[g], pf);
-#pragma unroll
-            for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-                for (int kt = 0; kt < 2; ++kt) {
-                    if (kt == 1 && !live1) break;
-#pragma unroll
-                    for (int sk = 0; sk < 2; ++sk)
-                        oacc[g][dt] = mfma32(frag_tr(Vi, 32 * kt, sk, 32 * dt, lane), pf[kt][sk], oacc[g][dt]);
-                }
+            // qg is a multiple of 32: the tile is full (k0 + 63 < qg), has the diagonal in its second
+            // subtile (qg = k0 + 32) or in its first with the second wholly masked (qg = k0)
+            const int rel = __builtin_amdgcn_readfirstlane(qg[g] - k0);
+            if (rel >= 64)
+                fwd_group_tile<DROP, 2, -1>(Ki, Vi, Qimg, qr[g], lane, scale_log2, m_run[g], l_run[g], oacc[g], mw[g]);
+            else if (rel == 32)
+                fwd_group_tile<DROP, 2, 1>(Ki, Vi, Qimg, qr[g], lane, scale_log2, m_run[g], l_run[g], oacc[g], mw[g]);
+            else
+                fwd_group_tile<DROP, 1, 0>(Ki, Vi, Qimg, qr[g], lane, scale_log2, m_run[g], l_run[g], oacc[g], mw[g]);
         }
         advance(st, mn);
     }
