@@ -48,6 +48,11 @@ def _cpu_info():
         cores = len(os.sched_getaffinity(0))
     except AttributeError:
         cores = os.cpu_count() or 1
+    # a container's CPU quota can be far below its affinity mask (the GPU box exports the share it
+    # grants as OMP_NUM_THREADS): more threads than that only contend
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        cores = min(cores, int(omp))
     return model, cores
 
 
@@ -179,8 +184,13 @@ def _time_ms(fn, reps=20):
 def kernel_census(cfg, Bsz, T, dev):
     """The non-GEMM kernels of the step at the step's shapes, each against its roofline (north_star:
     MFMA utilisation for attention, achieved HBM GB/s for the norm / optimizer kernels):
-      attention fwd (incl. the Philox keep-bit kernel) / bwd: causal algorithmic FLOPs
-        fwd 4*B*H*(T(T+1)/2)*D, bwd 2x fwd (S recompute not counted) vs the bf16 MFMA peak;
+      attention fwd (on premade keep bits: the Philox keep-bit kernel runs on the side stream at the
+        start of the forward, overlapped with the embedding / LN / QKV kernels, and is reported on its
+        own as attention_dropmask, VALU-bound decisions/s) / bwd: causal algorithmic FLOPs
+        fwd 4*B*H*(T(T+1)/2)*D, bwd 2x fwd (S recompute not counted) vs the bf16 MFMA peak, and their
+        algorithmic HBM bytes (fwd: q,k,v read + o written + lse + FWD keep words; bwd: q,k,v,o,dO
+        read + dq,dk,dv written + lse, delta + both keep-word halves) vs the HBM peak -- at T = 256
+        the attention kernels are memory/latency-bound (DESIGN §4);
       LayerNorm fwd: M*C*(4 read + 2 write) B; LayerNorm bwd (dy bf16, x, residual grad, dx, the
         consumer's dropout-applied bf16 copy): M*C*(2+4+4+4+2) B; AdamW: 30 B/param (p, g, m, v
         fp32 + bf16 shadow) -- vs HBM peak."""
@@ -194,18 +204,30 @@ def kernel_census(cfg, Bsz, T, dev):
     do = torch.randn(M, C, device=dev).to(torch.bfloat16)
     call = torch.zeros(1, dtype=torch.int64, device=dev)
     scale = C ** -0.5
-    st = {}
-
-    def fwd():
-        st["lse"], st["mask"] = Fn.attention_fwd(qkv, Bsz, T, H, D, o, scale, p, 1, call, 0)
-    t_f = _time_ms(fwd)
-    t_b = _time_ms(lambda: Fn.attention_bwd(qkv, Bsz, T, H, D, o, do, st["lse"], scale, p, 1, call, 0, st["mask"]))
+    mbytes = ops.attn_mask_bytes(Bsz, H, T) if p > 0 else 0
+    mask = torch.empty(max(mbytes, 8) // 8, dtype=torch.int64, device=dev)
+    lse = torch.empty((Bsz, H, T), dtype=torch.float32, device=dev)
+    if p > 0:
+        t_m = _time_ms(lambda: ops.attn_dropmask(Bsz, H, T, p, 1, call, 0, mask))
+        dec = Bsz * H * T * (T + 1) / 2
+        out["attention_dropmask"] = {"ms": round(t_m, 4), "decisions": dec, "achieved": round(dec / t_m / 1e6, 1),
+                                     "unit": "G keep decisions/s (VALU-bound Philox, side stream)"}
+        ops.attn_dropmask(Bsz, H, T, p, 1, call, 0, mask)
+    t_f = _time_ms(lambda: ops.attn_fwd(qkv, Bsz, T, H, D, 0, C, 2 * C, qkv.stride(0), o, C, lse, scale, p, 1, call,
+                                        0, mask if p > 0 else None, p > 0))
+    t_b = _time_ms(lambda: Fn.attention_bwd(qkv, Bsz, T, H, D, o, do, lse, scale, p, 1, call, 0,
+                                            mask if p > 0 else None))
     fl = 4.0 * Bsz * H * (T * (T + 1) / 2) * D
-    for name, t, f in (("attention_fwd", t_f, fl), ("attention_bwd", t_b, 2 * fl)):
+    stat = Bsz * H * T * 4
+    fbytes = 4 * M * C * 2 + stat + mbytes // 2
+    bbytes = 8 * M * C * 2 + 2 * stat + mbytes
+    for name, t, f, byts in (("attention_fwd", t_f, fl, fbytes), ("attention_bwd", t_b, 2 * fl, bbytes)):
         tf = f / (t * 1e-3) / 1e12
+        gbs = byts / (t * 1e-3) / 1e9
         out[name] = {"ms": round(t, 4), "achieved": round(tf, 1), "unit": "TFLOP/s", "peak": PEAK_BF16_TFLOPS,
-                     "frac": round(tf / PEAK_BF16_TFLOPS, 4)}
-    del qkv, o, do
+                     "frac": round(tf / PEAK_BF16_TFLOPS, 4), "bytes": byts, "GB/s": round(gbs, 1),
+                     "hbm_frac": round(gbs / PEAK_HBM_GBS, 4)}
+    del qkv, o, do, mask
     x = torch.randn(M, C, device=dev)
     w, b = torch.randn(C, device=dev), torch.randn(C, device=dev)
     y = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
@@ -325,6 +347,14 @@ def bench_generate(dev, B=256, new=500):
             "checksum": ck}
 
 
+_T_START = time.perf_counter()
+
+
+def _log(msg):
+    """Progress on stderr (stdout carries only the one JSON line)."""
+    print(f"[bench {time.perf_counter() - _T_START:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -367,6 +397,7 @@ def main():
     step = TrainStep(model, opt, sampler, reducer, use_graph=not args.no_graph, seg_layers=args.seg_layers,
                      overlap=None if args.overlap is None else bool(args.overlap))
     step.capture()
+    _log("captured; warmup")
     for _ in range(args.warmup):
         step.step()
     torch.cuda.synchronize()
@@ -393,6 +424,7 @@ def main():
     mfu = value * F / (world * PEAK_BF16_TFLOPS * 1e12)
 
     result = None
+    _log(f"timed {args.steps} steps: {elapsed / args.steps * 1e3:.3f} ms/step")
     if rank == 0:
         roofline, census = None, None
         if not args.no_census:
@@ -420,11 +452,14 @@ def main():
             "roofline": roofline,
         }
         if census is not None:
+            _log("gemm census done; kernel census")
             result["gemm_census_ms"] = {c["name"]: round(c["ms"], 4) for c in census}
             result["kernel_census"] = kernel_census(cfg, Bsz, T, dev)
         if world == 1 and not args.no_generate:
+            _log("generate (C5)")
             result["generate_c5"] = bench_generate(dev)
         if world == 1 and not args.no_cpu_baseline:
+            _log("cpu baseline")
             result["cpu_baseline"] = cpu_baseline(cfg)
         print(json.dumps(result), flush=True)
     if world > 1:
