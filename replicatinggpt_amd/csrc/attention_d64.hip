@@ -89,6 +89,11 @@ __device__ __forceinline__ uint32_t keep_mask(uint32_t w, int bit) {
     asm("" : "+v"(m));
     return m;
 }
+// kept ? a : b through the keep mask: one gfx950 v_bitop3_b32 (truth table 0xe4 = s2 ? s0 : s1,
+// bitwise); the plain C form became v_and, v_xor, v_and, v_or once the mask had a second use
+__device__ __forceinline__ float keep_sel2(uint32_t m, float a, float b) {
+    return __uint_as_float(__builtin_amdgcn_bitop3_b32(__float_as_uint(a), __float_as_uint(b), m, 0xe4));
+}
 __device__ __forceinline__ float keep_and(uint32_t w, int bit, float x) {
     return __uint_as_float(__float_as_uint(x) & keep_mask(w, bit));
 }
@@ -462,7 +467,9 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, cons
 }
 
 // =====================================================================================
-// dQ: S^T = K Q^T, dP^T = V dO^T, dS^T = P^T (keep/(1-p) dP^T - delta), dQ^T += K^T dS^T
+// dQ: S^T = K Q^T, dP^T = V dO^T, dS^T = P^T (keep/(1-p) dP^T - delta), dQ^T += K^T dS^T.
+// The 1/(1-p) is factored out of dS (dS = 1/(1-p) P (keep dP - (1-p) delta), applied with scale in
+// the epilogue), so an element costs dP - delta', one v_bfi_b32 select (dropped: -delta') and P x.
 // =====================================================================================
 template <bool DROP>
 __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t T_, int H, const bf16_t* __restrict__ q,
@@ -506,7 +513,7 @@ __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t 
             }
         }
         dsum += __shfl_xor(dsum, 32, 64);
-        dl[g] = dsum;
+        dl[g] = -dsum / dscale;   // -delta' = -(1-p) delta
         lse2[g] = act[g] ? lse[(int64_t)bh * T_ + qa] * LOG2E : 0.f;
         if (act[g] && lane < 32) delta[(int64_t)bh * T_ + qa] = dsum;
     }
@@ -545,9 +552,9 @@ __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t 
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lse2[g]));
-                    float d = dp[r];
-                    if (DROP) d = keep_and(mw[g], 16 * kt + r, d * dscale);
-                    s[r] = p * (d - dl[g]);
+                    float d = dp[r] + dl[g];
+                    if (DROP) d = keep_sel2(keep_mask(mw[g], 16 * kt + r), d, dl[g]);
+                    s[r] = p * d;
                 }
                 const sv8 d0 = pack16(s, 0), d1 = pack16(s, 1);
 #pragma unroll
@@ -566,7 +573,7 @@ __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t 
     for (int g = 0; g < 2; ++g) {
         if (!act[g]) continue;
         const int64_t qa = qg[g] + (lane & 31);
-        store_rows(dq + (boff + qa) * lddq + hh * 64, dqa[g], scale, lane);
+        store_rows(dq + (boff + qa) * lddq + hh * 64, dqa[g], scale * dscale, lane);
     }
 }
 
@@ -633,7 +640,7 @@ __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_
     auto stat_load = [&](int qt) {
         float s = 0.f;
         if (tid < 64) s = lse_b[qt * 64 + tid] * LOG2E;
-        else if (tid < 128) s = del_b[qt * 64 + tid - 64];
+        else if (tid < 128) s = -del_b[qt * 64 + tid - 64] / dscale;   // -delta' = -(1-p) delta
         return s;
     };
     {
@@ -659,7 +666,17 @@ __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_
             for (int qs = 0; qs < 2; ++qs) {
                 const int q0s = q0 + 32 * qs;
                 if (q0s + 31 < kq) continue;   // every query of the subtile precedes every key
-                fv16 s = fv16{}, dp = fv16{};
+                // dP starts from -delta' of its rows (the accumulator's initial value), so the MFMA
+                // chain leaves dP - delta'; dS = 1/(1-p) P (keep dP - delta'), the 1/(1-p) in the epilogue
+                fv16 s = fv16{}, dp;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float4 d4 = *(const float4*)(st_del + 32 * qs + 8 * i + 4 * (lane >> 5));
+                    dp[4 * i] = d4.x;
+                    dp[4 * i + 1] = d4.y;
+                    dp[4 * i + 2] = d4.z;
+                    dp[4 * i + 3] = d4.w;
+                }
 #pragma unroll
                 for (int ks = 0; ks < 4; ++ks) {
                     s = mfma32(frag_row(Qi, 32 * qs, ks, lane), kf[ks], s);
@@ -684,15 +701,15 @@ __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_
                     for (int e = 0; e < 4; ++e) {
                         const int r = 4 * i + e;
                         const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lv[e]));
-                        float d = dp[r];
+                        float d = dp[r];   // dP - delta'
                         if (DROP) {
                             const uint32_t kp = keep_mask(mw, 16 * qs + r);   // 1/(1-p) of dV: epilogue
                             z[r] = __uint_as_float(__float_as_uint(p) & kp);
-                            d = __uint_as_float(__float_as_uint(d * dscale) & kp);
+                            d = keep_sel2(kp, d, dvv[e]);                     // dropped: -delta'
                         } else {
                             z[r] = p;
                         }
-                        s[r] = p * (d - dvv[e]);
+                        s[r] = p * d;
                     }
                 }
                 const sv8 z0 = pack16(z, 0), z1 = pack16(z, 1), s0 = pack16(s, 0), s1 = pack16(s, 1);
@@ -712,7 +729,7 @@ __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_
         __syncthreads();
     }
     if (!act) return;
-    store_rows(dk + (boff + key) * lddkv + hh * 64, dka, scale, lane);
+    store_rows(dk + (boff + key) * lddkv + hh * 64, dka, scale * dscale, lane);
     store_rows(dv + (boff + key) * lddkv + hh * 64, dva, DROP ? dscale : 1.f, lane);
 }
 

@@ -376,6 +376,7 @@ int launch_generic(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, co
 namespace cg {
 int g_gemm_variant = 0;
 int g_gemm_max_grid = 0;
+int g_skip_splitk_reduce = 0;  // measurement knob (WRONG results): time a step without the split-K reduce
 extern int g_attn_variant;  // attention_d64.hip
 extern int g_ln_rpb;  // layernorm.hip
 }
@@ -396,6 +397,10 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     }
     if (!strcmp(key, "attn_variant")) {
         g_attn_variant = value;
+        return CG_OK;
+    }
+    if (!strcmp(key, "skip_splitk_reduce")) {
+        g_skip_splitk_reduce = value;
         return CG_OK;
     }
     if (!strcmp(key, "ln_rpb")) {   // takes effect for workspaces sized after the call
@@ -448,7 +453,7 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
                       (((uintptr_t)C | (uintptr_t)workspace | (uintptr_t)(e.bias ? e.bias : (const float*)C) |
                         (uintptr_t)(e.resid ? e.resid : (const float*)C)) & 15) == 0 &&
                       (!e.resid || e.ld_resid % 4 == 0);
-    if (split_k > 1 && vec4) {
+    if (split_k > 1 && vec4 && !g_skip_splitk_reduce) {
         const int n4 = (int)(M * N / 4);
 #define SKR(TC_, S_)                                                                                  \
     k_splitk_reduce4<TC_, S_><<<ceil_div(n4, 256), 256, 0, st>>>((const float*)workspace, split_k, (int)M, \

@@ -74,6 +74,9 @@ SIDE = SideStream()
 LN_REDUCE_SIDE = os.environ.get("CHARPT_LN_REDUCE_SIDE", "1") != "0"
 # FFN b1 gradient fused into the ReLU-backward dgrad epilogue (CHARPT_FUSE_COLPART=0: separate colsum)
 FUSE_COLPART = os.environ.get("CHARPT_FUSE_COLPART", "1") != "0"
+# Measurement-only what-if switches (results are WRONG with any of them): CHARPT_WHATIF=skip_wgrad,
+# skip_attn, skip_lnbwd drop those kernels from the step to see how much of the step time they hold.
+WHATIF = set(filter(None, os.environ.get("CHARPT_WHATIF", "").split(",")))
 
 
 def site_stream(call, site):
@@ -228,6 +231,8 @@ def _wgrad_split(M, N, K, fast):
 
 def linear_wgrad(dy2, x2, out, beta):
     """out[N,K] (+)= dy2[M,N]^T @ x2[M,K]   (fp32, deterministic split-K)"""
+    if "skip_wgrad" in WHATIF:
+        return out
     M, N = dy2.shape
     K = x2.shape[1]
     fast = _is_bf16(dy2.dtype) and N % 128 == 0 and K % 128 == 0 and M % 64 == 0
@@ -319,7 +324,9 @@ def layernorm_bwd(dy2, x2, w_reg, b_reg, mean, rstd, dres=None, want_lp=False, l
     side = LN_REDUCE_SIDE and SIDE.enabled and dev.type == "cuda" and (gw is not None or gb is not None or gcs is not None) and \
         (gw is None or gw is w_reg.slot) and (gb is None or gb is b_reg.slot) and \
         (gcs is None or gcs is link.bias.slot)
-    if side:
+    if "skip_lnbwd" in WHATIF:
+        pass
+    elif side:
         ops.layernorm_bwd_rows(dy2, x2, w_reg.master, mean, rstd, dres, dx, lp, ws, gcs is not None, p, seed, rng,
                                site)
         with SIDE.run(dev, ws):
@@ -348,6 +355,8 @@ def attention_fwd(qkv, B, T, H, D, out, scale, p, seed, rng_call, site, premask=
         ready = True
     elif p > 0 and T % 16 == 0:
         mask = torch.empty(ops.attn_mask_bytes(B, H, T) // 8, dtype=torch.int64, device=qkv.device)
+    if "skip_attn" in WHATIF:
+        return lse, mask
     ops.attn_fwd(qkv, B, T, H, D, 0, d, 2 * d, qkv.stride(0), out, out.stride(0), lse, float(scale), float(p),
                  int(seed), rng_call, int(site), mask, ready)
     return lse, mask
@@ -362,6 +371,8 @@ def attention_bwd(qkv, B, T, H, D, o, do, lse, scale, p, seed, rng_call, site, m
     d = H * D
     dqkv = torch.empty_like(qkv)
     ws = torch.empty(ops.attn_bwd_workspace(B, T, H, D) // 4 + 1, dtype=torch.float32, device=qkv.device)
+    if "skip_attn" in WHATIF:
+        return dqkv
     ops.attn_bwd(qkv, B, T, H, D, 0, d, 2 * d, qkv.stride(0), o, o.stride(0), do, do.stride(0), lse, dqkv,
                  dqkv.stride(0), float(scale), float(p), int(seed), rng_call, int(site), mask, ws)
     return dqkv
