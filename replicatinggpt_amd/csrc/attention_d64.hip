@@ -537,18 +537,18 @@ __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t 
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
             if (!act[g] || k0 > qg[g] + 31) continue;
-            const int qa = qg[g] + (lane & 31);
-            const bool diag = __builtin_amdgcn_readfirstlane(k0 + 63 > qg[g]);
 #pragma unroll
             for (int kt = 0; kt < 2; ++kt) {
                 if (k0 + 32 * kt > qg[g] + 31) break;   // subtile fully masked
+                // only the subtile whose first key is the group's first query holds the diagonal
+                const bool diag = __builtin_amdgcn_readfirstlane(k0 + 32 * kt == qg[g]);
                 fv16 s = fv16{}, dp = fv16{};
 #pragma unroll
                 for (int ks = 0; ks < 4; ++ks) {
                     s = mfma32(frag_row(Ki, 32 * kt, ks, lane), qf[g][ks], s);
                     dp = mfma32(frag_row(Vi, 32 * kt, ks, lane), df[g][ks], dp);
                 }
-                if (diag) mask_upper(s, qa, k0 + 32 * kt, lane, -INFINITY);
+                if (diag) mask_upper(s, lane & 31, 0, lane, -INFINITY);
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lse2[g]));
