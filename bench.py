@@ -276,17 +276,18 @@ def gemm_family(census):
 
 
 def pmc_traffic(config, dom):
-    """HBM bytes per launch of the dominant op from the committed rocprofv3 PMC passes
-    (tools/pmc_gemm.py -> profiles/r1_pmc_gemm_traffic_<config>.json); None when that file does not
-    cover this exact shape and split."""
-    path = os.path.join(ROOT, "profiles", f"r1_pmc_gemm_traffic_{config}.json")
-    try:
-        op = json.load(open(path))["ops"][dom["name"]]
-    except (OSError, KeyError, ValueError):
-        return None
-    if (op["M"], op["N"], op["K"], op["split"]) != (dom["M"], dom["N"], dom["K"], dom["split"]):
-        return None
-    return op["hbm_bytes"]
+    """HBM (L2-miss) bytes per launch of the dominant op from the committed rocprofv3 PMC passes
+    (tools/pmc_gemm_traffic.sh + tools/pmc_gemm.py -> profiles/r2_pmc_gemm_traffic_<config>.json,
+    the latest round's file first); None when no file covers this exact shape and split."""
+    for rnd in ("r2", "r1"):
+        path = os.path.join(ROOT, "profiles", f"{rnd}_pmc_gemm_traffic_{config}.json")
+        try:
+            op = json.load(open(path))["ops"][dom["name"]]
+        except (OSError, KeyError, ValueError):
+            continue
+        if (op["M"], op["N"], op["K"], op["split"]) == (dom["M"], dom["N"], dom["K"], dom["split"]):
+            return op["hbm_bytes"]
+    return None
 
 
 PEAK_FP32_TFLOPS = 157.3     # MI355X f32 MFMA / vector peak (MI355X_MICROARCH.md)
