@@ -463,6 +463,8 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
         case 2: SKR(TC_, 2); break;         \
         case 4: SKR(TC_, 4); break;         \
         case 8: SKR(TC_, 8); break;         \
+        case 12: SKR(TC_, 12); break;       \
+        case 14: SKR(TC_, 14); break;       \
         case 16: SKR(TC_, 16); break;       \
         case 32: SKR(TC_, 32); break;       \
         default: SKR(TC_, 0); break;        \

@@ -188,7 +188,8 @@ static int pick_variant(int at, int64_t M, int64_t N, int split_k) {
 }
 
 static bool fast_shape_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int split_k) {
-    return N % 128 == 0 && K % (FBK * split_k) == 0 && M % 128 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0;
+    return N % 128 == 0 && K % FBK == 0 && K / FBK >= split_k && M % 128 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
+           ldc % 8 == 0;
 }
 
 // column partials come from the 128x128 persistent kernel's per-item ReLU-backward epilogue (not its
@@ -211,6 +212,12 @@ bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf1
     if (e.resid && ((((uintptr_t)e.resid) & 15) || e.ld_resid % 4)) return false;
     if (e.aux && ((((uintptr_t)e.aux) & 15) || e.ld_aux % 8)) return false;
     int v = pick_variant(at, M, N, split_k);
+    if (K % (FBK * split_k)) {
+        // uneven split-K (the last split shorter): only the 128x128 persistent kernel, and only when
+        // every split is non-empty; otherwise the generic kernels (ceil-sized chunks) take it
+        const int64_t nkt = K / FBK, nkc = (nkt + split_k - 1) / split_k;
+        if (v != 9 || (split_k - 1) * nkc >= nkt) return false;
+    }
     if (e.colpart && (!colpart_ok(v, at, split_k) || e.kind != CG_EPI_RELU_BWD || e.aux_dtype != CG_BF16 ||
                       e.beta != 0.f || c_dtype != CG_BF16))
         return false;

@@ -238,10 +238,12 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     const int tilesN = (int)(N / BN);
     const int ntiles = (int)(M / BM) * tilesN;
     const int nitems = ntiles * split_k;
-    const int nk = (int)(kchunk / FBK);
+    // split s covers K-tiles [s*nkc, min((s+1)*nkc, nkt)): the last split may be shorter (uneven
+    // split-K: any split count, not only divisors of the K-tile count)
+    const int nkt = (int)(K / FBK), nkc = (int)(kchunk / FBK);
     const int P = gridDim.x, b = blockIdx.x;
     const int my_items = b < nitems ? (nitems - 1 - b) / P + 1 : 0;
-    const int total = my_items * nk;
+    auto split_nk = [&](int sp) { return nkt - sp * nkc < nkc ? nkt - sp * nkc : nkc; };
     const uint64_t stream =
         (epi.kind == CG_EPI_BIAS_DROP_RESID && epi.thr && split_k == 1) ? dropout_stream(epi.rng_call, epi.site) : 0;
 
@@ -257,9 +259,16 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         m0 = (int64_t)(t / tilesN) * BM;
         n0 = (int64_t)(t % tilesN) * BN;
     };
+    int total = 0;
+    for (int j = 0; j < my_items; ++j) {
+        int64_t m0, n0;
+        int sp;
+        decode(j, m0, n0, sp);
+        total += split_nk(sp);
+    }
 
     // DMA issue cursor (item ij, K-tile ikt) and its operand origins
-    int ij = 0, ikt = 0;
+    int ij = 0, ikt = 0, ink = 0;   // ink: K-tiles of the DMA cursor's item
     const bf16_t* oa = A;
     const bf16_t* ob = B;
     // The in-loop DMA is split from its address bookkeeping: prep_next() (branchy: item decode at
@@ -276,13 +285,14 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
                 int64_t m0, n0;
                 int sp;
                 decode(ij, m0, n0, sp);
+                ink = split_nk(sp);
                 const int64_t kb = sp * kchunk;
                 oa = AT ? A + kb * lda + m0 : A + m0 * lda + kb;
                 ob = BT ? B + kb * ldb + n0 : B + n0 * ldb + kb;
             }
             na = oa + ikt * da.kstep;
             nbp = ob + ikt * db.kstep;
-            if (++ikt == nk) {
+            if (++ikt == ink) {
                 ikt = 0;
                 ++ij;
             }
@@ -313,6 +323,13 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     // issue order).
     constexpr int EPI_OPS = 16;
     int cur = 0, cj = 0, ckt = 0;
+    int cnk;   // K-tiles of the compute cursor's item
+    {
+        int64_t m0, n0;
+        int sp;
+        decode(0, m0, n0, sp);
+        cnk = my_items ? split_nk(sp) : 0;
+    }
     bool stored = false;
     for (int g = 0; g < total; ++g) {
         const int ahead = total - 1 - g;  // steps issued after g that may stay in flight: min(NBUF-2, ahead)
@@ -380,7 +397,7 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         }
         __builtin_amdgcn_sched_barrier(0);
         cur = cur + 1 == NBUF ? 0 : cur + 1;
-        if (++ckt == nk) {
+        if (++ckt == cnk) {
             // item done: acc[i][j][r] = C[mw + 16i + (lane&15)][nw + 16j + 4(lane>>4) + r]
             int64_t m0, n0;
             int sp;
@@ -406,6 +423,12 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
                 for (int j = 0; j < 4; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
             ckt = 0;
             ++cj;
+            if (cj < my_items) {
+                int64_t m1, n1;
+                int sp1;
+                decode(cj, m1, n1, sp1);
+                cnk = split_nk(sp1);
+            }
             stored = true;
         }
     }
@@ -428,7 +451,7 @@ void launch_p(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
               int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, float* ws,
               hipStream_t st) {
     using G = GeoP<BM, BN, NBUF>;
-    const int64_t kchunk = K / split_k;
+    const int64_t kchunk = (K / FBK + split_k - 1) / split_k * FBK;   // K-tiles per split, last one short
     const int64_t nitems = (M / BM) * (N / BN) * split_k;
     int64_t slots = (int64_t)cu_count() * G::OCC;
     if (g_gemm_max_grid > 0 && g_gemm_max_grid < slots) slots = g_gemm_max_grid;

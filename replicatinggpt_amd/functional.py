@@ -207,18 +207,21 @@ def _gemm_slots():
 
 def _wgrad_split(M, N, K, fast):
     """Split-K factor of a weight-gradient GEMM (K = tokens).  bf16 path: the persistent kernel
-    hands each resident block ceil(items / slots) items of K/split reduction depth, and every
-    split adds an fp32 slab to write and reduce, so minimise
-        ceil(tiles * split / slots) * (K / split) * (1 + split / 50)
-    -- this picks the measured best split of every C2 / C4 weight-gradient shape
-    (tools/gemm_scan2.py, profiles/r1_gemm_scan_wgrad.txt)."""
+    hands each resident block ceil(items / slots) items of ceil(K-tiles / split) reduction depth
+    (any split: the last one is shorter), and every split adds an fp32 slab to write and reduce, so
+    minimise   ceil(tiles * split / slots) * ceil(K-tiles / split) * (1 + split / 50)
+    over splits 1..32 -- e.g. 14 / 16 / 14 / 32 at C2 and 7 / 4 / 7 / 14 at C4 (FFN2, QKV, FFN1, proj),
+    within 3 % of the measured best of each (tools/gemm_scan2.py, profiles/r2_gemm_scan_wgrad_splits.txt;
+    the power-of-two splits of round 1 were up to 25 % slower)."""
     if fast:
         tiles, slots = -(-M // 128) * -(-N // 128), _gemm_slots()
+        nkt = K // 64
         best, best_cost = 1, None
-        for split in (1, 2, 4, 8, 16, 32):
-            if K % (64 * split) or K // split < 256:
-                break
-            cost = -(-tiles * split // slots) * (K / split) * (1 + split / 50)
+        for split in range(1, 33):
+            per = -(-nkt // split)
+            if (split - 1) * per >= nkt or per < 4:   # an empty last split / too little depth
+                continue
+            cost = -(-tiles * split // slots) * per * (1 + split / 50)
             if best_cost is None or cost < best_cost:
                 best, best_cost = split, cost
         return best

@@ -253,9 +253,11 @@ def test_gemm_default_picks_large_tile(bt):
     assert relerr(o, want) < 1e-5
 
 
-@pytest.mark.parametrize("split", [2, 4, 8])
+@pytest.mark.parametrize("split", [2, 4, 8, 3, 5, 12, 14, 31])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_gemm_splitk_deterministic(split, dt):
+    """Split-K weight-gradient layout (TT), deterministic run to run and equal to fp64; splits that
+    do not divide the 32 K-tiles run the persistent kernel's uneven split (last split shorter)."""
     M, N, K = 128, 256, 2048
     torch.manual_seed(2)
     A = torch.randn(K, M).to(dt).to(DEV)
@@ -270,6 +272,23 @@ def test_gemm_splitk_deterministic(split, dt):
         outs.append(out.clone())
     assert torch.equal(outs[0], outs[1])
     assert relerr(outs[0], ref) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K,split", [(384, 1536, 16384, 14), (1152, 384, 16384, 18), (384, 384, 16384, 24),
+                                         (768, 3072, 65536, 10)])
+def test_gemm_uneven_splitk_wgrad_shapes(M, N, K, split):
+    """The C2 / C4 weight-gradient shapes at uneven split counts (the persistent 128x128 kernel's
+    ceil-sized K chunks) against an fp64 product of the same bf16 operands (fp32 accumulation:
+    1e-5 relative)."""
+    torch.manual_seed(11)
+    A = (torch.randn(K, M, device=DEV) * 0.5).to(torch.bfloat16)
+    B = (torch.randn(K, N, device=DEV) * 0.5).to(torch.bfloat16)
+    out = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    ws = torch.empty(ops().gemm_workspace(M, N, split) // 4, dtype=torch.float32, device=DEV)
+    ops().gemm(A, B, out, True, True, True, M, N, K, M, N, N, 0, None, None, 0, None, 0, 0.0, 0, None, 0, 0.0, split,
+               ws)
+    ref = A.double().t() @ B.double()
+    assert relerr(out, ref) < 1e-5
 
 
 @pytest.mark.parametrize("c_dt", [torch.float32, torch.bfloat16])

@@ -3,7 +3,7 @@ forward and dgrad products x variants, weight-gradient products x variants x spl
 is a hipGraph of 20 back-to-back launches (split-K includes its reduce kernel), best of 5.  GPU
 only.
 
-usage: python tools/gemm_scan2.py [c2|c4] [fwd variants] [wgrad variants]"""
+usage: python tools/gemm_scan2.py [c2|c4] [fwd variants] [wgrad variants] [wgrad splits]"""
 import os
 import sys
 
@@ -28,6 +28,7 @@ def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
     fv = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "9,10,12,21,22,23").split(",")]
     wv = [int(v) for v in (sys.argv[3] if len(sys.argv) > 3 else "9,10,12,21,22,23").split(",")]
+    splits = [int(v) for v in (sys.argv[4] if len(sys.argv) > 4 else "1,2,4,8,16,32").split(",")]
     d, M = (384, 16384) if cfg == "c2" else (768, 65536)
     F4 = 4 * d
     lib = L.load()
@@ -48,8 +49,8 @@ def main():
         print(line, flush=True)
     wg = [("proj_wgrad", d, d, M), ("qkv_wgrad", 3 * d, d, M), ("ffn2_wgrad", d, F4, M), ("ffn1_wgrad", F4, d, M)]
     for name, m, n, k in wg:
-        for split in (1, 2, 4, 8, 16, 32):
-            if k % (64 * split):
+        for split in splits:
+            if k // 64 < split or (split - 1) * (-(-(k // 64) // split)) >= k // 64:
                 continue
             line = f"{cfg} {name:11s} M={m:6d} N={n:5d} K={k:6d} split {split:2d} |"
             for v in wv:
