@@ -526,7 +526,9 @@ __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t 
     __syncthreads();
     for (int kv = 0; kv < nkv; ++kv) {
         const int nxt = kv + 1 < nkv ? kv + 1 : kv;
+#ifndef CG_ATTN_NOSTAGE
         const Stage2 st = stage_load(kb_, ld, vb_, ld, (int64_t)nxt * 64, tid);
+#endif
         uint32_t mn[2] = {0u, 0u};
 #pragma unroll
         for (int g = 0; g < 2; ++g)
@@ -564,7 +566,9 @@ __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t 
                 }
             }
         }
+#ifndef CG_ATTN_NOSTAGE
         stage_store(st, smem + ((kv + 1) & 1) * 2 * TILE, tid);
+#endif
         mw[0] = mn[0];
         mw[1] = mn[1];
         __syncthreads();
@@ -652,7 +656,9 @@ __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_
     for (int qt = qt0; qt < nq; ++qt) {
         const int it = qt - qt0;
         const int nxt = qt + 1 < nq ? qt + 1 : qt;
+#ifndef CG_ATTN_NOSTAGE
         const Stage2 st = stage_load(qb_, ld, ob_, ldd, (int64_t)nxt * 64, tid);
+#endif
         const float sn = stat_load(nxt);
         const uint32_t mn = (DROP && act && nxt >= qtm) ? mcol[(nxt - qtm) * 64] : 0u;
         const char* S0 = smem + (it & 1) * KV_STAGE;
@@ -723,7 +729,9 @@ __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_
             }
         }
         char* D = smem + ((it + 1) & 1) * KV_STAGE;
+#ifndef CG_ATTN_NOSTAGE
         stage_store(st, D, tid);
+#endif
         if (tid < 128) ((float*)(D + 2 * TILE))[tid] = sn;
         mw = mn;
         __syncthreads();

@@ -27,15 +27,23 @@ EPI = {"store": L.EPI_STORE, "bias": L.EPI_BIAS, "bias_relu": L.EPI_BIAS_RELU, "
 
 
 class SideStream:
-    """A second HIP stream for work off the backward's critical path (weight gradients, bias column
-    sums, their split-K reductions) and for the forward's dropout keep bits.  The dgrad chain keeps
-    the main stream; these kernels overlap it (hipGraph replay keeps the fork/join as graph edges,
-    so the two branches run concurrently on the device).  Tensors read by side work are kept alive
-    until ``join()``, which makes the main stream wait for everything forked so far; the model's
-    embedding backward (the last autograd node), AdamW.step and TrainStep call it."""
+    """An optional second HIP stream for work off the backward's critical path (weight gradients,
+    bias column sums, their split-K reductions) and for the forward's dropout keep bits.  The dgrad
+    chain keeps the main stream; hipGraph replay keeps the fork/join as graph edges, so the two
+    branches can run concurrently.  Tensors read by side work are kept alive until ``join()``,
+    which makes the main stream wait for everything forked so far; the model's embedding backward
+    (the last autograd node), AdamW.step and TrainStep call it.
+
+    OFF by default: measured on MI355X (profiles/r2_side_stream_ab.txt) the graph spreads the two
+    branches over hardware queues and every cross-queue edge costs ~10-20 us of idle GPU, more than
+    the overlap buys -- one stream is as fast or up to 1.7 % faster at C2 (GPU 100 % busy, 17 us idle per step) and
+    4.3 % faster at C4.  CHARPT_SIDE: "1" all of the above on the side stream, "mask" only the keep
+    bits, "0" (default) one stream."""
 
     def __init__(self):
-        self.enabled = True
+        mode = os.environ.get("CHARPT_SIDE", "0")
+        self.enabled = mode == "1"
+        self.premask = mode in ("1", "mask")
         self._streams = {}
         self._keep = []
         self._pending = set()

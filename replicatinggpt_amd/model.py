@@ -455,7 +455,7 @@ class BigramLanguageModel(nn.Module):
             ops.rng_snapshot(self._rng_counter, snap)
             self._fwd_rng = snap
             hs = cfg.n_embd // cfg.n_head
-            if Fn.SIDE.enabled and Fn.premask_ok(act, T, hs) and self.blocks[0].sa_heads.heads[0].dropout.p > 0:
+            if Fn.SIDE.premask and Fn.premask_ok(act, T, hs) and self.blocks[0].sa_heads.heads[0].dropout.p > 0:
                 self._launch_premasks(idx.device, B, T)
         try:
             wte, wpe = R["wte"], R["wpe"]

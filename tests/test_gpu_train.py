@@ -53,6 +53,31 @@ def test_capture_rollback_matches_eager():
     assert torch.equal(runs[0][1], runs[1][1])
 
 
+def test_side_stream_modes_bit_identical():
+    """The side stream (weight gradients, column sums and keep bits forked off the dgrad chain) only
+    changes scheduling: graph-replayed steps with it on, keep-bits-only and off give the same losses
+    and weights bit for bit (functional.SideStream; CHARPT_SIDE picks the default, off)."""
+    from replicatinggpt_amd import functional as Fn
+    from replicatinggpt_amd.engine import TrainStep
+    cfg = _cfg()
+    runs = []
+    saved = (Fn.SIDE.enabled, Fn.SIDE.premask)
+    try:
+        for mode in ((False, False), (False, True), (True, True)):
+            Fn.SIDE.enabled, Fn.SIDE.premask = mode
+            m, opt, s = _setup(cfg)
+            st = TrainStep(m, opt, s, use_graph=True)
+            st.capture(restore=True)
+            losses = [float(st.step().detach()) for _ in range(3)]
+            torch.cuda.synchronize()
+            runs.append((losses, m.flat.master.detach().cpu().clone()))
+    finally:
+        Fn.SIDE.enabled, Fn.SIDE.premask = saved
+    for r in runs[1:]:
+        assert r[0] == runs[0][0]
+        assert torch.equal(r[1], runs[0][1])
+
+
 def test_checkpoint_resume_is_bit_identical(tmp_path):
     """save_checkpoint after 3 steps, load into a fresh model/optimizer with a scrambled CPU
     generator: the next 3 steps (batch offsets, Philox dropout masks, AdamW) equal the
