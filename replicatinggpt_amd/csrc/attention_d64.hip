@@ -176,6 +176,22 @@ __device__ __forceinline__ void store_rows(bf16_t* row, const fv16 (&acc)[2], fl
         }
 }
 
+// LDS-DMA (global_load_lds_dwordx4, common.h dma16) of one [64][64] bf16 tile -- rows row0..row0+63 of a row-major
+// matrix -- into an aoff-swizzled image: 8 wave-instructions of 1 KB, two per wave.  LDS slot s of
+// image row r holds global chunk s ^ X(r), so each lane fetches that chunk.
+__device__ __forceinline__ void dma_tile(const bf16_t* X, int64_t ldx, int64_t row0, char* img, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int ins = 2 * wave + i, r = 8 * ins + (lane >> 3), c = (lane & 7) ^ ((((r >> 1) & 1) << 2) | ((r >> 2) & 3));
+        dma16(X + (row0 + r) * ldx + 8 * c, img + 1024 * ins);
+    }
+}
+
+// Resident kernels: wait for every vector-memory operation of this wave (the LDS-DMA tiles with
+// it), then a workgroup barrier: every wave's DMAs have landed.  One asm statement, so no LDS read
+// can be scheduled between the two.
+__device__ __forceinline__ void wait_all_barrier() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // =====================================================================================
 // forward
 // =====================================================================================
@@ -270,16 +286,17 @@ __device__ __forceinline__ void pv_tile(fv16 (&o)[2], const char* Vi, const sv8 
 // One query group's 64-key tile outside the pipeline: NSUB live 32-key subtiles (1 when the second
 // lies wholly above the diagonal); DIAG = the subtile holding the diagonal (-1: none) -- the only
 // one masked.  Straight-line code per case (the merged form copied accumulators between paths).
-template <bool DROP, int NSUB, int DIAG>
+// QREG: the group's Q fragments come from registers (qreg[4]) instead of the Q image.
+template <bool DROP, int NSUB, int DIAG, bool QREG = false>
 __device__ __forceinline__ void fwd_group_tile(const char* Ki, const char* Vi, const char* Qimg, int qr, int lane,
                                                float scale_log2, float& m_run, float& l_run, fv16 (&o)[2],
-                                               uint32_t mw) {
+                                               uint32_t mw, const sv8* qreg = nullptr) {
     fv16 s[2];
     s[0] = fv16{};
     s[1] = fv16{};
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-        const sv8 qf = frag_row(Qimg, qr, ks, lane);
+        const sv8 qf = QREG ? qreg[ks] : frag_row(Qimg, qr, ks, lane);
         s[0] = mfma32(frag_row(Ki, 0, ks, lane), qf, s[0]);
         if (NSUB == 2) s[1] = mfma32(frag_row(Ki, 32, ks, lane), qf, s[1]);
     }
@@ -471,6 +488,63 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, cons
 // The 1/(1-p) is factored out of dS (dS = 1/(1-p) P (keep dP - (1-p) delta), applied with scale in
 // the epilogue), so an element costs dP - delta', one v_bfi_b32 select (dropped: -delta') and P x.
 // =====================================================================================
+// query-side operands of one dQ group (query qa = qg + (lane & 31)): Q and dO fragments, lse in
+// log2 units and -delta' = -(1-p) delta, where delta = rowsum(dO * O) (dropout-invariant: O already
+// holds the dropped P) is also written for the dK/dV kernel.  Bases are the (b, h) row-0 pointers.
+__device__ __forceinline__ void dq_group_setup(bool act, int64_t qa, const bf16_t* qb, int64_t ld, const bf16_t* ob,
+                                               int64_t ldo, const bf16_t* db, int64_t ldd, const float* lse_bh,
+                                               float* delta_bh, float dscale, int lane, sv8 (&qf)[4], sv8 (&df)[4],
+                                               float& lse2, float& dl) {
+    float dsum = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        qf[ks] = act ? ld_frag(qb, ld, qa, ks, lane) : sv8{};
+        df[ks] = act ? ld_frag(db, ldd, qa, ks, lane) : sv8{};
+        if (act) {
+            const sv8 of = ld_frag(ob, ldo, qa, ks, lane);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dsum += bf2f((bf16_t)of[j]) * bf2f((bf16_t)df[ks][j]);
+        }
+    }
+    dsum += __shfl_xor(dsum, 32, 64);
+    dl = -dsum / dscale;   // -delta' = -(1-p) delta
+    lse2 = act ? lse_bh[qa] * LOG2E : 0.f;
+    if (act && lane < 32) delta_bh[qa] = dsum;
+}
+
+// one 64-key tile (K / V images, first key k0) of a dQ query group starting at query qg: its 32-key
+// subtiles up to the diagonal; only the subtile whose first key is qg holds the diagonal
+template <bool DROP>
+__device__ __forceinline__ void dq_group_tile(const char* Ki, const char* Vi, int k0, int qg, const sv8 (&qf)[4],
+                                              const sv8 (&df)[4], float lse2, float dl, uint32_t mw, float c2,
+                                              fv16 (&dqa)[2], int lane) {
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+        if (k0 + 32 * kt > qg + 31) break;   // subtile fully masked
+        const bool diag = __builtin_amdgcn_readfirstlane(k0 + 32 * kt == qg);
+        fv16 s = fv16{}, dp = fv16{};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            s = mfma32(frag_row(Ki, 32 * kt, ks, lane), qf[ks], s);
+            dp = mfma32(frag_row(Vi, 32 * kt, ks, lane), df[ks], dp);
+        }
+        if (diag) mask_upper(s, lane & 31, 0, lane, -INFINITY);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lse2));
+            float d = dp[r] + dl;
+            if (DROP) d = keep_sel2(keep_mask(mw, 16 * kt + r), d, dl);
+            s[r] = p * d;
+        }
+        const sv8 d0 = pack16(s, 0), d1 = pack16(s, 1);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+            dqa[dt] = mfma32(frag_tr(Ki, 32 * kt, 0, 32 * dt, lane), d0, dqa[dt]);
+            dqa[dt] = mfma32(frag_tr(Ki, 32 * kt, 1, 32 * dt, lane), d1, dqa[dt]);
+        }
+    }
+}
+
 template <bool DROP>
 __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t T_, int H, const bf16_t* __restrict__ q,
                                           const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, int64_t ld,
@@ -498,25 +572,10 @@ __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t 
     sv8 qf[2][4], df[2][4];
     float lse2[2], dl[2];
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
-        const int64_t qa = qg[g] + (lane & 31);
-        float dsum = 0.f;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-            qf[g][ks] = act[g] ? ld_frag(q + boff * ld + hh * 64, ld, qa, ks, lane) : sv8{};
-            df[g][ks] = act[g] ? ld_frag(dout + boff * ldd + hh * 64, ldd, qa, ks, lane) : sv8{};
-            if (act[g]) {
-                // delta = rowsum(dO * O) (dropout-invariant: O already holds the dropped P)
-                const sv8 of = ld_frag(o + boff * ldo + hh * 64, ldo, qa, ks, lane);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) dsum += bf2f((bf16_t)of[j]) * bf2f((bf16_t)df[g][ks][j]);
-            }
-        }
-        dsum += __shfl_xor(dsum, 32, 64);
-        dl[g] = -dsum / dscale;   // -delta' = -(1-p) delta
-        lse2[g] = act[g] ? lse[(int64_t)bh * T_ + qa] * LOG2E : 0.f;
-        if (act[g] && lane < 32) delta[(int64_t)bh * T_ + qa] = dsum;
-    }
+    for (int g = 0; g < 2; ++g)
+        dq_group_setup(act[g], qg[g] + (lane & 31), q + boff * ld + hh * 64, ld, o + boff * ldo + hh * 64, ldo,
+                       dout + boff * ldd + hh * 64, ldd, lse + (int64_t)bh * T_, delta + (int64_t)bh * T_, dscale, lane,
+                       qf[g], df[g], lse2[g], dl[g]);
     fv16 dqa[2][2];
 #pragma unroll
     for (int g = 0; g < 2; ++g) dqa[g][0] = dqa[g][1] = fv16{};
@@ -534,38 +593,11 @@ __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t 
         for (int g = 0; g < 2; ++g)
             if (DROP && act[g] && nxt * 64 <= qg[g] + 31) mn[g] = mrow[g][nxt * 64];
         const char* Ki = smem + (kv & 1) * 2 * TILE;
-        const char* Vi = Ki + TILE;
         const int k0 = kv * 64;
 #pragma unroll
-        for (int g = 0; g < 2; ++g) {
-            if (!act[g] || k0 > qg[g] + 31) continue;
-#pragma unroll
-            for (int kt = 0; kt < 2; ++kt) {
-                if (k0 + 32 * kt > qg[g] + 31) break;   // subtile fully masked
-                // only the subtile whose first key is the group's first query holds the diagonal
-                const bool diag = __builtin_amdgcn_readfirstlane(k0 + 32 * kt == qg[g]);
-                fv16 s = fv16{}, dp = fv16{};
-#pragma unroll
-                for (int ks = 0; ks < 4; ++ks) {
-                    s = mfma32(frag_row(Ki, 32 * kt, ks, lane), qf[g][ks], s);
-                    dp = mfma32(frag_row(Vi, 32 * kt, ks, lane), df[g][ks], dp);
-                }
-                if (diag) mask_upper(s, lane & 31, 0, lane, -INFINITY);
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lse2[g]));
-                    float d = dp[r] + dl[g];
-                    if (DROP) d = keep_sel2(keep_mask(mw[g], 16 * kt + r), d, dl[g]);
-                    s[r] = p * d;
-                }
-                const sv8 d0 = pack16(s, 0), d1 = pack16(s, 1);
-#pragma unroll
-                for (int dt = 0; dt < 2; ++dt) {
-                    dqa[g][dt] = mfma32(frag_tr(Ki, 32 * kt, 0, 32 * dt, lane), d0, dqa[g][dt]);
-                    dqa[g][dt] = mfma32(frag_tr(Ki, 32 * kt, 1, 32 * dt, lane), d1, dqa[g][dt]);
-                }
-            }
-        }
+        for (int g = 0; g < 2; ++g)
+            if (act[g] && k0 <= qg[g] + 31)
+                dq_group_tile<DROP>(Ki, Ki + TILE, k0, qg[g], qf[g], df[g], lse2[g], dl[g], mw[g], c2, dqa[g], lane);
 #ifndef CG_ATTN_NOSTAGE
         stage_store(st, smem + ((kv + 1) & 1) * 2 * TILE, tid);
 #endif
@@ -607,6 +639,73 @@ __global__ __launch_bounds__(256, 2) void k_attn_dq_d64(int64_t T_, int H, const
 // dK / dV: block = 4 waves x 32 keys; stream 64-query tiles (Q, dO, lse, delta)
 // =====================================================================================
 constexpr int KV_STAGE = 2 * TILE + 512;   // Q image, dO image, lse*log2e [64], delta [64]
+
+// one 64-query tile (Q / dO images, their lse*log2e and -delta' rows) of a dK/dV key group starting
+// at key kq (key = kq + (lane & 31)): the 32-query subtiles that reach the group's keys
+template <bool DROP>
+__device__ __forceinline__ void dkdv_tile(const char* Qi, const char* Oi, const float* st_lse, const float* st_del,
+                                          int q0, int kq, int key, const sv8 (&kf)[4], const sv8 (&vf)[4], uint32_t mw,
+                                          float c2, fv16 (&dka)[2], fv16 (&dva)[2], int lane) {
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+        const int q0s = q0 + 32 * qs;
+        if (q0s + 31 < kq) continue;   // every query of the subtile precedes every key
+        // dP starts from -delta' of its rows (the accumulator's initial value), so the MFMA
+        // chain leaves dP - delta'; dS = 1/(1-p) P (keep dP - delta'), the 1/(1-p) in the epilogue
+        fv16 s = fv16{}, dp;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float4 d4 = *(const float4*)(st_del + 32 * qs + 8 * i + 4 * (lane >> 5));
+            dp[4 * i] = d4.x;
+            dp[4 * i + 1] = d4.y;
+            dp[4 * i + 2] = d4.z;
+            dp[4 * i + 3] = d4.w;
+        }
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            s = mfma32(frag_row(Qi, 32 * qs, ks, lane), kf[ks], s);
+            dp = mfma32(frag_row(Oi, 32 * qs, ks, lane), vf[ks], dp);
+        }
+        if (__builtin_amdgcn_readfirstlane(q0s < kq + 31)) {
+            // diagonal subtile: queries (rows) before the key (column) are masked
+            const int rel = key - q0s - 4 * (lane >> 5);
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if ((r & 3) + 8 * (r >> 2) < rel) s[r] = -INFINITY;
+        }
+        fv16 z;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            // rows 8i + 4(lane>>5) + 0..3 of the subtile: one 16-B LDS read each (broadcast)
+            const int row = 32 * qs + 8 * i + 4 * (lane >> 5);
+            const float4 l4 = *(const float4*)(st_lse + row);
+            const float4 d4 = *(const float4*)(st_del + row);
+            const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dvv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int r = 4 * i + e;
+                const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lv[e]));
+                float d = dp[r];   // dP - delta'
+                if (DROP) {
+                    const uint32_t kp = keep_mask(mw, 16 * qs + r);   // 1/(1-p) of dV: epilogue
+                    z[r] = __uint_as_float(__float_as_uint(p) & kp);
+                    d = keep_sel2(kp, d, dvv[e]);                     // dropped: -delta'
+                } else {
+                    z[r] = p;
+                }
+                s[r] = p * d;
+            }
+        }
+        const sv8 z0 = pack16(z, 0), z1 = pack16(z, 1), s0 = pack16(s, 0), s1 = pack16(s, 1);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+            dva[dt] = mfma32(frag_tr(Oi, 32 * qs, 0, 32 * dt, lane), z0, dva[dt]);
+            dva[dt] = mfma32(frag_tr(Oi, 32 * qs, 1, 32 * dt, lane), z1, dva[dt]);
+            dka[dt] = mfma32(frag_tr(Qi, 32 * qs, 0, 32 * dt, lane), s0, dka[dt]);
+            dka[dt] = mfma32(frag_tr(Qi, 32 * qs, 1, 32 * dt, lane), s1, dka[dt]);
+        }
+    }
+}
 
 template <bool DROP>
 __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_t T_, int H,
@@ -667,67 +766,7 @@ __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_
         const float* st_lse = (const float*)(S0 + 2 * TILE);
         const float* st_del = st_lse + 64;
         const int q0 = qt * 64;
-        if (act && q0 + 63 >= kq) {
-#pragma unroll
-            for (int qs = 0; qs < 2; ++qs) {
-                const int q0s = q0 + 32 * qs;
-                if (q0s + 31 < kq) continue;   // every query of the subtile precedes every key
-                // dP starts from -delta' of its rows (the accumulator's initial value), so the MFMA
-                // chain leaves dP - delta'; dS = 1/(1-p) P (keep dP - delta'), the 1/(1-p) in the epilogue
-                fv16 s = fv16{}, dp;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float4 d4 = *(const float4*)(st_del + 32 * qs + 8 * i + 4 * (lane >> 5));
-                    dp[4 * i] = d4.x;
-                    dp[4 * i + 1] = d4.y;
-                    dp[4 * i + 2] = d4.z;
-                    dp[4 * i + 3] = d4.w;
-                }
-#pragma unroll
-                for (int ks = 0; ks < 4; ++ks) {
-                    s = mfma32(frag_row(Qi, 32 * qs, ks, lane), kf[ks], s);
-                    dp = mfma32(frag_row(Oi, 32 * qs, ks, lane), vf[ks], dp);
-                }
-                if (__builtin_amdgcn_readfirstlane(q0s < kq + 31)) {
-                    // diagonal subtile: queries (rows) before the key (column) are masked
-                    const int rel = key - q0s - 4 * (lane >> 5);
-#pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        if ((r & 3) + 8 * (r >> 2) < rel) s[r] = -INFINITY;
-                }
-                fv16 z;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    // rows 8i + 4(lane>>5) + 0..3 of the subtile: one 16-B LDS read each (broadcast)
-                    const int row = 32 * qs + 8 * i + 4 * (lane >> 5);
-                    const float4 l4 = *(const float4*)(st_lse + row);
-                    const float4 d4 = *(const float4*)(st_del + row);
-                    const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dvv[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int r = 4 * i + e;
-                        const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lv[e]));
-                        float d = dp[r];   // dP - delta'
-                        if (DROP) {
-                            const uint32_t kp = keep_mask(mw, 16 * qs + r);   // 1/(1-p) of dV: epilogue
-                            z[r] = __uint_as_float(__float_as_uint(p) & kp);
-                            d = keep_sel2(kp, d, dvv[e]);                     // dropped: -delta'
-                        } else {
-                            z[r] = p;
-                        }
-                        s[r] = p * d;
-                    }
-                }
-                const sv8 z0 = pack16(z, 0), z1 = pack16(z, 1), s0 = pack16(s, 0), s1 = pack16(s, 1);
-#pragma unroll
-                for (int dt = 0; dt < 2; ++dt) {
-                    dva[dt] = mfma32(frag_tr(Oi, 32 * qs, 0, 32 * dt, lane), z0, dva[dt]);
-                    dva[dt] = mfma32(frag_tr(Oi, 32 * qs, 1, 32 * dt, lane), z1, dva[dt]);
-                    dka[dt] = mfma32(frag_tr(Qi, 32 * qs, 0, 32 * dt, lane), s0, dka[dt]);
-                    dka[dt] = mfma32(frag_tr(Qi, 32 * qs, 1, 32 * dt, lane), s1, dka[dt]);
-                }
-            }
-        }
+        if (act && q0 + 63 >= kq) dkdv_tile<DROP>(Qi, Oi, st_lse, st_del, q0, kq, key, kf, vf, mw, c2, dka, dva, lane);
         char* D = smem + ((it + 1) & 1) * KV_STAGE;
 #ifndef CG_ATTN_NOSTAGE
         stage_store(st, D, tid);
@@ -763,11 +802,238 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, con
     }
 }
 
+// =====================================================================================
+// T <= 256: sequence-resident kernels (the C2 shape, T = 256)
+// =====================================================================================
+// At T = 256 the ring kernels above are latency-bound: a workgroup per (b, h) stages one 16-KB tile
+// at a time through registers (one tile in flight per 256 threads), and 384 workgroups fill 1.5 of
+// the 2 slots per CU (forward 23 us for 52.7 MB, 2.3 TB/s).  Here every K/V (or Q/dO) tile of the
+// (b, h) is requested at once by LDS-DMA (64 KB per workgroup), the query-side (key-side) operands
+// are loaded to registers right behind them, and after one wait + barrier the tile loop runs with
+// no staging barriers.  Same wave/group assignment, per-tile arithmetic and keep-bit words as the
+// ring kernels, so the results are bitwise the same.  (The register loads follow the DMAs: vmcnt
+// retires in order, so waiting for them covers the tiles too -- see common.h dma16.)
+template <bool DROP, int NT>
+__global__ __launch_bounds__(256, 2) void k_attn_fwd_d64r(int H, const bf16_t* __restrict__ q,
+                                                          const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                                                          int64_t ld, bf16_t* __restrict__ o, int64_t ldo,
+                                                          float* __restrict__ lse, float scale_log2,
+                                                          const uint32_t* __restrict__ mask, float dscale) {
+    constexpr int T = 64 * NT;
+    __shared__ __attribute__((aligned(16))) char smem[NT * 2 * TILE];   // K, V images of tile t at 2 t TILE
+    int x, bh;
+    block_coords<false>(x, bh);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int b = bh / H, hh = bh % H;
+    const int64_t boff = (int64_t)b * T, ntile = mask_tiles(T);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        dma_tile(k + boff * ld + hh * 64, ld, 64 * t, smem + 2 * t * TILE, wave, lane);
+        dma_tile(v + boff * ld + hh * 64, ld, 64 * t, smem + (2 * t + 1) * TILE, wave, lane);
+    }
+    const int qg[2] = {32 * (7 - wave), 32 * wave};   // A = 7 - w (longer causal prefix), B = w
+    const bool act[2] = {qg[0] < T, qg[1] < T};
+    sv8 qf[2][4];
+    uint32_t mw[2][NT];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+            qf[g][ks] = act[g] ? ld_frag(q + boff * ld + hh * 64, ld, qg[g] + (lane & 31), ks, lane) : sv8{};
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+            mw[g][t] = (DROP && act[g] && 64 * t <= qg[g] + 31)
+                           ? mask[((int64_t)bh * ntile + mask_fwd_tile(qg[g] >> 5, t)) * 64 + lane]
+                           : 0u;
+    }
+    fv16 oacc[2][2];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) oacc[g][0] = oacc[g][1] = fv16{};
+    float m_run[2] = {-FLT_MAX, -FLT_MAX}, l_run[2] = {0.f, 0.f};
+    wait_all_barrier();
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const char* Ki = smem + 2 * t * TILE;
+        const char* Vi = Ki + TILE;
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            if (!act[g] || 64 * t > qg[g] + 31) continue;
+            const int rel = __builtin_amdgcn_readfirstlane(qg[g] - 64 * t);
+            if (rel >= 64)
+                fwd_group_tile<DROP, 2, -1, true>(Ki, Vi, nullptr, 0, lane, scale_log2, m_run[g], l_run[g], oacc[g],
+                                                  mw[g][t], qf[g]);
+            else if (rel == 32)
+                fwd_group_tile<DROP, 2, 1, true>(Ki, Vi, nullptr, 0, lane, scale_log2, m_run[g], l_run[g], oacc[g],
+                                                 mw[g][t], qf[g]);
+            else
+                fwd_group_tile<DROP, 1, 0, true>(Ki, Vi, nullptr, 0, lane, scale_log2, m_run[g], l_run[g], oacc[g],
+                                                 mw[g][t], qf[g]);
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        if (!act[g]) continue;
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run[g]), __float_as_uint(l_run[g]), false,
+                                                         false);
+        const float lt = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+        const int64_t qa = qg[g] + (lane & 31);
+        store_rows(o + (boff + qa) * ldo + hh * 64, oacc[g], dscale / lt, lane);
+        if (lane < 32) lse[(int64_t)bh * T + qa] = (m_run[g] + __log2f(lt)) * LN2;
+    }
+}
+
+template <bool DROP, int NT>
+__global__ __launch_bounds__(256, 2) void k_attn_dq_d64r(int H, const bf16_t* __restrict__ q,
+                                                         const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                                                         int64_t ld, const bf16_t* __restrict__ o, int64_t ldo,
+                                                         const bf16_t* __restrict__ dout, int64_t ldd,
+                                                         const float* __restrict__ lse, float* __restrict__ delta,
+                                                         bf16_t* __restrict__ dq, int64_t lddq, float scale,
+                                                         const uint32_t* __restrict__ mask, float dscale) {
+    constexpr int T = 64 * NT;
+    __shared__ __attribute__((aligned(16))) char smem[NT * 2 * TILE];
+    int x, bh;
+    block_coords<false>(x, bh);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int b = bh / H, hh = bh % H;
+    const int64_t boff = (int64_t)b * T, ntile = mask_tiles(T);
+    const float c2 = scale * LOG2E;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        dma_tile(k + boff * ld + hh * 64, ld, 64 * t, smem + 2 * t * TILE, wave, lane);
+        dma_tile(v + boff * ld + hh * 64, ld, 64 * t, smem + (2 * t + 1) * TILE, wave, lane);
+    }
+    const int qg[2] = {32 * (7 - wave), 32 * wave};
+    const bool act[2] = {qg[0] < T, qg[1] < T};
+    uint32_t mw[2][NT];
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+            mw[g][t] = (DROP && act[g] && 64 * t <= qg[g] + 31)
+                           ? mask[((int64_t)bh * ntile + mask_fwd_tile(qg[g] >> 5, t)) * 64 + lane]
+                           : 0u;
+    sv8 qf[2][4], df[2][4];
+    float lse2[2], dl[2];
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+        dq_group_setup(act[g], qg[g] + (lane & 31), q + boff * ld + hh * 64, ld, o + boff * ldo + hh * 64, ldo,
+                       dout + boff * ldd + hh * 64, ldd, lse + (int64_t)bh * T, delta + (int64_t)bh * T, dscale, lane,
+                       qf[g], df[g], lse2[g], dl[g]);
+    fv16 dqa[2][2];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) dqa[g][0] = dqa[g][1] = fv16{};
+    wait_all_barrier();
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const char* Ki = smem + 2 * t * TILE;
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+            if (act[g] && 64 * t <= qg[g] + 31)
+                dq_group_tile<DROP>(Ki, Ki + TILE, 64 * t, qg[g], qf[g], df[g], lse2[g], dl[g], mw[g][t], c2, dqa[g],
+                                    lane);
+    }
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        if (!act[g]) continue;
+        const int64_t qa = qg[g] + (lane & 31);
+        store_rows(dq + (boff + qa) * lddq + hh * 64, dqa[g], scale * dscale, lane);
+    }
+}
+
+// dK/dV: one workgroup per (b, h); wave w takes key group w, then key group 7 - w (equal causal
+// work per wave: 8 + 1, 7 + 2, ... 32-query subtiles at T = 256), Q / dO / lse / delta resident
+template <bool DROP, int NT>
+__global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64r(int H, const bf16_t* __restrict__ q,
+                                                           const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                                                           int64_t ld, const bf16_t* __restrict__ dout, int64_t ldd,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ delta, bf16_t* __restrict__ dk,
+                                                           bf16_t* __restrict__ dv, int64_t lddkv, float scale,
+                                                           const uint32_t* __restrict__ mask, float dscale) {
+    constexpr int T = 64 * NT;
+    __shared__ __attribute__((aligned(16))) char smem[NT * 2 * TILE + 2 * T * 4];   // Q, dO images; lse, -delta'
+    float* st_lse = (float*)(smem + NT * 2 * TILE);
+    float* st_del = st_lse + T;
+    int x, bh;
+    block_coords<false>(x, bh);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int b = bh / H, hh = bh % H;
+    const int64_t boff = (int64_t)b * T, ntile = mask_tiles(T);
+    const float c2 = scale * LOG2E;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        dma_tile(q + boff * ld + hh * 64, ld, 64 * t, smem + 2 * t * TILE, wave, lane);
+        dma_tile(dout + boff * ldd + hh * 64, ldd, 64 * t, smem + (2 * t + 1) * TILE, wave, lane);
+    }
+    const int kqs[2] = {32 * wave, 32 * (7 - wave)};
+    const bf16_t* kb_ = k + boff * ld + hh * 64;
+    const bf16_t* vb_ = v + boff * ld + hh * 64;
+    if (tid < T) {
+        st_lse[tid] = lse[(int64_t)bh * T + tid] * LOG2E;
+        st_del[tid] = -delta[(int64_t)bh * T + tid] / dscale;   // -delta' = -(1-p) delta
+    }
+    uint32_t mw[2][NT];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const int kbw = kqs[p] >> 5, qtm = kbw >> 1;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+            mw[p][t] = (DROP && kqs[p] < T && t >= qtm)
+                           ? mask[((int64_t)bh * ntile + mask_bwd_tile(kbw, qtm, NT)) * 64 + lane + (t - qtm) * 64]
+                           : 0u;
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const int kq = kqs[p], key = kq + (lane & 31);
+        const bool act = kq < T;
+        sv8 kf[4], vf[4];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            kf[ks] = act ? ld_frag(kb_, ld, key, ks, lane) : sv8{};
+            vf[ks] = act ? ld_frag(vb_, ld, key, ks, lane) : sv8{};
+        }
+        if (!p) wait_all_barrier();
+        fv16 dka[2] = {fv16{}, fv16{}}, dva[2] = {fv16{}, fv16{}};
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+            if (act && 64 * t + 63 >= kq)
+                dkdv_tile<DROP>(smem + 2 * t * TILE, smem + (2 * t + 1) * TILE, st_lse + 64 * t, st_del + 64 * t,
+                                64 * t, kq, key, kf, vf, mw[p][t], c2, dka, dva, lane);
+        if (act) {
+            store_rows(dk + (boff + key) * lddkv + hh * 64, dka, scale * dscale, lane);
+            store_rows(dv + (boff + key) * lddkv + hh * 64, dva, DROP ? dscale : 1.f, lane);
+        }
+    }
+}
+
 }  // namespace
 
 namespace attn {
+// sequence-resident kernels for T <= 256 unless cg_set_tuning("attn_variant", 1) selects the ring
+// kernels (A/B and tests)
+static bool resident(int64_t T) { return T <= 256 && g_attn_variant != 1; }
+#define RES_SWITCH(T, ...)                  \
+    switch ((int)((T) / 64)) {              \
+        case 1: { constexpr int NT_ = 1; __VA_ARGS__; } break; \
+        case 2: { constexpr int NT_ = 2; __VA_ARGS__; } break; \
+        case 3: { constexpr int NT_ = 3; __VA_ARGS__; } break; \
+        default: { constexpr int NT_ = 4; __VA_ARGS__; } break; \
+    }
+
 void launch_fwd_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                     bf16_t* o, int64_t ldo, float* lse, float scale, const DropArgs& d, hipStream_t st) {
+    if (resident(T)) {
+        const float sl2 = scale * LOG2E;
+        RES_SWITCH(T, if (d.mask) k_attn_fwd_d64r<true, NT_><<<dim3(1, (unsigned)(B * H)), 256, 0, st>>>(
+                              H, q, k, v, ld, o, ldo, lse, sl2, d.mask, d.dscale);
+                   else k_attn_fwd_d64r<false, NT_><<<dim3(1, (unsigned)(B * H)), 256, 0, st>>>(
+                              H, q, k, v, ld, o, ldo, lse, sl2, nullptr, 1.f));
+        return;
+    }
     const dim3 grid((unsigned)((ceil_div(T, 256) + 1) / 2), (unsigned)(B * H));   // pairs of query blocks
     if (d.mask)
         k_attn_fwd_d64<true><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, lse, scale * LOG2E, d.mask, d.dscale);
@@ -777,6 +1043,13 @@ void launch_fwd_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* 
 void launch_dq_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                    const bf16_t* o, int64_t ldo, const bf16_t* dout, int64_t ldd, const float* lse, float* delta,
                    bf16_t* dq, int64_t lddq, float scale, const DropArgs& d, hipStream_t st) {
+    if (resident(T)) {
+        RES_SWITCH(T, if (d.mask) k_attn_dq_d64r<true, NT_><<<dim3(1, (unsigned)(B * H)), 256, 0, st>>>(
+                              H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale, d.mask, d.dscale);
+                   else k_attn_dq_d64r<false, NT_><<<dim3(1, (unsigned)(B * H)), 256, 0, st>>>(
+                              H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale, nullptr, 1.f));
+        return;
+    }
     const dim3 grid((unsigned)((ceil_div(T, 256) + 1) / 2), (unsigned)(B * H));
     if (d.mask)
         k_attn_dq_d64<true><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
@@ -788,6 +1061,13 @@ void launch_dq_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k
 void launch_dkdv_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                      const bf16_t* dout, int64_t ldd, const float* lse, const float* delta, bf16_t* dk, bf16_t* dv,
                      int64_t lddkv, float scale, const DropArgs& d, hipStream_t st) {
+    if (resident(T)) {
+        RES_SWITCH(T, if (d.mask) k_attn_dkdv_d64r<true, NT_><<<dim3(1, (unsigned)(B * H)), 256, 0, st>>>(
+                              H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale, d.mask_bwd, d.dscale);
+                   else k_attn_dkdv_d64r<false, NT_><<<dim3(1, (unsigned)(B * H)), 256, 0, st>>>(
+                              H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale, nullptr, 1.f));
+        return;
+    }
     const dim3 grid((unsigned)((ceil_div(T, 128) + 1) / 2), (unsigned)(B * H));
     if (d.mask)
         k_attn_dkdv_d64<true><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,

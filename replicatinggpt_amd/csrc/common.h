@@ -22,6 +22,27 @@ void launch_reduce_partials3(const float* part, int64_t K, int64_t N, float* out
                              int64_t S, int accumulate, int accumulate_c, hipStream_t st);
 }  // namespace cg
 
+namespace cg {
+// One 16-B-per-lane LDS-DMA (global_load_lds_dwordx4: lane l's 16 bytes from g land at LDS byte
+// lds + 16 l; lds must be wave-uniform) issued from inline asm, so the compiler does not see an LDS
+// DMA.  Seen (the __builtin_amdgcn_global_load_lds form), it makes every later LDS read it cannot
+// prove disjoint wait for ALL outstanding DMAs (s_waitcnt vmcnt(0) before the ds_read): a ring's
+// in-flight prefetch stages are then waited for before the current stage is read, i.e. no
+// pipelining beyond one stage.  Callers wait for these DMAs with their own s_waitcnt vmcnt(N).
+// vmcnt retires in issue order, so the compiler's own waits stay correct but count only the loads
+// it knows: a compiler-visible load issued BEFORE hidden DMAs is waited for as if the DMAs had
+// landed too -- issue register loads after the DMAs they should not wait for.  The "memory"
+// clobber keeps loads/stores from being scheduled across the DMA.  m0 is clobbered; nothing else
+// in these kernels uses it (gfx9+ LDS access does not).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void dma16(const void* g, const void* lds) {
+    const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds);
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+}  // namespace cg
+
 #define CG_REQUIRE(cond, ...)                \
     do {                                     \
         if (!(cond)) {                       \

@@ -60,8 +60,7 @@ struct Dma8 {
         const bf16_t* base = origin + kt * kstep;
 #pragma unroll
         for (int i = 0; i < PER_WAVE; ++i)
-            __builtin_amdgcn_global_load_lds((const void*)(base + off[i]),
-                                             (lds_void*)(img + (wave * PER_WAVE + i) * 1024), 16, 0, 0);
+            dma16(base + off[i], img + (wave * PER_WAVE + i) * 1024);
     }
 };
 

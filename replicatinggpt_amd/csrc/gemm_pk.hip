@@ -53,15 +53,13 @@ struct DmaP {
     }
     // instruction i (0..PER_WAVE-1) of one K-tile, from that K-tile's base address
     __device__ __forceinline__ void issue1(const bf16_t* base, int i, char* img, int wave) const {
-        __builtin_amdgcn_global_load_lds((const void*)(base + off[i]), (lds_void*)(img + (wave * PER_WAVE + i) * 1024),
-                                         16, 0, 0);
+        dma16(base + off[i], img + (wave * PER_WAVE + i) * 1024);
     }
     __device__ __forceinline__ void issue(const bf16_t* origin, int kt, char* img, int wave) const {
         const bf16_t* base = origin + kt * kstep;
 #pragma unroll
         for (int i = 0; i < PER_WAVE; ++i)
-            __builtin_amdgcn_global_load_lds((const void*)(base + off[i]),
-                                             (lds_void*)(img + (wave * PER_WAVE + i) * 1024), 16, 0, 0);
+            dma16(base + off[i], img + (wave * PER_WAVE + i) * 1024);
     }
 };
 
@@ -219,7 +217,12 @@ struct GeoP {
     static constexpr int OCC = OCC_LDS > 4 ? 4 : (OCC_LDS < 1 ? 1 : OCC_LDS);  // resident blocks per CU (LDS-bound)
 };
 
-template <bool AT, bool BT, int BM, int BN, int NBUF>
+// SLAB: split-K instantiation (split_k > 1), whose epilogue is only the fp32 slab stores.  The
+// full epilogue's load-carrying paths (ReLU-backward aux, residual, beta) leave the compiler's
+// wait-count state with a load it cannot retire at the loop head, and it puts s_waitcnt vmcnt(0)
+// before every K-tile's fragment reads -- which, with the DMAs hidden from it (common.h dma16),
+// waits for the prefetched stages too.  Without those paths the loop keeps NBUF-1 stages in flight.
+template <bool AT, bool BT, int BM, int BN, int NBUF, bool SLAB = false>
 // amdgpu_waves_per_eu: LDS caps residency at OCC blocks, so tell the scheduler the real occupancy;
 // left at its default it schedules for 8+ waves/SIMD, keeps ONE A fragment register and waits
 // lgkmcnt(0) before every 4 MFMAs (LDS latency exposed 8x per K-tile)
@@ -403,11 +406,12 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
             int sp;
             decode(cj, m0, n0, sp);
             const int64_t mr = m0 + wm * 64 + (lane & 15), nc = n0 + wn * 64 + 4 * (lane >> 4);
-            if (split_k > 1) {
+            if (SLAB || split_k > 1) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
                     for (int j = 0; j < 4; ++j) *(fv4*)(ws + ((int64_t)sp * M + mr + 16 * i) * N + nc + 16 * j) = acc[i][j];
+            } else if constexpr (SLAB) {
             } else if (flags & 2) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
@@ -456,9 +460,15 @@ void launch_p(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
     int64_t slots = (int64_t)cu_count() * G::OCC;
     if (g_gemm_max_grid > 0 && g_gemm_max_grid < slots) slots = g_gemm_max_grid;
     const unsigned grid = (unsigned)(nitems < slots ? nitems : slots);
-#define FG(AT_, BT_)                                                                                             \
-    k_gemm_pk<AT_, BT_, BM, BN, NBUF><<<grid, G::THREADS, G::LDS, st>>>(M, N, K, A, lda, B, ldb, C, c_dtype, ldc, \
-                                                                      e, split_k, kchunk, ws, g_pk_flags)
+#define FG(AT_, BT_)                                                                                              \
+    do {                                                                                                          \
+        if (split_k > 1)                                                                                          \
+            k_gemm_pk<AT_, BT_, BM, BN, NBUF, true><<<grid, G::THREADS, G::LDS, st>>>(                            \
+                M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, kchunk, ws, g_pk_flags);                    \
+        else                                                                                                      \
+            k_gemm_pk<AT_, BT_, BM, BN, NBUF, false><<<grid, G::THREADS, G::LDS, st>>>(                           \
+                M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, kchunk, ws, g_pk_flags);                    \
+    } while (0)
     // transposed LDS images need >= 128 rows (DmaP): narrower tiles serve only the layouts they can
     if (!at && !bt) FG(false, false);
     else if (!at && bt) {
