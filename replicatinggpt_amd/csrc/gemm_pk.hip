@@ -77,10 +77,13 @@ __device__ __forceinline__ void store4_plain(const fv4& v, int64_t m, int64_t n,
 // vmcnt(0) 16 times per item, each time also for the previous fragments' stores and the next
 // K-tile's DMA (measured: +10 us on the C2 FFN1 bias+ReLU forward, +14 us on the ReLU-backward
 // dgrad).  Arithmetic and order are exactly epi_store4's; beta != 0 keeps the per-fragment form.
+// EK >= 0: the epilogue kind fixed at compile time (CG_EPI_*; dispatch guarantees beta == 0 and the
+// kind's bias / residual pointers non-NULL), EK < 0: every kind at run time.
+template <int EK>
 __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t nc, int64_t N, void* Cv, int c_dtype,
                                          int64_t ldc, const EpiArgs& epi, uint64_t stream) {
-    const int kind = epi.kind;
-    if (epi.beta != 0.f) {
+    const int kind = EK >= 0 ? EK : epi.kind;
+    if (EK < 0 && epi.beta != 0.f) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -156,11 +159,11 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
         }
         return;
     }
-    const bool has_bias = kind != CG_EPI_STORE && epi.bias;
+    const bool has_bias = EK >= 0 ? (EK >= CG_EPI_BIAS && EK <= CG_EPI_BIAS_DROP_RESID) : (kind != CG_EPI_STORE && epi.bias);
     float4 bv[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) bv[j] = has_bias ? *(const float4*)(epi.bias + nc + 16 * j) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const bool has_resid = (kind == CG_EPI_BIAS_RESID || kind == CG_EPI_BIAS_DROP_RESID) && epi.resid;
+    const bool has_resid = (kind == CG_EPI_BIAS_RESID || kind == CG_EPI_BIAS_DROP_RESID) && (EK >= 0 || epi.resid);
     if (has_resid) {
         float4 r[4][4];
 #pragma unroll
@@ -217,12 +220,15 @@ struct GeoP {
     static constexpr int OCC = OCC_LDS > 4 ? 4 : (OCC_LDS < 1 ? 1 : OCC_LDS);  // resident blocks per CU (LDS-bound)
 };
 
-// SLAB: split-K instantiation (split_k > 1), whose epilogue is only the fp32 slab stores.  The
-// full epilogue's load-carrying paths (ReLU-backward aux, residual, beta) leave the compiler's
-// wait-count state with a load it cannot retire at the loop head, and it puts s_waitcnt vmcnt(0)
-// before every K-tile's fragment reads -- which, with the DMAs hidden from it (common.h dma16),
-// waits for the prefetched stages too.  Without those paths the loop keeps NBUF-1 stages in flight.
-template <bool AT, bool BT, int BM, int BN, int NBUF, bool SLAB = false>
+// EK: the item epilogue.  EK_SLAB = split-K (split_k > 1, fp32 slab stores only), 0..5 = one
+// CG_EPI_* kind fixed at compile time, EK_ANY = every kind, beta and the per-fragment form at run
+// time.  The run-time epilogue's conditional loads (bias present or not, residual, ReLU-backward aux,
+// beta) leave the compiler's wait-count state with a load it cannot retire at the loop head, and it
+// puts s_waitcnt vmcnt(0) before every K-tile's fragment reads -- waiting for the item's output
+// stores and, with the DMAs hidden from it (common.h dma16), for the prefetched stages too.  The
+// fixed-kind and slab instantiations have no such wait.
+constexpr int EK_ANY = -1, EK_SLAB = 6;
+template <bool AT, bool BT, int BM, int BN, int NBUF, int EK = EK_ANY>
 // amdgpu_waves_per_eu: LDS caps residency at OCC blocks, so tell the scheduler the real occupancy;
 // left at its default it schedules for 8+ waves/SIMD, keeps ONE A fragment register and waits
 // lgkmcnt(0) before every 4 MFMAs (LDS latency exposed 8x per K-tile)
@@ -406,20 +412,20 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
             int sp;
             decode(cj, m0, n0, sp);
             const int64_t mr = m0 + wm * 64 + (lane & 15), nc = n0 + wn * 64 + 4 * (lane >> 4);
-            if (SLAB || split_k > 1) {
+            if (EK == EK_SLAB || split_k > 1) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
                     for (int j = 0; j < 4; ++j) *(fv4*)(ws + ((int64_t)sp * M + mr + 16 * i) * N + nc + 16 * j) = acc[i][j];
-            } else if constexpr (SLAB) {
-            } else if (flags & 2) {
+            } else if constexpr (EK == EK_SLAB) {
+            } else if (EK < 0 && (flags & 2)) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
                         epi_store4(acc[i][j], mr + 16 * i, nc + 16 * j, N, Cv, c_dtype, ldc, epi, stream);
             } else {
-                epi_item(acc, mr, nc, N, Cv, c_dtype, ldc, epi, stream);
+                epi_item<EK < 0 ? EK_ANY : EK>(acc, mr, nc, N, Cv, c_dtype, ldc, epi, stream);
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -450,6 +456,45 @@ int cu_count() {
     return n;
 }
 
+template <bool AT_, bool BT_, int BM, int BN, int NBUF, int EK>
+void launch_1(unsigned grid, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
+              void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, int64_t kchunk, float* ws,
+              hipStream_t st) {
+    using G = GeoP<BM, BN, NBUF>;
+    k_gemm_pk<AT_, BT_, BM, BN, NBUF, EK><<<grid, G::THREADS, G::LDS, st>>>(M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e,
+                                                                         split_k, kchunk, ws, g_pk_flags);
+}
+
+// epilogue instantiation: slab for split-K; a fixed kind for the default 128x128 2-stage kernel's
+// non-transposed-A products (forward / dgrad) when the call allows it; otherwise the run-time one
+template <bool AT_, bool BT_, int BM, int BN, int NBUF>
+void launch_ek(unsigned grid, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
+               int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, int64_t kchunk, float* ws,
+               hipStream_t st) {
+#define L1(EK_) launch_1<AT_, BT_, BM, BN, NBUF, EK_>(grid, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, kchunk, ws, st)
+    if (split_k > 1) {
+        L1(EK_SLAB);
+        return;
+    }
+    if constexpr (!AT_ && BM == 128 && BN == 128 && NBUF == 2) {
+        const bool needs_bias = e.kind >= CG_EPI_BIAS && e.kind <= CG_EPI_BIAS_DROP_RESID;
+        const bool needs_resid = e.kind == CG_EPI_BIAS_RESID || e.kind == CG_EPI_BIAS_DROP_RESID;
+        if (!(g_pk_flags & 2) && e.beta == 0.f && (!needs_bias || e.bias) && (!needs_resid || e.resid)) {
+            switch (e.kind) {
+                case CG_EPI_STORE: L1(CG_EPI_STORE); return;
+                case CG_EPI_BIAS: L1(CG_EPI_BIAS); return;
+                case CG_EPI_BIAS_RELU: L1(CG_EPI_BIAS_RELU); return;
+                case CG_EPI_BIAS_RESID: L1(CG_EPI_BIAS_RESID); return;
+                case CG_EPI_BIAS_DROP_RESID: L1(CG_EPI_BIAS_DROP_RESID); return;
+                case CG_EPI_RELU_BWD: L1(CG_EPI_RELU_BWD); return;
+                default: break;
+            }
+        }
+    }
+    L1(EK_ANY);
+#undef L1
+}
+
 template <int BM, int BN, int NBUF>
 void launch_p(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
               int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, float* ws,
@@ -460,15 +505,7 @@ void launch_p(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
     int64_t slots = (int64_t)cu_count() * G::OCC;
     if (g_gemm_max_grid > 0 && g_gemm_max_grid < slots) slots = g_gemm_max_grid;
     const unsigned grid = (unsigned)(nitems < slots ? nitems : slots);
-#define FG(AT_, BT_)                                                                                              \
-    do {                                                                                                          \
-        if (split_k > 1)                                                                                          \
-            k_gemm_pk<AT_, BT_, BM, BN, NBUF, true><<<grid, G::THREADS, G::LDS, st>>>(                            \
-                M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, kchunk, ws, g_pk_flags);                    \
-        else                                                                                                      \
-            k_gemm_pk<AT_, BT_, BM, BN, NBUF, false><<<grid, G::THREADS, G::LDS, st>>>(                           \
-                M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, kchunk, ws, g_pk_flags);                    \
-    } while (0)
+#define FG(AT_, BT_) launch_ek<AT_, BT_, BM, BN, NBUF>(grid, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, kchunk, ws, st)
     // transposed LDS images need >= 128 rows (DmaP): narrower tiles serve only the layouts they can
     if (!at && !bt) FG(false, false);
     else if (!at && bt) {
