@@ -72,6 +72,36 @@ __device__ __forceinline__ void store4_plain(const fv4& v, int64_t m, int64_t n,
         *(float4*)((float*)Cv + m * ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
 }
 
+// Dropout keep bits of a wave's 64x64 item fragment, 4 per (i, j) -- bit q <-> column
+// nc + 16 j + q of row mr + 16 i.  Lanes l and l ^ 16 hold the two 4-column halves of the same
+// 8-element Philox group (same row, columns 8k..8k+7), so each evaluates 8 of the 16 groups (j in
+// {0,1} or {2,3}) and the pair trades bytes with one lane swap per j half: half the Philox calls
+// of one keep4_bits per fragment, same bits.
+__device__ __forceinline__ void drop_nibbles(const EpiArgs& epi, uint64_t stream, int64_t mr, int64_t nc, int64_t N,
+                                             uint32_t (&nib)[4][4]) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t odd = (lane >> 4) & 1;
+    const int64_t c8 = nc & ~(int64_t)7;
+    uint32_t mine[2] = {0u, 0u};
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint64_t idx = (uint64_t)(mr + 16 * i) * (uint64_t)N + (uint64_t)(c8 + 16 * (2 * odd + jj));
+            mine[jj] |= keep8_bits(philox_group(epi.seed, stream, idx >> 3), epi.thr) << (8 * i);
+        }
+    uint32_t other[2];
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) other[jj] = (uint32_t)__shfl_xor((int)mine[jj], 16, 64);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t w = ((uint32_t)(j >> 1) == odd) ? mine[j & 1] : other[j & 1];
+            nib[i][j] = (w >> (8 * i + 4 * odd)) & 0xfu;
+        }
+}
+
 // The whole 64x64 epilogue of one wave: every operand it reads (bias, residual, ReLU output) is
 // loaded for all 16 fragments before the first store.  Per-fragment load -> use made hipcc wait
 // vmcnt(0) 16 times per item, each time also for the previous fragments' stores and the next
@@ -171,6 +201,8 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
 #pragma unroll
             for (int j = 0; j < 4; ++j) r[i][j] = *(const float4*)(epi.resid + (mr + 16 * i) * epi.ld_resid + nc + 16 * j);
         const bool drop = kind == CG_EPI_BIAS_DROP_RESID && epi.thr;
+        uint32_t nib[4][4];
+        if (drop) drop_nibbles(epi, stream, mr, nc, N, nib);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -181,15 +213,17 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
                     v[0] += bv[j].x; v[1] += bv[j].y; v[2] += bv[j].z; v[3] += bv[j].w;
                 }
                 if (drop) {
-                    const uint32_t kb = keep4_bits(epi.seed, stream, (uint64_t)m * (uint64_t)N + (uint64_t)n, epi.thr);
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) v[q] = ((kb >> q) & 1u) ? v[q] * epi.dscale : 0.f;
+                    for (int q = 0; q < 4; ++q) v[q] = ((nib[i][j] >> q) & 1u) ? v[q] * epi.dscale : 0.f;
                 }
                 v[0] = r[i][j].x + v[0]; v[1] = r[i][j].y + v[1]; v[2] = r[i][j].z + v[2]; v[3] = r[i][j].w + v[3];
                 store4_plain(v, m, n, Cv, c_dtype, ldc);
             }
         return;
     }
+    const bool drop = kind == CG_EPI_BIAS_DROP_RESID && epi.thr;
+    uint32_t nib[4][4];
+    if (drop) drop_nibbles(epi, stream, mr, nc, N, nib);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -202,10 +236,9 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
             if (kind == CG_EPI_BIAS_RELU) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
-            } else if (kind == CG_EPI_BIAS_DROP_RESID && epi.thr) {
-                const uint32_t kb = keep4_bits(epi.seed, stream, (uint64_t)m * (uint64_t)N + (uint64_t)n, epi.thr);
+            } else if (drop) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) v[q] = ((kb >> q) & 1u) ? v[q] * epi.dscale : 0.f;
+                for (int q = 0; q < 4; ++q) v[q] = ((nib[i][j] >> q) & 1u) ? v[q] * epi.dscale : 0.f;
             }
             store4_plain(v, m, n, Cv, c_dtype, ldc);
         }

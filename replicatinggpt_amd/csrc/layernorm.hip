@@ -222,7 +222,26 @@ __global__ __launch_bounds__(64 * LN_BWD_WAVES) void k_ln_bwd(const TDY* __restr
             }
         }
     };
+    // Dropout keep bits of a row with C % 8 == 0: lane l evaluates Philox group l (+ 64 c) of the
+    // row -- one call per 64 groups instead of one per lane and 8 / VEC lanes per group -- and each
+    // lane fetches the byte of its own group with ds_bpermute (__shfl).  The group index c of
+    // element e = (64 j + lane) VEC is (j VEC) >> 3 for every lane (no carry: 8 VEC <= 64).
+    constexpr int NCALL = (NJ * VEC + 7) / 8;
+    const bool row_groups = (C & 7) == 0;
     auto process = [&](int64_t r, const LnRow<VEC, NJ>& b) {
+        uint32_t kbyte[NJ];   // keep bits of the 8-group holding this lane's element e, per j
+        if (lp.out && lp.thr && row_groups) {
+            uint32_t kb[NCALL];
+#pragma unroll
+            for (int c = 0; c < NCALL; ++c) {
+                const int gr = 64 * c + lane;
+                kb[c] = 8 * gr < C ? keep8_bits(philox_group(lp.seed, stream, (uint64_t)r * (uint64_t)(C >> 3) + gr), lp.thr)
+                                   : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)   // all lanes active (a bpermute source must be)
+                kbyte[j] = (uint32_t)__shfl((int)kb[(j * VEC) >> 3], (((j * 64 + lane) * VEC) >> 3) & 63, 64);
+        }
         float xh[NJ][VEC], g[NJ][VEC];
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -255,7 +274,10 @@ __global__ __launch_bounds__(64 * LN_BWD_WAVES) void k_ln_bwd(const TDY* __restr
                 VecIO<VEC>::st(dx + r * C + e, o);
                 if (lp.out) {
                     float z[VEC];
-                    if (lp.thr) {
+                    if (lp.thr && row_groups) {
+#pragma unroll
+                        for (int q = 0; q < VEC; ++q) z[q] = ((kbyte[j] >> ((e & 7) + q)) & 1u) ? o[q] * lp.dscale : 0.f;
+                    } else if (lp.thr) {
                         const uint64_t idx = (uint64_t)r * (uint64_t)C + (uint64_t)e;
                         u32x4 ph = philox_of(lp.seed, stream, idx);
 #pragma unroll

@@ -89,6 +89,8 @@ class TrainStep:
         self.g_fb = self.g_opt = None
         self.g_seg = []
         self.loss = None
+        # d loss / d loss = 1, allocated once: loss.backward() would launch a fill kernel per step
+        self._one = torch.ones((), dtype=torch.float32, device=dev)
         self.overlap = (reducer is not None and reducer.world > 1) if overlap is None else bool(overlap)
         # per-rank dropout key: the replicas must not draw identical masks
         if reducer is not None and reducer.world > 1:
@@ -99,7 +101,7 @@ class TrainStep:
     def _fwd_bwd(self):
         _, loss = self.model(self.x, self.y)           # GPT1.py:230
         self.opt.zero_grad(set_to_none=True)           # GPT1.py:231
-        loss.backward()                                # GPT1.py:232
+        loss.backward(self._one)                       # GPT1.py:232
         return loss
 
     def _eager(self):
@@ -138,7 +140,7 @@ class TrainStep:
         """Backward of segment i (0 = from the loss): stops at the next cut's leaf alias, whose
         .grad the following segment feeds into the real block-input tensor."""
         if i == 0:
-            torch.autograd.backward(loss)
+            torch.autograd.backward(loss, grad_tensors=self._one)
         else:
             src, leaf = xs[self.cuts[i - 1]]
             torch.autograd.backward(src, grad_tensors=leaf.grad)

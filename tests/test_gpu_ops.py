@@ -125,6 +125,30 @@ def test_layernorm_bwd_rows_then_reduce_is_bitwise_ex(C, with_link):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("C", [384, 768, 1024, 512, 126])
+def test_layernorm_bwd_link_dropout_matches_oracle(C):
+    """The LayerNorm backward's consumer copy with FeedForward's output dropout (GPT1.py:146; the
+    keep bits of a row shared across lanes, one Philox group per lane, when C % 8 == 0) equals
+    bf16(dx * keep / (1 - p)) with keep from the oracle's Philox stream, bit for bit."""
+    torch.manual_seed(4)
+    O = ops()
+    rows, p, seed, call_v, site = 700, 0.2, 11, 9, 4
+    x = (torch.randn(rows, C) * 2 + 0.5).to(DEV)
+    w = (torch.randn(C) * 0.1 + 1).to(DEV)
+    mean, rstd = x.mean(1), x.var(1, unbiased=False).add(1e-5).rsqrt()
+    dy = torch.randn(rows, C, device=DEV).to(torch.bfloat16)
+    dx = torch.empty(rows, C, device=DEV)
+    lp = torch.empty(rows, C, dtype=torch.bfloat16, device=DEV)
+    dw, db, cs = (torch.zeros(C, device=DEV) for _ in range(3))
+    ws = torch.empty(O.layernorm_bwd_workspace(rows, C) // 4 + 1, device=DEV)
+    call = torch.tensor([call_v], dtype=torch.int64, device=DEV)
+    O.layernorm_bwd(dy, x, w, mean, rstd, None, dx, lp, dw, db, False, ws, cs, False, p, seed, call, site)
+    torch.cuda.synchronize()
+    keep = torch.from_numpy(philox.keep_mask(seed, (call_v << 8) | site, np.arange(rows * C), p).reshape(rows, C))
+    want = (dx.cpu() * keep.float() * (1.0 / (1.0 - p))).to(torch.bfloat16)
+    assert torch.equal(lp.cpu(), want)
+
+
 @pytest.mark.parametrize("M,F,K", [(512, 384, 128), (1024, 1536, 384), (16384, 1536, 384), (32768, 3072, 768),
                                    (65536, 3072, 768)])
 def test_relu_bwd_colpart_matches_colsum(M, F, K):
