@@ -884,17 +884,13 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64r(int H, const bf16_t* _
 }
 
 template <bool DROP, int NT>
-__global__ __launch_bounds__(256, 2) void k_attn_dq_d64r(int H, const bf16_t* __restrict__ q,
-                                                         const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-                                                         int64_t ld, const bf16_t* __restrict__ o, int64_t ldo,
-                                                         const bf16_t* __restrict__ dout, int64_t ldd,
-                                                         const float* __restrict__ lse, float* __restrict__ delta,
-                                                         bf16_t* __restrict__ dq, int64_t lddq, float scale,
-                                                         const uint32_t* __restrict__ mask, float dscale) {
+__device__ __forceinline__ void dq_res(int bh, char* smem, int H, const bf16_t* __restrict__ q,
+                                       const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, int64_t ld,
+                                       const bf16_t* __restrict__ o, int64_t ldo, const bf16_t* __restrict__ dout,
+                                       int64_t ldd, const float* __restrict__ lse, float* __restrict__ delta,
+                                       bf16_t* __restrict__ dq, int64_t lddq, float scale,
+                                       const uint32_t* __restrict__ mask, float dscale) {
     constexpr int T = 64 * NT;
-    __shared__ __attribute__((aligned(16))) char smem[NT * 2 * TILE];
-    int x, bh;
-    block_coords<false>(x, bh);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b = bh / H, hh = bh % H;
@@ -943,22 +939,34 @@ __global__ __launch_bounds__(256, 2) void k_attn_dq_d64r(int H, const bf16_t* __
     }
 }
 
-// dK/dV: one workgroup per (b, h); wave w takes key group w, then key group 7 - w (equal causal
-// work per wave: 8 + 1, 7 + 2, ... 32-query subtiles at T = 256), Q / dO / lse / delta resident
 template <bool DROP, int NT>
-__global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64r(int H, const bf16_t* __restrict__ q,
-                                                           const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-                                                           int64_t ld, const bf16_t* __restrict__ dout, int64_t ldd,
-                                                           const float* __restrict__ lse,
-                                                           const float* __restrict__ delta, bf16_t* __restrict__ dk,
-                                                           bf16_t* __restrict__ dv, int64_t lddkv, float scale,
-                                                           const uint32_t* __restrict__ mask, float dscale) {
-    constexpr int T = 64 * NT;
-    __shared__ __attribute__((aligned(16))) char smem[NT * 2 * TILE + 2 * T * 4];   // Q, dO images; lse, -delta'
-    float* st_lse = (float*)(smem + NT * 2 * TILE);
-    float* st_del = st_lse + T;
+__global__ __launch_bounds__(256, 2) void k_attn_dq_d64r(int H, const bf16_t* __restrict__ q,
+                                                         const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                                                         int64_t ld, const bf16_t* __restrict__ o, int64_t ldo,
+                                                         const bf16_t* __restrict__ dout, int64_t ldd,
+                                                         const float* __restrict__ lse, float* __restrict__ delta,
+                                                         bf16_t* __restrict__ dq, int64_t lddq, float scale,
+                                                         const uint32_t* __restrict__ mask, float dscale) {
+    __shared__ __attribute__((aligned(16))) char smem[NT * 2 * TILE];
     int x, bh;
     block_coords<false>(x, bh);
+    dq_res<DROP, NT>(bh, smem, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale, mask, dscale);
+}
+
+// dK/dV: one workgroup per (b, h); wave w takes key group w, then key group 7 - w (equal causal
+// work per wave: 8 + 1, 7 + 2, ... 32-query subtiles at T = 256), Q / dO / lse / delta resident
+// o != NULL: delta = rowsum(dO * O) is computed here (in dq_group_setup's summation order, so
+// bitwise the dQ kernel's value) instead of read from `delta` -- the merged backward launch
+template <bool DROP, int NT>
+__device__ __forceinline__ void dkdv_res(int bh, char* smem, int H, const bf16_t* __restrict__ q,
+                                         const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, int64_t ld,
+                                         const bf16_t* __restrict__ dout, int64_t ldd, const float* __restrict__ lse,
+                                         const float* __restrict__ delta, const bf16_t* __restrict__ o, int64_t ldo,
+                                         bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int64_t lddkv, float scale,
+                                         const uint32_t* __restrict__ mask, float dscale) {
+    constexpr int T = 64 * NT;
+    float* st_lse = (float*)(smem + NT * 2 * TILE);
+    float* st_del = st_lse + T;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b = bh / H, hh = bh % H;
@@ -974,7 +982,28 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64r(int H, const bf16_t* 
     const bf16_t* vb_ = v + boff * ld + hh * 64;
     if (tid < T) {
         st_lse[tid] = lse[(int64_t)bh * T + tid] * LOG2E;
-        st_del[tid] = -delta[(int64_t)bh * T + tid] / dscale;   // -delta' = -(1-p) delta
+        float dsum;
+        if (o) {   // query tid: halves h = 0, 1 (columns 16 ks + 8 h + j) summed as dq_group_setup's lanes
+            float sh[2];
+            const bf16_t* orow = o + (boff + tid) * ldo + hh * 64;
+            const bf16_t* drow = dout + (boff + tid) * ldd + hh * 64;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                float acc = 0.f;
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) {
+                    const sv8 of = *(const sv8*)(orow + 16 * ks + 8 * h);
+                    const sv8 df = *(const sv8*)(drow + 16 * ks + 8 * h);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) acc += bf2f((bf16_t)of[j]) * bf2f((bf16_t)df[j]);
+                }
+                sh[h] = acc;
+            }
+            dsum = sh[0] + sh[1];
+        } else {
+            dsum = delta[(int64_t)bh * T + tid];
+        }
+        st_del[tid] = -dsum / dscale;   // -delta' = -(1-p) delta
     }
     uint32_t mw[2][NT];
 #pragma unroll
@@ -1010,11 +1039,52 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64r(int H, const bf16_t* 
     }
 }
 
+template <bool DROP, int NT>
+__global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64r(int H, const bf16_t* __restrict__ q,
+                                                           const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                                                           int64_t ld, const bf16_t* __restrict__ dout, int64_t ldd,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ delta, bf16_t* __restrict__ dk,
+                                                           bf16_t* __restrict__ dv, int64_t lddkv, float scale,
+                                                           const uint32_t* __restrict__ mask, float dscale) {
+    __shared__ __attribute__((aligned(16))) char smem[NT * 2 * TILE + 2 * 64 * NT * 4];
+    int x, bh;
+    block_coords<false>(x, bh);
+    dkdv_res<DROP, NT>(bh, smem, H, q, k, v, ld, dout, ldd, lse, delta, nullptr, 0, dk, dv, lddkv, scale, mask,
+                       dscale);
+}
+
+// The whole T <= 256 backward in one launch: workgroup 2i computes dQ of (b, h) = i, 2i + 1 its
+// dK/dV (with delta from O and dO itself, so the two do not depend on each other).  768
+// workgroups fill the 512 slots and the second wave of them starts as slots free up, where the
+// two separate 384-workgroup launches each ran 3/4 full and back to back.  The pair of one (b, h)
+// stays on one XCD (block_coords: consecutive logical ids), sharing its K/V/Q/dO lines in L2.
+template <bool DROP, int NT>
+__global__ __launch_bounds__(256, 2) void k_attn_bwd_d64r(int H, const bf16_t* __restrict__ q,
+                                                          const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                                                          int64_t ld, const bf16_t* __restrict__ o, int64_t ldo,
+                                                          const bf16_t* __restrict__ dout, int64_t ldd,
+                                                          const float* __restrict__ lse, float* __restrict__ delta,
+                                                          bf16_t* __restrict__ dq, int64_t lddq, bf16_t* __restrict__ dk,
+                                                          bf16_t* __restrict__ dv, int64_t lddkv, float scale,
+                                                          const uint32_t* __restrict__ mask_fwd,
+                                                          const uint32_t* __restrict__ mask_bwd, float dscale) {
+    __shared__ __attribute__((aligned(16))) char smem[NT * 2 * TILE + 2 * 64 * NT * 4];
+    int x, id;
+    block_coords<false>(x, id);
+    if (id & 1)
+        dkdv_res<DROP, NT>(id >> 1, smem, H, q, k, v, ld, dout, ldd, lse, delta, o, ldo, dk, dv, lddkv, scale, mask_bwd,
+                           dscale);
+    else
+        dq_res<DROP, NT>(id >> 1, smem, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale, mask_fwd,
+                         dscale);
+}
+
 }  // namespace
 
 namespace attn {
 // sequence-resident kernels for T <= 256 unless cg_set_tuning("attn_variant", 1) selects the ring
-// kernels (A/B and tests)
+// kernels (A/B and tests); attn_variant 2: resident dQ and dK/dV as two launches instead of one
 static bool resident(int64_t T) { return T <= 256 && g_attn_variant != 1; }
 #define RES_SWITCH(T, ...)                  \
     switch ((int)((T) / 64)) {              \
@@ -1058,6 +1128,24 @@ void launch_dq_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k
         k_attn_dq_d64<false><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
                                                    nullptr, 1.f);
 }
+void launch_bwd_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
+                    const bf16_t* o, int64_t ldo, const bf16_t* dout, int64_t ldd, const float* lse, float* delta,
+                    bf16_t* dq, int64_t lddq, bf16_t* dk, bf16_t* dv, int64_t lddkv, float scale, const DropArgs& d,
+                    hipStream_t st) {
+    if (resident(T) && g_attn_variant != 2) {   // 2: the two resident kernels back to back (A/B)
+        const dim3 grid(1, (unsigned)(2 * B * H));
+        RES_SWITCH(T, if (d.mask) k_attn_bwd_d64r<true, NT_><<<grid, 256, 0, st>>>(
+                              H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, dk, dv, lddkv, scale, d.mask,
+                              d.mask_bwd, d.dscale);
+                   else k_attn_bwd_d64r<false, NT_><<<grid, 256, 0, st>>>(
+                              H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, dk, dv, lddkv, scale, nullptr,
+                              nullptr, 1.f));
+        return;
+    }
+    launch_dq_d64(B, T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale, d, st);
+    launch_dkdv_d64(B, T, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale, d, st);
+}
+
 void launch_dkdv_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                      const bf16_t* dout, int64_t ldd, const float* lse, const float* delta, bf16_t* dk, bf16_t* dv,
                      int64_t lddkv, float scale, const DropArgs& d, hipStream_t st) {

@@ -669,10 +669,8 @@ extern "C" int cg_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D
             set_masks(d, mask, B, H, T);
         }
         const bf16_t *Q = (const bf16_t*)q, *K = (const bf16_t*)k, *V = (const bf16_t*)v, *DO = (const bf16_t*)dout;
-        attn::launch_dq_d64(B, T, (int)H, Q, K, V, ld_qkv, (const bf16_t*)o, ld_o, DO, ld_do, lse, delta, (bf16_t*)dq,
-                            ld_dqkv, scale, d, st);
-        attn::launch_dkdv_d64(B, T, (int)H, Q, K, V, ld_qkv, DO, ld_do, lse, delta, (bf16_t*)dk, (bf16_t*)dv, ld_dqkv,
-                              scale, d, st);
+        attn::launch_bwd_d64(B, T, (int)H, Q, K, V, ld_qkv, (const bf16_t*)o, ld_o, DO, ld_do, lse, delta,
+                             (bf16_t*)dq, ld_dqkv, (bf16_t*)dk, (bf16_t*)dv, ld_dqkv, scale, d, st);
     } else {
         dim3 grid(ceil_div(T, GB), (unsigned)(B * H));
         const size_t lds_dq = generic_lds<float>((int)D, 4, 1);

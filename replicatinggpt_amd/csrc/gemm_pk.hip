@@ -509,7 +509,7 @@ void launch_ek(unsigned grid, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
         L1(EK_SLAB);
         return;
     }
-    if constexpr (!AT_ && BM == 128 && BN == 128 && NBUF == 2) {
+    if constexpr (!AT_ && BM == 128 && BN == 128) {
         const bool needs_bias = e.kind >= CG_EPI_BIAS && e.kind <= CG_EPI_BIAS_DROP_RESID;
         const bool needs_resid = e.kind == CG_EPI_BIAS_RESID || e.kind == CG_EPI_BIAS_DROP_RESID;
         if (!(g_pk_flags & 2) && e.beta == 0.f && (!needs_bias || e.bias) && (!needs_resid || e.resid)) {

@@ -466,6 +466,38 @@ def test_attention_fast_block_shapes(T):
         assert relerr(dqkv[:, i * d:(i + 1) * d], t.grad.reshape(B * T, d)) < 3e-2
 
 
+@pytest.mark.parametrize("T", [256, 128, 64])
+@pytest.mark.parametrize("p", [0.0, 0.2])
+def test_attention_resident_kernels_match_ring_kernels(T, p):
+    """T <= 256 runs the sequence-resident kernels (forward; dQ and dK/dV merged into one launch
+    that computes delta itself).  Same per-tile arithmetic as the ring kernels (attn_variant 1)
+    and the two-launch resident backward (attn_variant 2): all three give identical bits."""
+    from replicatinggpt_amd import _lib as L
+    Fn = F()
+    lib = L.load()
+    B, H, D = 3, 6, 64
+    torch.manual_seed(40 + T)
+    d = H * D
+    qkv = (torch.randn(B * T, 3 * d) * 0.7).to(torch.bfloat16).to(DEV)
+    dout = torch.randn(B * T, d).to(torch.bfloat16).to(DEV)
+    call = torch.tensor([5], dtype=torch.int64, device=DEV)
+    scale = (3.0 * D) ** -0.5
+    outs = []
+    try:
+        for variant in (0, 1, 2):
+            L.check(lib.cg_set_tuning(b"attn_variant", variant))
+            o = torch.empty(B * T, d, dtype=torch.bfloat16, device=DEV)
+            lse, mask = Fn.attention_fwd(qkv, B, T, H, D, o, scale, p, 21, call, 4)
+            dqkv = Fn.attention_bwd(qkv, B, T, H, D, o, dout, lse, scale, p, 21, call, 4, mask)
+            torch.cuda.synchronize()
+            outs.append((o.cpu(), lse.cpu(), dqkv.cpu()))
+    finally:
+        L.check(lib.cg_set_tuning(b"attn_variant", 0))
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            assert torch.equal(a, b)
+
+
 def test_attention_forward_rescale_branch():
     """The forward's lazy rescale (running max moved only when a tile's max exceeds it by 2^8) with
     inputs that force it: one key row spiked against every query so that the max jumps at a late
