@@ -28,6 +28,12 @@ extern "C" {
 
 enum { CG_OK = 0, CG_EINVAL = 1, CG_EHIP = 2, CG_EUNSUPPORTED = 3 };
 enum { CG_F32 = 0, CG_BF16 = 1 };
+/* cg_epilogue_t.aux_dtype only: ReLU keep bits, uint32 words [M][ld_aux], bit n % 32 of word n / 32
+   of row m = (bf16 ReLU output (m, n) != 0).  CG_EPI_BIAS_RELU WRITES them (aux is an output there),
+   CG_EPI_RELU_BWD reads them instead of the bf16 ReLU output (1/16 of its bytes).  Only where
+   cg_gemm_relu_bits_supported() says so (bf16, split 1, beta 0, N % 64 == 0, persistent kernels);
+   elsewhere cg_gemm returns CG_EINVAL. */
+enum { CG_BITS = 2 };
 
 /* GEMM epilogues (applied to acc = sum_k A(m,k) B(n,k), per output element (m,n)) */
 enum {
@@ -138,6 +144,11 @@ int64_t cg_gemm_workspace(int64_t M, int64_t N, int split_k);
    -- the caller then computes the bias gradient with cg_colsum instead.                          */
 int cg_gemm_colpart_supported(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                               int64_t ldc);
+/* 1 if cg_gemm can write (CG_EPI_BIAS_RELU) and read (CG_EPI_RELU_BWD) CG_BITS ReLU keep bits for
+   this non-transposed-A bf16 problem (split 1, beta 0) under the current dispatch, else 0.  The
+   FeedForward uses them when both its W1 forward and its W2 dgrad products say yes.           */
+int cg_gemm_relu_bits_supported(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
+                                int64_t ldc);
 /* out[n] (=|+=) sum_r part[r*N + n] over rows r in order (fixed order: deterministic)          */
 int cg_reduce_rows(const float* part, int64_t rows, int64_t N, float* out, int accumulate, void* stream);
 int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CHARPT_LIB") or os.path.join(_HERE, "libcharpt_hip.so")   # CHARPT_LIB: A/B builds
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "charpt.h")
 
-CG_F32, CG_BF16 = 0, 1
+CG_F32, CG_BF16, CG_BITS = 0, 1, 2
 EPI_STORE, EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_RESID, EPI_BIAS_DROP_RESID, EPI_RELU_BWD = range(6)
 
 c_i64, c_int, c_dbl, c_flt, c_u64, P = ctypes.c_int64, ctypes.c_int, ctypes.c_double, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p
@@ -50,6 +50,7 @@ _SIGS = {
     "cg_layernorm_bwd_reduce": (c_int, [P, c_i64, c_i64, c_int, P, P, P, c_int, c_int, P]),
     "cg_gemm_workspace": (c_i64, [c_i64, c_i64, c_int]),
     "cg_gemm_colpart_supported": (c_int, [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64]),
+    "cg_gemm_relu_bits_supported": (c_int, [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64]),
     "cg_reduce_rows": (c_int, [P, c_i64, c_i64, P, c_int, P]),
     "cg_gemm": (c_int, [c_int, c_int, c_int, c_i64, c_i64, c_i64, P, c_i64, P, c_i64, P, c_int, c_i64,
                         ctypes.POINTER(Epilogue), c_int, P, P]),
@@ -124,6 +125,8 @@ def dtype_code(dt):
         return CG_F32
     if dt == torch.bfloat16:
         return CG_BF16
+    if dt == torch.int32:
+        return CG_BITS   # ReLU keep bits (uint32 words; cg_epilogue_t.aux only)
     raise TypeError(f"charpt: unsupported dtype {dt}")
 
 

@@ -416,6 +416,11 @@ extern "C" int cg_gemm_colpart_supported(int a_trans, int b_trans, int64_t M, in
     return gemm_colpart_supported(a_trans, b_trans, M, N, K, lda, ldb, ldc) ? 1 : 0;
 }
 
+extern "C" int cg_gemm_relu_bits_supported(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, int64_t lda,
+                                           int64_t ldb, int64_t ldc) {
+    return gemm_relu_bits_supported(a_trans, b_trans, M, N, K, lda, ldb, ldc) ? 1 : 0;
+}
+
 extern "C" int64_t cg_gemm_workspace(int64_t M, int64_t N, int split_k) {
     return split_k > 1 ? (int64_t)split_k * M * N * (int64_t)sizeof(float) : 0;
 }
@@ -435,6 +440,9 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
     if (op_dtype == CG_BF16 && fast_gemm_launch(a_trans, b_trans, M, N, K, (const bf16_t*)A, lda,
                                                 (const bf16_t*)B, ldb, C, c_dtype, ldc, e, split_k,
                                                 (float*)workspace, st)) {
+    } else if (e.aux_dtype == CG_BITS) {
+        set_error("cg_gemm: CG_BITS ReLU keep bits need a persistent bf16 kernel (cg_gemm_relu_bits_supported)");
+        return CG_EINVAL;
     } else if (e.colpart) {
         set_error("cg_gemm: colpart needs a persistent bf16 kernel (bf16 operands and output, NT/NN, beta 0, "
                   "split 1, M %% 128 == 0, default dispatch)");

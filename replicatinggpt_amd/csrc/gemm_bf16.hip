@@ -203,6 +203,17 @@ bool gemm_colpart_supported(int at, int bt, int64_t M, int64_t N, int64_t K, int
     return fast_shape_ok(M, N, K, lda, ldb, ldc, 1) && colpart_ok(pick_variant(at, M, N, 1), at, 1);
 }
 
+// CG_BITS ReLU keep bits are written / read by the same two kernels' item epilogues (64-column
+// wave fragments: k_gemm_pk 128x128, k_gemm_p8 256x256)
+static bool relu_bits_ok(int v, int at, int split_k, int64_t N) {
+    return colpart_ok(v, at, split_k) && N % 64 == 0;
+}
+
+bool gemm_relu_bits_supported(int at, int bt, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc) {
+    (void)bt;
+    return fast_shape_ok(M, N, K, lda, ldb, ldc, 1) && relu_bits_ok(pick_variant(at, M, N, 1), at, 1, N);
+}
+
 bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
                       int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, float* ws,
                       hipStream_t st) {
@@ -218,8 +229,12 @@ bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf1
         const int64_t nkt = K / FBK, nkc = (nkt + split_k - 1) / split_k;
         if (v != 9 || (split_k - 1) * nkc >= nkt) return false;
     }
-    if (e.colpart && (!colpart_ok(v, at, split_k) || e.kind != CG_EPI_RELU_BWD || e.aux_dtype != CG_BF16 ||
-                      e.beta != 0.f || c_dtype != CG_BF16))
+    if (e.colpart && (!colpart_ok(v, at, split_k) || e.kind != CG_EPI_RELU_BWD ||
+                      (e.aux_dtype != CG_BF16 && e.aux_dtype != CG_BITS) || e.beta != 0.f || c_dtype != CG_BF16))
+        return false;
+    if (e.aux_dtype == CG_BITS &&
+        (!relu_bits_ok(v, at, split_k, N) || (e.kind != CG_EPI_RELU_BWD && e.kind != CG_EPI_BIAS_RELU) ||
+         (e.kind == CG_EPI_BIAS_RELU && !e.bias) || !e.aux || e.beta != 0.f || c_dtype != CG_BF16))
         return false;
     if (v >= 20 && p8_gemm_launch(v, at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st))
         return true;

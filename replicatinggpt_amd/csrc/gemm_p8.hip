@@ -227,17 +227,32 @@ void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
                 // block (the layout of k_gemm_pk's colpart), 4 rows per lane then a butterfly over the
                 // column group's 16 lanes.  The partial stores go before the item's FM x FN output
                 // stores, which stay the youngest EPI_OPS vector-memory operations.
+                if (FN == 4 && epi.aux_dtype == CG_BITS) {   // ReLU keep bits: one word pair per row
 #pragma unroll
-                for (int i = 0; i < FM; ++i)
+                    for (int i = 0; i < FM; ++i) {
+                        const uint2 w =
+                            *(const uint2*)((const uint32_t*)epi.aux + (mr + 16 * i) * epi.ld_aux + ((nc - 4 * (lane >> 4)) >> 5));
 #pragma unroll
-                    for (int j = 0; j < FN; ++j) {
-                        const uint2 h = *(const uint2*)((const bf16_t*)epi.aux + (mr + 16 * i) * epi.ld_aux + nc + 16 * j);
-                        fv4& v = acc[i][j];
-                        v[0] = bf2f(f2bf(__uint_as_float(h.x << 16) > 0.f ? v[0] : 0.f));
-                        v[1] = bf2f(f2bf(__uint_as_float(h.x & 0xffff0000u) > 0.f ? v[1] : 0.f));
-                        v[2] = bf2f(f2bf(__uint_as_float(h.y << 16) > 0.f ? v[2] : 0.f));
-                        v[3] = bf2f(f2bf(__uint_as_float(h.y & 0xffff0000u) > 0.f ? v[3] : 0.f));
+                        for (int j = 0; j < FN; ++j) {
+                            const uint32_t kb = relu_nib(w, j, lane);
+                            fv4& v = acc[i][j];
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) v[q] = bf2f(f2bf(((kb >> q) & 1u) ? v[q] : 0.f));
+                        }
                     }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < FM; ++i)
+#pragma unroll
+                        for (int j = 0; j < FN; ++j) {
+                            const uint2 h = *(const uint2*)((const bf16_t*)epi.aux + (mr + 16 * i) * epi.ld_aux + nc + 16 * j);
+                            fv4& v = acc[i][j];
+                            v[0] = bf2f(f2bf(__uint_as_float(h.x << 16) > 0.f ? v[0] : 0.f));
+                            v[1] = bf2f(f2bf(__uint_as_float(h.x & 0xffff0000u) > 0.f ? v[1] : 0.f));
+                            v[2] = bf2f(f2bf(__uint_as_float(h.y << 16) > 0.f ? v[2] : 0.f));
+                            v[3] = bf2f(f2bf(__uint_as_float(h.y & 0xffff0000u) > 0.f ? v[3] : 0.f));
+                        }
+                }
 #pragma unroll
                 for (int ib = 0; ib < FM / 4; ++ib) {
                     float* cp = epi.colpart + ((mr - (lane & 15) + 64 * ib) >> 6) * N + nc;
@@ -267,6 +282,24 @@ void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
                             make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
                         acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
                     }
+            } else if (FN == 4 && split_k == 1 && epi.kind == CG_EPI_BIAS_RELU && epi.aux_dtype == CG_BITS) {
+                // bias + ReLU, bf16 output and its ReLU keep bits (checked on the host: bias, bf16, beta 0)
+                uint32_t kb[FM][4];
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const float4 b = *(const float4*)(epi.bias + nc + 16 * j);
+#pragma unroll
+                    for (int i = 0; i < FM; ++i) {
+                        fv4 v = acc[i][j];
+                        v[0] = fmaxf(v[0] + b.x, 0.f); v[1] = fmaxf(v[1] + b.y, 0.f);
+                        v[2] = fmaxf(v[2] + b.z, 0.f); v[3] = fmaxf(v[3] + b.w, 0.f);
+                        const uint2 pk = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+                        *(uint2*)((bf16_t*)Cv + (mr + 16 * i) * ldc + nc + 16 * j) = pk;
+                        kb[i][j & 3] = nz4_bf16(pk);
+                        acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
+                    }
+                }
+                relu_bits_store<FM>(kb, (uint32_t*)epi.aux, epi.ld_aux, mr, nc - 4 * (lane >> 4), lane);
             } else {
 #pragma unroll
                 for (int i = 0; i < FM; ++i)

@@ -121,23 +121,40 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
         return;
     }
     if (kind == CG_EPI_RELU_BWD) {
-        if (epi.aux_dtype == CG_BF16) {
-            uint2 h[4][4];
+        if (epi.aux_dtype == CG_BF16 || epi.aux_dtype == CG_BITS) {
+            if (epi.aux_dtype == CG_BITS) {   // keep bits: one 8-B word pair per row instead of 4 x 8 B of bf16
+                const int lane = threadIdx.x & 63;
+                uint2 w[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < 4; ++i)
+                    w[i] = *(const uint2*)((const uint32_t*)epi.aux + (mr + 16 * i) * epi.ld_aux + ((nc - 4 * (lane >> 4)) >> 5));
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    h[i][j] = *(const uint2*)((const bf16_t*)epi.aux + (mr + 16 * i) * epi.ld_aux + nc + 16 * j);
+                for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t kb = relu_nib(w[i], j, lane);
+                        fv4& v = acc[i][j];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    fv4& v = acc[i][j];
-                    v[0] = __uint_as_float(h[i][j].x << 16) > 0.f ? v[0] : 0.f;
-                    v[1] = __uint_as_float(h[i][j].x & 0xffff0000u) > 0.f ? v[1] : 0.f;
-                    v[2] = __uint_as_float(h[i][j].y << 16) > 0.f ? v[2] : 0.f;
-                    v[3] = __uint_as_float(h[i][j].y & 0xffff0000u) > 0.f ? v[3] : 0.f;
-                }
+                        for (int q = 0; q < 4; ++q) v[q] = ((kb >> q) & 1u) ? v[q] : 0.f;
+                    }
+            } else {
+                uint2 h[4][4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        h[i][j] = *(const uint2*)((const bf16_t*)epi.aux + (mr + 16 * i) * epi.ld_aux + nc + 16 * j);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        fv4& v = acc[i][j];
+                        v[0] = __uint_as_float(h[i][j].x << 16) > 0.f ? v[0] : 0.f;
+                        v[1] = __uint_as_float(h[i][j].x & 0xffff0000u) > 0.f ? v[1] : 0.f;
+                        v[2] = __uint_as_float(h[i][j].y << 16) > 0.f ? v[2] : 0.f;
+                        v[3] = __uint_as_float(h[i][j].y & 0xffff0000u) > 0.f ? v[3] : 0.f;
+                    }
+            }
             if (epi.colpart) {
                 // the consumer's bias gradient, fused: column sums of this wave's 64 rows (rows
                 // 16i + lane&15 of each column 16j + 4(lane>>4) + q: 4 rows per lane, then a
@@ -219,6 +236,23 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
                 v[0] = r[i][j].x + v[0]; v[1] = r[i][j].y + v[1]; v[2] = r[i][j].z + v[2]; v[3] = r[i][j].w + v[3];
                 store4_plain(v, m, n, Cv, c_dtype, ldc);
             }
+        return;
+    }
+    if (kind == CG_EPI_BIAS_RELU && epi.aux_dtype == CG_BITS) {   // bf16 output + its ReLU keep bits
+        const int lane = threadIdx.x & 63;
+        uint32_t kb[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                fv4 v = acc[i][j];
+                v[0] = fmaxf(v[0] + bv[j].x, 0.f); v[1] = fmaxf(v[1] + bv[j].y, 0.f);
+                v[2] = fmaxf(v[2] + bv[j].z, 0.f); v[3] = fmaxf(v[3] + bv[j].w, 0.f);
+                const uint2 pk = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+                *(uint2*)((bf16_t*)Cv + (mr + 16 * i) * ldc + nc + 16 * j) = pk;
+                kb[i][j] = nz4_bf16(pk);
+            }
+        relu_bits_store<4>(kb, (uint32_t*)epi.aux, epi.ld_aux, mr, nc - 4 * (lane >> 4), lane);
         return;
     }
     const bool drop = kind == CG_EPI_BIAS_DROP_RESID && epi.thr;

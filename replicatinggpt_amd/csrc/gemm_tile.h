@@ -69,7 +69,11 @@ __device__ __forceinline__ void epi_store8(float (&v)[8], int64_t m, int64_t n, 
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = ((kb >> q) & 1u) ? v[q] * epi.dscale : 0.f;
     } else if (kind == CG_EPI_RELU_BWD) {
-        if (epi.aux_dtype == CG_BF16) {
+        if (epi.aux_dtype == CG_BITS) {   // keep bits: columns n..n+3 (n % 4 == 0) share one word
+            const uint32_t kb = (((const uint32_t*)epi.aux)[m * epi.ld_aux + (n >> 5)] >> (n & 31)) & 0xfu;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = ((kb >> q) & 1u) ? v[q] : 0.f;
+        } else if (epi.aux_dtype == CG_BF16) {
             const uint4 h = *(const uint4*)((const bf16_t*)epi.aux + m * epi.ld_aux + n);
             const uint32_t hw[4] = {h.x, h.y, h.z, h.w};
 #pragma unroll
@@ -131,7 +135,11 @@ __device__ __forceinline__ void epi_store4(fv4 v, int64_t m, int64_t n, int64_t 
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = ((kb >> q) & 1u) ? v[q] * epi.dscale : 0.f;
     } else if (kind == CG_EPI_RELU_BWD) {
-        if (epi.aux_dtype == CG_BF16) {
+        if (epi.aux_dtype == CG_BITS) {   // keep bits: columns n..n+3 (n % 4 == 0) share one word
+            const uint32_t kb = (((const uint32_t*)epi.aux)[m * epi.ld_aux + (n >> 5)] >> (n & 31)) & 0xfu;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = ((kb >> q) & 1u) ? v[q] : 0.f;
+        } else if (epi.aux_dtype == CG_BF16) {
             const uint2 h = *(const uint2*)((const bf16_t*)epi.aux + m * epi.ld_aux + n);
             v[0] = __uint_as_float(h.x << 16) > 0.f ? v[0] : 0.f;
             v[1] = __uint_as_float(h.x & 0xffff0000u) > 0.f ? v[1] : 0.f;
@@ -224,4 +232,34 @@ __device__ __forceinline__ void epilogue(fv4 (&acc)[4][4], char* smem, int tid, 
 }
 
 }  // namespace gt
+
+// ReLU keep bits (CG_BITS) of a wave's FM x 4 fragments of 16x16 (64 columns from the wave's column
+// base cb = nc - 4 (lane >> 4)); nib[i][j] bit q <-> (row rb + 16 i, column cb + 16 j + 4 (lane >> 4)
+// + q), rb = this lane's row.  Word jp of a row = columns cb + 32 jp .. + 31 (bit = column - base).
+// Lanes l, l^16, l^32, l^48 hold the four column quarters of each fragment row: OR-reduced across
+// them, then lane group g = lane >> 4 stores the two words of rows i = g (mod 4) as one 8-B store.
+template <int FM>
+__device__ __forceinline__ void relu_bits_store(const uint32_t (&nib)[FM][4], uint32_t* bits, int64_t ldw, int64_t rb,
+                                                int64_t cb, int lane) {
+    const int g = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+        uint32_t w0 = (nib[i][0] << (4 * g)) | (nib[i][1] << (16 + 4 * g));
+        uint32_t w1 = (nib[i][2] << (4 * g)) | (nib[i][3] << (16 + 4 * g));
+        w0 |= (uint32_t)__shfl_xor((int)w0, 16, 64);
+        w1 |= (uint32_t)__shfl_xor((int)w1, 16, 64);
+        w0 |= (uint32_t)__shfl_xor((int)w0, 32, 64);
+        w1 |= (uint32_t)__shfl_xor((int)w1, 32, 64);
+        if ((i & 3) == g) *(uint2*)(bits + (rb + 16 * i) * ldw + (cb >> 5)) = make_uint2(w0, w1);
+    }
+}
+// nonzero-ness of the 4 bf16 values of a packed fragment (bit q <-> value q): the ReLU keep bits
+__device__ __forceinline__ uint32_t nz4_bf16(uint2 pk) {
+    return (uint32_t)((pk.x & 0x7fffu) != 0) | ((uint32_t)((pk.x & 0x7fff0000u) != 0) << 1) |
+           ((uint32_t)((pk.y & 0x7fffu) != 0) << 2) | ((uint32_t)((pk.y & 0x7fff0000u) != 0) << 3);
+}
+// the keep nibble of fragment (i, j) from its row's two words (uint2 at column base cb)
+__device__ __forceinline__ uint32_t relu_nib(uint2 w, int j, int lane) {
+    return (((j >> 1) ? w.y : w.x) >> (16 * (j & 1) + 4 * (lane >> 4))) & 0xfu;
+}
 }  // namespace cg

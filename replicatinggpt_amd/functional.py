@@ -82,6 +82,8 @@ SIDE = SideStream()
 LN_REDUCE_SIDE = os.environ.get("CHARPT_LN_REDUCE_SIDE", "1") != "0"
 # FFN b1 gradient fused into the ReLU-backward dgrad epilogue (CHARPT_FUSE_COLPART=0: separate colsum)
 FUSE_COLPART = os.environ.get("CHARPT_FUSE_COLPART", "1") != "0"
+# ReLU keep bits (1 bit per hidden unit) for the W2 dgrad instead of re-reading the bf16 h: set 0 for A/B
+RELU_BITS = os.environ.get("CHARPT_RELU_BITS", "1") != "0"
 # Measurement-only what-if switches (results are WRONG with any of them): CHARPT_WHATIF=skip_wgrad,
 # skip_attn, skip_lnbwd drop those kernels from the step to see how much of the step time they hold.
 WHATIF = set(filter(None, os.environ.get("CHARPT_WHATIF", "").split(",")))
@@ -269,6 +271,18 @@ def _colpart_ok(dy2, w, aux, out_ld):
     M, K = dy2.shape
     F = w.shape[1]
     return bool(L.load().cg_gemm_colpart_supported(0, 1, M, F, K, dy2.stride(0), w.stride(0), out_ld))
+
+
+def _relu_bits_ok(a, w1, w2, F):
+    """Whether the FeedForward can keep ReLU keep bits instead of reading h back in its W2 dgrad:
+    both its W1 forward (writes them) and W2 dgrad (reads them) products must take a persistent
+    kernel (cg_gemm_relu_bits_supported, asked from the library itself)."""
+    if not (RELU_BITS and _is_bf16(a.dtype) and a.is_cuda and a.stride(1) == 1):
+        return False
+    M, C = a.shape
+    lib = L.load()
+    return bool(lib.cg_gemm_relu_bits_supported(0, 0, M, F, C, a.stride(0), w1.stride(0), F) and
+                lib.cg_gemm_relu_bits_supported(0, 1, M, F, C, C, w2.stride(0), F))
 
 
 def colsum_into(x2, out, beta):
@@ -521,11 +535,19 @@ class FFNSublayerFn(torch.autograd.Function):
         a, mean, rstd = layernorm(x2, ln_w.master, ln_b.master, act)
         F4 = w1.master.shape[0]
         h = torch.empty((B * T, F4), dtype=act, device=x.device)
-        linear_fwd(a, w1.operand(act), h, "bias_relu", bias=b1.master)
+        bits = None
+        if _relu_bits_ok(a, w1.operand(act), w2.operand(act), F4):
+            # the W2 dgrad's ReLU mask as 1 bit per element (h itself stays for the W2 weight gradient)
+            bits = torch.empty((B * T, F4 // 32), dtype=torch.int32, device=x.device)
+            w1op = w1.operand(act)
+            ops.gemm_bias_relu_bits(a, w1op, h, B * T, F4, C, a.stride(0), w1op.stride(0), h.stride(0), b1.master,
+                                    bits, bits.stride(0))
+        else:
+            linear_fwd(a, w1.operand(act), h, "bias_relu", bias=b1.master)
         out = torch.empty((B * T, C), dtype=torch.float32, device=x.device)
         linear_fwd(h, w2.operand(act), out, "bias_drop_resid", bias=b2.master, resid=x2, dropout_p=lc.p,
                    seed=lc.seed, rng_call=lc.rng_call, site=lc.site)
-        ctx.save_for_backward(x2, a, mean, rstd, h)
+        ctx.save_for_backward(x2, a, mean, rstd, h, bits)
         ctx.lc, ctx.regs, ctx.shape = lc, (ln_w, ln_b, w1, b1, w2, b2), (B, T, C)
         ctx.in_link = _link_of(x)
         ctx.link = GradLink(lc.p, lc.seed, lc.rng_call, lc.site, b2, act)
@@ -535,7 +557,7 @@ class FFNSublayerFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        x2, a, mean, rstd, h = ctx.saved_tensors
+        x2, a, mean, rstd, h, bits = ctx.saved_tensors
         lc = ctx.lc
         ln_w, ln_b, w1, b1, w2, b2 = ctx.regs
         B, T, C = ctx.shape
@@ -563,10 +585,11 @@ class FFNSublayerFn(torch.autograd.Function):
             M, F4 = h.shape
             part = torch.empty((M // 64, F4), dtype=torch.float32, device=dev)
             wt = w2.operand(act)
+            mk = h if bits is None else bits
             ops.gemm_relu_bwd_colpart(dz2, wt, dz1, M, F4, dz2.shape[1], dz2.stride(0), wt.stride(0), dz1.stride(0),
-                                      h, h.stride(0), part)
+                                      mk, mk.stride(0), part)
         else:
-            linear_dgrad(dz2, w2.operand(act), dz1, "relu_bwd", aux=h)
+            linear_dgrad(dz2, w2.operand(act), dz1, "relu_bwd", aux=h if bits is None else bits)
         with SIDE.run(dev, dz1, a, part):
             if g_w1 is not None:
                 linear_wgrad(dz1, a, g_w1, beta_w1)

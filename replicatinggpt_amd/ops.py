@@ -153,6 +153,17 @@ def gemm(a: Tensor, b: Tensor, out: Tensor, op_bf16: bool, a_trans: bool, b_tran
             "gemm")
 
 
+@_op("gemm_bias_relu_bits", ("out", "bits"))
+def gemm_bias_relu_bits(a: Tensor, b: Tensor, out: Tensor, M: int, N: int, K: int, lda: int, ldb: int, ldc: int,
+                        bias: Tensor, bits: Tensor, ld_bits: int) -> None:
+    """out = bf16 relu(a[M,K] @ b[N,K]^T + bias) and its ReLU keep bits (CG_BITS: int32 words
+    [M, ld_bits], bit n % 32 of word n / 32 = out[m, n] != 0) for the ReLU-backward dgrad.  Fails
+    (CG_EINVAL) unless cg_gemm_relu_bits_supported."""
+    e = L.Epilogue(L.EPI_BIAS_RELU, L.ptr(bias), None, 0, L.ptr(bits), L.CG_BITS, ld_bits, 0.0, 0, None, 0, 0.0)
+    L.check(L.load().cg_gemm(L.CG_BF16, 0, 0, M, N, K, L.ptr(a), lda, L.ptr(b), ldb, L.ptr(out),
+                             L.dtype_code(out.dtype), ldc, e, 1, None, _s(out)), "gemm_bias_relu_bits")
+
+
 @_op("gemm_relu_bwd_colpart", ("out", "colpart"))
 def gemm_relu_bwd_colpart(a: Tensor, b: Tensor, out: Tensor, M: int, N: int, K: int, lda: int, ldb: int, ldc: int,
                           aux: Tensor, ld_aux: int, colpart: Tensor) -> None:

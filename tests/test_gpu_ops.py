@@ -125,6 +125,44 @@ def test_layernorm_bwd_rows_then_reduce_is_bitwise_ex(C, with_link):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("M,Fh,C", [(2048, 1536, 384), (16384, 3072, 768)])
+def test_relu_keep_bits_roundtrip(M, Fh, C):
+    """FeedForward's ReLU keep bits (CG_BITS): the W1 forward with bits gives the same bf16 h as the
+    plain bias+ReLU epilogue and bits == (h != 0) packed 32 per word; the W2 ReLU-backward dgrad
+    reading the bits (plain and with the fused b1 column partials) equals the one reading h, bit for
+    bit.  C2 shapes take the 128x128 kernel, the C4-width ones the 8-wave 256x256 kernel."""
+    Fn = F()
+    O = ops()
+    torch.manual_seed(8)
+    a = (torch.randn(M, C, device=DEV) * 0.5).to(torch.bfloat16)
+    w1 = (torch.randn(Fh, C, device=DEV) * 0.05).to(torch.bfloat16)
+    b1 = torch.randn(Fh, device=DEV) * 0.1
+    w2 = (torch.randn(C, Fh, device=DEV) * 0.05).to(torch.bfloat16)
+    dz2 = torch.randn(M, C, device=DEV).to(torch.bfloat16)
+    assert Fn._relu_bits_ok(a, w1, w2, Fh)
+    h_ref = torch.empty(M, Fh, dtype=torch.bfloat16, device=DEV)
+    Fn.linear_fwd(a, w1, h_ref, "bias_relu", bias=b1)
+    h = torch.empty_like(h_ref)
+    bits = torch.empty(M, Fh // 32, dtype=torch.int32, device=DEV)
+    O.gemm_bias_relu_bits(a, w1, h, M, Fh, C, C, C, Fh, b1, bits, Fh // 32)
+    torch.cuda.synchronize()
+    assert torch.equal(h, h_ref)
+    nz = (h.view(torch.int16) & 0x7FFF) != 0
+    weights = (torch.ones(32, dtype=torch.int64, device=DEV) << torch.arange(32, device=DEV))
+    want = (nz.view(M, Fh // 32, 32).long() * weights).sum(-1)
+    assert torch.equal(bits.long() & 0xFFFFFFFF, want)
+    d_ref, d_bits = torch.empty_like(h), torch.empty_like(h)
+    Fn.linear_dgrad(dz2, w2, d_ref, "relu_bwd", aux=h)
+    Fn.linear_dgrad(dz2, w2, d_bits, "relu_bwd", aux=bits)
+    p_ref, p_bits = (torch.empty(M // 64, Fh, device=DEV) for _ in range(2))
+    c_ref, c_bits = torch.empty_like(h), torch.empty_like(h)
+    O.gemm_relu_bwd_colpart(dz2, w2, c_ref, M, Fh, C, C, Fh, Fh, h, Fh, p_ref)
+    O.gemm_relu_bwd_colpart(dz2, w2, c_bits, M, Fh, C, C, Fh, Fh, bits, Fh // 32, p_bits)
+    torch.cuda.synchronize()
+    assert torch.equal(d_ref, d_bits) and torch.equal(c_ref, c_bits) and torch.equal(p_ref, p_bits)
+    assert torch.equal(c_ref, d_ref)
+
+
 @pytest.mark.parametrize("C", [384, 768, 1024, 512, 126])
 def test_layernorm_bwd_link_dropout_matches_oracle(C):
     """The LayerNorm backward's consumer copy with FeedForward's output dropout (GPT1.py:146; the
