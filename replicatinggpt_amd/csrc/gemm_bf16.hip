@@ -238,6 +238,7 @@ bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf1
         return false;
     if (v >= 20 && p8_gemm_launch(v, at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st))
         return true;
+    if (e.aux_dtype == CG_BITS && v != 9) return false;   // only the two persistent kernels read / write keep bits
     if (v >= 20) v = 2;
     if (v >= 5 && glds_gemm_launch(v, at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st))
         return true;

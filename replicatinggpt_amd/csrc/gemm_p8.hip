@@ -72,8 +72,16 @@ struct Geo8 {
 };
 
 // WM = waves along M (8 / WM along N); per-wave tile (BM/WM) x (BN/(8/WM)) in 16x16 fragments.
-// COLPART: the ReLU-backward epilogue with fused bias-gradient column partials (bf16 output)
-template <bool AT, bool BT, int BM, int BN, int WM, int NBUF, bool COLPART>
+// EP: the item epilogue, one per instantiation (each path alone keeps the 256x256 tile's 128
+// accumulators out of scratch; both colpart mask forms in one kernel spilled 228 B/lane and ran the
+// C4 FFN2 dgrad at 1.04 ms instead of 0.36):
+//   P8_GENERIC    per-fragment epi_store4 (any kind) or split-K slabs
+//   P8_CP_BF16    ReLU backward + fused bias-gradient column partials, mask from the bf16 ReLU output
+//   P8_CP_BITS    the same with the mask from CG_BITS keep bits
+//   P8_RELU_BITS  bias + ReLU, bf16 output and its CG_BITS keep bits
+//   P8_BWD_BITS   ReLU backward from CG_BITS keep bits, no column partials
+enum { P8_GENERIC = 0, P8_CP_BF16 = 1, P8_CP_BITS = 2, P8_RELU_BITS = 3, P8_BWD_BITS = 4 };
+template <bool AT, bool BT, int BM, int BN, int WM, int NBUF, int EP>
 __global__ __launch_bounds__(P8_THREADS, (Geo8<BM, BN, NBUF>::OCC))
 void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
                const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype, int64_t ldc,
@@ -221,13 +229,14 @@ void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
             int sp;
             decode(cj, m0, n0, sp);
             const int64_t mr = m0 + wm * (BM / WM) + (lane & 15), nc = n0 + wn * (BN / WN) + 4 * (lane >> 4);
-            if (COLPART) {
+            constexpr bool COLPART = EP == P8_CP_BF16 || EP == P8_CP_BITS;
+            if constexpr (COLPART) {
                 // ReLU backward (bf16 ReLU output as the mask, beta 0: checked on the host) with the
                 // consumer's bias gradient fused: column sums of the bf16-rounded outputs per 64-row
                 // block (the layout of k_gemm_pk's colpart), 4 rows per lane then a butterfly over the
                 // column group's 16 lanes.  The partial stores go before the item's FM x FN output
                 // stores, which stay the youngest EPI_OPS vector-memory operations.
-                if (FN == 4 && epi.aux_dtype == CG_BITS) {   // ReLU keep bits: one word pair per row
+                if constexpr (EP == P8_CP_BITS) {   // ReLU keep bits: one word pair per row (FN == 4)
 #pragma unroll
                     for (int i = 0; i < FM; ++i) {
                         const uint2 w =
@@ -282,7 +291,24 @@ void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
                             make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
                         acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
                     }
-            } else if (FN == 4 && split_k == 1 && epi.kind == CG_EPI_BIAS_RELU && epi.aux_dtype == CG_BITS) {
+            } else if constexpr (EP == P8_BWD_BITS) {
+                // ReLU backward from keep bits (bf16 output, beta 0: checked on the host)
+#pragma unroll
+                for (int i = 0; i < FM; ++i) {
+                    const uint2 w =
+                        *(const uint2*)((const uint32_t*)epi.aux + (mr + 16 * i) * epi.ld_aux + ((nc - 4 * (lane >> 4)) >> 5));
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) {
+                        const uint32_t kb = relu_nib(w, j, lane);
+                        fv4 v = acc[i][j];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) v[q] = ((kb >> q) & 1u) ? v[q] : 0.f;
+                        *(uint2*)((bf16_t*)Cv + (mr + 16 * i) * ldc + nc + 16 * j) =
+                            make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+                        acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
+                    }
+                }
+            } else if constexpr (EP == P8_RELU_BITS) {
                 // bias + ReLU, bf16 output and its ReLU keep bits (checked on the host: bias, bf16, beta 0)
                 uint32_t kb[FM][4];
 #pragma unroll
@@ -332,7 +358,7 @@ int cu_count8() {
 }
 
 template <int BM, int BN, int WM, int NBUF>
-void launch8(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
+bool launch8(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
              int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, float* ws,
              hipStream_t st) {
     using G = Geo8<BM, BN, NBUF>;
@@ -342,17 +368,32 @@ void launch8(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, i
     int64_t slots = (int64_t)cu_count8() * occ;
     if (g_gemm_max_grid > 0 && g_gemm_max_grid < slots) slots = g_gemm_max_grid;
     const unsigned grid = (unsigned)(nitems < slots ? nitems : slots);
-#define FG(AT_, BT_, CP_)                                                                                \
-    k_gemm_p8<AT_, BT_, BM, BN, WM, NBUF, CP_><<<grid, P8_THREADS, G::LDS, st>>>(M, N, K, A, lda, B, ldb, C,     \
+#define FG(AT_, BT_, EP_)                                                                                \
+    k_gemm_p8<AT_, BT_, BM, BN, WM, NBUF, EP_><<<grid, P8_THREADS, G::LDS, st>>>(M, N, K, A, lda, B, ldb, C,     \
                                                                                  c_dtype, ldc, e, split_k, kchunk, ws)
-    if (e.colpart) {   // non-transposed A, split 1, RELU_BWD with bf16 aux and output (host-checked)
-        if (!bt) FG(false, false, true);
-        else FG(false, true, true);
-    } else if (!at && !bt) FG(false, false, false);
-    else if (!at && bt) FG(false, true, false);
-    else if (at && !bt) FG(true, false, false);
-    else FG(true, true, false);
+    // keep bits (host-checked: split 1, bf16 output, beta 0) need 64-column wave fragments (FN == 4)
+    const bool bits = e.aux_dtype == CG_BITS;
+    constexpr bool FN4 = BN / (8 / WM) == 64;
+    if (bits) {
+        if constexpr (FN4) {
+            if (e.colpart && !at && bt) FG(false, true, P8_CP_BITS);
+            else if (e.colpart && !at) FG(false, false, P8_CP_BITS);
+            else if (e.kind == CG_EPI_BIAS_RELU && !at && !bt) FG(false, false, P8_RELU_BITS);
+            else if (e.kind == CG_EPI_RELU_BWD && !at && bt) FG(false, true, P8_BWD_BITS);
+            else return false;
+            return true;
+        }
+        return false;
+    }
+    if (e.colpart) {   // non-transposed A, split 1, RELU_BWD with bf16 aux, bf16 output (host-checked)
+        if (!bt) FG(false, false, P8_CP_BF16);
+        else FG(false, true, P8_CP_BF16);
+    } else if (!at && !bt) FG(false, false, P8_GENERIC);
+    else if (!at && bt) FG(false, true, P8_GENERIC);
+    else if (at && !bt) FG(true, false, P8_GENERIC);
+    else FG(true, true, P8_GENERIC);
 #undef FG
+    return true;
 }
 
 }  // namespace
@@ -376,24 +417,19 @@ bool p8_gemm_launch(int v, int at, int bt, int64_t M, int64_t N, int64_t K, cons
     switch (v) {
         case 21:
             if (M % 256 || N % 128) return false;
-            launch8<256, 128, 4, 3>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
-            return true;
+            return launch8<256, 128, 4, 3>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
         case 22:
             if (M % 128 || N % 256) return false;
-            launch8<128, 256, 2, 3>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
-            return true;
+            return launch8<128, 256, 2, 3>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
         case 23:
             if (M % 128 || N % 128) return false;
-            launch8<128, 128, 2, 4>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
-            return true;
+            return launch8<128, 128, 2, 4>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
         case 24:
             if (M % 256 || N % 256) return false;
-            launch8<256, 256, 2, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
-            return true;
+            return launch8<256, 256, 2, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
         case 25:
             if (M % 256 || N % 128) return false;
-            launch8<256, 128, 4, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
-            return true;
+            return launch8<256, 128, 4, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
         default:
             return false;
     }

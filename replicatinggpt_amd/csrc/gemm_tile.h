@@ -69,11 +69,7 @@ __device__ __forceinline__ void epi_store8(float (&v)[8], int64_t m, int64_t n, 
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = ((kb >> q) & 1u) ? v[q] * epi.dscale : 0.f;
     } else if (kind == CG_EPI_RELU_BWD) {
-        if (epi.aux_dtype == CG_BITS) {   // keep bits: columns n..n+3 (n % 4 == 0) share one word
-            const uint32_t kb = (((const uint32_t*)epi.aux)[m * epi.ld_aux + (n >> 5)] >> (n & 31)) & 0xfu;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = ((kb >> q) & 1u) ? v[q] : 0.f;
-        } else if (epi.aux_dtype == CG_BF16) {
+        if (epi.aux_dtype == CG_BF16) {
             const uint4 h = *(const uint4*)((const bf16_t*)epi.aux + m * epi.ld_aux + n);
             const uint32_t hw[4] = {h.x, h.y, h.z, h.w};
 #pragma unroll
@@ -135,11 +131,7 @@ __device__ __forceinline__ void epi_store4(fv4 v, int64_t m, int64_t n, int64_t 
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = ((kb >> q) & 1u) ? v[q] * epi.dscale : 0.f;
     } else if (kind == CG_EPI_RELU_BWD) {
-        if (epi.aux_dtype == CG_BITS) {   // keep bits: columns n..n+3 (n % 4 == 0) share one word
-            const uint32_t kb = (((const uint32_t*)epi.aux)[m * epi.ld_aux + (n >> 5)] >> (n & 31)) & 0xfu;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = ((kb >> q) & 1u) ? v[q] : 0.f;
-        } else if (epi.aux_dtype == CG_BF16) {
+        if (epi.aux_dtype == CG_BF16) {
             const uint2 h = *(const uint2*)((const bf16_t*)epi.aux + m * epi.ld_aux + n);
             v[0] = __uint_as_float(h.x << 16) > 0.f ? v[0] : 0.f;
             v[1] = __uint_as_float(h.x & 0xffff0000u) > 0.f ? v[1] : 0.f;
