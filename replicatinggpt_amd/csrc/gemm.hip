@@ -379,6 +379,7 @@ int g_gemm_max_grid = 0;
 int g_skip_splitk_reduce = 0;  // measurement knob (WRONG results): time a step without the split-K reduce
 extern int g_attn_variant;  // attention_d64.hip
 extern int g_ln_rpb;  // layernorm.hip
+extern int g_ln_waves;  // layernorm.hip
 }
 
 extern "C" int cg_set_tuning(const char* key, int value) {
@@ -401,6 +402,10 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     }
     if (!strcmp(key, "skip_splitk_reduce")) {
         g_skip_splitk_reduce = value;
+        return CG_OK;
+    }
+    if (!strcmp(key, "ln_waves")) {   // takes effect for workspaces sized after the call
+        g_ln_waves = value;
         return CG_OK;
     }
     if (!strcmp(key, "ln_rpb")) {   // takes effect for workspaces sized after the call

@@ -141,18 +141,26 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ x, con
 // Backward rows per block: sized so the grid has ~512 blocks (2 per CU) at any token count, 8..256,
 // a multiple of the 8 waves.  The per-block column partials (dgamma, dbeta, consumer bias) are
 // [nblk][NP*C]: 512 x 2304 floats at C4.
-constexpr int LN_BWD_WAVES = 8;
 namespace cg {
-int g_ln_rpb = 0;   // cg_set_tuning("ln_rpb"): rows per backward block (0 = automatic)
+int g_ln_rpb = 0;     // cg_set_tuning("ln_rpb"): rows per backward block (0 = automatic)
+int g_ln_waves = 0;   // cg_set_tuning("ln_waves"): waves per backward block, 4 or 8 (0 = automatic)
 }  // namespace cg
-static int ln_bwd_rpb(int64_t rows) {
-    if (g_ln_rpb > 0) return (g_ln_rpb + 7) / 8 * 8;
-    int64_t r = rows / 512;
-    r = r < 8 ? 8 : (r > 256 ? 256 : r);
-    return (int)((r + 7) / 8 * 8);
+// Waves per backward block: 8, or 4 where the row kernel's registers cap a SIMD at 3 waves (the
+// VEC 4 variants, C = 512..1024: 166 VGPRs at C = 768) -- 8-wave blocks then fit once per CU (8 of
+// 12 wave slots), 4-wave blocks three times.  Blocks target one round over the CUs' slots.
+static int ln_bwd_waves(int64_t C) {
+    if (g_ln_waves == 4 || g_ln_waves == 8) return g_ln_waves;
+    return (C >= 512 && C <= 1024 && C % 4 == 0) ? 4 : 8;
 }
-static int64_t ln_bwd_blocks(int64_t rows) {
-    const int rpb = ln_bwd_rpb(rows);
+static int ln_bwd_rpb(int64_t rows, int64_t C) {
+    const int W = ln_bwd_waves(C);
+    if (g_ln_rpb > 0) return (g_ln_rpb + W - 1) / W * W;
+    int64_t r = rows / (W == 8 ? 512 : 768);
+    r = r < W ? W : (r > 256 ? 256 : r);
+    return (int)((r + W - 1) / W * W);
+}
+static int64_t ln_bwd_blocks(int64_t rows, int64_t C) {
+    const int rpb = ln_bwd_rpb(rows, C);
     return (rows + rpb - 1) / rpb;
 }
 
@@ -183,8 +191,8 @@ struct LnRow {
 // column sums), summed over the 8 waves in a fixed order.  Measured (tools/ln_bench.py): issuing
 // the next row's loads before reducing the current one (double-buffered rows) gained nothing at
 // C4 and lost 15-25 % at C2 (occupancy); ~4.8 TB/s at C4, 5.2 TB/s at C2 without dropout.
-template <int VEC, int NJ, typename TDY>
-__global__ __launch_bounds__(64 * LN_BWD_WAVES) void k_ln_bwd(const TDY* __restrict__ dy, const float* __restrict__ x,
+template <int VEC, int NJ, typename TDY, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ dy, const float* __restrict__ x,
                                                            const float* __restrict__ w, const float* __restrict__ mean,
                                                            const float* __restrict__ rstd,
                                                            const float* __restrict__ dres, float* __restrict__ dx,
@@ -196,7 +204,7 @@ __global__ __launch_bounds__(64 * LN_BWD_WAVES) void k_ln_bwd(const TDY* __restr
     const int wave = threadIdx.x >> 6;
     const float invC = 1.0f / (float)C;
     const uint64_t stream = lp.thr ? dropout_stream(lp.rng_call, lp.site) : 0;
-    const int rpw = rpb / LN_BWD_WAVES;
+    const int rpw = rpb / WAVES;
     float adw[NJ][VEC], adb[NJ][VEC], acs[NJ][VEC], wv[NJ][VEC];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -322,9 +330,13 @@ __global__ __launch_bounds__(64 * LN_BWD_WAVES) void k_ln_bwd(const TDY* __restr
             }
         }
     };
-    if (wave >= 4) put(false);
-    __syncthreads();
-    if (wave < 4) put(true);
+    if (WAVES == 8) {
+        if (wave >= 4) put(false);
+        __syncthreads();
+        if (wave < 4) put(true);
+    } else {
+        put(false);
+    }
     __syncthreads();
     for (int c = threadIdx.x; c < NC; c += blockDim.x)
         part[(int64_t)blockIdx.x * NC + c] = ((red[c] + red[NC + c]) + red[2 * NC + c]) + red[3 * NC + c];
@@ -354,13 +366,20 @@ int launch_ln_bwd(const TDY* dy, const float* x, const float* w, const float* me
                   int dbias_accumulate, float* part, int64_t rows, int C, int defer, hipStream_t st) {
     const bool al16 = (((uintptr_t)x | (uintptr_t)w | (uintptr_t)dx | (uintptr_t)(dres ? dres : x)) & 15) == 0 &&
                       (((uintptr_t)dy) & 7) == 0 && (((uintptr_t)(lp.out ? lp.out : (bf16_t*)x)) & 7) == 0;
-    const int64_t nblk = ln_bwd_blocks(rows);
+    const int64_t nblk = ln_bwd_blocks(rows, C);
     const int NP = lp.csum ? 3 : 2;
     const size_t lds = (size_t)4 * NP * C * sizeof(float);
-    const int rpb = ln_bwd_rpb(rows);
+    const int rpb = ln_bwd_rpb(rows, C);
+    const int waves = ln_bwd_waves(C);
 #define LNB(V, N)                                                                                              \
-    k_ln_bwd<V, N, TDY><<<(unsigned)nblk, 64 * LN_BWD_WAVES, lds, st>>>(dy, x, w, mean, rstd, dres, dx, lp, part, rows, \
-                                                                       C, rpb)
+    do {                                                                                                       \
+        if (waves == 4)                                                                                        \
+            k_ln_bwd<V, N, TDY, 4><<<(unsigned)nblk, 256, lds, st>>>(dy, x, w, mean, rstd, dres, dx, lp, part, rows, C, \
+                                                                     rpb);                                     \
+        else                                                                                                   \
+            k_ln_bwd<V, N, TDY, 8><<<(unsigned)nblk, 512, lds, st>>>(dy, x, w, mean, rstd, dres, dx, lp, part, rows, C, \
+                                                                     rpb);                                     \
+    } while (0)
     if (C == 384 && al16) LNB(2, 3);
     else if (C == 768 && al16) LNB(4, 3);
     else if (C == 512 && al16) LNB(4, 2);
@@ -384,7 +403,7 @@ extern "C" int cg_layernorm_fwd(const float* x, const float* w, const float* b, 
 }
 
 extern "C" int64_t cg_layernorm_bwd_workspace(int64_t rows, int64_t C) {
-    return ln_bwd_blocks(rows) * 3 * C * (int64_t)sizeof(float);
+    return ln_bwd_blocks(rows, C) * 3 * C * (int64_t)sizeof(float);
 }
 
 static int layernorm_bwd_impl(const void* dy, int dy_dtype, const float* x, const float* w, const float* mean,
@@ -441,7 +460,7 @@ extern "C" int cg_layernorm_bwd_reduce(const void* workspace, int64_t rows, int6
     CG_REQUIRE(rows > 0 && C > 0 && C <= 1024, "cg_layernorm_bwd_reduce: need 0 < C <= 1024");
     CG_REQUIRE(!lp_colsum || lp_colsum_partials, "cg_layernorm_bwd_reduce: lp_colsum needs the colsum partials");
     if (!dw && !db && !lp_colsum) return CG_OK;
-    const int64_t nblk = ln_bwd_blocks(rows);
+    const int64_t nblk = ln_bwd_blocks(rows, C);
     const int NP = lp_colsum_partials ? 3 : 2;
     launch_reduce_partials3((const float*)workspace, nblk, NP * C, dw, db, lp_colsum, C, accumulate,
                             colsum_accumulate, (hipStream_t)stream);

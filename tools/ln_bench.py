@@ -1,7 +1,7 @@
 """Times the LayerNorm backward at the C2 / C4 shapes as the model calls it (bf16 dy, fp32 residual
 gradient, bf16 consumer copy with dropout, consumer column sums): the whole call, the row kernel
 alone and the partials reduce alone, over rows-per-block values (cg_set_tuning ln_rpb).  GPU only.
-usage: python tools/ln_bench.py [rpb,rpb,...]"""
+usage: python tools/ln_bench.py [rpb,rpb,...] [waves,waves,...]   (waves: cg_set_tuning ln_waves, 0 = automatic)"""
 import os
 import sys
 
@@ -36,11 +36,15 @@ def run(M, C, p):
 if __name__ == "__main__":
     lib = L.load()
     rpbs = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0]
+    waves = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0]
     for M, C in ((16384, 384), (65536, 768)):
         for p in (0.0, 0.2):
-            for rpb in rpbs:
-                L.check(lib.cg_set_tuning(b"ln_rpb", rpb), "tuning")
-                full, rows, red, byts = run(M, C, p)
-                print(f"M={M} C={C} p={p} rpb={rpb}: full {full:7.1f} us  rows {rows:7.1f} us "
-                      f"({byts / rows / 1e3:6.0f} GB/s)  reduce {red:6.1f} us", flush=True)
+            for wv in waves:
+                for rpb in rpbs:
+                    L.check(lib.cg_set_tuning(b"ln_waves", wv), "tuning")
+                    L.check(lib.cg_set_tuning(b"ln_rpb", rpb), "tuning")
+                    full, rows, red, byts = run(M, C, p)
+                    print(f"M={M} C={C} p={p} waves={wv} rpb={rpb}: full {full:7.1f} us  rows {rows:7.1f} us "
+                          f"({byts / rows / 1e3:6.0f} GB/s)  reduce {red:6.1f} us", flush=True)
     L.check(lib.cg_set_tuning(b"ln_rpb", 0), "tuning")
+    L.check(lib.cg_set_tuning(b"ln_waves", 0), "tuning")
