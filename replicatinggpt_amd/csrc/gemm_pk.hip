@@ -102,6 +102,35 @@ __device__ __forceinline__ void drop_nibbles(const EpiArgs& epi, uint64_t stream
         }
 }
 
+// The item's 16 output fragments.  WIDE with a bf16 output: 16-B row segments instead of 8-B ones --
+// for each fragment pair (j, j+1) lanes of rows 1 and 3 (lane >> 4 odd) trade their fragment-j
+// quarter for the other row's fragment-(j+1) quarter (v_permlane16_swap: odd 16-lane rows of vdst
+// <-> even rows of src), so lane quarter q then holds 8 contiguous columns: 8 dwordx4 stores, each
+// writing 64 contiguous bytes of 16 rows, instead of 16 dwordx2 (cdna_hip_programming.md T21).
+template <bool WIDE>
+__device__ __forceinline__ void store_item(const fv4 (&v)[4][4], int64_t mr, int64_t nc, void* Cv, int c_dtype,
+                                           int64_t ldc) {
+    if (WIDE && c_dtype == CG_BF16) {
+        const int q = (threadIdx.x & 63) >> 4;
+        const int64_t col = nc - 4 * q + ((q & 1) ? 16 : 0) + ((q >> 1) ? 8 : 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int jp = 0; jp < 4; jp += 2) {
+                uint32_t ax = pack_bf2(v[i][jp][0], v[i][jp][1]), ay = pack_bf2(v[i][jp][2], v[i][jp][3]);
+                uint32_t bx = pack_bf2(v[i][jp + 1][0], v[i][jp + 1][1]), by = pack_bf2(v[i][jp + 1][2], v[i][jp + 1][3]);
+                const auto sx = __builtin_amdgcn_permlane16_swap(ax, bx, false, false);
+                const auto sy = __builtin_amdgcn_permlane16_swap(ay, by, false, false);
+                *(uint4*)((bf16_t*)Cv + (mr + 16 * i) * ldc + col + 16 * jp) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+            }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) store4_plain(v[i][j], mr + 16 * i, nc + 16 * j, Cv, c_dtype, ldc);
+}
+
 // The whole 64x64 epilogue of one wave: every operand it reads (bias, residual, ReLU output) is
 // loaded for all 16 fragments before the first store.  Per-fragment load -> use made hipcc wait
 // vmcnt(0) 16 times per item, each time also for the previous fragments' stores and the next
@@ -113,6 +142,7 @@ template <int EK>
 __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t nc, int64_t N, void* Cv, int c_dtype,
                                          int64_t ldc, const EpiArgs& epi, uint64_t stream) {
     const int kind = EK >= 0 ? EK : epi.kind;
+    constexpr bool WIDE = EK == CG_EPI_STORE || EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_RELU_BWD;
     if (EK < 0 && epi.beta != 0.f) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -181,10 +211,7 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) store4_plain(acc[i][j], mr + 16 * i, nc + 16 * j, Cv, c_dtype, ldc);
+            store_item<WIDE>(acc, mr, nc, Cv, c_dtype, ldc);
         } else {
             float4 h[4][4];
 #pragma unroll
@@ -245,13 +272,12 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                fv4 v = acc[i][j];
+                fv4& v = acc[i][j];
                 v[0] = fmaxf(v[0] + bv[j].x, 0.f); v[1] = fmaxf(v[1] + bv[j].y, 0.f);
                 v[2] = fmaxf(v[2] + bv[j].z, 0.f); v[3] = fmaxf(v[3] + bv[j].w, 0.f);
-                const uint2 pk = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
-                *(uint2*)((bf16_t*)Cv + (mr + 16 * i) * ldc + nc + 16 * j) = pk;
-                kb[i][j] = nz4_bf16(pk);
+                kb[i][j] = nz4_bf16(make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])));
             }
+        store_item<WIDE>(acc, mr, nc, Cv, CG_BF16, ldc);
         relu_bits_store<4>(kb, (uint32_t*)epi.aux, epi.ld_aux, mr, nc - 4 * (lane >> 4), lane);
         return;
     }
@@ -262,8 +288,7 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int64_t m = mr + 16 * i, n = nc + 16 * j;
-            fv4 v = acc[i][j];
+            fv4& v = acc[i][j];
             if (has_bias) {
                 v[0] += bv[j].x; v[1] += bv[j].y; v[2] += bv[j].z; v[3] += bv[j].w;
             }
@@ -274,8 +299,8 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] = ((nib[i][j] >> q) & 1u) ? v[q] * epi.dscale : 0.f;
             }
-            store4_plain(v, m, n, Cv, c_dtype, ldc);
         }
+    store_item<WIDE>(acc, mr, nc, Cv, c_dtype, ldc);
 }
 
 template <int BM, int BN, int NBUF>
@@ -397,7 +422,10 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     // the next step's wait, so the count below lets them drain under the next MFMAs instead of
     // stalling the next K-tile on the store latency (vmcnt counts loads, LDS-DMA and stores in
     // issue order).
-    constexpr int EPI_OPS = 16;
+    // (8 for the fixed kinds whose bf16 output goes out as 16-B row segments -- store_item: with an
+    // fp32 output they issue 16, more than counted, which only makes the wait conservative)
+    constexpr int EPI_OPS =
+        (EK == CG_EPI_STORE || EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_RELU_BWD) ? 8 : 16;
     int cur = 0, cj = 0, ckt = 0;
     int cnk;   // K-tiles of the compute cursor's item
     {
