@@ -80,7 +80,10 @@ struct Geo8 {
 //   P8_CP_BITS    the same with the mask from CG_BITS keep bits
 //   P8_RELU_BITS  bias + ReLU, bf16 output and its CG_BITS keep bits
 //   P8_BWD_BITS   ReLU backward from CG_BITS keep bits, no column partials
-enum { P8_GENERIC = 0, P8_CP_BF16 = 1, P8_CP_BITS = 2, P8_RELU_BITS = 3, P8_BWD_BITS = 4 };
+//   P8_BF16       STORE / BIAS / BIAS_RELU with a bf16 output (beta 0, split 1)
+// Every path but P8_GENERIC writes its bf16 output as 16-B row segments (store_bf16_wide: FM x 2
+// stores per item), so their EPI_OPS is half the generic path's FM x FN.
+enum { P8_GENERIC = 0, P8_CP_BF16 = 1, P8_CP_BITS = 2, P8_RELU_BITS = 3, P8_BWD_BITS = 4, P8_BF16 = 5 };
 template <bool AT, bool BT, int BM, int BN, int WM, int NBUF, int EP>
 __global__ __launch_bounds__(P8_THREADS, (Geo8<BM, BN, NBUF>::OCC))
 void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
@@ -91,7 +94,8 @@ void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     using DB = Dma8<BT, BN>;
     constexpr int WN = P8_WAVES / WM, FM = BM / WM / 16, FN = BN / WN / 16;
     constexpr int LPT = DA::PER_WAVE + DB::PER_WAVE;  // DMA instructions per lane per K-tile
-    constexpr int EPI_OPS = FM * FN;                  // vector-memory stores per lane per item
+    // vector-memory output stores per lane per item (the youngest VMEM operations at the next wait)
+    constexpr int EPI_OPS = (EP == P8_GENERIC || FN != 4) ? FM * FN : FM * 2;
     static_assert(NBUF >= 2 && NBUF <= 4, "ring depth");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -282,15 +286,22 @@ void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);
+                if constexpr (FN == 4) {
+                    store_bf16_wide<FM>(acc, (bf16_t*)Cv, ldc, mr, nc);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < FM; ++i)
+#pragma unroll
+                        for (int j = 0; j < FN; ++j) {
+                            const fv4& v = acc[i][j];
+                            *(uint2*)((bf16_t*)Cv + (mr + 16 * i) * ldc + nc + 16 * j) =
+                                make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+                        }
+                }
 #pragma unroll
                 for (int i = 0; i < FM; ++i)
 #pragma unroll
-                    for (int j = 0; j < FN; ++j) {
-                        const fv4& v = acc[i][j];
-                        *(uint2*)((bf16_t*)Cv + (mr + 16 * i) * ldc + nc + 16 * j) =
-                            make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
-                        acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
-                    }
+                    for (int j = 0; j < FN; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
             } else if constexpr (EP == P8_BWD_BITS) {
                 // ReLU backward from keep bits (bf16 output, beta 0: checked on the host)
 #pragma unroll
@@ -300,14 +311,16 @@ void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
 #pragma unroll
                     for (int j = 0; j < FN; ++j) {
                         const uint32_t kb = relu_nib(w, j, lane);
-                        fv4 v = acc[i][j];
+                        fv4& v = acc[i][j];
 #pragma unroll
                         for (int q = 0; q < 4; ++q) v[q] = ((kb >> q) & 1u) ? v[q] : 0.f;
-                        *(uint2*)((bf16_t*)Cv + (mr + 16 * i) * ldc + nc + 16 * j) =
-                            make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
-                        acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
                     }
                 }
+                store_bf16_wide<FM>(acc, (bf16_t*)Cv, ldc, mr, nc);
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
             } else if constexpr (EP == P8_RELU_BITS) {
                 // bias + ReLU, bf16 output and its ReLU keep bits (checked on the host: bias, bf16, beta 0)
                 uint32_t kb[FM][4];
@@ -316,16 +329,40 @@ void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
                     const float4 b = *(const float4*)(epi.bias + nc + 16 * j);
 #pragma unroll
                     for (int i = 0; i < FM; ++i) {
-                        fv4 v = acc[i][j];
+                        fv4& v = acc[i][j];
                         v[0] = fmaxf(v[0] + b.x, 0.f); v[1] = fmaxf(v[1] + b.y, 0.f);
                         v[2] = fmaxf(v[2] + b.z, 0.f); v[3] = fmaxf(v[3] + b.w, 0.f);
-                        const uint2 pk = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
-                        *(uint2*)((bf16_t*)Cv + (mr + 16 * i) * ldc + nc + 16 * j) = pk;
-                        kb[i][j & 3] = nz4_bf16(pk);
-                        acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
+                        kb[i][j & 3] = nz4_bf16(make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])));
                     }
                 }
+                store_bf16_wide<FM>(acc, (bf16_t*)Cv, ldc, mr, nc);
                 relu_bits_store<FM>(kb, (uint32_t*)epi.aux, epi.ld_aux, mr, nc - 4 * (lane >> 4), lane);
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
+            } else if constexpr (EP == P8_BF16) {
+                // STORE / BIAS / BIAS_RELU, bf16 output (host-checked: beta 0, split 1, bias present
+                // for the bias kinds)
+                const bool bias = epi.kind != CG_EPI_STORE, relu = epi.kind == CG_EPI_BIAS_RELU;
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const float4 b = bias ? *(const float4*)(epi.bias + nc + 16 * j) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                    for (int i = 0; i < FM; ++i) {
+                        fv4& v = acc[i][j];
+                        v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+                        if (relu) {
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+                        }
+                    }
+                }
+                store_bf16_wide<FM>(acc, (bf16_t*)Cv, ldc, mr, nc);
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
             } else {
 #pragma unroll
                 for (int i = 0; i < FM; ++i)
@@ -388,7 +425,17 @@ bool launch8(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, i
     if (e.colpart) {   // non-transposed A, split 1, RELU_BWD with bf16 aux, bf16 output (host-checked)
         if (!bt) FG(false, false, P8_CP_BF16);
         else FG(false, true, P8_CP_BF16);
-    } else if (!at && !bt) FG(false, false, P8_GENERIC);
+        return true;
+    }
+    if constexpr (FN4) {
+        const bool plain = e.kind == CG_EPI_STORE || ((e.kind == CG_EPI_BIAS || e.kind == CG_EPI_BIAS_RELU) && e.bias);
+        if (plain && !at && split_k == 1 && c_dtype == CG_BF16 && e.beta == 0.f) {
+            if (!bt) FG(false, false, P8_BF16);
+            else FG(false, true, P8_BF16);
+            return true;
+        }
+    }
+    if (!at && !bt) FG(false, false, P8_GENERIC);
     else if (!at && bt) FG(false, true, P8_GENERIC);
     else if (at && !bt) FG(true, false, P8_GENERIC);
     else FG(true, true, P8_GENERIC);

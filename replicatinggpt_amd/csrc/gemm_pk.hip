@@ -110,19 +110,8 @@ __device__ __forceinline__ void drop_nibbles(const EpiArgs& epi, uint64_t stream
 template <bool WIDE>
 __device__ __forceinline__ void store_item(const fv4 (&v)[4][4], int64_t mr, int64_t nc, void* Cv, int c_dtype,
                                            int64_t ldc) {
-    if (WIDE && c_dtype == CG_BF16) {
-        const int q = (threadIdx.x & 63) >> 4;
-        const int64_t col = nc - 4 * q + ((q & 1) ? 16 : 0) + ((q >> 1) ? 8 : 0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int jp = 0; jp < 4; jp += 2) {
-                uint32_t ax = pack_bf2(v[i][jp][0], v[i][jp][1]), ay = pack_bf2(v[i][jp][2], v[i][jp][3]);
-                uint32_t bx = pack_bf2(v[i][jp + 1][0], v[i][jp + 1][1]), by = pack_bf2(v[i][jp + 1][2], v[i][jp + 1][3]);
-                const auto sx = __builtin_amdgcn_permlane16_swap(ax, bx, false, false);
-                const auto sy = __builtin_amdgcn_permlane16_swap(ay, by, false, false);
-                *(uint4*)((bf16_t*)Cv + (mr + 16 * i) * ldc + col + 16 * jp) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
-            }
+    if (WIDE && c_dtype == CG_BF16) {   // 16-B row segments (gemm_tile.h store_bf16_wide): 8 stores
+        store_bf16_wide<4>(v, (bf16_t*)Cv, ldc, mr, nc);
         return;
     }
 #pragma unroll

@@ -254,4 +254,25 @@ __device__ __forceinline__ uint32_t nz4_bf16(uint2 pk) {
 __device__ __forceinline__ uint32_t relu_nib(uint2 w, int j, int lane) {
     return (((j >> 1) ? w.y : w.x) >> (16 * (j & 1) + 4 * (lane >> 4))) & 0xfu;
 }
+// bf16 stores of a wave's FM x 4 output fragments (16x16, lane: row rb = mr + 16 i, columns
+// nc + 16 j .. +3 with nc = cb + 4 (lane >> 4)) as 16-B row segments: for each fragment pair
+// (j, j+1) the lanes of odd 16-lane rows trade their fragment-j quarter for the even row's
+// fragment-(j+1) quarter (v_permlane16_swap), so lane quarter q holds 8 contiguous columns: FM x 2
+// dwordx4 stores, each 64 contiguous bytes of 16 rows, instead of FM x 4 dwordx2
+// (cdna_hip_programming.md T21).  The callers' wait counts know it is FM x 2 stores.
+template <int FM>
+__device__ __forceinline__ void store_bf16_wide(const fv4 (&v)[FM][4], bf16_t* C, int64_t ldc, int64_t mr, int64_t nc) {
+    const int q = (threadIdx.x & 63) >> 4;
+    const int64_t col = nc - 4 * q + ((q & 1) ? 16 : 0) + ((q >> 1) ? 8 : 0);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int jp = 0; jp < 4; jp += 2) {
+            const uint32_t ax = pack_bf2(v[i][jp][0], v[i][jp][1]), ay = pack_bf2(v[i][jp][2], v[i][jp][3]);
+            const uint32_t bx = pack_bf2(v[i][jp + 1][0], v[i][jp + 1][1]), by = pack_bf2(v[i][jp + 1][2], v[i][jp + 1][3]);
+            const auto sx = __builtin_amdgcn_permlane16_swap(ax, bx, false, false);
+            const auto sy = __builtin_amdgcn_permlane16_swap(ay, by, false, false);
+            *(uint4*)(C + (mr + 16 * i) * ldc + col + 16 * jp) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+        }
+}
 }  // namespace cg
