@@ -149,6 +149,12 @@ int cg_gemm_colpart_supported(int a_trans, int b_trans, int64_t M, int64_t N, in
    FeedForward uses them when both its W1 forward and its W2 dgrad products say yes.           */
 int cg_gemm_relu_bits_supported(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                                 int64_t ldc);
+/* cg_set_tuning("defer_splitk", 1): a split-K cg_gemm with an fp32 CG_EPI_STORE output (the weight
+   gradients) leaves its slab reduce pending -- its workspace must stay allocated -- and the next
+   persistent bf16 GEMM launch on the stream performs it in its tail (same summation order, same
+   bits); only a launch on the stream the reduce was enqueued on takes it.  cg_flush_deferred
+   launches whatever is still pending (on that stream); call it before reading the outputs. */
+int cg_flush_deferred(void* stream);
 /* out[n] (=|+=) sum_r part[r*N + n] over rows r in order (fixed order: deterministic)          */
 int cg_reduce_rows(const float* part, int64_t rows, int64_t N, float* out, int accumulate, void* stream);
 int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,

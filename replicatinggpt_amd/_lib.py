@@ -51,6 +51,7 @@ _SIGS = {
     "cg_gemm_workspace": (c_i64, [c_i64, c_i64, c_int]),
     "cg_gemm_colpart_supported": (c_int, [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64]),
     "cg_gemm_relu_bits_supported": (c_int, [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64]),
+    "cg_flush_deferred": (c_int, [P]),
     "cg_reduce_rows": (c_int, [P, c_i64, c_i64, P, c_int, P]),
     "cg_gemm": (c_int, [c_int, c_int, c_int, c_i64, c_i64, c_i64, P, c_i64, P, c_i64, P, c_int, c_i64,
                         ctypes.POINTER(Epilogue), c_int, P, P]),

@@ -376,6 +376,30 @@ int launch_generic(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, co
 namespace cg {
 int g_gemm_variant = 0;
 int g_gemm_max_grid = 0;
+int g_defer_splitk = 0;   // cg_set_tuning("defer_splitk"): split-K reduces of fp32 STORE outputs deferred
+RedJobs g_red_pending = {};
+hipStream_t g_red_stream = nullptr;   // the stream the pending jobs were enqueued on
+
+// pending jobs for a launch on stream st: only a launch on the jobs' own stream takes them (a
+// launch on another stream is not ordered after the slab writes)
+RedJobs take_pending_reduces(hipStream_t st) {
+    RedJobs r = {};
+    if (g_red_pending.n && st == g_red_stream) {
+        r = g_red_pending;
+        g_red_pending.n = 0;
+    }
+    return r;
+}
+
+static void launch_splitk_reduce_job(const RedJob& j, hipStream_t st);
+
+// the pending jobs as standalone reduce kernels on their own stream (cg_flush_deferred, a full
+// queue, or a job arriving from another stream)
+static void flush_pending() {
+    const RedJobs r = take_pending_reduces(g_red_stream);
+    for (int q = 0; q < r.n; ++q) launch_splitk_reduce_job(r.j[q], g_red_stream);
+}
+
 int g_skip_splitk_reduce = 0;  // measurement knob (WRONG results): time a step without the split-K reduce
 extern int g_attn_variant;  // attention_d64.hip
 extern int g_ln_rpb;  // layernorm.hip
@@ -402,6 +426,10 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     }
     if (!strcmp(key, "skip_splitk_reduce")) {
         g_skip_splitk_reduce = value;
+        return CG_OK;
+    }
+    if (!strcmp(key, "defer_splitk")) {   // off: pending reduces are flushed on the caller's next cg_flush_deferred
+        g_defer_splitk = value;
         return CG_OK;
     }
     if (!strcmp(key, "ln_waves")) {   // takes effect for workspaces sized after the call
@@ -442,9 +470,11 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
     EpiArgs e = make_epi(epi);
     CG_REQUIRE(split_k == 1 || e.kind == CG_EPI_STORE || e.kind == CG_EPI_BIAS || e.kind == CG_EPI_BIAS_RESID,
                "cg_gemm: split-K supports STORE/BIAS/BIAS_RESID epilogues only");
+    bool fast = false;
     if (op_dtype == CG_BF16 && fast_gemm_launch(a_trans, b_trans, M, N, K, (const bf16_t*)A, lda,
                                                 (const bf16_t*)B, ldb, C, c_dtype, ldc, e, split_k,
                                                 (float*)workspace, st)) {
+        fast = true;
     } else if (e.aux_dtype == CG_BITS) {
         set_error("cg_gemm: CG_BITS ReLU keep bits need a persistent bf16 kernel (cg_gemm_relu_bits_supported)");
         return CG_EINVAL;
@@ -466,7 +496,15 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
                       (((uintptr_t)C | (uintptr_t)workspace | (uintptr_t)(e.bias ? e.bias : (const float*)C) |
                         (uintptr_t)(e.resid ? e.resid : (const float*)C)) & 15) == 0 &&
                       (!e.resid || e.ld_resid % 4 == 0);
-    if (split_k > 1 && vec4 && !g_skip_splitk_reduce) {
+    // (slab sets above 40 MB -- the C4 FFN / QKV weight gradients -- keep their own reduce kernel: in
+    // the next 256x256 GEMM's tail they measured no gain, C4 58.2 vs 57.9 ms/step)
+    if (split_k > 1 && vec4 && !g_skip_splitk_reduce && g_defer_splitk && fast && e.kind == CG_EPI_STORE &&
+        c_dtype == CG_F32 && ldc == N && (int64_t)split_k * M * N * 4 <= ((int64_t)40 << 20)) {
+        // deferred: summed in the tail of the next persistent GEMM launch (or cg_flush_deferred)
+        if (g_red_pending.n == MAX_RED || (g_red_pending.n && g_red_stream != st)) flush_pending();
+        g_red_stream = st;
+        g_red_pending.j[g_red_pending.n++] = RedJob{(const float*)workspace, (float*)C, M * N / 4, split_k, e.beta};
+    } else if (split_k > 1 && vec4 && !g_skip_splitk_reduce) {
         const int n4 = (int)(M * N / 4);
 #define SKR(TC_, S_)                                                                                  \
     k_splitk_reduce4<TC_, S_><<<ceil_div(n4, 256), 256, 0, st>>>((const float*)workspace, split_k, (int)M, \
@@ -525,5 +563,31 @@ extern "C" int cg_colsum(const void* X, int x_dtype, int64_t rows, int64_t N, in
         k_colsum_partial<float><<<grid, 256, 0, st>>>((const float*)X, rows, N, ldx, (float*)workspace);
     launch_reduce_partials((const float*)workspace, nchunk, N, out, nullptr, N, accumulate, st);
     CG_LAUNCH_CHECK("cg_colsum");
+    return CG_OK;
+}
+
+namespace cg {
+static void launch_splitk_reduce_job(const RedJob& j, hipStream_t st) {
+    EpiArgs e = make_epi(nullptr);
+    e.beta = j.beta;
+    const int64_t n = 4 * j.n4;
+    const int n4 = (int)j.n4;
+    // one row of n elements: the same kernel and summation order as the in-line reduce
+    switch (j.S) {
+#define SKJ(S_) k_splitk_reduce4<float, S_><<<ceil_div(n4, 256), 256, 0, st>>>(j.ws, j.S, 1, (int)n, j.out, n, e)
+        case 8: SKJ(8); break;
+        case 14: SKJ(14); break;
+        case 16: SKJ(16); break;
+        case 32: SKJ(32); break;
+        default: SKJ(0); break;
+#undef SKJ
+    }
+}
+}  // namespace cg
+
+extern "C" int cg_flush_deferred(void* stream) {
+    (void)stream;   // pending jobs go out on the stream they were enqueued on
+    cg::flush_pending();
+    CG_LAUNCH_CHECK("cg_flush_deferred");
     return CG_OK;
 }

@@ -64,6 +64,43 @@ __device__ __forceinline__ void store_out(TC* C, int64_t off, float v, float bet
 }
 
 
+// A split-K reduce deferred out of its own cg_gemm call (cg_set_tuning("defer_splitk", 1), the
+// training backward): out[i] = sum_{s < S} ws[s n + i] (+ beta out[i]) over n = 4 n4 fp32 elements,
+// run in the tail of the next persistent GEMM launch on the stream (each thread takes float4
+// chunks once its block's own items are done) or by cg_flush_deferred.  Slab 0 first, then 1, ...:
+// k_splitk_reduce4's order, so the same bits.
+struct RedJob {
+    const float* ws;
+    float* out;
+    int64_t n4;
+    int S;
+    float beta;
+};
+constexpr int MAX_RED = 2;
+struct RedJobs {
+    RedJob j[MAX_RED];
+    int n;
+};
+RedJobs take_pending_reduces(hipStream_t st);   // gemm.hip: pending jobs (cleared) for a launch on st
+
+__device__ __forceinline__ void red_tail(const RedJobs& r) {
+    const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int q = 0; q < r.n; ++q) {
+        const RedJob& J = r.j[q];
+        const int64_t slab = 4 * J.n4;
+        for (int64_t i = t0; i < J.n4; i += nthr) {
+            const float* p = J.ws + 4 * i;
+            fv4 s = __builtin_nontemporal_load((const fv4*)p);
+#pragma unroll 8
+            for (int k = 1; k < J.S; ++k) s += __builtin_nontemporal_load((const fv4*)(p + k * slab));
+            fv4* o = (fv4*)(J.out + 4 * i);
+            if (J.beta != 0.f) s += J.beta * *o;
+            *o = s;
+        }
+    }
+}
+
 // tuning knob (cg_set_tuning("gemm_variant", v)); 0 = automatic choice
 extern int g_gemm_variant;
 // test knob (cg_set_tuning("gemm_max_grid", n)): cap on persistent-kernel blocks; 0 = resident slots

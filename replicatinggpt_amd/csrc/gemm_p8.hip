@@ -88,7 +88,7 @@ template <bool AT, bool BT, int BM, int BN, int WM, int NBUF, int EP>
 __global__ __launch_bounds__(P8_THREADS, (Geo8<BM, BN, NBUF>::OCC))
 void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
                const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype, int64_t ldc,
-               EpiArgs epi, int split_k, int64_t kchunk, float* __restrict__ ws) {
+               EpiArgs epi, int split_k, int64_t kchunk, float* __restrict__ ws, RedJobs red) {
     using G = Geo8<BM, BN, NBUF>;
     using DA = Dma8<AT, BM>;
     using DB = Dma8<BT, BN>;
@@ -381,6 +381,7 @@ void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
             stored = true;
         }
     }
+    if (red.n) red_tail(red);   // a deferred split-K reduce of an earlier launch (gemm_common.h)
 }
 
 int cu_count8() {
@@ -407,7 +408,8 @@ bool launch8(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, i
     const unsigned grid = (unsigned)(nitems < slots ? nitems : slots);
 #define FG(AT_, BT_, EP_)                                                                                \
     k_gemm_p8<AT_, BT_, BM, BN, WM, NBUF, EP_><<<grid, P8_THREADS, G::LDS, st>>>(M, N, K, A, lda, B, ldb, C,     \
-                                                                                 c_dtype, ldc, e, split_k, kchunk, ws)
+                                                                                 c_dtype, ldc, e, split_k, kchunk, ws, \
+                                                                                 take_pending_reduces(st))
     // keep bits (host-checked: split 1, bf16 output, beta 0) need 64-column wave fragments (FN == 4)
     const bool bits = e.aux_dtype == CG_BITS;
     constexpr bool FN4 = BN / (8 / WM) == 64;

@@ -317,7 +317,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, (GeoP<BM, BN, NBUF>::OC
 __attribute__((amdgpu_waves_per_eu(1, (BM / 64) * (BN / 64) * GeoP<BM, BN, NBUF>::OCC / 4)))
 void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
                const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype, int64_t ldc,
-               EpiArgs epi, int split_k, int64_t kchunk, float* __restrict__ ws, int flags) {
+               EpiArgs epi, int split_k, int64_t kchunk, float* __restrict__ ws, int flags, RedJobs red) {
     using G = GeoP<BM, BN, NBUF>;
     using DA = DmaP<AT, BM, G::WAVES>;
     using DB = DmaP<BT, BN, G::WAVES>;
@@ -527,6 +527,7 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         }
     }
     wait_vm<0>();  // the dummy DMAs past the last K-tile land before the workgroup's LDS is released
+    if (red.n) red_tail(red);   // a deferred split-K reduce of an earlier launch (gemm_common.h)
 }
 
 int cu_count() {
@@ -546,7 +547,8 @@ void launch_1(unsigned grid, int64_t M, int64_t N, int64_t K, const bf16_t* A, i
               hipStream_t st) {
     using G = GeoP<BM, BN, NBUF>;
     k_gemm_pk<AT_, BT_, BM, BN, NBUF, EK><<<grid, G::THREADS, G::LDS, st>>>(M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e,
-                                                                         split_k, kchunk, ws, g_pk_flags);
+                                                                         split_k, kchunk, ws, g_pk_flags,
+                                                                         take_pending_reduces(st));
 }
 
 // epilogue instantiation: slab for split-K; a fixed kind for the default 128x128 2-stage kernel's

@@ -101,7 +101,8 @@ class TrainStep:
     def _fwd_bwd(self):
         _, loss = self.model(self.x, self.y)           # GPT1.py:230
         self.opt.zero_grad(set_to_none=True)           # GPT1.py:231
-        loss.backward(self._one)                       # GPT1.py:232
+        with Fn.DEFER:                                 # split-K reduces in later GEMMs' tails
+            loss.backward(self._one)                   # GPT1.py:232
         return loss
 
     def _eager(self):
@@ -139,11 +140,12 @@ class TrainStep:
     def _segment(self, i, loss, xs):
         """Backward of segment i (0 = from the loss): stops at the next cut's leaf alias, whose
         .grad the following segment feeds into the real block-input tensor."""
-        if i == 0:
-            torch.autograd.backward(loss, grad_tensors=self._one)
-        else:
-            src, leaf = xs[self.cuts[i - 1]]
-            torch.autograd.backward(src, grad_tensors=leaf.grad)
+        with Fn.DEFER:   # flushed at the segment's end, before its gradient range is all-reduced
+            if i == 0:
+                torch.autograd.backward(loss, grad_tensors=self._one)
+            else:
+                src, leaf = xs[self.cuts[i - 1]]
+                torch.autograd.backward(src, grad_tensors=leaf.grad)
         Fn.SIDE.join()
 
     def _eager_segmented(self):

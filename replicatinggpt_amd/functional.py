@@ -14,6 +14,7 @@ buffer ("grad slots"), see ``Region``; the residual-stream gradient is fp32, act
 GEMM operands are bf16 (or fp32 in exact mode).
 """
 import contextlib
+import ctypes
 import os
 import math
 
@@ -78,6 +79,42 @@ class SideStream:
 
 
 SIDE = SideStream()
+
+
+class DeferredReduces:
+    """The training backward's split-K weight-gradient reduces, deferred into the tail of the next
+    persistent GEMM launch on the stream (cg_set_tuning "defer_splitk"; csrc/gemm_common.h RedJob:
+    same summation order, same bits) instead of a separate kernel each.  Inside ``with DEFER:``
+    linear_wgrad keeps its slab workspaces alive; the exit launches whatever is still pending
+    (before anything reads the gradients: the optimizer or the DP all-reduce) and releases them.
+    CHARPT_DEFER_SPLITK=0 turns it off (A/B)."""
+
+    def __init__(self):
+        self.enabled = os.environ.get("CHARPT_DEFER_SPLITK", "1") != "0"
+        self.active = False
+        self.keep = []
+
+    def __enter__(self):
+        if self.enabled and torch.cuda.is_available():
+            L.check(L.load().cg_set_tuning(b"defer_splitk", 1), "defer_splitk")
+            self.active = True
+        return self
+
+    def __exit__(self, *exc):
+        if self.active:
+            lib = L.load()
+            L.check(lib.cg_flush_deferred(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+                    "flush_deferred")
+            L.check(lib.cg_set_tuning(b"defer_splitk", 0), "defer_splitk")
+            if SIDE.enabled:   # the flush runs on the stream its reduces were enqueued on: join it
+                dev = torch.device("cuda", torch.cuda.current_device())
+                torch.cuda.current_stream(dev).wait_stream(SIDE.stream(dev))
+            self.active = False
+            self.keep.clear()
+        return False
+
+
+DEFER = DeferredReduces()
 # LayerNorm backward column-sum reduce on the side stream (CHARPT_LN_REDUCE_SIDE=0: in line, for A/B runs)
 LN_REDUCE_SIDE = os.environ.get("CHARPT_LN_REDUCE_SIDE", "1") != "0"
 # FFN b1 gradient fused into the ReLU-backward dgrad epilogue (CHARPT_FUSE_COLPART=0: separate colsum)
@@ -253,6 +290,8 @@ def linear_wgrad(dy2, x2, out, beta):
     ws = None
     if split > 1:
         ws = torch.empty(ops.gemm_workspace(N, K, split) // 4, dtype=torch.float32, device=dy2.device)
+        if DEFER.active:
+            DEFER.keep.append(ws)   # its reduce may run after this call returns
     ops.gemm(dy2, x2, out, _is_bf16(dy2.dtype), True, True, N, K, M, N, K, out.stride(0), L.EPI_STORE, None, None, 0,
              None, 0, 0.0, 0, None, 0, float(beta), split, ws)
     return out
