@@ -545,7 +545,9 @@ __device__ __forceinline__ void dq_group_tile(const char* Ki, const char* Vi, in
     }
 }
 
-template <bool DROP>
+// RD: K/V tiles by LDS-DMA (common.h dma16, no staging registers or ds_writes) instead of register
+// staging; attn_variant 3 selects the register-staged form (A/B)
+template <bool DROP, bool RD>
 __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t T_, int H, const bf16_t* __restrict__ q,
                                           const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, int64_t ld,
                                           const bf16_t* __restrict__ o, int64_t ldo, const bf16_t* __restrict__ dout,
@@ -581,13 +583,26 @@ __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t 
     for (int g = 0; g < 2; ++g) dqa[g][0] = dqa[g][1] = fv16{};
     const int qlast = (Q0 + 255 < T - 1) ? Q0 + 255 : T - 1;
     const int nkv = qlast / 64 + 1;
-    stage_store(stage_load(kb_, ld, vb_, ld, 0, tid), smem, tid);
-    __syncthreads();
+    const int wave_ = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if constexpr (RD) {
+        dma_tile(kb_, ld, 0, smem, wave_, lane);
+        dma_tile(vb_, ld, 0, smem + TILE, wave_, lane);
+        wait_all_barrier();
+    } else {
+        stage_store(stage_load(kb_, ld, vb_, ld, 0, tid), smem, tid);
+        __syncthreads();
+    }
     for (int kv = 0; kv < nkv; ++kv) {
         const int nxt = kv + 1 < nkv ? kv + 1 : kv;
-#ifndef CG_ATTN_NOSTAGE
-        const Stage2 st = stage_load(kb_, ld, vb_, ld, (int64_t)nxt * 64, tid);
-#endif
+        Stage2 st;
+        if constexpr (RD) {
+            if (kv + 1 < nkv) {   // slot (kv + 1) & 1 was last read before the previous barrier
+                dma_tile(kb_, ld, (int64_t)nxt * 64, smem + ((kv + 1) & 1) * 2 * TILE, wave_, lane);
+                dma_tile(vb_, ld, (int64_t)nxt * 64, smem + ((kv + 1) & 1) * 2 * TILE + TILE, wave_, lane);
+            }
+        } else {
+            st = stage_load(kb_, ld, vb_, ld, (int64_t)nxt * 64, tid);
+        }
         uint32_t mn[2] = {0u, 0u};
 #pragma unroll
         for (int g = 0; g < 2; ++g)
@@ -598,12 +613,11 @@ __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t 
         for (int g = 0; g < 2; ++g)
             if (act[g] && k0 <= qg[g] + 31)
                 dq_group_tile<DROP>(Ki, Ki + TILE, k0, qg[g], qf[g], df[g], lse2[g], dl[g], mw[g], c2, dqa[g], lane);
-#ifndef CG_ATTN_NOSTAGE
-        stage_store(st, smem + ((kv + 1) & 1) * 2 * TILE, tid);
-#endif
+        if constexpr (!RD) stage_store(st, smem + ((kv + 1) & 1) * 2 * TILE, tid);
         mw[0] = mn[0];
         mw[1] = mn[1];
-        __syncthreads();
+        if constexpr (RD) wait_all_barrier();   // the next tile has landed for every wave
+        else __syncthreads();
     }
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
@@ -614,7 +628,7 @@ __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t 
 }
 
 // pairs of query blocks per workgroup, as the forward
-template <bool DROP>
+template <bool DROP, bool RD>
 __global__ __launch_bounds__(256, 2) void k_attn_dq_d64(int64_t T_, int H, const bf16_t* __restrict__ q,
                                                         const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
                                                         int64_t ld, const bf16_t* __restrict__ o, int64_t ldo,
@@ -630,7 +644,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_dq_d64(int64_t T_, int H, const
 #pragma unroll 1
     for (int pass = 0; pass < npass; ++pass) {
         if (pass) __syncthreads();
-        dq_qblock<DROP>(pass ? x : first, bh, smem, T_, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
+        dq_qblock<DROP, RD>(pass ? x : first, bh, smem, T_, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
                         mask, dscale);
     }
 }
@@ -707,7 +721,7 @@ __device__ __forceinline__ void dkdv_tile(const char* Qi, const char* Oi, const 
     }
 }
 
-template <bool DROP>
+template <bool DROP, bool RD>
 __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_t T_, int H,
                                             const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                             const bf16_t* __restrict__ v, int64_t ld, const bf16_t* __restrict__ dout,
@@ -746,18 +760,31 @@ __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_
         else if (tid < 128) s = -del_b[qt * 64 + tid - 64] / dscale;   // -delta' = -(1-p) delta
         return s;
     };
+    const int wave_ = __builtin_amdgcn_readfirstlane(tid >> 6);
     {
-        stage_store(stage_load(qb_, ld, ob_, ldd, (int64_t)qt0 * 64, tid), smem, tid);
+        if constexpr (RD) {
+            dma_tile(qb_, ld, (int64_t)qt0 * 64, smem, wave_, lane);
+            dma_tile(ob_, ldd, (int64_t)qt0 * 64, smem + TILE, wave_, lane);
+        } else {
+            stage_store(stage_load(qb_, ld, ob_, ldd, (int64_t)qt0 * 64, tid), smem, tid);
+        }
         const float s = stat_load(qt0);
         if (tid < 128) ((float*)(smem + 2 * TILE))[tid] = s;
     }
-    __syncthreads();
+    if constexpr (RD) wait_all_barrier();
+    else __syncthreads();
     for (int qt = qt0; qt < nq; ++qt) {
         const int it = qt - qt0;
         const int nxt = qt + 1 < nq ? qt + 1 : qt;
-#ifndef CG_ATTN_NOSTAGE
-        const Stage2 st = stage_load(qb_, ld, ob_, ldd, (int64_t)nxt * 64, tid);
-#endif
+        Stage2 st;
+        if constexpr (RD) {
+            if (qt + 1 < nq) {   // slot (it + 1) & 1 was last read before the previous barrier
+                dma_tile(qb_, ld, (int64_t)nxt * 64, smem + ((it + 1) & 1) * KV_STAGE, wave_, lane);
+                dma_tile(ob_, ldd, (int64_t)nxt * 64, smem + ((it + 1) & 1) * KV_STAGE + TILE, wave_, lane);
+            }
+        } else {
+            st = stage_load(qb_, ld, ob_, ldd, (int64_t)nxt * 64, tid);
+        }
         const float sn = stat_load(nxt);
         const uint32_t mn = (DROP && act && nxt >= qtm) ? mcol[(nxt - qtm) * 64] : 0u;
         const char* S0 = smem + (it & 1) * KV_STAGE;
@@ -768,12 +795,11 @@ __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_
         const int q0 = qt * 64;
         if (act && q0 + 63 >= kq) dkdv_tile<DROP>(Qi, Oi, st_lse, st_del, q0, kq, key, kf, vf, mw, c2, dka, dva, lane);
         char* D = smem + ((it + 1) & 1) * KV_STAGE;
-#ifndef CG_ATTN_NOSTAGE
-        stage_store(st, D, tid);
-#endif
+        if constexpr (!RD) stage_store(st, D, tid);
         if (tid < 128) ((float*)(D + 2 * TILE))[tid] = sn;
         mw = mn;
-        __syncthreads();
+        if constexpr (RD) wait_all_barrier();
+        else __syncthreads();
     }
     if (!act) return;
     store_rows(dk + (boff + key) * lddkv + hh * 64, dka, scale * dscale, lane);
@@ -781,7 +807,7 @@ __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_
 }
 
 // pairs of 128-key blocks per workgroup (x, then nk - 1 - x): uniform causal work per workgroup
-template <bool DROP>
+template <bool DROP, bool RD>
 __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, const bf16_t* __restrict__ q,
                                                           const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
                                                           int64_t ld, const bf16_t* __restrict__ dout, int64_t ldd,
@@ -797,7 +823,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, con
 #pragma unroll 1
     for (int pass = 0; pass < npass; ++pass) {
         if (pass) __syncthreads();
-        dkdv_kblock<DROP>(pass ? second : x, bh, smem, T_, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
+        dkdv_kblock<DROP, RD>(pass ? second : x, bh, smem, T_, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
                           mask, dscale);
     }
 }
@@ -1110,6 +1136,18 @@ void launch_fwd_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* 
     else
         k_attn_fwd_d64<false><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, lse, scale * LOG2E, nullptr, 1.f);
 }
+// ring kernels: LDS-DMA tile staging unless attn_variant 3 (register staging, A/B)
+#define RD_SWITCH(...)                        \
+    do {                                      \
+        if (g_attn_variant == 3) {            \
+            constexpr bool RD_ = false;       \
+            __VA_ARGS__;                      \
+        } else {                              \
+            constexpr bool RD_ = true;        \
+            __VA_ARGS__;                      \
+        }                                     \
+    } while (0)
+
 void launch_dq_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                    const bf16_t* o, int64_t ldo, const bf16_t* dout, int64_t ldd, const float* lse, float* delta,
                    bf16_t* dq, int64_t lddq, float scale, const DropArgs& d, hipStream_t st) {
@@ -1122,11 +1160,11 @@ void launch_dq_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k
     }
     const dim3 grid((unsigned)((ceil_div(T, 256) + 1) / 2), (unsigned)(B * H));
     if (d.mask)
-        k_attn_dq_d64<true><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
-                                                  d.mask, d.dscale);
+        RD_SWITCH(k_attn_dq_d64<true, RD_><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
+                                                  d.mask, d.dscale));
     else
-        k_attn_dq_d64<false><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
-                                                   nullptr, 1.f);
+        RD_SWITCH(k_attn_dq_d64<false, RD_><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
+                                                   nullptr, 1.f));
 }
 void launch_bwd_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                     const bf16_t* o, int64_t ldo, const bf16_t* dout, int64_t ldd, const float* lse, float* delta,
@@ -1158,11 +1196,11 @@ void launch_dkdv_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t*
     }
     const dim3 grid((unsigned)((ceil_div(T, 128) + 1) / 2), (unsigned)(B * H));
     if (d.mask)
-        k_attn_dkdv_d64<true><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
-                                                    d.mask_bwd, d.dscale);
+        RD_SWITCH(k_attn_dkdv_d64<true, RD_><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
+                                                    d.mask_bwd, d.dscale));
     else
-        k_attn_dkdv_d64<false><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
-                                                     nullptr, 1.f);
+        RD_SWITCH(k_attn_dkdv_d64<false, RD_><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
+                                                     nullptr, 1.f));
 }
 }  // namespace attn
 
