@@ -105,6 +105,8 @@ __device__ __forceinline__ void red_tail(const RedJobs& r) {
 extern int g_gemm_variant;
 // test knob (cg_set_tuning("gemm_max_grid", n)): cap on persistent-kernel blocks; 0 = resident slots
 extern int g_gemm_max_grid;
+extern int g_gemm_group_p8;
+extern int g_gemm_group_pk;
 // test knob (cg_set_tuning("pk_flags", f)) for the persistent kernel's epilogue (gemm_pk.hip)
 extern int g_pk_flags;
 int gemm_cu_count();  // compute units of the current device (cached; gemm_pk.hip)

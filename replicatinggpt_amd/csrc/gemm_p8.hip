@@ -88,7 +88,7 @@ template <bool AT, bool BT, int BM, int BN, int WM, int NBUF, int EP>
 __global__ __launch_bounds__(P8_THREADS, (Geo8<BM, BN, NBUF>::OCC))
 void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
                const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype, int64_t ldc,
-               EpiArgs epi, int split_k, int64_t kchunk, float* __restrict__ ws, RedJobs red) {
+               EpiArgs epi, int split_k, int64_t kchunk, float* __restrict__ ws, int gm, RedJobs red) {
     using G = Geo8<BM, BN, NBUF>;
     using DA = Dma8<AT, BM>;
     using DB = Dma8<BT, BN>;
@@ -118,9 +118,10 @@ void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     auto decode = [&](int j, int64_t& m0, int64_t& n0, int& split) {
         const int it = xcd_remap(b + j * P, nitems);
         split = it / ntiles;
-        const int t = it - split * ntiles;
-        m0 = (int64_t)(t / tilesN) * BM;
-        n0 = (int64_t)(t % tilesN) * BN;
+        int tm, tn;
+        tile_rc(it - split * ntiles, ntiles / tilesN, tilesN, gm, tm, tn);
+        m0 = (int64_t)tm * BM;
+        n0 = (int64_t)tn * BN;
     };
 
     // DMA issue cursor (item ij, K-tile ikt) and its operand origins
@@ -409,7 +410,7 @@ bool launch8(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, i
 #define FG(AT_, BT_, EP_)                                                                                \
     k_gemm_p8<AT_, BT_, BM, BN, WM, NBUF, EP_><<<grid, P8_THREADS, G::LDS, st>>>(M, N, K, A, lda, B, ldb, C,     \
                                                                                  c_dtype, ldc, e, split_k, kchunk, ws, \
-                                                                                 take_pending_reduces(st))
+                                                                                 g_gemm_group_p8, take_pending_reduces(st))
     // keep bits (host-checked: split 1, bf16 output, beta 0) need 64-column wave fragments (FN == 4)
     const bool bits = e.aux_dtype == CG_BITS;
     constexpr bool FN4 = BN / (8 / WM) == 64;

@@ -345,9 +345,10 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     auto decode = [&](int j, int64_t& m0, int64_t& n0, int& split) {
         const int it = xcd_remap(b + j * P, nitems);
         split = it / ntiles;
-        const int t = it - split * ntiles;
-        m0 = (int64_t)(t / tilesN) * BM;
-        n0 = (int64_t)(t % tilesN) * BN;
+        int tm, tn;
+        tile_rc(it - split * ntiles, ntiles / tilesN, tilesN, flags >> 8, tm, tn);
+        m0 = (int64_t)tm * BM;
+        n0 = (int64_t)tn * BN;
     };
     int total = 0;
     for (int j = 0; j < my_items; ++j) {
@@ -547,7 +548,8 @@ void launch_1(unsigned grid, int64_t M, int64_t N, int64_t K, const bf16_t* A, i
               hipStream_t st) {
     using G = GeoP<BM, BN, NBUF>;
     k_gemm_pk<AT_, BT_, BM, BN, NBUF, EK><<<grid, G::THREADS, G::LDS, st>>>(M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e,
-                                                                         split_k, kchunk, ws, g_pk_flags,
+                                                                         split_k, kchunk, ws,
+                                                                         g_pk_flags | (g_gemm_group_pk << 8),
                                                                          take_pending_reduces(st));
 }
 

@@ -51,6 +51,22 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
+// output tile (tm, tn) of flattened tile index t.  gm <= 1: row-major.  gm > 1: grouped order --
+// gm row panels walked column by column (the last group may be shorter), so the items one XCD runs
+// at once (consecutive after xcd_remap) share fewer A and B panels in its L2.  Bijective.
+__device__ __forceinline__ void tile_rc(int t, int tilesM, int tilesN, int gm, int& tm, int& tn) {
+    if (gm <= 1) {
+        tm = t / tilesN;
+        tn = t - tm * tilesN;
+        return;
+    }
+    const int per = gm * tilesN, g = t / per, first = g * gm;
+    const int rows = tilesM - first < gm ? tilesM - first : gm;
+    const int r = t - g * per;
+    tn = r / rows;
+    tm = first + (r - tn * rows);
+}
+
 // 8 consecutive output columns of one row: bias / relu / dropout / relu-bwd / residual / beta, store
 __device__ __forceinline__ void epi_store8(float (&v)[8], int64_t m, int64_t n, int64_t N, void* Cv, int c_dtype,
                                            int64_t ldc, const EpiArgs& epi, uint64_t stream) {
