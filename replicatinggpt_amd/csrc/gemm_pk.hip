@@ -308,6 +308,9 @@ struct GeoP {
 // puts s_waitcnt vmcnt(0) before every K-tile's fragment reads -- waiting for the item's output
 // stores and, with the DMAs hidden from it (common.h dma16), for the prefetched stages too.  The
 // fixed-kind and slab instantiations have no such wait.
+#ifndef CG_PK_DPG
+#define CG_PK_DPG 1   // next-stage DMA instructions issued per group of 4 MFMAs
+#endif
 constexpr int EK_ANY = -1, EK_SLAB = 6;
 template <bool AT, bool BT, int BM, int BN, int NBUF, int EK = EK_ANY>
 // amdgpu_waves_per_eu: LDS caps residency at OCC blocks, so tell the scheduler the real occupancy;
@@ -468,26 +471,29 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
             for (int i = 0; i < 4; ++i) af[s][i] = frag<AT, BM>(imgA, wm * 64 + i * 16, s, lane);
         }
         __builtin_amdgcn_sched_barrier(0);
-        // 8 groups of 4 MFMAs (half s, A fragment i); the next stage's DMA instructions in between
+        // 8 groups of 4 MFMAs (half s, A fragment i); the next stage's DMA instructions in between,
+        // CG_PK_DPG of them after each group (1: spread over the whole step)
+        auto issue_dma = [&](int t) {
+            if (t < DA::PER_WAVE) da.issue1(na, t, dimg, wave);
+            else db.issue1(nbp, t - DA::PER_WAVE, dimg + G::IMG_A, wave);
+        };
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             const int s = t >> 2, i = t & 3;
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[i][j] = mfma_bf16(bf[s][j], af[s][i], acc[i][j]);
-            if (t < LPT) {
-                if (t < DA::PER_WAVE) da.issue1(na, t, dimg, wave);
-                else db.issue1(nbp, t - DA::PER_WAVE, dimg + G::IMG_A, wave);
-            }
+#pragma unroll
+            for (int d = 0; d < CG_PK_DPG; ++d)
+                if (t * CG_PK_DPG + d < LPT) issue_dma(t * CG_PK_DPG + d);
         }
 #pragma unroll
-        for (int t = 8; t < LPT; ++t) {
-            if (t < DA::PER_WAVE) da.issue1(na, t, dimg, wave);
-            else db.issue1(nbp, t - DA::PER_WAVE, dimg + G::IMG_A, wave);
-        }
+        for (int t = 8 * CG_PK_DPG; t < LPT; ++t) issue_dma(t);
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-            if (t < LPT) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+#pragma unroll
+            for (int d = 0; d < CG_PK_DPG; ++d)
+                if (t * CG_PK_DPG + d < LPT) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
         cur = cur + 1 == NBUF ? 0 : cur + 1;
