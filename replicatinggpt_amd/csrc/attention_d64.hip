@@ -187,6 +187,19 @@ __device__ __forceinline__ void dma_tile(const bf16_t* X, int64_t ldx, int64_t r
     }
 }
 
+// Tell hipcc that registers loaded by compiler-counted loads before a loop are ready here (after a
+// hidden wait that drained them): otherwise its wait-count pass puts the s_waitcnt for them at their
+// first use INSIDE the loop, where it runs every iteration -- vmcnt(0), which also waits for the
+// next tile's DMAs issued at the iteration head (no prefetch left).
+template <typename R>
+__device__ __forceinline__ void ready1(const R& r) {
+    asm volatile("" ::"v"(r));
+}
+template <typename... R>
+__device__ __forceinline__ void mark_ready(const R&... r) {
+    (ready1(r), ...);
+}
+
 // Resident kernels: wait for every vector-memory operation of this wave (the LDS-DMA tiles with
 // it), then a workgroup barrier: every wave's DMAs have landed.  One asm statement, so no LDS read
 // can be scheduled between the two.
@@ -291,20 +304,94 @@ template <bool DROP, int NSUB, int DIAG, bool QREG = false>
 __device__ __forceinline__ void fwd_group_tile(const char* Ki, const char* Vi, const char* Qimg, int qr, int lane,
                                                float scale_log2, float& m_run, float& l_run, fv16 (&o)[2],
                                                uint32_t mw, const sv8* qreg = nullptr) {
+    // every fragment of a product is read before its first MFMA (pinned: hipcc otherwise issues each
+    // read next to its MFMA and waits for it there)
+    sv8 kf[NSUB][4], qf[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        qf[ks] = QREG ? qreg[ks] : frag_row(Qimg, qr, ks, lane);
+#pragma unroll
+        for (int kt = 0; kt < NSUB; ++kt) kf[kt][ks] = frag_row(Ki, 32 * kt, ks, lane);
+    }
+    __builtin_amdgcn_sched_barrier(0);
     fv16 s[2];
     s[0] = fv16{};
     s[1] = fv16{};
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-        const sv8 qf = QREG ? qreg[ks] : frag_row(Qimg, qr, ks, lane);
-        s[0] = mfma32(frag_row(Ki, 0, ks, lane), qf, s[0]);
-        if (NSUB == 2) s[1] = mfma32(frag_row(Ki, 32, ks, lane), qf, s[1]);
+        s[0] = mfma32(kf[0][ks], qf[ks], s[0]);
+        if (NSUB == 2) s[1] = mfma32(kf[NSUB - 1][ks], qf[ks], s[1]);
     }
     if (DIAG >= 0) mask_upper(s[DIAG], lane & 31, 0, lane, -INFINITY);   // key0 = the group's first query
     rescale_if(tile_max<NSUB>(s) * scale_log2, m_run, l_run, o);
     sv8 pf[2][2];
     softmax_pack<DROP, NSUB>(s, scale_log2, m_run, l_run, mw, pf);
-    pv_tile<NSUB>(o, Vi, pf, lane);
+    sv8 vf[NSUB][2][2];
+#pragma unroll
+    for (int kt = 0; kt < NSUB; ++kt)
+#pragma unroll
+        for (int sk = 0; sk < 2; ++sk)
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt) vf[kt][sk][dt] = frag_tr(Vi, 32 * kt, sk, 32 * dt, lane);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kt = 0; kt < NSUB; ++kt)
+#pragma unroll
+        for (int sk = 0; sk < 2; ++sk) {
+            o[0] = mfma32(vf[kt][sk][0], pf[kt][sk], o[0]);
+            o[1] = mfma32(vf[kt][sk][1], pf[kt][sk], o[1]);
+        }
+}
+
+// Phase helpers of the pipelined forward loop.  hipcc left to itself issues each LDS fragment read
+// right before the MFMA that consumes it and waits lgkmcnt(0) there (one exposed LDS round trip per
+// MFMA: 46 % of the forward's wave cycles waiting, profiles/r2_pmc_attention_c4_p02.txt), and runs
+// the other group's softmax VALU as one block beside no MFMA.  So each phase reads all its fragments
+// first (pinned by sched_barrier), then interleaves its 8 MFMAs with the other group's VALU work
+// (sched_group_barrier: one MFMA, then a share of the VALU).
+__device__ __forceinline__ void read_qk(const char* Ki, const char* Qimg, int qr, int lane, sv8 (&kf)[2][4],
+                                        sv8 (&qf)[4]) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        qf[ks] = frag_row(Qimg, qr, ks, lane);
+        kf[0][ks] = frag_row(Ki, 0, ks, lane);
+        kf[1][ks] = frag_row(Ki, 32, ks, lane);
+    }
+}
+__device__ __forceinline__ void mfma_qk(fv16 (&s)[2], const sv8 (&kf)[2][4], const sv8 (&qf)[4]) {
+    s[0] = fv16{};
+    s[1] = fv16{};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        s[0] = mfma32(kf[0][ks], qf[ks], s[0]);
+        s[1] = mfma32(kf[1][ks], qf[ks], s[1]);
+    }
+}
+__device__ __forceinline__ void read_v(const char* Vi, int lane, sv8 (&vf)[2][2][2]) {
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int sk = 0; sk < 2; ++sk)
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt) vf[kt][sk][dt] = frag_tr(Vi, 32 * kt, sk, 32 * dt, lane);
+}
+__device__ __forceinline__ void mfma_pv(fv16 (&o)[2], const sv8 (&vf)[2][2][2], const sv8 (&pf)[2][2]) {
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int sk = 0; sk < 2; ++sk) {
+            o[0] = mfma32(vf[kt][sk][0], pf[kt][sk], o[0]);
+            o[1] = mfma32(vf[kt][sk][1], pf[kt][sk], o[1]);
+        }
+}
+// 8 MFMAs, each followed by NV instructions of the region's VALU (ID: the region's group chain)
+template <int NV>
+__device__ __forceinline__ void interleave8() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+    }
 }
 
 // Forward.  Tiles where both of a wave's query groups (A = 7 - w, B = w) are full (before B's
@@ -405,17 +492,40 @@ __device__ __forceinline__ void fwd_qblock(int qblk, int bh, char* smem, int64_t
         const char* Ki = smem + cs * SLOT;
         const char* Vi = Ki + TILE;
         const char* Vp = smem + ps * SLOT + TILE;
-        // at kv = 0, B's "previous tile" is sB = -inf against a zeroed V slot: it adds exactly 0
-        qk_tile(sA, Ki, Qimg, qr[0], lane);
+        sv8 kf[2][4], qf[4], vf[2][2][2];
+        // [1] S_A(kv) || P_B(kv - 1).  At kv = 0, B's "previous tile" is sB = -inf against a zeroed
+        // V slot: it adds exactly 0
+        read_qk(Ki, Qimg, qr[0], lane, kf, qf);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_qk(sA, kf, qf);
         softmax_pack<DROP>(sB, scale_log2, m_run[1], l_run[1], mwBp, pfB);
-        pv_tile(oacc[1], Vp, pfB, lane);
-        rescale_if(tile_max(sA) * scale_log2, m_run[0], l_run[0], oacc[0]);
+        interleave8<20>();
+        __builtin_amdgcn_sched_barrier(0);
+        // [2] O_B += P_B V(kv - 1) || max_A(kv), then A's rescale decision
+        read_v(Vp, lane, vf);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_pv(oacc[1], vf, pfB);
+        const float mA = tile_max(sA) * scale_log2;
+        interleave8<3>();
+        __builtin_amdgcn_sched_barrier(0);
+        rescale_if(mA, m_run[0], l_run[0], oacc[0]);
         stage_store1(stk, smem + ns * SLOT, tid);
         const Stage1 stv = stage_load1(vb_, ld, (int64_t)nxt * 64, tid);
-        qk_tile(sB, Ki, Qimg, qr[1], lane);
+        // [3] S_B(kv) || P_A(kv)
+        read_qk(Ki, Qimg, qr[1], lane, kf, qf);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_qk(sB, kf, qf);
         softmax_pack<DROP>(sA, scale_log2, m_run[0], l_run[0], mw[0], pfA);
-        pv_tile(oacc[0], Vi, pfA, lane);
-        rescale_if(tile_max(sB) * scale_log2, m_run[1], l_run[1], oacc[1]);
+        interleave8<20>();
+        __builtin_amdgcn_sched_barrier(0);
+        // [4] O_A += P_A V(kv) || max_B(kv), then B's rescale decision
+        read_v(Vi, lane, vf);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_pv(oacc[0], vf, pfA);
+        const float mB = tile_max(sB) * scale_log2;
+        interleave8<3>();
+        __builtin_amdgcn_sched_barrier(0);
+        rescale_if(mB, m_run[1], l_run[1], oacc[1]);
         stage_store1(stv, smem + ns * SLOT + TILE, tid);
         mwBp = mw[1];
         mw[0] = mn[0];
@@ -545,9 +655,9 @@ __device__ __forceinline__ void dq_group_tile(const char* Ki, const char* Vi, in
     }
 }
 
-// RD: K/V tiles by LDS-DMA (common.h dma16, no staging registers or ds_writes) instead of register
-// staging; attn_variant 3 selects the register-staged form (A/B)
-template <bool DROP, bool RD>
+// K/V tiles by LDS-DMA (common.h dma16) into a 2-slot ring, the next tile's DMAs issued before the
+// current tile's products (round 2: register staging measured 706 -> 686 us for the C4 backward)
+template <bool DROP>
 __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t T_, int H, const bf16_t* __restrict__ q,
                                           const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, int64_t ld,
                                           const bf16_t* __restrict__ o, int64_t ldo, const bf16_t* __restrict__ dout,
@@ -584,40 +694,38 @@ __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t 
     const int qlast = (Q0 + 255 < T - 1) ? Q0 + 255 : T - 1;
     const int nkv = qlast / 64 + 1;
     const int wave_ = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if constexpr (RD) {
-        dma_tile(kb_, ld, 0, smem, wave_, lane);
-        dma_tile(vb_, ld, 0, smem + TILE, wave_, lane);
-        wait_all_barrier();
-    } else {
-        stage_store(stage_load(kb_, ld, vb_, ld, 0, tid), smem, tid);
-        __syncthreads();
-    }
+    dma_tile(kb_, ld, 0, smem, wave_, lane);
+    dma_tile(vb_, ld, 0, smem + TILE, wave_, lane);
+    wait_all_barrier();
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) mark_ready(qf[g][ks], df[g][ks]);
+    mark_ready(mw[0], mw[1], lse2[0], lse2[1], dl[0], dl[1]);
     for (int kv = 0; kv < nkv; ++kv) {
         const int nxt = kv + 1 < nkv ? kv + 1 : kv;
-        Stage2 st;
-        if constexpr (RD) {
-            if (kv + 1 < nkv) {   // slot (kv + 1) & 1 was last read before the previous barrier
-                dma_tile(kb_, ld, (int64_t)nxt * 64, smem + ((kv + 1) & 1) * 2 * TILE, wave_, lane);
-                dma_tile(vb_, ld, (int64_t)nxt * 64, smem + ((kv + 1) & 1) * 2 * TILE + TILE, wave_, lane);
-            }
-        } else {
-            st = stage_load(kb_, ld, vb_, ld, (int64_t)nxt * 64, tid);
+        if (kv + 1 < nkv) {   // slot (kv + 1) & 1 was last read before the previous barrier
+            dma_tile(kb_, ld, (int64_t)nxt * 64, smem + ((kv + 1) & 1) * 2 * TILE, wave_, lane);
+            dma_tile(vb_, ld, (int64_t)nxt * 64, smem + ((kv + 1) & 1) * 2 * TILE + TILE, wave_, lane);
         }
+        // the next tile's keep words by hidden loads: a compiler-counted load issued after the DMAs
+        // made hipcc wait vmcnt(0) -- for the DMAs too -- at the head of the tile (no prefetch left)
         uint32_t mn[2] = {0u, 0u};
+        if constexpr (DROP) {
 #pragma unroll
-        for (int g = 0; g < 2; ++g)
-            if (DROP && act[g] && nxt * 64 <= qg[g] + 31) mn[g] = mrow[g][nxt * 64];
+            for (int g = 0; g < 2; ++g)
+                if (act[g] && nxt * 64 <= qg[g] + 31) gload4(mn[g], mrow[g] + nxt * 64);
+        }
         const char* Ki = smem + (kv & 1) * 2 * TILE;
         const int k0 = kv * 64;
 #pragma unroll
         for (int g = 0; g < 2; ++g)
             if (act[g] && k0 <= qg[g] + 31)
                 dq_group_tile<DROP>(Ki, Ki + TILE, k0, qg[g], qf[g], df[g], lse2[g], dl[g], mw[g], c2, dqa[g], lane);
-        if constexpr (!RD) stage_store(st, smem + ((kv + 1) & 1) * 2 * TILE, tid);
+        wait_all_barrier();   // the next tile (and the keep words) have landed for every wave
+        asm volatile("" : "+v"(mn[0]), "+v"(mn[1]));
         mw[0] = mn[0];
         mw[1] = mn[1];
-        if constexpr (RD) wait_all_barrier();   // the next tile has landed for every wave
-        else __syncthreads();
     }
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
@@ -628,7 +736,7 @@ __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t 
 }
 
 // pairs of query blocks per workgroup, as the forward
-template <bool DROP, bool RD>
+template <bool DROP>
 __global__ __launch_bounds__(256, 2) void k_attn_dq_d64(int64_t T_, int H, const bf16_t* __restrict__ q,
                                                         const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
                                                         int64_t ld, const bf16_t* __restrict__ o, int64_t ldo,
@@ -644,7 +752,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_dq_d64(int64_t T_, int H, const
 #pragma unroll 1
     for (int pass = 0; pass < npass; ++pass) {
         if (pass) __syncthreads();
-        dq_qblock<DROP, RD>(pass ? x : first, bh, smem, T_, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
+        dq_qblock<DROP>(pass ? x : first, bh, smem, T_, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
                         mask, dscale);
     }
 }
@@ -721,7 +829,7 @@ __device__ __forceinline__ void dkdv_tile(const char* Qi, const char* Oi, const 
     }
 }
 
-template <bool DROP, bool RD>
+template <bool DROP>
 __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_t T_, int H,
                                             const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                             const bf16_t* __restrict__ v, int64_t ld, const bf16_t* __restrict__ dout,
@@ -762,31 +870,28 @@ __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_
     };
     const int wave_ = __builtin_amdgcn_readfirstlane(tid >> 6);
     {
-        if constexpr (RD) {
-            dma_tile(qb_, ld, (int64_t)qt0 * 64, smem, wave_, lane);
-            dma_tile(ob_, ldd, (int64_t)qt0 * 64, smem + TILE, wave_, lane);
-        } else {
-            stage_store(stage_load(qb_, ld, ob_, ldd, (int64_t)qt0 * 64, tid), smem, tid);
-        }
+        dma_tile(qb_, ld, (int64_t)qt0 * 64, smem, wave_, lane);
+        dma_tile(ob_, ldd, (int64_t)qt0 * 64, smem + TILE, wave_, lane);
         const float s = stat_load(qt0);
         if (tid < 128) ((float*)(smem + 2 * TILE))[tid] = s;
     }
-    if constexpr (RD) wait_all_barrier();
-    else __syncthreads();
+    wait_all_barrier();
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) mark_ready(kf[ks], vf[ks]);
+    mark_ready(mw);
     for (int qt = qt0; qt < nq; ++qt) {
         const int it = qt - qt0;
         const int nxt = qt + 1 < nq ? qt + 1 : qt;
-        Stage2 st;
-        if constexpr (RD) {
-            if (qt + 1 < nq) {   // slot (it + 1) & 1 was last read before the previous barrier
-                dma_tile(qb_, ld, (int64_t)nxt * 64, smem + ((it + 1) & 1) * KV_STAGE, wave_, lane);
-                dma_tile(ob_, ldd, (int64_t)nxt * 64, smem + ((it + 1) & 1) * KV_STAGE + TILE, wave_, lane);
-            }
-        } else {
-            st = stage_load(qb_, ld, ob_, ldd, (int64_t)nxt * 64, tid);
+        if (qt + 1 < nq) {   // slot (it + 1) & 1 was last read before the previous barrier
+            dma_tile(qb_, ld, (int64_t)nxt * 64, smem + ((it + 1) & 1) * KV_STAGE, wave_, lane);
+            dma_tile(ob_, ldd, (int64_t)nxt * 64, smem + ((it + 1) & 1) * KV_STAGE + TILE, wave_, lane);
         }
-        const float sn = stat_load(nxt);
-        const uint32_t mn = (DROP && act && nxt >= qtm) ? mcol[(nxt - qtm) * 64] : 0u;
+        // the next tile's row statistics and keep word by hidden loads (compiler-counted loads issued
+        // after the DMAs made hipcc wait vmcnt(0) -- for the DMAs too -- inside this tile's products)
+        uint32_t sw = 0u, mn = 0u;
+        if (tid < 64) gload4(sw, lse_b + nxt * 64 + tid);
+        else if (tid < 128) gload4(sw, del_b + nxt * 64 + tid - 64);
+        if (DROP && act && nxt >= qtm) gload4(mn, mcol + (nxt - qtm) * 64);
         const char* S0 = smem + (it & 1) * KV_STAGE;
         const char* Qi = S0;
         const char* Oi = S0 + TILE;
@@ -795,11 +900,13 @@ __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_
         const int q0 = qt * 64;
         if (act && q0 + 63 >= kq) dkdv_tile<DROP>(Qi, Oi, st_lse, st_del, q0, kq, key, kf, vf, mw, c2, dka, dva, lane);
         char* D = smem + ((it + 1) & 1) * KV_STAGE;
-        if constexpr (!RD) stage_store(st, D, tid);
-        if (tid < 128) ((float*)(D + 2 * TILE))[tid] = sn;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile, its statistics and keep word
+        asm volatile("" : "+v"(sw), "+v"(mn));
+        // stat_load's arithmetic on the loaded word
+        if (tid < 64) ((float*)(D + 2 * TILE))[tid] = __uint_as_float(sw) * LOG2E;
+        else if (tid < 128) ((float*)(D + 2 * TILE))[tid] = -__uint_as_float(sw) / dscale;
         mw = mn;
-        if constexpr (RD) wait_all_barrier();
-        else __syncthreads();
+        wait_all_barrier();
     }
     if (!act) return;
     store_rows(dk + (boff + key) * lddkv + hh * 64, dka, scale * dscale, lane);
@@ -807,7 +914,7 @@ __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_
 }
 
 // pairs of 128-key blocks per workgroup (x, then nk - 1 - x): uniform causal work per workgroup
-template <bool DROP, bool RD>
+template <bool DROP>
 __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, const bf16_t* __restrict__ q,
                                                           const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
                                                           int64_t ld, const bf16_t* __restrict__ dout, int64_t ldd,
@@ -823,7 +930,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, con
 #pragma unroll 1
     for (int pass = 0; pass < npass; ++pass) {
         if (pass) __syncthreads();
-        dkdv_kblock<DROP, RD>(pass ? second : x, bh, smem, T_, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
+        dkdv_kblock<DROP>(pass ? second : x, bh, smem, T_, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
                           mask, dscale);
     }
 }
@@ -839,6 +946,32 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, con
 // no staging barriers.  Same wave/group assignment, per-tile arithmetic and keep-bit words as the
 // ring kernels, so the results are bitwise the same.  (The register loads follow the DMAs: vmcnt
 // retires in order, so waiting for them covers the tiles too -- see common.h dma16.)
+// O^T accumulator pair of one query (lane & 31; dims 32 dt + acc_row) as bf16, x mult, in 16-B
+// row segments: lanes l and l + 32 hold the two 4-dim halves of each 8-dim group, so for each
+// pair of groups (i, i + 1) one v_permlane32_swap per dword leaves lanes 0-31 with dims 8i..8i+7
+// and lanes 32-63 with 8(i+1)..8(i+1)+7 (cdna_hip_programming.md T21): 4 dwordx4 stores per lane
+// instead of 8 dwordx2.  Same bytes as store_rows.
+__device__ __forceinline__ void store_rows_wide(bf16_t* row, const fv16 (&acc)[2], float mult, int lane) {
+    const int h = lane >> 5;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+            const float* x = &((const float*)&acc[dt])[4 * i];
+            const float* y = &((const float*)&acc[dt])[4 * i + 4];
+            const uint32_t a0 = pack_bf2(x[0] * mult, x[1] * mult), a1 = pack_bf2(x[2] * mult, x[3] * mult);
+            const uint32_t b0 = pack_bf2(y[0] * mult, y[1] * mult), b1 = pack_bf2(y[2] * mult, y[3] * mult);
+            const auto s0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+            const auto s1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+            *(uint4*)(row + 32 * dt + 8 * (i + h)) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        }
+}
+
+// Resident forward (T = 64 NT <= 256).  Every load is issued up front -- the query-side operands
+// first (Q fragments and keep words: hidden register loads, common.h gload16/gload4), then the
+// K/V tiles in tile order by LDS-DMA -- and tile t waits only for what it reads: the register
+// loads and tiles 0..t (vmcnt counts them in issue order), so the first tile's MFMAs start while
+// the later tiles are still in flight.  Same per-tile arithmetic and keep words as the ring kernel.
 template <bool DROP, int NT>
 __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64r(int H, const bf16_t* __restrict__ q,
                                                           const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
@@ -853,33 +986,64 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64r(int H, const bf16_t* _
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b = bh / H, hh = bh % H;
     const int64_t boff = (int64_t)b * T, ntile = mask_tiles(T);
+    const int qg[2] = {32 * (7 - wave), 32 * wave};   // A = 7 - w (longer causal prefix), B = w
+    const bool act[2] = {qg[0] < T, qg[1] < T};
+    sv8 qv[2][4];
+    uint32_t mw[2][NT];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        const int qa = (act[g] ? qg[g] : 0) + (lane & 31);   // inactive groups load a valid row, unused
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) gload16(qv[g][ks], q + (boff + qa) * ld + hh * 64 + 16 * ks + 8 * (lane >> 5));
+        if constexpr (DROP) {
+            const int qb = act[g] ? qg[g] >> 5 : 0;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {   // tiles past the group's diagonal re-read tile 0 (unused)
+                const int tt = 64 * t <= 32 * qb + 31 ? t : 0;
+                gload4(mw[g][t], mask + ((int64_t)bh * ntile + mask_fwd_tile(qb, tt)) * 64 + lane);
+            }
+        }
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         dma_tile(k + boff * ld + hh * 64, ld, 64 * t, smem + 2 * t * TILE, wave, lane);
         dma_tile(v + boff * ld + hh * 64, ld, 64 * t, smem + (2 * t + 1) * TILE, wave, lane);
     }
-    const int qg[2] = {32 * (7 - wave), 32 * wave};   // A = 7 - w (longer causal prefix), B = w
-    const bool act[2] = {qg[0] < T, qg[1] < T};
-    sv8 qf[2][4];
-    uint32_t mw[2][NT];
+    // the register loads and tile 0 have landed (4 DMA instructions per tile per wave stay younger)
+    if constexpr (!DROP) {
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) mw[g][t] = 0u;
+    }
+    // then every destination is named "+v" by an (ordered, volatile) empty statement after the wait,
+    // so nothing reads it earlier
+    asm volatile("s_waitcnt vmcnt(%c0)\n\ts_barrier" ::"i"(4 * (NT - 1)) : "memory");
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-            qf[g][ks] = act[g] ? ld_frag(q + boff * ld + hh * 64, ld, qg[g] + (lane & 31), ks, lane) : sv8{};
+        for (int ks = 0; ks < 4; ++ks) asm volatile("" : "+v"(qv[g][ks]));
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
-            mw[g][t] = (DROP && act[g] && 64 * t <= qg[g] + 31)
-                           ? mask[((int64_t)bh * ntile + mask_fwd_tile(qg[g] >> 5, t)) * 64 + lane]
-                           : 0u;
+        for (int t = 0; t < NT; ++t) asm volatile("" : "+v"(mw[g][t]));
     }
+    const sv8 (&qf)[2][4] = qv;
     fv16 oacc[2][2];
 #pragma unroll
     for (int g = 0; g < 2; ++g) oacc[g][0] = oacc[g][1] = fv16{};
     float m_run[2] = {-FLT_MAX, -FLT_MAX}, l_run[2] = {0.f, 0.f};
-    wait_all_barrier();
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
+        if (t) {   // tile t's DMAs (every wave's) have landed
+            if constexpr (NT >= 2) {
+                if (t == 1) asm volatile("s_waitcnt vmcnt(%c0)\n\ts_barrier" ::"i"(4 * (NT > 1 ? NT - 2 : 0)) : "memory");
+            }
+            if constexpr (NT >= 3) {
+                if (t == 2) asm volatile("s_waitcnt vmcnt(%c0)\n\ts_barrier" ::"i"(4 * (NT > 2 ? NT - 3 : 0)) : "memory");
+            }
+            if constexpr (NT >= 4) {
+                if (t == 3) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+            }
+        }
         const char* Ki = smem + 2 * t * TILE;
         const char* Vi = Ki + TILE;
 #pragma unroll
@@ -904,11 +1068,31 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64r(int H, const bf16_t* _
                                                          false);
         const float lt = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
         const int64_t qa = qg[g] + (lane & 31);
-        store_rows(o + (boff + qa) * ldo + hh * 64, oacc[g], dscale / lt, lane);
+        store_rows_wide(o + (boff + qa) * ldo + hh * 64, oacc[g], dscale / lt, lane);
         if (lane < 32) lse[(int64_t)bh * T + qa] = (m_run[g] + __log2f(lt)) * LN2;
     }
 }
 
+// tile t > 0 of a resident kernel: this wave's DMAs of tiles 0..t have landed (4 DMA instructions per
+// tile per wave, issued in tile order after the first register loads; X hidden loads issued after the
+// DMAs stay in flight too), then every wave's (barrier)
+template <int NT, int X = 0>
+__device__ __forceinline__ void res_tile_wait(int t) {
+    if constexpr (NT >= 2) {
+        if (t == 1) asm volatile("s_waitcnt vmcnt(%c0)\n\ts_barrier" ::"i"(4 * (NT > 1 ? NT - 2 : 0) + X) : "memory");
+    }
+    if constexpr (NT >= 3) {
+        if (t == 2) asm volatile("s_waitcnt vmcnt(%c0)\n\ts_barrier" ::"i"(4 * (NT > 2 ? NT - 3 : 0) + X) : "memory");
+    }
+    if constexpr (NT >= 4) {
+        if (t == 3) asm volatile("s_waitcnt vmcnt(%c0)\n\ts_barrier" ::"i"(X) : "memory");
+    }
+}
+
+// Resident dQ (T = 64 NT <= 256): the query-side operands (Q, dO and O fragments, lse, keep words)
+// by hidden register loads first, then the K/V tiles by LDS-DMA in tile order; tile t waits only
+// for tiles 0..t (as k_attn_fwd_d64r).  Per-group setup (delta in dq_group_setup's summation order)
+// and per-tile arithmetic as the ring kernel.
 template <bool DROP, int NT>
 __device__ __forceinline__ void dq_res(int bh, char* smem, int H, const bf16_t* __restrict__ q,
                                        const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, int64_t ld,
@@ -922,34 +1106,74 @@ __device__ __forceinline__ void dq_res(int bh, char* smem, int H, const bf16_t* 
     const int b = bh / H, hh = bh % H;
     const int64_t boff = (int64_t)b * T, ntile = mask_tiles(T);
     const float c2 = scale * LOG2E;
+    const int qg[2] = {32 * (7 - wave), 32 * wave};
+    const bool act[2] = {qg[0] < T, qg[1] < T};
+    sv8 qf[2][4], df[2][4], of[2][4];
+    uint32_t lsew[2], mw[2][NT];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        const int64_t qa = (act[g] ? qg[g] : 0) + (lane & 31);   // inactive groups: a valid row, unused
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const int col = hh * 64 + 16 * ks + 8 * (lane >> 5);
+            gload16(qf[g][ks], q + (boff + qa) * ld + col);
+            gload16(df[g][ks], dout + (boff + qa) * ldd + col);
+            gload16(of[g][ks], o + (boff + qa) * ldo + col);
+        }
+        gload4(lsew[g], lse + (int64_t)bh * T + qa);
+        if constexpr (DROP) {
+            const int qb = act[g] ? qg[g] >> 5 : 0;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const int tt = 64 * t <= 32 * qb + 31 ? t : 0;
+                gload4(mw[g][t], mask + ((int64_t)bh * ntile + mask_fwd_tile(qb, tt)) * 64 + lane);
+            }
+        }
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         dma_tile(k + boff * ld + hh * 64, ld, 64 * t, smem + 2 * t * TILE, wave, lane);
         dma_tile(v + boff * ld + hh * 64, ld, 64 * t, smem + (2 * t + 1) * TILE, wave, lane);
     }
-    const int qg[2] = {32 * (7 - wave), 32 * wave};
-    const bool act[2] = {qg[0] < T, qg[1] < T};
-    uint32_t mw[2][NT];
+    if constexpr (!DROP) {
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
+        for (int g = 0; g < 2; ++g)
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
-            mw[g][t] = (DROP && act[g] && 64 * t <= qg[g] + 31)
-                           ? mask[((int64_t)bh * ntile + mask_fwd_tile(qg[g] >> 5, t)) * 64 + lane]
-                           : 0u;
-    sv8 qf[2][4], df[2][4];
+            for (int t = 0; t < NT; ++t) mw[g][t] = 0u;
+    }
+    asm volatile("s_waitcnt vmcnt(%c0)\n\ts_barrier" ::"i"(4 * (NT - 1)) : "memory");
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            asm volatile("" : "+v"(qf[g][ks]));
+            asm volatile("" : "+v"(df[g][ks]));
+            asm volatile("" : "+v"(of[g][ks]));
+        }
+        asm volatile("" : "+v"(lsew[g]));
+#pragma unroll
+        for (int t = 0; t < NT; ++t) asm volatile("" : "+v"(mw[g][t]));
+    }
     float lse2[2], dl[2];
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
-        dq_group_setup(act[g], qg[g] + (lane & 31), q + boff * ld + hh * 64, ld, o + boff * ldo + hh * 64, ldo,
-                       dout + boff * ldd + hh * 64, ldd, lse + (int64_t)bh * T, delta + (int64_t)bh * T, dscale, lane,
-                       qf[g], df[g], lse2[g], dl[g]);
+    for (int g = 0; g < 2; ++g) {   // dq_group_setup's arithmetic on the loaded fragments
+        float dsum = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dsum += bf2f((bf16_t)of[g][ks][j]) * bf2f((bf16_t)df[g][ks][j]);
+        if (!act[g]) dsum = 0.f;
+        dsum += __shfl_xor(dsum, 32, 64);
+        dl[g] = -dsum / dscale;
+        lse2[g] = act[g] ? __uint_as_float(lsew[g]) * LOG2E : 0.f;
+        if (act[g] && lane < 32) delta[(int64_t)bh * T + qg[g] + (lane & 31)] = dsum;
+    }
     fv16 dqa[2][2];
 #pragma unroll
     for (int g = 0; g < 2; ++g) dqa[g][0] = dqa[g][1] = fv16{};
-    wait_all_barrier();
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
+        res_tile_wait<NT>(t);
         const char* Ki = smem + 2 * t * TILE;
 #pragma unroll
         for (int g = 0; g < 2; ++g)
@@ -961,7 +1185,7 @@ __device__ __forceinline__ void dq_res(int bh, char* smem, int H, const bf16_t* 
     for (int g = 0; g < 2; ++g) {
         if (!act[g]) continue;
         const int64_t qa = qg[g] + (lane & 31);
-        store_rows(dq + (boff + qa) * lddq + hh * 64, dqa[g], scale * dscale, lane);
+        store_rows_wide(dq + (boff + qa) * lddq + hh * 64, dqa[g], scale * dscale, lane);
     }
 }
 
@@ -980,10 +1204,13 @@ __global__ __launch_bounds__(256, 2) void k_attn_dq_d64r(int H, const bf16_t* __
 }
 
 // dK/dV: one workgroup per (b, h); wave w takes key group w, then key group 7 - w (equal causal
-// work per wave: 8 + 1, 7 + 2, ... 32-query subtiles at T = 256), Q / dO / lse / delta resident
+// work per wave: 8 + 1, 7 + 2, ... 32-query subtiles at T = 256), Q / dO / lse / delta resident.
 // o != NULL: delta = rowsum(dO * O) is computed here (in dq_group_setup's summation order, so
-// bitwise the dQ kernel's value) instead of read from `delta` -- the merged backward launch
-template <bool DROP, int NT>
+// bitwise the dQ kernel's value) instead of read from `delta` -- the merged backward launch.
+// Register operands (row statistics, the first key group's K / V fragments, keep words) by hidden
+// loads first, then the Q / dO tiles by LDS-DMA; the first key group's tile t waits only for tiles
+// 0..t.  OD: delta from O and dO (o != NULL), else read from `delta`.
+template <bool DROP, int NT, bool OD>
 __device__ __forceinline__ void dkdv_res(int bh, char* smem, int H, const bf16_t* __restrict__ q,
                                          const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, int64_t ld,
                                          const bf16_t* __restrict__ dout, int64_t ldd, const float* __restrict__ lse,
@@ -998,69 +1225,137 @@ __device__ __forceinline__ void dkdv_res(int bh, char* smem, int H, const bf16_t
     const int b = bh / H, hh = bh % H;
     const int64_t boff = (int64_t)b * T, ntile = mask_tiles(T);
     const float c2 = scale * LOG2E;
+    const int kqs[2] = {32 * wave, 32 * (7 - wave)};
+    const bf16_t* kb_ = k + boff * ld + hh * 64;
+    const bf16_t* vb_ = v + boff * ld + hh * 64;
+    const bool srow = tid < T;   // whole waves (T % 64 == 0)
+    const int64_t sr = srow ? tid : 0;
+    uint32_t lsew = 0u, delw = 0u;
+    sv8 ov[2][4], dv_[2][4];   // O / dO row of query tid: halves h, columns 16 ks + 8 h .. +7
+    if (srow) {
+        gload4(lsew, lse + (int64_t)bh * T + sr);
+        if constexpr (OD) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) {
+                    gload16(ov[h][ks], o + (boff + sr) * ldo + hh * 64 + 16 * ks + 8 * h);
+                    gload16(dv_[h][ks], dout + (boff + sr) * ldd + hh * 64 + 16 * ks + 8 * h);
+                }
+        } else {
+            gload4(delw, delta + (int64_t)bh * T + sr);
+        }
+    }
+    uint32_t mw[2][NT];
+    if constexpr (DROP) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int kbw = kqs[p] >> 5, qtm = kbw >> 1;
+            const bool ok = kqs[p] < T;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {   // tiles before the key group's first query tile re-read its first
+                const int tt = ok && t >= qtm ? t - qtm : 0;
+                gload4(mw[p][t], mask + ((int64_t)bh * ntile + mask_bwd_tile(ok ? kbw : 0, ok ? qtm : 0, NT)) * 64 +
+                                     lane + tt * 64);
+            }
+        }
+    }
+    sv8 kf[4], vf[4];
+    {
+        const int key0 = (kqs[0] < T ? kqs[0] : 0) + (lane & 31);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            gload16(kf[ks], kb_ + (int64_t)key0 * ld + 16 * ks + 8 * (lane >> 5));
+            gload16(vf[ks], vb_ + (int64_t)key0 * ld + 16 * ks + 8 * (lane >> 5));
+        }
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         dma_tile(q + boff * ld + hh * 64, ld, 64 * t, smem + 2 * t * TILE, wave, lane);
         dma_tile(dout + boff * ldd + hh * 64, ldd, 64 * t, smem + (2 * t + 1) * TILE, wave, lane);
     }
-    const int kqs[2] = {32 * wave, 32 * (7 - wave)};
-    const bf16_t* kb_ = k + boff * ld + hh * 64;
-    const bf16_t* vb_ = v + boff * ld + hh * 64;
-    if (tid < T) {
-        st_lse[tid] = lse[(int64_t)bh * T + tid] * LOG2E;
+    // the second key group's K / V fragments behind the tiles (in flight until that group starts)
+    sv8 kf1[4], vf1[4];
+    {
+        const int key1 = (kqs[1] < T ? kqs[1] : 0) + (lane & 31);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            gload16(kf1[ks], kb_ + (int64_t)key1 * ld + 16 * ks + 8 * (lane >> 5));
+            gload16(vf1[ks], vb_ + (int64_t)key1 * ld + 16 * ks + 8 * (lane >> 5));
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(%c0)" ::"i"(4 * (NT - 1) + 8) : "memory");
+    asm volatile("" : "+v"(lsew), "+v"(delw));
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            asm volatile("" : "+v"(ov[h][ks]));
+            asm volatile("" : "+v"(dv_[h][ks]));
+        }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        asm volatile("" : "+v"(kf[ks]));
+        asm volatile("" : "+v"(vf[ks]));
+    }
+    if constexpr (DROP) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) asm volatile("" : "+v"(mw[p][t]));
+    } else {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) mw[p][t] = 0u;
+    }
+    if (srow) {
+        st_lse[tid] = __uint_as_float(lsew) * LOG2E;
         float dsum;
-        if (o) {   // query tid: halves h = 0, 1 (columns 16 ks + 8 h + j) summed as dq_group_setup's lanes
+        if constexpr (OD) {   // query tid: halves h = 0, 1 (columns 16 ks + 8 h + j) summed as dq_group_setup's lanes
             float sh[2];
-            const bf16_t* orow = o + (boff + tid) * ldo + hh * 64;
-            const bf16_t* drow = dout + (boff + tid) * ldd + hh * 64;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 float acc = 0.f;
 #pragma unroll
-                for (int ks = 0; ks < 4; ++ks) {
-                    const sv8 of = *(const sv8*)(orow + 16 * ks + 8 * h);
-                    const sv8 df = *(const sv8*)(drow + 16 * ks + 8 * h);
+                for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) acc += bf2f((bf16_t)of[j]) * bf2f((bf16_t)df[j]);
-                }
+                    for (int j = 0; j < 8; ++j) acc += bf2f((bf16_t)ov[h][ks][j]) * bf2f((bf16_t)dv_[h][ks][j]);
                 sh[h] = acc;
             }
             dsum = sh[0] + sh[1];
         } else {
-            dsum = delta[(int64_t)bh * T + tid];
+            dsum = __uint_as_float(delw);
         }
         st_del[tid] = -dsum / dscale;   // -delta' = -(1-p) delta
     }
-    uint32_t mw[2][NT];
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-        const int kbw = kqs[p] >> 5, qtm = kbw >> 1;
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-            mw[p][t] = (DROP && kqs[p] < T && t >= qtm)
-                           ? mask[((int64_t)bh * ntile + mask_bwd_tile(kbw, qtm, NT)) * 64 + lane + (t - qtm) * 64]
-                           : 0u;
-    }
+    // the row statistics are visible to every wave, and tile 0 has landed for every wave
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
         const int kq = kqs[p], key = kq + (lane & 31);
         const bool act = kq < T;
-        sv8 kf[4], vf[4];
+        if (p) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-            kf[ks] = act ? ld_frag(kb_, ld, key, ks, lane) : sv8{};
-            vf[ks] = act ? ld_frag(vb_, ld, key, ks, lane) : sv8{};
+            for (int ks = 0; ks < 4; ++ks) {
+                asm volatile("" : "+v"(kf1[ks]));
+                asm volatile("" : "+v"(vf1[ks]));
+                kf[ks] = kf1[ks];
+                vf[ks] = vf1[ks];
+            }
         }
-        if (!p) wait_all_barrier();
         fv16 dka[2] = {fv16{}, fv16{}}, dva[2] = {fv16{}, fv16{}};
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
+        for (int t = 0; t < NT; ++t) {
+            if (!p) res_tile_wait<NT, 8>(t);
             if (act && 64 * t + 63 >= kq)
                 dkdv_tile<DROP>(smem + 2 * t * TILE, smem + (2 * t + 1) * TILE, st_lse + 64 * t, st_del + 64 * t,
                                 64 * t, kq, key, kf, vf, mw[p][t], c2, dka, dva, lane);
+        }
         if (act) {
-            store_rows(dk + (boff + key) * lddkv + hh * 64, dka, scale * dscale, lane);
-            store_rows(dv + (boff + key) * lddkv + hh * 64, dva, DROP ? dscale : 1.f, lane);
+            store_rows_wide(dk + (boff + key) * lddkv + hh * 64, dka, scale * dscale, lane);
+            store_rows_wide(dv + (boff + key) * lddkv + hh * 64, dva, DROP ? dscale : 1.f, lane);
         }
     }
 }
@@ -1076,7 +1371,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64r(int H, const bf16_t* 
     __shared__ __attribute__((aligned(16))) char smem[NT * 2 * TILE + 2 * 64 * NT * 4];
     int x, bh;
     block_coords<false>(x, bh);
-    dkdv_res<DROP, NT>(bh, smem, H, q, k, v, ld, dout, ldd, lse, delta, nullptr, 0, dk, dv, lddkv, scale, mask,
+    dkdv_res<DROP, NT, false>(bh, smem, H, q, k, v, ld, dout, ldd, lse, delta, nullptr, 0, dk, dv, lddkv, scale, mask,
                        dscale);
 }
 
@@ -1099,7 +1394,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_d64r(int H, const bf16_t* _
     int x, id;
     block_coords<false>(x, id);
     if (id & 1)
-        dkdv_res<DROP, NT>(id >> 1, smem, H, q, k, v, ld, dout, ldd, lse, delta, o, ldo, dk, dv, lddkv, scale, mask_bwd,
+        dkdv_res<DROP, NT, true>(id >> 1, smem, H, q, k, v, ld, dout, ldd, lse, delta, o, ldo, dk, dv, lddkv, scale, mask_bwd,
                            dscale);
     else
         dq_res<DROP, NT>(id >> 1, smem, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale, mask_fwd,
@@ -1136,17 +1431,6 @@ void launch_fwd_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* 
     else
         k_attn_fwd_d64<false><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, lse, scale * LOG2E, nullptr, 1.f);
 }
-// ring kernels: LDS-DMA tile staging unless attn_variant 3 (register staging, A/B)
-#define RD_SWITCH(...)                        \
-    do {                                      \
-        if (g_attn_variant == 3) {            \
-            constexpr bool RD_ = false;       \
-            __VA_ARGS__;                      \
-        } else {                              \
-            constexpr bool RD_ = true;        \
-            __VA_ARGS__;                      \
-        }                                     \
-    } while (0)
 
 void launch_dq_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                    const bf16_t* o, int64_t ldo, const bf16_t* dout, int64_t ldd, const float* lse, float* delta,
@@ -1160,11 +1444,11 @@ void launch_dq_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k
     }
     const dim3 grid((unsigned)((ceil_div(T, 256) + 1) / 2), (unsigned)(B * H));
     if (d.mask)
-        RD_SWITCH(k_attn_dq_d64<true, RD_><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
-                                                  d.mask, d.dscale));
+        k_attn_dq_d64<true><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
+                                                  d.mask, d.dscale);
     else
-        RD_SWITCH(k_attn_dq_d64<false, RD_><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
-                                                   nullptr, 1.f));
+        k_attn_dq_d64<false><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
+                                                   nullptr, 1.f);
 }
 void launch_bwd_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                     const bf16_t* o, int64_t ldo, const bf16_t* dout, int64_t ldd, const float* lse, float* delta,
@@ -1196,11 +1480,11 @@ void launch_dkdv_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t*
     }
     const dim3 grid((unsigned)((ceil_div(T, 128) + 1) / 2), (unsigned)(B * H));
     if (d.mask)
-        RD_SWITCH(k_attn_dkdv_d64<true, RD_><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
-                                                    d.mask_bwd, d.dscale));
+        k_attn_dkdv_d64<true><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
+                                                    d.mask_bwd, d.dscale);
     else
-        RD_SWITCH(k_attn_dkdv_d64<false, RD_><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
-                                                     nullptr, 1.f));
+        k_attn_dkdv_d64<false><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
+                                                     nullptr, 1.f);
 }
 }  // namespace attn
 

@@ -38,7 +38,7 @@ namespace cg {
 #pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ void dma16(const void* g, const void* lds) {
     const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds);
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
 }
 #pragma clang diagnostic pop
 }  // namespace cg
@@ -65,6 +65,15 @@ namespace cg {
 typedef unsigned short bf16_t;  // raw bf16 bits in memory
 typedef short sv8 __attribute__((ext_vector_type(8)));
 typedef short sv4 __attribute__((ext_vector_type(4)));
+// Register loads hidden from hipcc's wait-count model, like dma16: a kernel that issues them ahead of
+// its DMAs counts them in its own vmcnt and must name every destination "+v" in the statement that
+// waits for them (cdna_hip_programming.md 5.7 item 1 (ii)) before anything reads them.
+__device__ __forceinline__ void gload16(sv8& dst, const void* g) {
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(g) : "memory");
+}
+__device__ __forceinline__ void gload4(uint32_t& dst, const void* g) {
+    asm volatile("global_load_dword %0, %1, off" : "=v"(dst) : "v"(g) : "memory");
+}
 typedef float fv4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bfv8 __attribute__((ext_vector_type(8)));
 

@@ -381,12 +381,19 @@ int g_gemm_group_pk = 0;
 int g_defer_splitk = 0;   // cg_set_tuning("defer_splitk"): split-K reduces of fp32 STORE outputs deferred
 RedJobs g_red_pending = {};
 hipStream_t g_red_stream = nullptr;   // the stream the pending jobs were enqueued on
+int g_red_device = -1;                // ... and that stream's device (stream handles repeat across devices)
 
-// pending jobs for a launch on stream st: only a launch on the jobs' own stream takes them (a
-// launch on another stream is not ordered after the slab writes)
+static int current_device() {
+    int d = -1;
+    return hipGetDevice(&d) == hipSuccess ? d : -1;
+}
+
+// pending jobs for a launch on stream st of the current device: only a launch on the jobs' own
+// stream and device takes them (a launch on another stream is not ordered after the slab writes).
+// Single-threaded use only, like the rest of the tuning state.
 RedJobs take_pending_reduces(hipStream_t st) {
     RedJobs r = {};
-    if (g_red_pending.n && st == g_red_stream) {
+    if (g_red_pending.n && st == g_red_stream && current_device() == g_red_device) {
         r = g_red_pending;
         g_red_pending.n = 0;
     }
@@ -395,11 +402,16 @@ RedJobs take_pending_reduces(hipStream_t st) {
 
 static void launch_splitk_reduce_job(const RedJob& j, hipStream_t st);
 
-// the pending jobs as standalone reduce kernels on their own stream (cg_flush_deferred, a full
-// queue, or a job arriving from another stream)
+// the pending jobs as standalone reduce kernels on their own stream and device (cg_flush_deferred,
+// a full queue, or a job arriving from another stream / device)
 static void flush_pending() {
-    const RedJobs r = take_pending_reduces(g_red_stream);
+    if (!g_red_pending.n) return;
+    const int cur = current_device();
+    if (g_red_device >= 0 && cur != g_red_device) (void)hipSetDevice(g_red_device);
+    const RedJobs r = g_red_pending;
+    g_red_pending.n = 0;
     for (int q = 0; q < r.n; ++q) launch_splitk_reduce_job(r.j[q], g_red_stream);
+    if (g_red_device >= 0 && cur >= 0 && cur != g_red_device) (void)hipSetDevice(cur);
 }
 
 int g_skip_splitk_reduce = 0;  // measurement knob (WRONG results): time a step without the split-K reduce
@@ -511,10 +523,14 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
     // (slab sets above 40 MB -- the C4 FFN / QKV weight gradients -- keep their own reduce kernel: in
     // the next 256x256 GEMM's tail they measured no gain, C4 58.2 vs 57.9 ms/step)
     if (split_k > 1 && vec4 && !g_skip_splitk_reduce && g_defer_splitk && fast && e.kind == CG_EPI_STORE &&
-        c_dtype == CG_F32 && ldc == N && (int64_t)split_k * M * N * 4 <= ((int64_t)40 << 20)) {
-        // deferred: summed in the tail of the next persistent GEMM launch (or cg_flush_deferred)
-        if (g_red_pending.n == MAX_RED || (g_red_pending.n && g_red_stream != st)) flush_pending();
+        c_dtype == CG_F32 && ldc == N && st != nullptr && (int64_t)split_k * M * N * 4 <= ((int64_t)40 << 20)) {
+        // deferred: summed in the tail of the next persistent GEMM launch (or cg_flush_deferred); never
+        // on the null stream, whose handle names a different queue on every device
+        const int dev = current_device();
+        if (g_red_pending.n == MAX_RED || (g_red_pending.n && (g_red_stream != st || g_red_device != dev)))
+            flush_pending();
         g_red_stream = st;
+        g_red_device = dev;
         g_red_pending.j[g_red_pending.n++] = RedJob{(const float*)workspace, (float*)C, M * N / 4, split_k, e.beta};
     } else if (split_k > 1 && vec4 && !g_skip_splitk_reduce) {
         const int n4 = (int)(M * N / 4);

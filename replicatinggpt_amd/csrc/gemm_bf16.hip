@@ -192,10 +192,13 @@ static bool fast_shape_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t 
            ldc % 8 == 0;
 }
 
+// the 128x128 persistent kernel (gemm_pk.hip)
+static bool pk128(int v) { return v == 9; }
+
 // column partials come from the 128x128 persistent kernel's per-item ReLU-backward epilogue (not its
 // pk_flags bit-1 per-fragment form) and from the 8-wave 256x256 persistent kernel
 static bool colpart_ok(int v, int at, int split_k) {
-    return (v == 24 || (v == 9 && !(g_pk_flags & 2))) && split_k == 1 && !at;
+    return (v == 24 || (pk128(v) && !(g_pk_flags & 2))) && split_k == 1 && !at;
 }
 
 bool gemm_colpart_supported(int at, int bt, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc) {
@@ -227,7 +230,7 @@ bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf1
         // uneven split-K (the last split shorter): only the 128x128 persistent kernel, and only when
         // every split is non-empty; otherwise the generic kernels (ceil-sized chunks) take it
         const int64_t nkt = K / FBK, nkc = (nkt + split_k - 1) / split_k;
-        if (v != 9 || (split_k - 1) * nkc >= nkt) return false;
+        if (!pk128(v) || (split_k - 1) * nkc >= nkt) return false;
     }
     if (e.colpart && (!colpart_ok(v, at, split_k) || e.kind != CG_EPI_RELU_BWD ||
                       (e.aux_dtype != CG_BF16 && e.aux_dtype != CG_BITS) || e.beta != 0.f || c_dtype != CG_BF16))
@@ -238,7 +241,7 @@ bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf1
         return false;
     if (v >= 20 && p8_gemm_launch(v, at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st))
         return true;
-    if (e.aux_dtype == CG_BITS && v != 9) return false;   // only the two persistent kernels read / write keep bits
+    if (e.aux_dtype == CG_BITS && !pk128(v)) return false;   // only the two persistent kernels read / write keep bits
     if (v >= 20) v = 2;
     if (v >= 5 && glds_gemm_launch(v, at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st))
         return true;

@@ -15,6 +15,25 @@
 // so that consecutive items (same row panel / same split) share an XCD's L2.
 #include "gemm_tile.h"
 
+#ifdef CG_PK_STAMPS
+// Diagnostic build only (tools/gemm_stamps.py, make stamps): per-wave s_memtime cycle sums of the
+// K-step segments of k_gemm_pk -- [0] the head wait (vmcnt + barrier), [1] fragment reads + MFMA
+// and DMA issue, [2] item epilogues, [3] K-steps, [4] whole wave, [5] s_memrealtime ticks of the
+// wave (100 MHz) -- summed over all waves.  Never in the product library.
+__device__ unsigned long long g_pk_stamps[8];
+__device__ __forceinline__ uint64_t pk_clk() { return __builtin_amdgcn_s_memtime(); }
+extern "C" int cg_debug_pk_stamps(unsigned long long* host8) {
+    return hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_pk_stamps), 8 * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
+}
+extern "C" int cg_debug_pk_stamps_reset() {
+    unsigned long long z[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_pk_stamps), z, sizeof(z)) == hipSuccess ? 0 : 1;
+}
+#define PK_STAMP(v) const uint64_t v = pk_clk()
+#else
+#define PK_STAMP(v)
+#endif
+
 namespace cg {
 int g_pk_flags = 0;  // cg_set_tuning("pk_flags"): bit 0 = drain epilogue stores each step, bit 1 = per-fragment epilogue
 namespace {
@@ -27,10 +46,10 @@ __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// per-lane part of one operand's LDS-DMA sources: R rows (K-contiguous) or R columns (TR) x 64 k
-template <bool TR, int R, int WAVES>
+// per-lane part of one operand's LDS-DMA sources: R rows (K-contiguous) or R columns (TR) x BK k
+template <bool TR, int R, int WAVES, int BK>
 struct DmaP {
-    static constexpr int INSTR = R * FBK * 2 / 1024;  // 1-KB wave instructions per K-tile
+    static constexpr int INSTR = R * BK * 2 / 1024;  // 1-KB wave instructions per K-tile
     static constexpr int PER_WAVE = INSTR / WAVES;
     static_assert(PER_WAVE * WAVES == INSTR, "tile/wave mismatch");
     static_assert(!TR || R >= 128, "transposed image swizzle needs >= 16 chunks per row");
@@ -42,14 +61,15 @@ struct DmaP {
         for (int i = 0; i < PER_WAVE; ++i) {
             const int pos = (wave * PER_WAVE + i) * 1024 + lane * 16;
             if (!TR) {
-                const int r = pos >> 7, c = ((pos >> 4) & 7) ^ row_swz(r);
+                const int r = BK == 64 ? pos >> 7 : pos >> 6;
+                const int c = BK == 64 ? ((pos >> 4) & 7) ^ row_swz(r) : ((pos >> 4) & 3) ^ row_swz32(r);
                 off[i] = (int)(r * ld) + c * 8;
             } else {
                 const int k = pos / (2 * R), c = ((pos % (2 * R)) >> 4) ^ col_swz(k);
                 off[i] = (int)(k * ld) + c * 8;
             }
         }
-        kstep = TR ? (int64_t)FBK * ld : (int64_t)FBK;
+        kstep = TR ? (int64_t)BK * ld : (int64_t)BK;
     }
     // instruction i (0..PER_WAVE-1) of one K-tile, from that K-tile's base address
     __device__ __forceinline__ void issue1(const bf16_t* base, int i, char* img, int wave) const {
@@ -292,10 +312,10 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
     store_item<WIDE>(acc, mr, nc, Cv, c_dtype, ldc);
 }
 
-template <int BM, int BN, int NBUF>
+template <int BM, int BN, int NBUF, int BK = FBK>
 struct GeoP {
     static constexpr int WM = BM / 64, WN = BN / 64, WAVES = WM * WN, THREADS = WAVES * 64;
-    static constexpr int IMG_A = BM * FBK * 2, IMG_B = BN * FBK * 2, STAGE = IMG_A + IMG_B;
+    static constexpr int IMG_A = BM * BK * 2, IMG_B = BN * BK * 2, STAGE = IMG_A + IMG_B;
     static constexpr int LDS = NBUF * STAGE;
     static constexpr int OCC_LDS = (160 * 1024) / LDS;
     static constexpr int OCC = OCC_LDS > 4 ? 4 : (OCC_LDS < 1 ? 1 : OCC_LDS);  // resident blocks per CU (LDS-bound)
@@ -312,18 +332,24 @@ struct GeoP {
 #define CG_PK_DPG 1   // next-stage DMA instructions issued per group of 4 MFMAs
 #endif
 constexpr int EK_ANY = -1, EK_SLAB = 6;
-template <bool AT, bool BT, int BM, int BN, int NBUF, int EK = EK_ANY>
+// BK: K depth of one LDS stage, 64 or 32 (32: the same 64 KB per block holds 4 stages, 3 K-tiles in
+// flight at two blocks per CU; same bits -- kchunk stays a multiple of 64, same k order.  Measured
+// 10-15 % slower on every C2 shape: 64-B row segments double the TA/TCP requests,
+// profiles/r3_gemm_bk32.txt -- no launcher instantiates it)
+template <bool AT, bool BT, int BM, int BN, int NBUF, int EK = EK_ANY, int BK = FBK>
 // amdgpu_waves_per_eu: LDS caps residency at OCC blocks, so tell the scheduler the real occupancy;
 // left at its default it schedules for 8+ waves/SIMD, keeps ONE A fragment register and waits
 // lgkmcnt(0) before every 4 MFMAs (LDS latency exposed 8x per K-tile)
-__global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, (GeoP<BM, BN, NBUF>::OCC))
-__attribute__((amdgpu_waves_per_eu(1, (BM / 64) * (BN / 64) * GeoP<BM, BN, NBUF>::OCC / 4)))
+__global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, (GeoP<BM, BN, NBUF, BK>::OCC))
+__attribute__((amdgpu_waves_per_eu(1, (BM / 64) * (BN / 64) * GeoP<BM, BN, NBUF, BK>::OCC / 4)))
 void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
                const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype, int64_t ldc,
                EpiArgs epi, int split_k, int64_t kchunk, float* __restrict__ ws, int flags, RedJobs red) {
-    using G = GeoP<BM, BN, NBUF>;
-    using DA = DmaP<AT, BM, G::WAVES>;
-    using DB = DmaP<BT, BN, G::WAVES>;
+    static_assert(BK == 64 || BK == 32, "BK");
+    constexpr int NS = BK / 32;   // 32-deep MFMA slices per K-tile
+    using G = GeoP<BM, BN, NBUF, BK>;
+    using DA = DmaP<AT, BM, G::WAVES, BK>;
+    using DB = DmaP<BT, BN, G::WAVES, BK>;
     constexpr int LPT = DA::PER_WAVE + DB::PER_WAVE;  // DMA instructions per thread per K-tile
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -333,7 +359,7 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     const int nitems = ntiles * split_k;
     // split s covers K-tiles [s*nkc, min((s+1)*nkc, nkt)): the last split may be shorter (uneven
     // split-K: any split count, not only divisors of the K-tile count)
-    const int nkt = (int)(K / FBK), nkc = (int)(kchunk / FBK);
+    const int nkt = (int)(K / BK), nkc = (int)(kchunk / BK);
     const int P = gridDim.x, b = blockIdx.x;
     const int my_items = b < nitems ? (nitems - 1 - b) / P + 1 : 0;
     auto split_nk = [&](int sp) { return nkt - sp * nkc < nkc ? nkt - sp * nkc : nkc; };
@@ -428,7 +454,12 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         cnk = my_items ? split_nk(sp) : 0;
     }
     bool stored = false;
+#ifdef CG_PK_STAMPS
+    uint64_t sw = 0, sm = 0, se = 0;
+    const uint64_t w0 = pk_clk(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
     for (int g = 0; g < total; ++g) {
+        PK_STAMP(ta);
         const int ahead = total - 1 - g;  // steps issued after g that may stay in flight: min(NBUF-2, ahead)
         if (stored && !(flags & 1)) {
             if constexpr (NBUF >= 4) {
@@ -454,6 +485,7 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         stored = false;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        PK_STAMP(tb);
         int nb = cur + NBUF - 1;
         if (nb >= NBUF) nb -= NBUF;
         prep_next(g + NBUF - 1 < total);
@@ -462,13 +494,20 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         const char* imgB = imgA + G::IMG_A;
         // both 32-deep halves' fragments are read before the first MFMA (sched_barrier pins it):
         // otherwise the scheduler sinks each A read next to its 4 MFMAs and waits lgkmcnt(0) on it
-        sv8 af[2][4], bf[2][4];
+        sv8 af[NS][4], bf[NS][4];
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < NS; ++s) {
+            if constexpr (BK == 64) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) bf[s][j] = frag<BT, BN>(imgB, wn * 64 + j * 16, s, lane);
+                for (int j = 0; j < 4; ++j) bf[s][j] = frag<BT, BN>(imgB, wn * 64 + j * 16, s, lane);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) af[s][i] = frag<AT, BM>(imgA, wm * 64 + i * 16, s, lane);
+                for (int i = 0; i < 4; ++i) af[s][i] = frag<AT, BM>(imgA, wm * 64 + i * 16, s, lane);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) bf[s][j] = frag32<BT, BN>(imgB, wn * 64 + j * 16, lane);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) af[s][i] = frag32<AT, BM>(imgA, wm * 64 + i * 16, lane);
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
         // 8 groups of 4 MFMAs (half s, A fragment i); the next stage's DMA instructions in between,
@@ -478,7 +517,7 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
             else db.issue1(nbp, t - DA::PER_WAVE, dimg + G::IMG_A, wave);
         };
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
+        for (int t = 0; t < 4 * NS; ++t) {
             const int s = t >> 2, i = t & 3;
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[i][j] = mfma_bf16(bf[s][j], af[s][i], acc[i][j]);
@@ -487,9 +526,9 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
                 if (t * CG_PK_DPG + d < LPT) issue_dma(t * CG_PK_DPG + d);
         }
 #pragma unroll
-        for (int t = 8 * CG_PK_DPG; t < LPT; ++t) issue_dma(t);
+        for (int t = 4 * NS * CG_PK_DPG; t < LPT; ++t) issue_dma(t);
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
+        for (int t = 0; t < 4 * NS; ++t) {
             __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
 #pragma unroll
             for (int d = 0; d < CG_PK_DPG; ++d)
@@ -497,6 +536,11 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         }
         __builtin_amdgcn_sched_barrier(0);
         cur = cur + 1 == NBUF ? 0 : cur + 1;
+        PK_STAMP(tc);
+#ifdef CG_PK_STAMPS
+        sw += tb - ta;
+        sm += tc - tb;
+#endif
         if (++ckt == cnk) {
             // item done: acc[i][j][r] = C[mw + 16i + (lane&15)][nw + 16j + 4(lane>>4) + r]
             int64_t m0, n0;
@@ -531,8 +575,22 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
                 cnk = split_nk(sp1);
             }
             stored = true;
+#ifdef CG_PK_STAMPS
+            se += pk_clk() - tc;
+#endif
         }
     }
+#ifdef CG_PK_STAMPS
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&g_pk_stamps[0], (unsigned long long)sw);
+        atomicAdd(&g_pk_stamps[1], (unsigned long long)sm);
+        atomicAdd(&g_pk_stamps[2], (unsigned long long)se);
+        atomicAdd(&g_pk_stamps[3], (unsigned long long)total);
+        atomicAdd(&g_pk_stamps[4], (unsigned long long)(pk_clk() - w0));
+        atomicAdd(&g_pk_stamps[5], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - r0));
+        atomicAdd(&g_pk_stamps[6], 1ull);
+    }
+#endif
     wait_vm<0>();  // the dummy DMAs past the last K-tile land before the workgroup's LDS is released
     if (red.n) red_tail(red);   // a deferred split-K reduce of an earlier launch (gemm_common.h)
 }
@@ -548,12 +606,12 @@ int cu_count() {
     return n;
 }
 
-template <bool AT_, bool BT_, int BM, int BN, int NBUF, int EK>
+template <bool AT_, bool BT_, int BM, int BN, int NBUF, int EK, int BK>
 void launch_1(unsigned grid, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
               void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, int64_t kchunk, float* ws,
               hipStream_t st) {
-    using G = GeoP<BM, BN, NBUF>;
-    k_gemm_pk<AT_, BT_, BM, BN, NBUF, EK><<<grid, G::THREADS, G::LDS, st>>>(M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e,
+    using G = GeoP<BM, BN, NBUF, BK>;
+    k_gemm_pk<AT_, BT_, BM, BN, NBUF, EK, BK><<<grid, G::THREADS, G::LDS, st>>>(M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e,
                                                                          split_k, kchunk, ws,
                                                                          g_pk_flags | (g_gemm_group_pk << 8),
                                                                          take_pending_reduces(st));
@@ -561,11 +619,11 @@ void launch_1(unsigned grid, int64_t M, int64_t N, int64_t K, const bf16_t* A, i
 
 // epilogue instantiation: slab for split-K; a fixed kind for the default 128x128 2-stage kernel's
 // non-transposed-A products (forward / dgrad) when the call allows it; otherwise the run-time one
-template <bool AT_, bool BT_, int BM, int BN, int NBUF>
+template <bool AT_, bool BT_, int BM, int BN, int NBUF, int BK>
 void launch_ek(unsigned grid, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
                int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, int64_t kchunk, float* ws,
                hipStream_t st) {
-#define L1(EK_) launch_1<AT_, BT_, BM, BN, NBUF, EK_>(grid, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, kchunk, ws, st)
+#define L1(EK_) launch_1<AT_, BT_, BM, BN, NBUF, EK_, BK>(grid, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, kchunk, ws, st)
     if (split_k > 1) {
         L1(EK_SLAB);
         return;
@@ -589,17 +647,17 @@ void launch_ek(unsigned grid, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
 #undef L1
 }
 
-template <int BM, int BN, int NBUF>
+template <int BM, int BN, int NBUF, int BK = FBK>
 void launch_p(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
               int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, float* ws,
               hipStream_t st) {
-    using G = GeoP<BM, BN, NBUF>;
+    using G = GeoP<BM, BN, NBUF, BK>;
     const int64_t kchunk = (K / FBK + split_k - 1) / split_k * FBK;   // K-tiles per split, last one short
     const int64_t nitems = (M / BM) * (N / BN) * split_k;
     int64_t slots = (int64_t)cu_count() * G::OCC;
     if (g_gemm_max_grid > 0 && g_gemm_max_grid < slots) slots = g_gemm_max_grid;
     const unsigned grid = (unsigned)(nitems < slots ? nitems : slots);
-#define FG(AT_, BT_) launch_ek<AT_, BT_, BM, BN, NBUF>(grid, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, kchunk, ws, st)
+#define FG(AT_, BT_) launch_ek<AT_, BT_, BM, BN, NBUF, BK>(grid, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, kchunk, ws, st)
     // transposed LDS images need >= 128 rows (DmaP): narrower tiles serve only the layouts they can
     if (!at && !bt) FG(false, false);
     else if (!at && bt) {

@@ -39,6 +39,19 @@ __device__ __forceinline__ sv8 frag(const char* img, int rb, int s, int lane) {
     }
 }
 
+// 32-deep K-tiles (k_gemm_pk BK = 32): K-contiguous image [R][32] bf16, 64-B rows, chunk c (0..3) at
+// c ^ ((r>>2)&2).  A 16x16x32 fragment read (ds_read_b128, lane l: row rb + (l&15), chunk l>>4) then
+// puts each 16-lane group of the instruction on 16 distinct 16-B slots of the 256-B bank row
+// (lanes {0-3,12-15,20-27}: rows j, 12+j, 4+j, 8+j of chunks 0,0,1,1 -> slots 4j + {0,2,1,3}).  The
+// M/N-contiguous image is the 64-deep one cut to 32 k-rows (same col_swz).
+__device__ __forceinline__ int row_swz32(int r) { return (r >> 2) & 2; }
+__device__ __forceinline__ int img_row_off32(int r, int c) { return r * 64 + ((c ^ row_swz32(r)) << 4); }
+template <bool TR, int R>
+__device__ __forceinline__ sv8 frag32(const char* img, int rb, int lane) {
+    if (!TR) return *(const sv8*)(img + img_row_off32(rb + (lane & 15), lane >> 4));
+    return frag<true, R>(img, rb, 0, lane);
+}
+
 __device__ __forceinline__ fv4 mfma_bf16(sv8 a, sv8 b, fv4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bfv8, a), __builtin_bit_cast(bfv8, b), c, 0, 0,
                                                    0);

@@ -100,11 +100,15 @@ class DeferredReduces:
             self.active = True
         return self
 
+    def flush(self):
+        """Launch every pending reduce now, on the current stream (their outputs complete in stream order)."""
+        L.check(L.load().cg_flush_deferred(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+                "flush_deferred")
+
     def __exit__(self, *exc):
         if self.active:
             lib = L.load()
-            L.check(lib.cg_flush_deferred(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
-                    "flush_deferred")
+            self.flush()
             L.check(lib.cg_set_tuning(b"defer_splitk", 0), "defer_splitk")
             if SIDE.enabled:   # the flush runs on the stream its reduces were enqueued on: join it
                 dev = torch.device("cuda", torch.cuda.current_device())
@@ -279,8 +283,13 @@ def _wgrad_split(M, N, K, fast):
     return split
 
 
-def linear_wgrad(dy2, x2, out, beta):
-    """out[N,K] (+)= dy2[M,N]^T @ x2[M,K]   (fp32, deterministic split-K)"""
+def linear_wgrad(dy2, x2, out, beta, into_slot=False):
+    """out[N,K] (+)= dy2[M,N]^T @ x2[M,K]   (fp32, deterministic split-K).
+
+    into_slot: ``out`` is a region's flat gradient slot, which nothing reads before DEFER closes,
+    so inside ``with DEFER:`` its split-K reduce may stay pending past this call.  Any other
+    output (a temporary, a tensor handed to autograd) gets its pending reduces flushed right after
+    the GEMM, so it is complete when this returns."""
     if "skip_wgrad" in WHATIF:
         return out
     M, N = dy2.shape
@@ -288,12 +297,15 @@ def linear_wgrad(dy2, x2, out, beta):
     fast = _is_bf16(dy2.dtype) and N % 128 == 0 and K % 128 == 0 and M % 64 == 0
     split = _wgrad_split(N, K, M, fast)
     ws = None
+    defer = DEFER.active and into_slot
     if split > 1:
         ws = torch.empty(ops.gemm_workspace(N, K, split) // 4, dtype=torch.float32, device=dy2.device)
-        if DEFER.active:
+        if defer:
             DEFER.keep.append(ws)   # its reduce may run after this call returns
     ops.gemm(dy2, x2, out, _is_bf16(dy2.dtype), True, True, N, K, M, N, K, out.stride(0), L.EPI_STORE, None, None, 0,
              None, 0, 0.0, 0, None, 0, float(beta), split, ws)
+    if DEFER.active and not defer and split > 1:
+        DEFER.flush()
     return out
 
 
@@ -546,7 +558,7 @@ class AttnSublayerFn(torch.autograd.Function):
         g_pb, beta_pb, f_pb = proj_b.grad_target()
         with SIDE.run(dev, dy, o):
             if g_pw is not None:
-                linear_wgrad(dy, o, g_pw, beta_pw)
+                linear_wgrad(dy, o, g_pw, beta_pw, g_pw is proj_w.slot)
             if g_pb is not None and not bias_done:
                 colsum_into(dy, g_pb, beta_pb)
         do = torch.empty((B * T, C), dtype=act, device=x2.device)
@@ -556,7 +568,7 @@ class AttnSublayerFn(torch.autograd.Function):
         g, beta, f_qkv = qkv_w.grad_target()
         if g is not None:
             with SIDE.run(dev, dqkv, a):
-                linear_wgrad(dqkv, a, g, beta)
+                linear_wgrad(dqkv, a, g, beta, g is qkv_w.slot)
         da = torch.empty((B * T, C), dtype=act, device=x2.device)
         linear_dgrad(dqkv, qkv_w.operand(act), da)
         dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd, dres=d32, link=ctx.in_link)
@@ -611,7 +623,7 @@ class FFNSublayerFn(torch.autograd.Function):
         g_b2, beta_b2, f_b2 = b2.grad_target()
         with SIDE.run(dev, dz2, h):
             if g_w2 is not None:
-                linear_wgrad(dz2, h, g_w2, beta_w2)
+                linear_wgrad(dz2, h, g_w2, beta_w2, g_w2 is w2.slot)
             if g_b2 is not None and not bias_done:
                 colsum_into(dz2, g_b2, beta_b2)
         dz1 = torch.empty_like(h)
@@ -631,7 +643,7 @@ class FFNSublayerFn(torch.autograd.Function):
             linear_dgrad(dz2, w2.operand(act), dz1, "relu_bwd", aux=h if bits is None else bits)
         with SIDE.run(dev, dz1, a, part):
             if g_w1 is not None:
-                linear_wgrad(dz1, a, g_w1, beta_w1)
+                linear_wgrad(dz1, a, g_w1, beta_w1, g_w1 is w1.slot)
             if g_b1 is not None:
                 if part is not None:
                     ops.reduce_rows(part, part.shape[0], part.shape[1], g_b1, bool(beta_b1))
@@ -703,7 +715,7 @@ class HeadLossFn(torch.autograd.Function):
         dl_op = dl if act == torch.float32 else to_act(dl, act)
         g, beta, f_lw = lm_w.grad_target()
         if g is not None:
-            linear_wgrad(dl_op, a, g, beta)
+            linear_wgrad(dl_op, a, g, beta, g is lm_w.slot)
         g, beta, f_lb = lm_b.grad_target()
         if g is not None:
             colsum_into(dl, g, beta)
@@ -755,7 +767,7 @@ class HeadLossFn(torch.autograd.Function):
         if g is not None:
             if g.data_ptr() == lm_w.slot.data_ptr():
                 with SIDE.run(x2.device, dl, a):
-                    linear_wgrad(dl, a, gpad, beta)   # rows >= V get exact zeros (dl pad columns are 0)
+                    linear_wgrad(dl, a, gpad, beta, True)   # rows >= V get exact zeros (dl pad columns are 0)
             else:
                 tmp = torch.empty((KP, C), dtype=torch.float32, device=x2.device)
                 linear_wgrad(dl, a, tmp, 0.0)
@@ -833,7 +845,7 @@ class MHAFn(torch.autograd.Function):
             dy = to_act(d32, act)
             g, beta, f_pw = proj_w.grad_target()
             if g is not None:
-                linear_wgrad(dy, o, g, beta)
+                linear_wgrad(dy, o, g, beta, g is proj_w.slot)
             g, beta, f_pb = proj_b.grad_target()
             if g is not None:
                 colsum_into(dy, g, beta)
@@ -846,7 +858,7 @@ class MHAFn(torch.autograd.Function):
                              lc.site, ctx.mask)
         g, beta, f_qkv = qkv_w.grad_target()
         if g is not None:
-            linear_wgrad(dqkv, x2, g, beta)
+            linear_wgrad(dqkv, x2, g, beta, g is qkv_w.slot)
         dx = torch.empty((B * T, C), dtype=torch.float32, device=o.device)
         linear_dgrad(dqkv, qkv_w.operand(act), dx)
         return (dx.view(B, T, C), None, None, None, None, *f_qkv(), *rets)
@@ -881,7 +893,7 @@ class FFNFn(torch.autograd.Function):
         ops.dropout_apply(d32, dz2, float(lc.p), int(lc.seed), lc.rng_call, int(lc.site))
         g, beta, f_w2 = w2.grad_target()
         if g is not None:
-            linear_wgrad(dz2, h, g, beta)
+            linear_wgrad(dz2, h, g, beta, g is w2.slot)
         g, beta, f_b2 = b2.grad_target()
         if g is not None:
             colsum_into(dz2, g, beta)
@@ -889,7 +901,7 @@ class FFNFn(torch.autograd.Function):
         linear_dgrad(dz2, w2.operand(act), dz1, "relu_bwd", aux=h)
         g, beta, f_w1 = w1.grad_target()
         if g is not None:
-            linear_wgrad(dz1, x2, g, beta)
+            linear_wgrad(dz1, x2, g, beta, g is w1.slot)
         g, beta, f_b1 = b1.grad_target()
         if g is not None:
             colsum_into(dz1, g, beta)
@@ -920,7 +932,7 @@ class LinearFn(torch.autograd.Function):
         d2 = _flat2(dy.float().contiguous())
         g, beta, fw = w_reg.grad_target()
         if g is not None:
-            linear_wgrad(d2, x2, g, beta)
+            linear_wgrad(d2, x2, g, beta, g is w_reg.slot)
         rets = fw()
         if b_reg is not None:
             g, beta, fb = b_reg.grad_target()

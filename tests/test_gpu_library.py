@@ -125,3 +125,46 @@ def test_opcheck_causal_attention(dt, T, H, D, p):
     assert relerr(o, ref) < tol
     want = torch.cat([t.grad.reshape(B, T, d) for t in (q, k, v)], -1)
     assert relerr(qkv.grad, want) < gtol
+
+
+def test_linear_backward_inside_defer_matches_eager():
+    """inside functional.DEFER the split-K reduce of a weight gradient may stay
+    pending past linear_wgrad only when its output is a flat gradient slot.  charpt::linear's
+    backward writes a temporary it reads right away (to_act / autograd), so its reduce must be
+    complete when linear_wgrad returns: the same bits with DEFER on and off, at a shape whose
+    weight gradient takes split-K (K = 4096 tokens), followed by another GEMM that would pick up a
+    still-pending reduce in its tail."""
+    from replicatinggpt_amd import functional as Fn
+    O = _ops()
+    torch.manual_seed(3)
+    x = torch.randn(4096, 256, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(384, 256, device=DEV) * 0.1).to(torch.bfloat16)
+    dy = torch.randn(4096, 384, device=DEV).to(torch.bfloat16)
+    assert Fn._wgrad_split(384, 256, 4096, True) > 1
+    ref = O.linear_backward(dy, x, w, True)
+    torch.cuda.synchronize()
+    with Fn.DEFER:
+        got = O.linear_backward(dy, x, w, True)
+        dw_now = got[1].clone()       # read before DEFER closes
+        O.linear_backward(dy, x, w, False)   # a later persistent GEMM on the same stream
+    torch.cuda.synchronize()
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+    assert torch.equal(dw_now, ref[1])
+
+
+def test_wgrad_into_temporary_inside_defer_is_complete():
+    """linear_wgrad into a non-slot fp32 target inside DEFER (the HeadLossFn non-slot fallback's
+    form): the output is complete on return, bitwise the eager result."""
+    from replicatinggpt_amd import functional as Fn
+    torch.manual_seed(4)
+    dy = torch.randn(8192, 128, device=DEV).to(torch.bfloat16)
+    a = torch.randn(8192, 384, device=DEV).to(torch.bfloat16)
+    ref = torch.empty(128, 384, device=DEV)
+    Fn.linear_wgrad(dy, a, ref, 0.0)
+    tmp = torch.full((128, 384), float("nan"), device=DEV)
+    with Fn.DEFER:
+        Fn.linear_wgrad(dy, a, tmp, 0.0)
+        snap = tmp.clone()
+    torch.cuda.synchronize()
+    assert torch.equal(snap, ref)
