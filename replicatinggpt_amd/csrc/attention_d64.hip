@@ -304,94 +304,20 @@ template <bool DROP, int NSUB, int DIAG, bool QREG = false>
 __device__ __forceinline__ void fwd_group_tile(const char* Ki, const char* Vi, const char* Qimg, int qr, int lane,
                                                float scale_log2, float& m_run, float& l_run, fv16 (&o)[2],
                                                uint32_t mw, const sv8* qreg = nullptr) {
-    // every fragment of a product is read before its first MFMA (pinned: hipcc otherwise issues each
-    // read next to its MFMA and waits for it there)
-    sv8 kf[NSUB][4], qf[4];
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-        qf[ks] = QREG ? qreg[ks] : frag_row(Qimg, qr, ks, lane);
-#pragma unroll
-        for (int kt = 0; kt < NSUB; ++kt) kf[kt][ks] = frag_row(Ki, 32 * kt, ks, lane);
-    }
-    __builtin_amdgcn_sched_barrier(0);
     fv16 s[2];
     s[0] = fv16{};
     s[1] = fv16{};
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-        s[0] = mfma32(kf[0][ks], qf[ks], s[0]);
-        if (NSUB == 2) s[1] = mfma32(kf[NSUB - 1][ks], qf[ks], s[1]);
+        const sv8 qf = QREG ? qreg[ks] : frag_row(Qimg, qr, ks, lane);
+        s[0] = mfma32(frag_row(Ki, 0, ks, lane), qf, s[0]);
+        if (NSUB == 2) s[1] = mfma32(frag_row(Ki, 32, ks, lane), qf, s[1]);
     }
     if (DIAG >= 0) mask_upper(s[DIAG], lane & 31, 0, lane, -INFINITY);   // key0 = the group's first query
     rescale_if(tile_max<NSUB>(s) * scale_log2, m_run, l_run, o);
     sv8 pf[2][2];
     softmax_pack<DROP, NSUB>(s, scale_log2, m_run, l_run, mw, pf);
-    sv8 vf[NSUB][2][2];
-#pragma unroll
-    for (int kt = 0; kt < NSUB; ++kt)
-#pragma unroll
-        for (int sk = 0; sk < 2; ++sk)
-#pragma unroll
-            for (int dt = 0; dt < 2; ++dt) vf[kt][sk][dt] = frag_tr(Vi, 32 * kt, sk, 32 * dt, lane);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int kt = 0; kt < NSUB; ++kt)
-#pragma unroll
-        for (int sk = 0; sk < 2; ++sk) {
-            o[0] = mfma32(vf[kt][sk][0], pf[kt][sk], o[0]);
-            o[1] = mfma32(vf[kt][sk][1], pf[kt][sk], o[1]);
-        }
-}
-
-// Phase helpers of the pipelined forward loop.  hipcc left to itself issues each LDS fragment read
-// right before the MFMA that consumes it and waits lgkmcnt(0) there (one exposed LDS round trip per
-// MFMA: 46 % of the forward's wave cycles waiting, profiles/r2_pmc_attention_c4_p02.txt), and runs
-// the other group's softmax VALU as one block beside no MFMA.  So each phase reads all its fragments
-// first (pinned by sched_barrier), then interleaves its 8 MFMAs with the other group's VALU work
-// (sched_group_barrier: one MFMA, then a share of the VALU).
-__device__ __forceinline__ void read_qk(const char* Ki, const char* Qimg, int qr, int lane, sv8 (&kf)[2][4],
-                                        sv8 (&qf)[4]) {
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-        qf[ks] = frag_row(Qimg, qr, ks, lane);
-        kf[0][ks] = frag_row(Ki, 0, ks, lane);
-        kf[1][ks] = frag_row(Ki, 32, ks, lane);
-    }
-}
-__device__ __forceinline__ void mfma_qk(fv16 (&s)[2], const sv8 (&kf)[2][4], const sv8 (&qf)[4]) {
-    s[0] = fv16{};
-    s[1] = fv16{};
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-        s[0] = mfma32(kf[0][ks], qf[ks], s[0]);
-        s[1] = mfma32(kf[1][ks], qf[ks], s[1]);
-    }
-}
-__device__ __forceinline__ void read_v(const char* Vi, int lane, sv8 (&vf)[2][2][2]) {
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int sk = 0; sk < 2; ++sk)
-#pragma unroll
-            for (int dt = 0; dt < 2; ++dt) vf[kt][sk][dt] = frag_tr(Vi, 32 * kt, sk, 32 * dt, lane);
-}
-__device__ __forceinline__ void mfma_pv(fv16 (&o)[2], const sv8 (&vf)[2][2][2], const sv8 (&pf)[2][2]) {
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int sk = 0; sk < 2; ++sk) {
-            o[0] = mfma32(vf[kt][sk][0], pf[kt][sk], o[0]);
-            o[1] = mfma32(vf[kt][sk][1], pf[kt][sk], o[1]);
-        }
-}
-// 8 MFMAs, each followed by NV instructions of the region's VALU (ID: the region's group chain)
-template <int NV>
-__device__ __forceinline__ void interleave8() {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
-    }
+    pv_tile<NSUB>(o, Vi, pf, lane);
 }
 
 // Forward.  Tiles where both of a wave's query groups (A = 7 - w, B = w) are full (before B's
@@ -492,40 +418,17 @@ __device__ __forceinline__ void fwd_qblock(int qblk, int bh, char* smem, int64_t
         const char* Ki = smem + cs * SLOT;
         const char* Vi = Ki + TILE;
         const char* Vp = smem + ps * SLOT + TILE;
-        sv8 kf[2][4], qf[4], vf[2][2][2];
-        // [1] S_A(kv) || P_B(kv - 1).  At kv = 0, B's "previous tile" is sB = -inf against a zeroed
-        // V slot: it adds exactly 0
-        read_qk(Ki, Qimg, qr[0], lane, kf, qf);
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_qk(sA, kf, qf);
+        // at kv = 0, B's "previous tile" is sB = -inf against a zeroed V slot: it adds exactly 0
+        qk_tile(sA, Ki, Qimg, qr[0], lane);
         softmax_pack<DROP>(sB, scale_log2, m_run[1], l_run[1], mwBp, pfB);
-        interleave8<20>();
-        __builtin_amdgcn_sched_barrier(0);
-        // [2] O_B += P_B V(kv - 1) || max_A(kv), then A's rescale decision
-        read_v(Vp, lane, vf);
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_pv(oacc[1], vf, pfB);
-        const float mA = tile_max(sA) * scale_log2;
-        interleave8<3>();
-        __builtin_amdgcn_sched_barrier(0);
-        rescale_if(mA, m_run[0], l_run[0], oacc[0]);
+        pv_tile(oacc[1], Vp, pfB, lane);
+        rescale_if(tile_max(sA) * scale_log2, m_run[0], l_run[0], oacc[0]);
         stage_store1(stk, smem + ns * SLOT, tid);
         const Stage1 stv = stage_load1(vb_, ld, (int64_t)nxt * 64, tid);
-        // [3] S_B(kv) || P_A(kv)
-        read_qk(Ki, Qimg, qr[1], lane, kf, qf);
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_qk(sB, kf, qf);
+        qk_tile(sB, Ki, Qimg, qr[1], lane);
         softmax_pack<DROP>(sA, scale_log2, m_run[0], l_run[0], mw[0], pfA);
-        interleave8<20>();
-        __builtin_amdgcn_sched_barrier(0);
-        // [4] O_A += P_A V(kv) || max_B(kv), then B's rescale decision
-        read_v(Vi, lane, vf);
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_pv(oacc[0], vf, pfA);
-        const float mB = tile_max(sB) * scale_log2;
-        interleave8<3>();
-        __builtin_amdgcn_sched_barrier(0);
-        rescale_if(mB, m_run[1], l_run[1], oacc[1]);
+        pv_tile(oacc[0], Vi, pfA, lane);
+        rescale_if(tile_max(sB) * scale_log2, m_run[1], l_run[1], oacc[1]);
         stage_store1(stv, smem + ns * SLOT + TILE, tid);
         mwBp = mw[1];
         mw[0] = mn[0];

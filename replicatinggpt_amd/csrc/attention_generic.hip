@@ -26,18 +26,20 @@ namespace {
 // (query tile QT, key tile KT <= QT) region, TPW regions per wave: its four 32x32 sub-blocks
 // (qs, ks) give FWD tiles (2 QT + qs, KT) and BWD tiles (2 KT + ks, QT) whole.  Per sub-block, lane l
 // takes query 32 qb + (l & 31) and keys 32 kb + 16 (l >> 5) .. +15 -- two Philox calls, 16 decisions.
+// All of a region's Philox calls are issued first (8 independent chains), then:
 // FWD word: the lane's register keys 4h + {0-3, 8-11, 16-19, 24-27} (h = l >> 5) are nibbles of its
-// own and its lane^32 partner's decisions; BWD word: bit (key & 15) of the 16 query rows the lane's
-// registers hold, read back from a wave-private LDS copy of the 64 lanes' decisions.
+// own and its lane^32 partner's decisions (v_permlane32_swap); BWD word: bit (key & 15) of the 16
+// query rows the lane's registers hold, read back from ONE wave-private LDS copy of the region's
+// decisions (one wave barrier per region instead of two per sub-block).
 constexpr int DM_TPW = 2;
 __global__ __launch_bounds__(256) void k_attn_dropmask(int64_t T_, int64_t nbh, uint32_t* __restrict__ mask_f,
                                                        uint32_t* __restrict__ mask_b, DropArgs d) {
-    __shared__ __attribute__((aligned(16))) uint16_t sbits[4][64];
+    __shared__ __attribute__((aligned(16))) uint32_t sbits[4][2][64];   // [wave][qs][lane]: ks 0 | ks 1 << 16
     const int NB = (int)(T_ >> 5), NP = NB >> 1;
     const int64_t nreg = (int64_t)NP * (NP + 1) / 2, ntile = mask_tiles(T_);
     const int64_t total = nbh * nreg;
     const int lane = threadIdx.x & 63, h = lane >> 5, lq = lane & 31, w = threadIdx.x >> 6;
-    const int kk = lq, e = kk & 15, hh = kk >> 4;
+    const int kk = lq, e = kk & 15, hk = kk >> 4;
     const uint64_t stream = dropout_stream(d.rng_call, d.site);
     const int64_t first = ((int64_t)blockIdx.x * 4 + w) * DM_TPW;
     if (first >= total) return;
@@ -57,42 +59,58 @@ __global__ __launch_bounds__(256) void k_attn_dropmask(int64_t T_, int64_t nbh, 
                 ++bh;
             }
         }
-        uint32_t fw[2] = {0u, 0u}, bw[2] = {0u, 0u};
+        const bool diag = QT == KT;   // wave-uniform
+        uint32_t bits[2][2];
 #pragma unroll
         for (int qs = 0; qs < 2; ++qs)
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
-                if (QT == KT && ks > qs) continue;   // sub-block above the diagonal: zero bits
-                const int qb = 2 * QT + qs, kb = 2 * KT + ks;
-                const uint64_t q = (uint64_t)qb * 32 + lq, key0 = (uint64_t)kb * 32 + 16 * h;
+                const uint64_t q = (uint64_t)(2 * QT + qs) * 32 + lq, key0 = (uint64_t)(2 * KT + ks) * 32 + 16 * h;
                 const uint64_t grp = ((bh * T_ + q) * T_ + key0) >> 3;
-                const uint32_t bits = keep8_bits(philox_group(d.seed, stream, grp), d.thr) |
-                                      (keep8_bits(philox_group(d.seed, stream, grp + 1), d.thr) << 8);
-                const uint32_t part = (uint32_t)__shfl_xor((int)bits, 32, 64);
-                const uint32_t lo = h ? part : bits, hi = h ? bits : part, sh = 4 * h;
+                // (the sub-block above the diagonal is computed too -- branch-free -- and zeroed below)
+                bits[qs][ks] = keep8_bits(philox_group(d.seed, stream, grp), d.thr) |
+                               (keep8_bits(philox_group(d.seed, stream, grp + 1), d.thr) << 8);
+            }
+        if (diag) bits[0][1] = 0u;   // sub-block wholly above the diagonal: zero bits
+        uint32_t fw[2] = {0u, 0u}, bw[2] = {0u, 0u};
+#pragma unroll
+        for (int qs = 0; qs < 2; ++qs) {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                // v_permlane32_swap of a value with itself: [0] = lanes 0-31 own / 32-63 the lower half's,
+                // [1] = lanes 0-31 the upper half's / 32-63 own -- lane l ^ 32's decisions are [h ? 0 : 1]
+                const auto sw = __builtin_amdgcn_permlane32_swap(bits[qs][ks], bits[qs][ks], false, false);
+                const uint32_t part = h ? sw[0] : sw[1];
+                const uint32_t lo = h ? part : bits[qs][ks], hi = h ? bits[qs][ks] : part, sh = 4 * h;
                 const uint32_t f16 = ((lo >> sh) & 0xFu) | (((lo >> (8 + sh)) & 0xFu) << 4) |
                                      (((hi >> sh) & 0xFu) << 8) | (((hi >> (8 + sh)) & 0xFu) << 12);
                 fw[qs] |= f16 << (16 * ks);
-                sbits[w][lane] = (uint16_t)bits;          // lane q + 32 h': keys 16 h' .. +15 of query q
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                uint32_t b16 = 0;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {   // query rows 4h + 8j + 0..3 of key kk
-                    const uint2 v = *(const uint2*)&sbits[w][32 * hh + 4 * h + 8 * j];
-                    b16 |= ((v.x >> e) & 1u) << (4 * j) | ((v.x >> (16 + e)) & 1u) << (4 * j + 1) |
-                           ((v.y >> e) & 1u) << (4 * j + 2) | ((v.y >> (16 + e)) & 1u) << (4 * j + 3);
-                }
-                bw[ks] |= b16 << (16 * qs);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
+            sbits[w][qs][lane] = bits[qs][0] | (bits[qs][1] << 16);   // lane q + 32 h': keys 16 h' .. +15 of query q
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            mask_f[((int64_t)bh * ntile + mask_fwd_tile(2 * QT + s, KT)) * 64 + lane] = fw[s];
-            mask_b[((int64_t)bh * ntile + mask_bwd_tile(2 * KT + s, QT, NP)) * 64 + lane] = bw[s];
+        for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {   // query rows 4h + 8j + 0..3 of key kk: source lanes 32 hk + 4h + 8j ..
+                const uint4 v = *(const uint4*)&sbits[w][qs][32 * hk + 4 * h + 8 * j];
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    const int bit = 16 * ks + e;
+                    const uint32_t nib = ((v.x >> bit) & 1u) | (((v.y >> bit) & 1u) << 1) | (((v.z >> bit) & 1u) << 2) |
+                                         (((v.w >> bit) & 1u) << 3);
+                    bw[ks] |= nib << (16 * qs + 4 * j);
+                }
+            }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            mask_f[((int64_t)bh * ntile + mask_fwd_tile(2 * QT + s2, KT)) * 64 + lane] = fw[s2];
+            mask_b[((int64_t)bh * ntile + mask_bwd_tile(2 * KT + s2, QT, NP)) * 64 + lane] = bw[s2];
         }
     }
 }

@@ -52,13 +52,16 @@ __global__ void k_decode_kv_append(const float* __restrict__ qkv, int64_t ld, in
 }
 
 // one wave per (b, h): the newest query against cached keys 0..n-1 (causal by construction),
-// scale = n_embd^-0.5.  Online softmax over chunks of 16 keys, so any key count works
-// (no LDS score buffer): a chunk is read by the whole wave -- 4 lanes per key, each a contiguous
-// 16-float quarter of the row (float4 loads, coalesced 64-B pieces) -- the 4 partial dots meet in
-// two shuffles, then lane e < D accumulates o[e] += p_j v_j[e] over the chunk (rows of V read
-// contiguously across lanes).  D <= 64.
+// scale = n_embd^-0.5.  Keys are spread over the lanes -- chunk c holds key 64 c + lane
+// -- and each lane keeps its key's whole dot product and its own partial output row acc[0..D) (D
+// padded to DP at compile time): a chunk's softmax statistics are two wave reductions (online over
+// chunks), every K / V element load of a chunk is independent, and the output row is one DPP wave
+// sum per dimension at the end.  (The previous form put 4 lanes on a key and accumulated V with a
+// serial 16-step __shfl + dependent-load loop per chunk, and its vector loads needed D == 64: 73 us
+// per call for the C5 model's head size 21, 10 % of generate().)
 // K/V element (b, h, key j, e) at base + b*sb + h*sh + j*sj + e: the [B, H, Tmax, D] cache
 // (sb = H*Tmax*D, sh = Tmax*D, sj = D) or the rows of a window's qkv buffer (sb = T*ld, sh = D, sj = ld).
+template <int DP>
 __global__ __launch_bounds__(256) void k_decode_attn(const float* __restrict__ q, int64_t ldq,
                                                      const float* __restrict__ kc, const float* __restrict__ vc,
                                                      int64_t sb, int64_t sh, int64_t sj, int64_t B, int64_t H,
@@ -71,48 +74,46 @@ __global__ __launch_bounds__(256) void k_decode_attn(const float* __restrict__ q
     const int64_t n = len_dev ? *len_dev : nfix;  // keys 0..n-1
     const float* K = kc + b * sb + h * sh;
     const float* V = vc + b * sb + h * sh;
-    const int part = lane & 3, e0 = 16 * part;     // this lane's quarter of the head dimension
-    const bool vec = (D == 64) && ((sj & 3) == 0) && ((((uintptr_t)K) & 15) == 0);
-    float qv[16];
+    float qv[DP], acc[DP];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) qv[i] = e0 + i < D ? q[b * ldq + h * D + e0 + i] : 0.f;
-    float m = -INFINITY, l = 0.f, acc = 0.f;
-    for (int64_t j0 = 0; j0 < n; j0 += 16) {
-        const int64_t j = j0 + (lane >> 2);
-        float s = 0.f;
-        if (j < n) {
-            const float* kr = K + j * sj + e0;
-            if (vec) {
+    for (int e = 0; e < DP; ++e) {
+        qv[e] = e < D ? q[b * ldq + h * D + e] : 0.f;
+        acc[e] = 0.f;
+    }
+    float m = -INFINITY, l = 0.f;
+    for (int64_t c0 = 0; c0 < n; c0 += 64) {
+        const int64_t j = c0 + lane;
+        const bool ok = j < n;
+        const float* kr = K + (ok ? j : 0) * sj;
+        const float* vr = V + (ok ? j : 0) * sj;
+        float kv[DP], vv[DP];
 #pragma unroll
-                for (int i = 0; i < 16; i += 4) {
-                    const float4 k4 = *(const float4*)(kr + i);
-                    s = fmaf(qv[i], k4.x, s);
-                    s = fmaf(qv[i + 1], k4.y, s);
-                    s = fmaf(qv[i + 2], k4.z, s);
-                    s = fmaf(qv[i + 3], k4.w, s);
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < 16; ++i)
-                    if (e0 + i < D) s = fmaf(qv[i], kr[i], s);
-            }
+        for (int e = 0; e < DP; ++e) {   // every load of the chunk in flight together
+            kv[e] = e < D ? kr[e] : 0.f;
+            vv[e] = e < D ? vr[e] : 0.f;
         }
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
-        s = j < n ? s * scale : -INFINITY;
+        float s = 0.f;
+#pragma unroll
+        for (int e = 0; e < DP; ++e) s = fmaf(qv[e], kv[e], s);
+        s = ok ? s * scale : -INFINITY;
         const float m_new = fmaxf(m, wave_max(s));
         const float alpha = __expf(m - m_new);
-        const float p = j < n ? __expf(s - m_new) : 0.f;
-        l = l * alpha + wave_sum(p) * 0.25f;   // every key's p is held by its 4 lanes
+        const float p = ok ? __expf(s - m_new) : 0.f;
+        l = l * alpha + wave_sum(p);
         m = m_new;
-        acc *= alpha;
-        const int jn = (int)(n - j0 < 16 ? n - j0 : 16);
-        for (int jj = 0; jj < jn; ++jj) {
-            const float pj = __shfl(p, 4 * jj, 64);
-            if (lane < D) acc = fmaf(pj, V[(j0 + jj) * sj + lane], acc);
+#pragma unroll
+        for (int e = 0; e < DP; ++e) acc[e] = fmaf(p, vv[e], acc[e] * alpha);
+    }
+    const float inv = 1.f / l;
+    float out = 0.f;
+#pragma unroll
+    for (int e = 0; e < DP; ++e) {
+        if (e < D) {   // wave-uniform
+            const float t = wave_sum_dpp(acc[e]);
+            out = lane == e ? t * inv : out;
         }
     }
-    if (lane < D) o[b * ldo + h * D + lane] = acc / l;
+    if (lane < D) o[b * ldo + h * D + lane] = out;
 }
 
 // next token per row from logits [B, V]: greedy = first argmax (torch.argmax tie rule); else
@@ -192,8 +193,12 @@ extern "C" int cg_decode_attn(const float* q, int64_t ldq, const float* k, const
                               float scale, float* o, int64_t ldo, void* stream) {
     CG_REQUIRE(B > 0 && H > 0 && D > 0 && D <= 64, "cg_decode_attn: needs D <= 64");
     CG_REQUIRE(len_dev || nkeys > 0, "cg_decode_attn: needs at least one key");
-    k_decode_attn<<<ceil_div(B * H, 4), 256, 0, (hipStream_t)stream>>>(q, ldq, k, v, sb, sh, sj, B, H, D, len_dev,
-                                                                       nkeys, scale, o, ldo);
+    if (D <= 24)
+        k_decode_attn<24><<<ceil_div(B * H, 4), 256, 0, (hipStream_t)stream>>>(q, ldq, k, v, sb, sh, sj, B, H, D,
+                                                                               len_dev, nkeys, scale, o, ldo);
+    else
+        k_decode_attn<64><<<ceil_div(B * H, 4), 256, 0, (hipStream_t)stream>>>(q, ldq, k, v, sb, sh, sj, B, H, D,
+                                                                               len_dev, nkeys, scale, o, ldo);
     CG_LAUNCH_CHECK("cg_decode_attn");
     return CG_OK;
 }

@@ -1,7 +1,8 @@
 // charpt: LayerNorm forward/backward (nn.LayerNorm, GPT1.py:159-160,173), fp32 statistics.
 // One wave64 per row; the row lives in registers: lane owns NJ chunks of VEC consecutive
 // floats at e = (j*64 + lane)*VEC.  Specialised shapes: C = 384 (VEC 2, NJ 3), 768 (4, 3),
-// 512 (4, 2), 1024 (4, 4); any other C <= 2048 uses (1, 32) with bounds checks.
+// 512 (4, 2), 1024 (4, 4), even C <= 128 (2, 1; forward); any other C <= 2048 uses (1, 32) with
+// bounds checks.
 #include "common.h"
 
 using namespace cg;
@@ -347,6 +348,17 @@ template <typename TY>
 int launch_ln_fwd(const float* x, const float* w, const float* b, TY* y, float* mean, float* rstd, int64_t rows,
                   int C, float eps, hipStream_t st) {
     const bool al16 = (((uintptr_t)x | (uintptr_t)w | (uintptr_t)b) & 15) == 0;
+    const bool al8 = (((uintptr_t)x | (uintptr_t)w | (uintptr_t)b) & 7) == 0;
+    if (C <= 128 && C % 2 == 0 && al8) {
+        // narrow rows (C1 / C5: C = 126, 504 B): one 8-B chunk per lane and 8 rows per wave in flight --
+        // the generic (1, 32) form issued 4-B loads through 32 bounds-checked chunks, 2 rows per wave
+        // (28 us for the [65536, 126] decode window: 2.4 TB/s)
+        constexpr int RPW8 = 8;
+        int grid8 = ceil_div(rows, 4 * RPW8);
+        grid8 = grid8 > 4096 ? 4096 : grid8;
+        k_ln_fwd<2, 1, TY, RPW8><<<grid8, 256, 0, st>>>(x, w, b, y, mean, rstd, rows, C, eps);
+        return CG_OK;
+    }
     constexpr int RPW = 2;
     int grid = ceil_div(rows, 4 * RPW);
     grid = grid > 4096 ? 4096 : grid;

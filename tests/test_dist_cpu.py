@@ -99,3 +99,66 @@ def test_segment_plan_partitions_flat_buffer():
             base = m.flat.master.data_ptr()
             idx = {next(i for i, (r0, r1) in enumerate(ranges) if r0 <= (o - base) // 4 < r1) for o in offs}
             assert len(idx) == 1
+
+
+def _avg_worker(rank, world, port, q):
+    """GradReducer's RCCL branch (avg_native: backend "nccl" -> one all_reduce(AVG), no division
+    afterwards) run under gloo with the backend query and the collective replaced by a fake that
+    implements AVG as SUM / world -- the op, bucket ranges and finish() arithmetic the RCCL path
+    takes, on CPU."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from replicatinggpt_amd import engine
+        seen = []
+        real_all_reduce, real_backend = dist.all_reduce, dist.get_backend
+
+        def fake_all_reduce(t, op=None, group=None, async_op=False):
+            seen.append(op)
+            assert op == dist.ReduceOp.AVG
+            w = real_all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True)
+            w.wait()
+            t.div_(world)
+
+            class _Done:
+                def wait(self):
+                    return True
+            return _Done()
+
+        engine.dist.all_reduce = fake_all_reduce
+        engine.dist.get_backend = lambda group=None: "nccl"
+        try:
+            g = torch.arange(1000, dtype=torch.float32) * (rank + 1)
+            red = engine.GradReducer(g, bucket_bytes=1024)
+            assert red.avg_native
+            ranges = [(700, 1000), (0, 700)]
+            works = []
+            for r0, r1 in ranges:
+                works += red.launch(r0, r1)
+            red.finish(works, ranges)          # must not divide a second time
+        finally:
+            engine.dist.all_reduce, engine.dist.get_backend = real_all_reduce, real_backend
+        q.put((rank, g.tolist(), len(seen)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_reducer_avg_native_branch():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_avg_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, g, n = q.get(timeout=120)
+        res[r] = (g, n)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = (torch.arange(1000, dtype=torch.float32) * 1.5).tolist()
+    for r in range(world):
+        assert res[r][0] == want
+        assert res[r][1] == 2 + 3          # 256-element buckets: 300 -> 2, 700 -> 3

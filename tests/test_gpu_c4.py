@@ -6,10 +6,14 @@ is ~50 MB per layer at B = 64, and cg_gemm dispatches the forward / dgrad produc
 256x256 kernel and the weight gradients to the 128x128 kernel with split-K.  Each is checked here
 at the C4 geometry against an fp64 reference (attention: with the oracle's Philox keep mask), and a
 2-layer C4-width model against the CPU oracle (fp32) and against itself in bf16.
-Tolerances: the north_star's -- fp32 1e-5 relative, bf16 2e-2 (outputs) / 3e-2 (attention grads)."""
+Tolerances: the north_star's -- fp32 1e-5 relative, bf16 2e-2 (conftest.bf16_close: per element, by
+max and by norm)."""
 import numpy as np
 import pytest
+
 import torch
+
+from conftest import bf16_close
 
 from oracle import gpt1_oracle as O
 from oracle import philox
@@ -70,7 +74,10 @@ def test_c4_attention_fwd_bwd_vs_fp64(p):
     torch.cuda.synchronize()
     assert relerr(o, ref.reshape(B * T4, d)) < 2e-2
     for i, t in enumerate((q, k, v)):
-        assert relerr(dqkv[:, i * d:(i + 1) * d], t.grad.reshape(B * T4, d)) < 3e-2, "qkv"[i]
+        ok, st = bf16_close(dqkv[:, i * d:(i + 1) * d], t.grad.reshape(B * T4, d))
+        assert ok, ("qkv"[i], st)
+    ok, st = bf16_close(o, ref.reshape(B * T4, d))
+    assert ok, ("o", st)
     # logsumexp (fp32, per (b, h, t)) of the unmasked-row softmax
     s = torch.einsum("bthd,bshd->bhts", q.detach(), k.detach()) * scale
     s = s.masked_fill(~torch.tril(torch.ones(T4, T4, dtype=torch.bool)), float("-inf"))

@@ -290,6 +290,35 @@ def test_c2_full_size_bf16_step_close_to_fp32():
         assert float(torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0)) > 0.998, n
 
 
+def test_c2_full_size_bf16_step_matches_oracle():
+    """the benchmarked configuration itself (C2: B=64, T=256, d=384, H=6, L=6 --
+    BASELINE configs[1]) on the bf16 path, in training mode at dropout 0.2, against the CPU oracle
+    (fp32 restatement of GPT1.py:176-194 with the same Philox masks) from the same seeded init: one
+    forward / backward.  Loss within 1e-4 relative (measured 2.5e-6); every parameter's gradient
+    within 5e-2 by norm and cosine > 0.999 (measured: median 1.1 %, worst 3.9 % -- the LayerNorm-2 and
+    FFN-1 weight gradients, which sum bf16-rounded activations over all 16 384 tokens;
+    tools/parity_probe.py, profiles/r3_parity_probe.txt)."""
+    from replicatinggpt_amd import BigramLanguageModel, PRESETS
+    cfg = PRESETS["c2"].with_(dtype="bf16")
+    ocfg = O.OracleConfig(block_size=256, n_embd=384, n_head=6, n_layers=6, dropout=cfg.dropout)
+    assert cfg.dropout == 0.2
+    g = torch.Generator().manual_seed(17)
+    idx = torch.randint(0, 65, (64, 256), generator=g)
+    tgt = torch.randint(0, 65, (64, 256), generator=g)
+    torch.manual_seed(1337)
+    m = BigramLanguageModel(cfg).to(DEV)
+    _, loss = m(idx.to(DEV), tgt.to(DEV))
+    loss.backward()
+    torch.manual_seed(1337)
+    P = O.init_params(ocfg)
+    _, rl, rg = O.loss_and_grads(P, idx, tgt, ocfg, train=True, seed=cfg.dropout_seed, call=0)
+    assert abs(float(loss.detach()) - float(rl)) < 1e-4 * float(rl)
+    for name, prm in m.named_parameters():
+        a, b = prm.grad.double().cpu().flatten(), rg[name].double().flatten()
+        assert float((a - b).norm() / b.norm()) < 5e-2, name
+        assert float(torch.nn.functional.cosine_similarity(a, b, dim=0)) > 0.999, name
+
+
 def test_adamw_skips_params_without_grad_like_torch():
     """optim.AdamW with some .grad None skips those parameters exactly like torch.optim.AdamW (no
     weight decay, no moment update, no step count), and its state dict carries per-parameter steps."""

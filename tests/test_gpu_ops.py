@@ -5,7 +5,10 @@ import math
 
 import numpy as np
 import pytest
+
 import torch
+
+from conftest import bf16_close
 
 from oracle import philox
 
@@ -56,7 +59,7 @@ def test_dropout_mask_matches_oracle(p):
     assert np.array_equal(out.cpu().numpy() > 0.5, want)
 
 
-@pytest.mark.parametrize("C", [126, 384, 512, 768, 1024, 33])
+@pytest.mark.parametrize("C", [126, 384, 512, 768, 1024, 33, 128, 64, 2])
 @pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
 def test_layernorm(C, out_dtype):
     torch.manual_seed(0)
@@ -450,9 +453,14 @@ def test_attention_fwd_bwd(B, T, H, D, p, dt):
     assert relerr(o, ref.reshape(B * T, d)) < tol
     dqkv = Fn.attention_bwd(qkv_d, B, T, H, D, o, dout.reshape(B * T, d).to(DEV), lse, scale, p, 11, call, 7, mask)
     dq, dk, dv = dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:]
-    assert relerr(dq, q.grad.reshape(B * T, d)) < (1e-5 if dt == torch.float32 else 3e-2)
-    assert relerr(dk, k.grad.reshape(B * T, d)) < (1e-5 if dt == torch.float32 else 3e-2)
-    assert relerr(dv, v.grad.reshape(B * T, d)) < (1e-5 if dt == torch.float32 else 3e-2)
+    if dt == torch.float32:
+        assert relerr(dq, q.grad.reshape(B * T, d)) < 1e-5
+        assert relerr(dk, k.grad.reshape(B * T, d)) < 1e-5
+        assert relerr(dv, v.grad.reshape(B * T, d)) < 1e-5
+    else:
+        for name, got, t in (("dq", dq, q), ("dk", dk, k), ("dv", dv, v)):
+            ok, st = bf16_close(got, t.grad.reshape(B * T, d))
+            assert ok, (name, st)
 
 
 def test_attention_fast_matches_generic_bf16():
@@ -501,7 +509,8 @@ def test_attention_fast_block_shapes(T):
     torch.cuda.synchronize()
     assert relerr(o, ref.reshape(B * T, d)) < 2e-2
     for i, t in enumerate((q, k, v)):
-        assert relerr(dqkv[:, i * d:(i + 1) * d], t.grad.reshape(B * T, d)) < 3e-2
+        ok, st = bf16_close(dqkv[:, i * d:(i + 1) * d], t.grad.reshape(B * T, d))
+        assert ok, ("qkv"[i], T, st)
 
 
 @pytest.mark.parametrize("T", [256, 128, 64])
