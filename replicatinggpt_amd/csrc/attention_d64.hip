@@ -205,6 +205,16 @@ __device__ __forceinline__ void mark_ready(const R&... r) {
 // can be scheduled between the two.
 __device__ __forceinline__ void wait_all_barrier() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// end of a ring tile: this wave's vector-memory operations older than the N DMA instructions just
+// requested have landed, then every wave's (LDS reads drained too: the slot read now is rewritten
+// after a later barrier)
+template <int N>
+__device__ __forceinline__ void ring_wait(bool pf) {
+    if (pf) asm volatile("s_waitcnt vmcnt(%c0) lgkmcnt(0)\n\ts_barrier" ::"i"(N) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+
 // =====================================================================================
 // forward
 // =====================================================================================
@@ -334,6 +344,7 @@ __device__ __forceinline__ void fwd_group_tile(const char* Ki, const char* Vi, c
 constexpr int FWD_SLOT = 2 * TILE;
 constexpr int FWD_LDS = 3 * FWD_SLOT + 4 * TILE;   // K/V ring + Q image: 80 KB
 
+#ifdef CG_AB_VARIANTS   // A/B-only since round 3 (attn_variant 5): the register-staged forward ring
 template <bool DROP>
 __device__ __forceinline__ void fwd_qblock(int qblk, int bh, char* smem, int64_t T_, int H, const bf16_t* __restrict__ q,
                                            const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, int64_t ld,
@@ -495,6 +506,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64(int64_t T_, int H, cons
         fwd_qblock<DROP>(pass ? x : first, bh, smem, T_, H, q, k, v, ld, o, ldo, lse, scale_log2, mask, dscale);
     }
 }
+#endif
 
 // =====================================================================================
 // dQ: S^T = K Q^T, dP^T = V dO^T, dS^T = P^T (keep/(1-p) dP^T - delta), dQ^T += K^T dS^T.
@@ -560,7 +572,7 @@ __device__ __forceinline__ void dq_group_tile(const char* Ki, const char* Vi, in
 
 // K/V tiles by LDS-DMA (common.h dma16) into a 2-slot ring, the next tile's DMAs issued before the
 // current tile's products (round 2: register staging measured 706 -> 686 us for the C4 backward)
-template <bool DROP>
+template <bool DROP, int NS>
 __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t T_, int H, const bf16_t* __restrict__ q,
                                           const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, int64_t ld,
                                           const bf16_t* __restrict__ o, int64_t ldo, const bf16_t* __restrict__ dout,
@@ -597,9 +609,18 @@ __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t 
     const int qlast = (Q0 + 255 < T - 1) ? Q0 + 255 : T - 1;
     const int nkv = qlast / 64 + 1;
     const int wave_ = __builtin_amdgcn_readfirstlane(tid >> 6);
-    dma_tile(kb_, ld, 0, smem, wave_, lane);
-    dma_tile(vb_, ld, 0, smem + TILE, wave_, lane);
-    wait_all_barrier();
+    // K/V ring of NS slots, tile kv + AH requested at the head of tile kv into the slot of tile
+    // kv + AH - NS (read before an earlier barrier); NS = 4: two tiles of compute to land
+    constexpr int AH = NS / 2;
+    auto slot = [&](int t) { return smem + (t & (NS - 1)) * 2 * TILE; };
+#pragma unroll
+    for (int t = 0; t < AH; ++t) {
+        if (t < nkv) {
+            dma_tile(kb_, ld, (int64_t)t * 64, slot(t), wave_, lane);
+            dma_tile(vb_, ld, (int64_t)t * 64, slot(t) + TILE, wave_, lane);
+        }
+    }
+    ring_wait<AH == 2 ? 4 : 0>(AH == 2 && nkv > 1);   // operands and tile 0 have landed
 #pragma unroll
     for (int g = 0; g < 2; ++g)
 #pragma unroll
@@ -607,25 +628,27 @@ __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t 
     mark_ready(mw[0], mw[1], lse2[0], lse2[1], dl[0], dl[1]);
     for (int kv = 0; kv < nkv; ++kv) {
         const int nxt = kv + 1 < nkv ? kv + 1 : kv;
-        if (kv + 1 < nkv) {   // slot (kv + 1) & 1 was last read before the previous barrier
-            dma_tile(kb_, ld, (int64_t)nxt * 64, smem + ((kv + 1) & 1) * 2 * TILE, wave_, lane);
-            dma_tile(vb_, ld, (int64_t)nxt * 64, smem + ((kv + 1) & 1) * 2 * TILE + TILE, wave_, lane);
-        }
-        // the next tile's keep words by hidden loads: a compiler-counted load issued after the DMAs
-        // made hipcc wait vmcnt(0) -- for the DMAs too -- at the head of the tile (no prefetch left)
+        // the next tile's keep words by hidden loads, issued before the DMAs so that the counted wait
+        // at the tile's end retires them (a compiler-counted load issued after the DMAs made hipcc
+        // wait vmcnt(0) -- for the DMAs too -- at the head of the tile)
         uint32_t mn[2] = {0u, 0u};
         if constexpr (DROP) {
 #pragma unroll
             for (int g = 0; g < 2; ++g)
                 if (act[g] && nxt * 64 <= qg[g] + 31) gload4(mn[g], mrow[g] + nxt * 64);
         }
-        const char* Ki = smem + (kv & 1) * 2 * TILE;
+        const bool pf = kv + AH < nkv;
+        if (pf) {
+            dma_tile(kb_, ld, (int64_t)(kv + AH) * 64, slot(kv + AH), wave_, lane);
+            dma_tile(vb_, ld, (int64_t)(kv + AH) * 64, slot(kv + AH) + TILE, wave_, lane);
+        }
+        const char* Ki = slot(kv);
         const int k0 = kv * 64;
 #pragma unroll
         for (int g = 0; g < 2; ++g)
             if (act[g] && k0 <= qg[g] + 31)
                 dq_group_tile<DROP>(Ki, Ki + TILE, k0, qg[g], qf[g], df[g], lse2[g], dl[g], mw[g], c2, dqa[g], lane);
-        wait_all_barrier();   // the next tile (and the keep words) have landed for every wave
+        ring_wait<AH == 2 ? 4 : 0>(pf);   // tile kv + 1 (and the keep words) have landed for every wave
         asm volatile("" : "+v"(mn[0]), "+v"(mn[1]));
         mw[0] = mn[0];
         mw[1] = mn[1];
@@ -639,7 +662,7 @@ __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t 
 }
 
 // pairs of query blocks per workgroup, as the forward
-template <bool DROP>
+template <bool DROP, int NS>
 __global__ __launch_bounds__(256, 2) void k_attn_dq_d64(int64_t T_, int H, const bf16_t* __restrict__ q,
                                                         const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
                                                         int64_t ld, const bf16_t* __restrict__ o, int64_t ldo,
@@ -647,7 +670,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_dq_d64(int64_t T_, int H, const
                                                         const float* __restrict__ lse, float* __restrict__ delta,
                                                         bf16_t* __restrict__ dq, int64_t lddq, float scale,
                                                         const uint32_t* __restrict__ mask, float dscale) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
+    __shared__ __attribute__((aligned(16))) char smem[NS * 2 * TILE];
     int x, bh;
     block_coords<false>(x, bh);
     const int nq = (int)((T_ + 255) / 256), first = nq - 1 - x;
@@ -655,7 +678,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_dq_d64(int64_t T_, int H, const
 #pragma unroll 1
     for (int pass = 0; pass < npass; ++pass) {
         if (pass) __syncthreads();
-        dq_qblock<DROP>(pass ? x : first, bh, smem, T_, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
+        dq_qblock<DROP, NS>(pass ? x : first, bh, smem, T_, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
                         mask, dscale);
     }
 }
@@ -732,7 +755,7 @@ __device__ __forceinline__ void dkdv_tile(const char* Qi, const char* Oi, const 
     }
 }
 
-template <bool DROP>
+template <bool DROP, int NS>
 __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_t T_, int H,
                                             const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                             const bf16_t* __restrict__ v, int64_t ld, const bf16_t* __restrict__ dout,
@@ -772,44 +795,62 @@ __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_
         return s;
     };
     const int wave_ = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // Q/dO ring of NS slots (images + row statistics), tile qt + AH requested at the head of tile qt
+    // into the slot of tile qt + AH - NS (read before an earlier barrier); NS = 4: two tiles of
+    // compute to land.  A slot's statistics are written from hidden loads issued with its DMA.
+    constexpr int AH = NS / 2;
+    auto slot = [&](int it_) { return smem + (it_ & (NS - 1)) * KV_STAGE; };
     {
-        dma_tile(qb_, ld, (int64_t)qt0 * 64, smem, wave_, lane);
-        dma_tile(ob_, ldd, (int64_t)qt0 * 64, smem + TILE, wave_, lane);
-        const float s = stat_load(qt0);
-        if (tid < 128) ((float*)(smem + 2 * TILE))[tid] = s;
+        const float s0 = stat_load(qt0);
+        const float s1 = (AH == 2 && qt0 + 1 < nq) ? stat_load(qt0 + 1) : 0.f;
+#pragma unroll
+        for (int t = 0; t < AH; ++t) {
+            if (qt0 + t < nq) {
+                dma_tile(qb_, ld, (int64_t)(qt0 + t) * 64, slot(t), wave_, lane);
+                dma_tile(ob_, ldd, (int64_t)(qt0 + t) * 64, slot(t) + TILE, wave_, lane);
+                if (tid < 128) ((float*)(slot(t) + 2 * TILE))[tid] = t ? s1 : s0;
+            }
+        }
     }
-    wait_all_barrier();
+    ring_wait<AH == 2 ? 4 : 0>(AH == 2 && qt0 + 1 < nq);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) mark_ready(kf[ks], vf[ks]);
     mark_ready(mw);
     for (int qt = qt0; qt < nq; ++qt) {
         const int it = qt - qt0;
         const int nxt = qt + 1 < nq ? qt + 1 : qt;
-        if (qt + 1 < nq) {   // slot (it + 1) & 1 was last read before the previous barrier
-            dma_tile(qb_, ld, (int64_t)nxt * 64, smem + ((it + 1) & 1) * KV_STAGE, wave_, lane);
-            dma_tile(ob_, ldd, (int64_t)nxt * 64, smem + ((it + 1) & 1) * KV_STAGE + TILE, wave_, lane);
-        }
-        // the next tile's row statistics and keep word by hidden loads (compiler-counted loads issued
+        const bool pf = qt + AH < nq;
+        // tile qt + AH's row statistics and tile qt + 1's keep word by hidden loads issued before the
+        // DMAs, so the counted wait at the tile's end retires them (compiler-counted loads issued
         // after the DMAs made hipcc wait vmcnt(0) -- for the DMAs too -- inside this tile's products)
         uint32_t sw = 0u, mn = 0u;
-        if (tid < 64) gload4(sw, lse_b + nxt * 64 + tid);
-        else if (tid < 128) gload4(sw, del_b + nxt * 64 + tid - 64);
+        if (pf) {
+            if (tid < 64) gload4(sw, lse_b + (qt + AH) * 64 + tid);
+            else if (tid < 128) gload4(sw, del_b + (qt + AH) * 64 + tid - 64);
+        }
         if (DROP && act && nxt >= qtm) gload4(mn, mcol + (nxt - qtm) * 64);
-        const char* S0 = smem + (it & 1) * KV_STAGE;
+        if (pf) {
+            dma_tile(qb_, ld, (int64_t)(qt + AH) * 64, slot(it + AH), wave_, lane);
+            dma_tile(ob_, ldd, (int64_t)(qt + AH) * 64, slot(it + AH) + TILE, wave_, lane);
+        }
+        const char* S0 = slot(it);
         const char* Qi = S0;
         const char* Oi = S0 + TILE;
         const float* st_lse = (const float*)(S0 + 2 * TILE);
         const float* st_del = st_lse + 64;
         const int q0 = qt * 64;
         if (act && q0 + 63 >= kq) dkdv_tile<DROP>(Qi, Oi, st_lse, st_del, q0, kq, key, kf, vf, mw, c2, dka, dva, lane);
-        char* D = smem + ((it + 1) & 1) * KV_STAGE;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile, its statistics and keep word
+        // tile qt + 1, the statistics and the keep word have landed (tile qt + AH's DMAs may not)
+        if (AH == 2 && pf) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("" : "+v"(sw), "+v"(mn));
-        // stat_load's arithmetic on the loaded word
-        if (tid < 64) ((float*)(D + 2 * TILE))[tid] = __uint_as_float(sw) * LOG2E;
-        else if (tid < 128) ((float*)(D + 2 * TILE))[tid] = -__uint_as_float(sw) / dscale;
+        if (pf) {   // stat_load's arithmetic on the loaded word
+            char* D = slot(it + AH);
+            if (tid < 64) ((float*)(D + 2 * TILE))[tid] = __uint_as_float(sw) * LOG2E;
+            else if (tid < 128) ((float*)(D + 2 * TILE))[tid] = -__uint_as_float(sw) / dscale;
+        }
         mw = mn;
-        wait_all_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
     if (!act) return;
     store_rows(dk + (boff + key) * lddkv + hh * 64, dka, scale * dscale, lane);
@@ -817,7 +858,7 @@ __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_
 }
 
 // pairs of 128-key blocks per workgroup (x, then nk - 1 - x): uniform causal work per workgroup
-template <bool DROP>
+template <bool DROP, int NS>
 __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, const bf16_t* __restrict__ q,
                                                           const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
                                                           int64_t ld, const bf16_t* __restrict__ dout, int64_t ldd,
@@ -825,7 +866,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, con
                                                           const float* __restrict__ delta, bf16_t* __restrict__ dk,
                                                           bf16_t* __restrict__ dv, int64_t lddkv, float scale,
                                                           const uint32_t* __restrict__ mask, float dscale) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * KV_STAGE];
+    __shared__ __attribute__((aligned(16))) char smem[NS * KV_STAGE];
     int x, bh;
     block_coords<false>(x, bh);
     const int nk = (int)((T_ + 127) / 128), second = nk - 1 - x;
@@ -833,7 +874,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64(int64_t T_, int H, con
 #pragma unroll 1
     for (int pass = 0; pass < npass; ++pass) {
         if (pass) __syncthreads();
-        dkdv_kblock<DROP>(pass ? second : x, bh, smem, T_, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
+        dkdv_kblock<DROP, NS>(pass ? second : x, bh, smem, T_, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
                           mask, dscale);
     }
 }
@@ -1304,6 +1345,253 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_d64r(int H, const bf16_t* _
                          dscale);
 }
 
+// =====================================================================================
+// Forward at T > 256 with an LDS-DMA K/V ring.  Same two-group software pipeline and per-tile
+// arithmetic as fwd_qblock (identical bits), but K/V tiles arrive by LDS-DMA requested at the head
+// of a tile (no staging VGPRs or ds_writes in the loop), so a tile has a whole tile of compute (QR:
+// two) to land instead of the half tile the register staging gave it.  The keep words of tile kv + 1
+// are hidden register loads issued just before the DMA, retired by the same counted wait.
+//   QR = false: Q image in LDS (32 KB) + 3-slot ring (48 KB), tile kv + 1 requested at tile kv into
+//               the slot tile kv - 2 used (B read V(kv - 2) during tile kv - 1);
+//   QR = true:  the groups' Q fragments in registers (hidden loads) + 4-slot ring (64 KB), tile kv + 2
+//               requested at tile kv.
+// Both fit two blocks per CU.
+// =====================================================================================
+template <bool QR>
+struct FwdRing {
+    static constexpr int NSLOT = QR ? 4 : 3, AHEAD = QR ? 2 : 1;
+    static constexpr int LDS = NSLOT * 2 * TILE + (QR ? 0 : 4 * TILE);
+    static __device__ __forceinline__ int slot_of(int t) { return QR ? (t & 3) : (t + 3) % 3; }
+};
+
+// dma_tile with a uniform tile base and the per-lane byte offsets precomputed (dma_lane_offs): the
+// same 8 wave-instructions, 2 per wave
+__device__ __forceinline__ void dma_lane_offs(int64_t ldx, int wave, int lane, uint32_t (&off)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int ins = 2 * wave + i, r = 8 * ins + (lane >> 3), c = (lane & 7) ^ ((((r >> 1) & 1) << 2) | ((r >> 2) & 3));
+        off[i] = (uint32_t)((r * ldx + 8 * c) * 2);
+    }
+}
+__device__ __forceinline__ void dma_tile_s(const bf16_t* X, int64_t ldx, int64_t row0, const uint32_t (&off)[2],
+                                           char* img, int wave) {
+    const bf16_t* base = X + row0 * ldx;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) dma16s(base, off[i], img + 1024 * (2 * wave + i));
+}
+
+__device__ __forceinline__ void qk_tile_reg(fv16 (&s)[2], const char* Ki, const sv8 (&qf)[4], int lane) {
+    s[0] = fv16{};
+    s[1] = fv16{};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        s[0] = mfma32(frag_row(Ki, 0, ks, lane), qf[ks], s[0]);
+        s[1] = mfma32(frag_row(Ki, 32, ks, lane), qf[ks], s[1]);
+    }
+}
+
+template <bool DROP, bool QR>
+__device__ __forceinline__ void fwd_qblock_dma(int qblk, int bh, char* smem, int64_t T_, int H,
+                                               const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+                                               const bf16_t* __restrict__ v, int64_t ld, bf16_t* __restrict__ o,
+                                               int64_t ldo, float* __restrict__ lse, float scale_log2,
+                                               const uint32_t* __restrict__ mask, float dscale) {
+    using R = FwdRing<QR>;
+    constexpr int AH = R::AHEAD;
+    // tile kv + AH is requested at tile kv: 4 DMA instructions per wave stay in flight at its end
+    // when AH = 2 (tile kv + 1 must have landed), none when AH = 1
+    constexpr int NWAIT = AH == 2 ? 4 : 0;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int T = (int)T_, b = bh / H, hh = bh % H;
+    const int Q0 = qblk * 256;
+    const int64_t boff = (int64_t)b * T_, ntile = mask_tiles(T_);
+    const bf16_t* kb_ = k + boff * ld + hh * 64;
+    const bf16_t* vb_ = v + boff * ld + hh * 64;
+    const bf16_t* qb_ = q + boff * ld + hh * 64;
+    char* const Qimg = smem + R::NSLOT * 2 * TILE;   // !QR only
+    const int qg[2] = {Q0 + 32 * (7 - wave), Q0 + 32 * wave};   // g = 0 (A): the longer causal prefix
+    const int qr[2] = {32 * (7 - wave), 32 * wave};             // the groups' rows in the Q image
+    const bool act[2] = {qg[0] < T, qg[1] < T};
+    uint32_t doff[2];   // per-lane DMA byte offsets (K, V and Q share ld and the image layout)
+    dma_lane_offs(ld, wave, lane, doff);
+    auto slot = [&](int t) { return smem + R::slot_of(t) * 2 * TILE; };
+    // keep words of (group, key tile t) at mrow[g] + 64 t + lane (uniform bases, one lane offset); an
+    // inactive group reads block 0's (unused)
+    const uint32_t* mrow[2];
+    const uint32_t loff = 4u * lane;
+    sv8 qf[2][4];
+    uint32_t mw[2] = {0u, 0u};
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        mrow[g] = mask + ((int64_t)bh * ntile + mask_fwd_tile(act[g] ? qg[g] >> 5 : 0, 0)) * 64;
+        if constexpr (QR) {
+            const int qa = (act[g] ? qg[g] : 0) + (lane & 31);
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) gload16(qf[g][ks], qb_ + (int64_t)qa * ld + 16 * ks + 8 * (lane >> 5));
+        }
+        if constexpr (DROP) gload4s(mw[g], mrow[g], loff);
+    }
+    const int qlast = (Q0 + 255 < T - 1) ? Q0 + 255 : T - 1;
+    const int nkv = qlast / 64 + 1;
+    const int npipe = act[1] ? (qg[1] + 31) / 64 : 0;   // B's diagonal tile: first unpipelined tile
+    {   // the V half of tile -1's slot is the pipeline head's "previous tile": zeros
+        const int r = tid >> 3, c = tid & 7;
+        *(uint4*)(slot(-1) + TILE + aoff(r, c)) = make_uint4(0, 0, 0, 0);
+        *(uint4*)(slot(-1) + TILE + aoff(r + 32, c)) = make_uint4(0, 0, 0, 0);
+    }
+    if constexpr (!QR) {   // Q image: the block's 64-row tiles by LDS-DMA, rows past T zero
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            if (Q0 + 64 * t < T) {
+                dma_tile_s(qb_, ld, Q0 + 64 * t, doff, Qimg + t * TILE, wave);
+            } else {
+                const int r = tid >> 3, c = tid & 7;
+                *(uint4*)(Qimg + t * TILE + aoff(r, c)) = make_uint4(0, 0, 0, 0);
+                *(uint4*)(Qimg + t * TILE + aoff(r + 32, c)) = make_uint4(0, 0, 0, 0);
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < AH; ++t) {
+        if (t < nkv) {
+            dma_tile_s(kb_, ld, (int64_t)t * 64, doff, slot(t), wave);
+            dma_tile_s(vb_, ld, (int64_t)t * 64, doff, slot(t) + TILE, wave);
+        }
+    }
+    ring_wait<NWAIT>(AH == 2 && nkv > 1);   // the register loads, Q and tile 0 have landed
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        if constexpr (QR) {
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) asm volatile("" : "+v"(qf[g][ks]));
+        }
+        asm volatile("" : "+v"(mw[g]));
+    }
+    if constexpr (!DROP) mw[0] = mw[1] = 0u;
+    auto qk = [&](fv16 (&s)[2], const char* Ki, int g) {
+        if constexpr (QR) qk_tile_reg(s, Ki, qf[g], lane);
+        else qk_tile(s, Ki, Qimg, qr[g], lane);
+    };
+    fv16 oacc[2][2];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) oacc[g][0] = oacc[g][1] = fv16{};
+    float m_run[2] = {-FLT_MAX, -FLT_MAX}, l_run[2] = {0.f, 0.f};
+    fv16 sA[2], sB[2] = {fv16{} - INFINITY, fv16{} - INFINITY};
+    sv8 pfA[2][2], pfB[2][2];
+    uint32_t mwBp = 0u;   // B's keep word of the previous tile
+    int kv = 0;
+    for (; kv < npipe; ++kv) {
+        uint32_t mn[2] = {0u, 0u};   // tile kv + 1 <= npipe: both groups full through it
+        if constexpr (DROP) {
+            gload4s(mn[0], mrow[0] + (kv + 1) * 64, loff);
+            gload4s(mn[1], mrow[1] + (kv + 1) * 64, loff);
+        }
+        const bool pf = kv + AH < nkv;
+        if (pf) {
+            dma_tile_s(kb_, ld, (int64_t)(kv + AH) * 64, doff, slot(kv + AH), wave);
+            dma_tile_s(vb_, ld, (int64_t)(kv + AH) * 64, doff, slot(kv + AH) + TILE, wave);
+        }
+        const char* Ki = slot(kv);
+        const char* Vi = Ki + TILE;
+        const char* Vp = slot(kv - 1) + TILE;
+        // at kv = 0, B's "previous tile" is sB = -inf against the zeroed V slot: it adds exactly 0
+        qk(sA, Ki, 0);
+        softmax_pack<DROP>(sB, scale_log2, m_run[1], l_run[1], mwBp, pfB);
+        pv_tile(oacc[1], Vp, pfB, lane);
+        rescale_if(tile_max(sA) * scale_log2, m_run[0], l_run[0], oacc[0]);
+        qk(sB, Ki, 1);
+        softmax_pack<DROP>(sA, scale_log2, m_run[0], l_run[0], mw[0], pfA);
+        pv_tile(oacc[0], Vi, pfA, lane);
+        rescale_if(tile_max(sB) * scale_log2, m_run[1], l_run[1], oacc[1]);
+        ring_wait<NWAIT>(pf);
+        if constexpr (DROP) asm volatile("" : "+v"(mn[0]), "+v"(mn[1]));
+        mwBp = mw[1];
+        mw[0] = mn[0];
+        mw[1] = mn[1];
+    }
+    if (npipe > 0) {   // pipeline tail: B's pending tile npipe - 1 (its V still in that tile's slot)
+        softmax_pack<DROP>(sB, scale_log2, m_run[1], l_run[1], mwBp, pfB);
+        pv_tile(oacc[1], slot(npipe - 1) + TILE, pfB, lane);   // the tail requests kv + AH: another slot
+    }
+    for (; kv < nkv; ++kv) {
+        uint32_t mn[2] = {0u, 0u};
+        const int nxt = kv + 1 < nkv ? kv + 1 : kv;
+        if constexpr (DROP) {
+#pragma unroll
+            for (int g = 0; g < 2; ++g)   // past a group's diagonal: re-read its tile 0 (unused)
+                gload4s(mn[g], mrow[g] + (act[g] && nxt * 64 <= qg[g] + 31 ? nxt : 0) * 64, loff);
+        }
+        const bool pf = kv + AH < nkv;
+        if (pf) {
+            dma_tile_s(kb_, ld, (int64_t)(kv + AH) * 64, doff, slot(kv + AH), wave);
+            dma_tile_s(vb_, ld, (int64_t)(kv + AH) * 64, doff, slot(kv + AH) + TILE, wave);
+        }
+        const char* Ki = slot(kv);
+        const char* Vi = Ki + TILE;
+        const int k0 = kv * 64;
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            if (!act[g] || k0 > qg[g] + 31) continue;
+            const int rel = __builtin_amdgcn_readfirstlane(qg[g] - k0);
+            if constexpr (QR) {
+                if (rel >= 64)
+                    fwd_group_tile<DROP, 2, -1, true>(Ki, Vi, nullptr, 0, lane, scale_log2, m_run[g], l_run[g],
+                                                      oacc[g], mw[g], qf[g]);
+                else if (rel == 32)
+                    fwd_group_tile<DROP, 2, 1, true>(Ki, Vi, nullptr, 0, lane, scale_log2, m_run[g], l_run[g],
+                                                     oacc[g], mw[g], qf[g]);
+                else
+                    fwd_group_tile<DROP, 1, 0, true>(Ki, Vi, nullptr, 0, lane, scale_log2, m_run[g], l_run[g],
+                                                     oacc[g], mw[g], qf[g]);
+            } else {
+                if (rel >= 64)
+                    fwd_group_tile<DROP, 2, -1>(Ki, Vi, Qimg, qr[g], lane, scale_log2, m_run[g], l_run[g], oacc[g],
+                                                mw[g]);
+                else if (rel == 32)
+                    fwd_group_tile<DROP, 2, 1>(Ki, Vi, Qimg, qr[g], lane, scale_log2, m_run[g], l_run[g], oacc[g],
+                                               mw[g]);
+                else
+                    fwd_group_tile<DROP, 1, 0>(Ki, Vi, Qimg, qr[g], lane, scale_log2, m_run[g], l_run[g], oacc[g],
+                                               mw[g]);
+            }
+        }
+        ring_wait<NWAIT>(pf);
+        if constexpr (DROP) asm volatile("" : "+v"(mn[0]), "+v"(mn[1]));
+        mw[0] = mn[0];
+        mw[1] = mn[1];
+    }
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        if (!act[g]) continue;
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run[g]), __float_as_uint(l_run[g]), false,
+                                                         false);
+        const float lt = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+        const int64_t qa = qg[g] + (lane & 31);
+        store_rows_wide(o + (boff + qa) * ldo + hh * 64, oacc[g], dscale / lt, lane);
+        if (lane < 32) lse[(int64_t)bh * T_ + qa] = (m_run[g] + __log2f(lt)) * LN2;
+    }
+}
+
+template <bool DROP, bool QR>
+__global__ __launch_bounds__(256, 2) void k_attn_fwd_d64d(int64_t T_, int H, const bf16_t* __restrict__ q,
+                                                          const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                                                          int64_t ld, bf16_t* __restrict__ o, int64_t ldo,
+                                                          float* __restrict__ lse, float scale_log2,
+                                                          const uint32_t* __restrict__ mask, float dscale) {
+    __shared__ __attribute__((aligned(16))) char smem[FwdRing<QR>::LDS];
+    int x, bh;
+    block_coords<false>(x, bh);
+    const int nq = (int)((T_ + 255) / 256), first = nq - 1 - x;
+    const int npass = x == first ? 1 : 2;
+#pragma unroll 1
+    for (int pass = 0; pass < npass; ++pass) {
+        if (pass) __syncthreads();
+        fwd_qblock_dma<DROP, QR>(pass ? x : first, bh, smem, T_, H, q, k, v, ld, o, ldo, lse, scale_log2, mask,
+                                 dscale);
+    }
+}
+
 }  // namespace
 
 namespace attn {
@@ -1329,10 +1617,33 @@ void launch_fwd_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* 
         return;
     }
     const dim3 grid((unsigned)((ceil_div(T, 256) + 1) / 2), (unsigned)(B * H));   // pairs of query blocks
+#ifdef CG_AB_VARIANTS
+    if (g_attn_variant == 5) {   // A/B: the register-staged ring with the Q image in LDS
+        if (d.mask)
+            k_attn_fwd_d64<true><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, lse, scale * LOG2E, d.mask, d.dscale);
+        else
+            k_attn_fwd_d64<false><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, lse, scale * LOG2E, nullptr, 1.f);
+        return;
+    }
+    if (g_attn_variant == 6) {   // A/B: Q image in LDS, 3-slot DMA ring one tile ahead
+        if (d.mask)
+            k_attn_fwd_d64d<true, false><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, lse, scale * LOG2E, d.mask,
+                                                               d.dscale);
+        else
+            k_attn_fwd_d64d<false, false><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, lse, scale * LOG2E,
+                                                                nullptr, 1.f);
+        return;
+    }
+#endif
+    // Q fragments in registers, 4-slot LDS-DMA ring two tiles ahead: C4 forward 248 -> 223 us against
+    // the register-staged ring, 244 us for the one-tile-ahead DMA ring with the Q image in LDS
+    // (same-process interleaved A/B, profiles/r3_attn_fwd_ring_ab.txt)
     if (d.mask)
-        k_attn_fwd_d64<true><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, lse, scale * LOG2E, d.mask, d.dscale);
+        k_attn_fwd_d64d<true, true><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, lse, scale * LOG2E, d.mask,
+                                                          d.dscale);
     else
-        k_attn_fwd_d64<false><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, lse, scale * LOG2E, nullptr, 1.f);
+        k_attn_fwd_d64d<false, true><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, lse, scale * LOG2E, nullptr,
+                                                           1.f);
 }
 
 void launch_dq_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
@@ -1346,12 +1657,23 @@ void launch_dq_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k
         return;
     }
     const dim3 grid((unsigned)((ceil_div(T, 256) + 1) / 2), (unsigned)(B * H));
-    if (d.mask)
-        k_attn_dq_d64<true><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
-                                                  d.mask, d.dscale);
-    else
-        k_attn_dq_d64<false><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale,
-                                                   nullptr, 1.f);
+#define DQ(NS_)                                                                                                    \
+    do {                                                                                                           \
+        if (d.mask)                                                                                                \
+            k_attn_dq_d64<true, NS_><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, \
+                                                           scale, d.mask, d.dscale);                               \
+        else                                                                                                       \
+            k_attn_dq_d64<false, NS_><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq,      \
+                                                            lddq, scale, nullptr, 1.f);                            \
+    } while (0)
+#ifdef CG_AB_VARIANTS
+    if (g_attn_variant == 7) {   // A/B: the 2-slot ring one tile ahead
+        DQ(2);
+        return;
+    }
+#endif
+    DQ(4);
+#undef DQ
 }
 void launch_bwd_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                     const bf16_t* o, int64_t ldo, const bf16_t* dout, int64_t ldd, const float* lse, float* delta,
@@ -1382,12 +1704,23 @@ void launch_dkdv_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t*
         return;
     }
     const dim3 grid((unsigned)((ceil_div(T, 128) + 1) / 2), (unsigned)(B * H));
-    if (d.mask)
-        k_attn_dkdv_d64<true><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
-                                                    d.mask_bwd, d.dscale);
-    else
-        k_attn_dkdv_d64<false><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, scale,
-                                                     nullptr, 1.f);
+#define DKDV(NS_)                                                                                                  \
+    do {                                                                                                           \
+        if (d.mask)                                                                                                \
+            k_attn_dkdv_d64<true, NS_><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv, lddkv, \
+                                                             scale, d.mask_bwd, d.dscale);                         \
+        else                                                                                                       \
+            k_attn_dkdv_d64<false, NS_><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, dout, ldd, lse, delta, dk, dv,      \
+                                                              lddkv, scale, nullptr, 1.f);                         \
+    } while (0)
+#ifdef CG_AB_VARIANTS
+    if (g_attn_variant == 7) {   // A/B: the 2-slot ring one tile ahead
+        DKDV(2);
+        return;
+    }
+#endif
+    DKDV(4);
+#undef DKDV
 }
 }  // namespace attn
 

@@ -83,11 +83,25 @@ __device__ __forceinline__ float adam_one(float p, float g, float& m, float& v, 
     return __fadd_rn(p, __fdiv_rn(__fmul_rn(s.neg_step, m), denom));
 }
 
-template <bool VEC>
-__global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const float* __restrict__ g,
-                                               float* __restrict__ m, float* __restrict__ v, bf16_t* __restrict__ pb,
-                                               int64_t n, double lr, double beta1, double beta2, double eps,
-                                               double wd, const int64_t* __restrict__ step_ptr) {
+typedef float nf4 __attribute__((ext_vector_type(4)));
+typedef unsigned nu2 __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ float4 ld4(const float* p) {
+    if constexpr (NT) {
+        const nf4 x = __builtin_nontemporal_load((const nf4*)p);
+        return make_float4(x[0], x[1], x[2], x[3]);
+    } else {
+        return *(const float4*)p;
+    }
+}
+template <bool NT>
+__device__ __forceinline__ void st4(float* p, float4 x) {
+    if constexpr (NT) __builtin_nontemporal_store(nf4{x.x, x.y, x.z, x.w}, (nf4*)p);
+    else *(float4*)p = x;
+}
+
+__device__ __forceinline__ AdamScalars adam_scalars(double lr, double beta1, double beta2, double eps, double wd,
+                                                    const int64_t* step_ptr) {
     const double t = (double)*step_ptr;
     AdamScalars s;
     s.decay = (float)(1.0 - lr * wd);
@@ -99,18 +113,59 @@ __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const floa
     const double bc2 = 1.0 - pow(beta2, t);
     s.neg_step = (float)(-(lr / bc1));
     s.bc2_sqrt = (float)sqrt(bc2);
+    return s;
+}
+
+// U float4 groups per thread per iteration (all loads issued before any arithmetic); NT: the
+// 30 B/param stream bypasses the caches (non-temporal loads and stores) -- every byte is touched once
+template <bool VEC, bool NT, int U>
+__global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const float* __restrict__ g,
+                                               float* __restrict__ m, float* __restrict__ v, bf16_t* __restrict__ pb,
+                                               int64_t n, double lr, double beta1, double beta2, double eps,
+                                               double wd, const int64_t* __restrict__ step_ptr) {
+    const AdamScalars s = adam_scalars(lr, beta1, beta2, eps, wd, step_ptr);
     const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
-    for (int64_t i = i0; i < n; i += stride) {
+    int64_t i = i0;
+    if (VEC) {
+        for (; i + (U - 1) * stride + 3 < n; i += U * stride) {
+            float4 pv[U], gv[U], mv[U], vv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t j = i + u * stride;
+                pv[u] = ld4<NT>(p + j);
+                gv[u] = ld4<NT>(g + j);
+                mv[u] = ld4<NT>(m + j);
+                vv[u] = ld4<NT>(v + j);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t j = i + u * stride;
+                pv[u].x = adam_one(pv[u].x, gv[u].x, mv[u].x, vv[u].x, s);
+                pv[u].y = adam_one(pv[u].y, gv[u].y, mv[u].y, vv[u].y, s);
+                pv[u].z = adam_one(pv[u].z, gv[u].z, mv[u].z, vv[u].z, s);
+                pv[u].w = adam_one(pv[u].w, gv[u].w, mv[u].w, vv[u].w, s);
+                st4<NT>(p + j, pv[u]);
+                st4<NT>(m + j, mv[u]);
+                st4<NT>(v + j, vv[u]);
+                if (pb) {
+                    const uint2 w = make_uint2(pack_bf2(pv[u].x, pv[u].y), pack_bf2(pv[u].z, pv[u].w));
+                    if constexpr (NT) __builtin_nontemporal_store(nu2{w.x, w.y}, (nu2*)(pb + j));
+                    else *(uint2*)(pb + j) = w;
+                }
+            }
+        }
+    }
+    for (; i < n; i += stride) {
         if (VEC && i + 3 < n) {
-            float4 pv = *(float4*)(p + i), gv = *(const float4*)(g + i), mv = *(float4*)(m + i), vv = *(float4*)(v + i);
+            float4 pv = ld4<NT>(p + i), gv = ld4<NT>(g + i), mv = ld4<NT>(m + i), vv = ld4<NT>(v + i);
             pv.x = adam_one(pv.x, gv.x, mv.x, vv.x, s);
             pv.y = adam_one(pv.y, gv.y, mv.y, vv.y, s);
             pv.z = adam_one(pv.z, gv.z, mv.z, vv.z, s);
             pv.w = adam_one(pv.w, gv.w, mv.w, vv.w, s);
-            *(float4*)(p + i) = pv;
-            *(float4*)(m + i) = mv;
-            *(float4*)(v + i) = vv;
+            st4<NT>(p + i, pv);
+            st4<NT>(m + i, mv);
+            st4<NT>(v + i, vv);
             if (pb) *(uint2*)(pb + i) = make_uint2(pack_bf2(pv.x, pv.y), pack_bf2(pv.z, pv.w));
         } else {
             for (int64_t j = i; j < n && j < i + 4; ++j) {
@@ -125,6 +180,15 @@ __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const floa
     }
 }
 
+namespace cg {
+// cg_set_tuning("adamw_mode"): 0 automatic -- non-temporal loads/stores with two float4 groups per
+// thread in flight once the 30 B/param stream is far past the 256 MB Infinity Cache (n >= 32 M: C4
+// 86 M params, -2.4 % same-box interleaved A/B), plain loads/stores below (C2 10.8 M: the NT form is
+// 16 % slower there, the gradients just written by the backward are still partly cache-resident);
+// 1 plain, 2 NT + 2 groups, 3 plain + 2 groups (A/B: profiles/r3_adamw_ab.txt)
+int g_adamw_mode = 0;
+}
+
 extern "C" int cg_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, double lr,
                         double beta1, double beta2, double eps, double weight_decay, const int64_t* step_ptr,
                         void* stream) {
@@ -136,12 +200,16 @@ extern "C" int cg_adamw(float* p, const float* g, float* m, float* v, uint16_t* 
                      (((uintptr_t)p_bf16) & 7) == 0;
     int grid = ceil_div((n + 3) / 4, 256);
     grid = grid > 8192 ? 8192 : grid;
-    if (vec)
-        k_adamw<true><<<grid, 256, 0, (hipStream_t)stream>>>(p, g, m, v, (bf16_t*)p_bf16, n, lr, beta1, beta2, eps,
-                                                             weight_decay, step_ptr);
-    else
-        k_adamw<false><<<grid, 256, 0, (hipStream_t)stream>>>(p, g, m, v, (bf16_t*)p_bf16, n, lr, beta1, beta2, eps,
-                                                              weight_decay, step_ptr);
+    hipStream_t st = (hipStream_t)stream;
+#define ADAMW(VEC_, NT_, U_)                                                                                \
+    k_adamw<VEC_, NT_, U_><<<grid, 256, 0, st>>>(p, g, m, v, (bf16_t*)p_bf16, n, lr, beta1, beta2, eps, \
+                                                 weight_decay, step_ptr)
+    const int mode = g_adamw_mode ? g_adamw_mode : (n >= (int64_t)1 << 25 ? 2 : 1);
+    if (!vec) ADAMW(false, false, 1);
+    else if (mode == 2) ADAMW(true, true, 2);
+    else if (mode == 3) ADAMW(true, false, 2);
+    else ADAMW(true, false, 1);
+#undef ADAMW
     CG_LAUNCH_CHECK("cg_adamw");
     return CG_OK;
 }

@@ -40,6 +40,13 @@ __device__ __forceinline__ void dma16(const void* g, const void* lds) {
     const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds);
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
 }
+// the same with a wave-uniform base in an SGPR pair and a per-lane 32-bit byte offset (saddr form):
+// one VGPR per lane instead of a 64-bit address, and loop-invariant lane offsets
+__device__ __forceinline__ void dma16s(const void* sbase, uint32_t voff, const void* lds) {
+    const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds);
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(l)
+                 : "memory", "m0");
+}
 #pragma clang diagnostic pop
 }  // namespace cg
 
@@ -73,6 +80,10 @@ __device__ __forceinline__ void gload16(sv8& dst, const void* g) {
 }
 __device__ __forceinline__ void gload4(uint32_t& dst, const void* g) {
     asm volatile("global_load_dword %0, %1, off" : "=v"(dst) : "v"(g) : "memory");
+}
+// saddr forms: wave-uniform base in an SGPR pair + per-lane 32-bit byte offset
+__device__ __forceinline__ void gload4s(uint32_t& dst, const void* sbase, uint32_t voff) {
+    asm volatile("global_load_dword %0, %1, %2" : "=v"(dst) : "v"(voff), "s"(sbase) : "memory");
 }
 typedef float fv4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bfv8 __attribute__((ext_vector_type(8)));

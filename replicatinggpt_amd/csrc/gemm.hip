@@ -417,12 +417,20 @@ static void flush_pending() {
 int g_skip_splitk_reduce = 0;  // measurement knob (WRONG results): time a step without the split-K reduce
 extern int g_attn_variant;  // attention_d64.hip
 extern int g_ln_rpb;  // layernorm.hip
+extern int g_adamw_mode;  // ce_adamw.hip
 extern int g_ln_waves;  // layernorm.hip
 }
 
 extern "C" int cg_set_tuning(const char* key, int value) {
     CG_REQUIRE(key, "cg_set_tuning: null key");
     if (!strcmp(key, "gemm_variant")) {
+        // default build: automatic (0), the register-staged fallback (2), the persistent 128x128 (9)
+        // and 256x256 (24) tiles, the generic kernels (99); the measured-slower A/B tiles only in
+        // libcharpt_hip_ab.so (`make ab`, CG_AB_VARIANTS)
+#ifndef CG_AB_VARIANTS
+        CG_REQUIRE(value == 0 || value == 2 || value == 9 || value == 24 || value == 99,
+                   "cg_set_tuning: gemm_variant %d is an A/B variant, not in this build (make ab)", value);
+#endif
         g_gemm_variant = value;
         return CG_OK;
     }
@@ -445,6 +453,10 @@ extern "C" int cg_set_tuning(const char* key, int value) {
         return CG_OK;
     }
     if (!strcmp(key, "attn_variant")) {
+#ifndef CG_AB_VARIANTS
+        CG_REQUIRE(value >= 0 && value <= 2, "cg_set_tuning: attn_variant %d is an A/B variant, not in this build (make ab)",
+                   value);
+#endif
         g_attn_variant = value;
         return CG_OK;
     }
@@ -458,6 +470,11 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     }
     if (!strcmp(key, "ln_waves")) {   // takes effect for workspaces sized after the call
         g_ln_waves = value;
+        return CG_OK;
+    }
+    if (!strcmp(key, "adamw_mode")) {
+        CG_REQUIRE(value >= 0 && value <= 3, "cg_set_tuning: adamw_mode out of range");
+        g_adamw_mode = value;
         return CG_OK;
     }
     if (!strcmp(key, "ln_rpb")) {   // takes effect for workspaces sized after the call

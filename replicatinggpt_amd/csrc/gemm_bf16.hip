@@ -245,13 +245,17 @@ bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf1
     if (v >= 20) v = 2;
     if (v >= 5 && glds_gemm_launch(v, at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st))
         return true;
+#ifdef CG_AB_VARIANTS
     if ((v == 3 || v == 4) && M % 256) v = 1;
     switch (v) {
-        case 2: launch<128, 128, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st); break;
-        case 3: launch<256, 128, 1>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st); break;
-        case 4: launch<256, 128, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st); break;
-        default: launch<128, 128, 1>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st); break;
+        case 3: launch<256, 128, 1>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st); return true;
+        case 4: launch<256, 128, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st); return true;
+        case 1: launch<128, 128, 1>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st); return true;
+        default: break;
     }
+#endif
+    // the register-staged 128x128 kernel: the fallback when the persistent tile cannot take the call
+    launch<128, 128, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
     return true;
 }
 

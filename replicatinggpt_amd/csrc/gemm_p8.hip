@@ -455,6 +455,9 @@ bool p8_gemm_launch(int v, int at, int bt, int64_t M, int64_t N, int64_t K, cons
                     const bf16_t* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k,
                     float* ws, hipStream_t st) {
     if (K % (FBK * split_k)) return false;
+#ifndef CG_AB_VARIANTS   // the default build has the 256x256 tile only (the others: `make ab`)
+    if (v != 24) return false;
+#endif
     if (v == 20) {
         // largest tile that divides the problem and still yields >= ~3/4 of a block per CU
         const int64_t cus = cu_count8();
@@ -465,6 +468,7 @@ bool p8_gemm_launch(int v, int at, int bt, int64_t M, int64_t N, int64_t K, cons
         else return false;
     }
     switch (v) {
+#ifdef CG_AB_VARIANTS
         case 21:
             if (M % 256 || N % 128) return false;
             return launch8<256, 128, 4, 3>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
@@ -474,12 +478,13 @@ bool p8_gemm_launch(int v, int at, int bt, int64_t M, int64_t N, int64_t K, cons
         case 23:
             if (M % 128 || N % 128) return false;
             return launch8<128, 128, 2, 4>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
-        case 24:
-            if (M % 256 || N % 256) return false;
-            return launch8<256, 256, 2, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
         case 25:
             if (M % 256 || N % 128) return false;
             return launch8<256, 128, 4, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
+#endif
+        case 24:
+            if (M % 256 || N % 256) return false;
+            return launch8<256, 256, 2, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
         default:
             return false;
     }

@@ -679,6 +679,7 @@ bool pk_gemm_launch(int v, int at, int bt, int64_t M, int64_t N, int64_t K, cons
                     float* ws, hipStream_t st) {
     switch (v) {
         case 9: launch_p<128, 128, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st); return true;
+#ifdef CG_AB_VARIANTS   // measured-slower A/B tiles (profiles/r1_gemm_scan*.txt, r2_gemm_ring_depth_scan.txt)
         case 10: launch_p<128, 128, 3>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st); return true;
         case 11:
             if (M % 256) return false;
@@ -702,6 +703,7 @@ bool pk_gemm_launch(int v, int at, int bt, int64_t M, int64_t N, int64_t K, cons
             if (at) return false;
             launch_p<64, 128, 4>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
             return true;
+#endif
         default: return false;
     }
 }

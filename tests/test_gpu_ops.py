@@ -249,9 +249,13 @@ def test_gemm_layouts(at, bt, shape, dt):
 def test_gemm_kernel_variants(variant, max_grid, at, bt, M, N, K):
     """Every bf16 MFMA kernel variant (register-staged 1-4, LDS-DMA 5-8, persistent LDS-DMA 9-12,
     persistent 8-wave LDS-DMA 20-25 -- with the grid capped so that each block walks several tiles)
-    on all four layouts, with split-K and the fused bias+ReLU and bias+dropout+residual epilogues."""
+    on all four layouts, with split-K and the fused bias+ReLU and bias+dropout+residual epilogues.
+    The product library carries 2, 9 and 24; the others only the A/B build (`make ab`,
+    CHARPT_LIB=replicatinggpt_amd/libcharpt_hip_ab.so), where the whole matrix runs."""
     from replicatinggpt_amd import _lib as L
     lib = L.load()
+    if lib.cg_set_tuning(b"gemm_variant", variant) != 0:
+        pytest.skip(f"gemm_variant {variant} is A/B-only (not in this library build)")
     torch.manual_seed(7)
     A = (torch.randn(K, M) if at else torch.randn(M, K)).to(torch.bfloat16)
     B = (torch.randn(K, N) if bt else torch.randn(N, K)).to(torch.bfloat16)
@@ -538,6 +542,39 @@ def test_attention_resident_kernels_match_ring_kernels(T, p):
             dqkv = Fn.attention_bwd(qkv, B, T, H, D, o, dout, lse, scale, p, 21, call, 4, mask)
             torch.cuda.synchronize()
             outs.append((o.cpu(), lse.cpu(), dqkv.cpu()))
+    finally:
+        L.check(lib.cg_set_tuning(b"attn_variant", 0))
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("T", [1024, 576, 320])
+@pytest.mark.parametrize("p", [0.0, 0.2])
+def test_attention_forward_ring_variants_identical(T, p):
+    """T > 256 forward rings: the default LDS-DMA ring (Q fragments in registers, 4 slots, two tiles
+    ahead), attn_variant 6 (Q image in LDS, 3 slots, one tile ahead) and attn_variant 5 (the
+    register-staged ring) run the same per-tile arithmetic: identical o and lse bits (the A/B build
+    runs all three; the product library the default against itself).  T = 576 / 320
+    leave the last 256-query block partly empty (inactive query groups, short rings)."""
+    from replicatinggpt_amd import _lib as L
+    Fn = F()
+    lib = L.load()
+    B, H, D = 2, 3, 64
+    torch.manual_seed(70 + T)
+    d = H * D
+    qkv = (torch.randn(B * T, 3 * d) * 0.7).to(torch.bfloat16).to(DEV)
+    call = torch.tensor([3], dtype=torch.int64, device=DEV)
+    scale = (3.0 * D) ** -0.5
+    outs = []
+    try:
+        for variant in (0, 6, 5):   # 5 / 6: A/B build only (CHARPT_LIB=...libcharpt_hip_ab.so)
+            if lib.cg_set_tuning(b"attn_variant", variant) != 0:
+                continue
+            o = torch.empty(B * T, d, dtype=torch.bfloat16, device=DEV)
+            lse, _ = Fn.attention_fwd(qkv, B, T, H, D, o, scale, p, 21, call, 4)
+            torch.cuda.synchronize()
+            outs.append((o.cpu(), lse.cpu()))
     finally:
         L.check(lib.cg_set_tuning(b"attn_variant", 0))
     for other in outs[1:]:
