@@ -22,11 +22,13 @@ struct DropArgs {
 // canonical Philox stream (same bits as keep_of on element ((b*H + h)*T + q)*T + k) and read by the
 // forward, dQ and dK/dV kernels with one coalesced 32-bit load per lane per 64-row tile, prefetched
 // a tile ahead (a VGPR: no scalar-load latency in the inner loop, one v_bfe_i32 + v_and per use).
-// T % 64 == 0; NB = T/32 blocks of 32, NP = T/64 tiles of 64.  Bit 16 s + r of a lane's word is
-// accumulator register r of 32x32 sub-block s (32x32x16 MFMA layout: column = lane & 31,
-// row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5) =: row(r, l)):
+// T % 64 == 0; NB = T/32 blocks of 32, NP = T/64 tiles of 64.  Accumulator register r of 32x32
+// sub-block s (32x32x16 MFMA layout: column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+// =: row(r, l)) is bit f(s, r) = 8 s + (r >> 1) + 16 (r & 1) of a FWD word -- the two registers the
+// forward packs into one bf16 pair at bits j and j + 16, so one shift + v_perm_b32 makes the pair's
+// mask -- and bit 16 s + r of a BWD word:
 //   FWD (forward, dQ: swapped products, lane = query), tile (qb, kt) for kt <= qb/2:
-//        bit 16 s + r of lane l = keep(q = 32 qb + (l & 31), k = 64 kt + 32 s + row(r, l))
+//        bit f(s, r) of lane l = keep(q = 32 qb + (l & 31), k = 64 kt + 32 s + row(r, l))
 //   BWD (dK/dV: lane = key), tile (kb, qt) for qt >= kb/2:
 //        bit 16 s + r of lane l = keep(q = 64 qt + 32 s + row(r, l), k = 32 kb + (l & 31))
 // Sub-blocks wholly above the diagonal are 0; diagonal sub-blocks are stored whole (the kernels

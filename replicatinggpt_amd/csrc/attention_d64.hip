@@ -39,6 +39,23 @@ __device__ __forceinline__ fv16 mfma32(sv8 a, sv8 b, fv16 c) {
                                                    0);
 }
 
+// Forward row sums on the matrix core.  A 32x32x16 B-operand fragment of P^T (lane l: keys 8 (l>>5) + j,
+// query l & 31) read as the B operand of v_mfma_f32_16x16x32_bf16 (lane l: k' = 8 (l>>4) + j, column
+// l & 15) mixes two queries per column; the A operand below is 1 exactly where the k' group's query
+// half ((k'>>3) & 1 = (l>>4) & 1 of the source lane) equals the output row's ((m>>2) & 1), so output
+// row m, column n sums the 16 keys of query n + 16 ((m>>2) & 1), and lane l's four accumulator
+// registers (rows 4 (l>>4) + i) all hold the running sum of query l & 31.  One 16-cycle MFMA per
+// 16 keys replaces 16 v_add_f32 per lane (the sum is over the bf16-rounded P that O^T also sums).
+typedef float fv4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ fv4 mfma16(sv8 a, sv8 b, fv4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bfv8, a), __builtin_bit_cast(bfv8, b), c, 0, 0,
+                                                   0);
+}
+__device__ __forceinline__ sv8 rowsum_ones(int lane) {
+    const short o = (((lane >> 4) ^ (lane >> 2)) & 1) ? (short)0 : (short)0x3F80;   // bf16 1.0
+    return sv8{o, o, o, o, o, o, o, o};
+}
+
 // [64][64] bf16 image, 128-B rows; 16-B chunk c of row r at r*128 + ((c ^ X(r)) << 4) with
 // X(r) = ((r>>1)&1)<<2 | (r>>2)&3.  Row reads of the 32x32x16 operand (16-lane groups of
 // ds_read_b128 over rows {0-3,12-15,20-27} / {4-11,16-19,28-31}) land on 16 distinct 16-B slots;
@@ -63,6 +80,10 @@ __device__ __forceinline__ sv8 frag_tr(const char* img, int rb, int ks, int cb, 
     const sv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_sv4*)(img + aoff(r0 + 8, chunk) + byte));
     return sv8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
+
+// FWD keep-word bit of accumulator register r of 32-key subtile kt (attention_common.h: the two
+// registers packed into one bf16 pair sit at bits j and j + 16, j = 8 kt + (r >> 1))
+__device__ __forceinline__ constexpr int fwd_bit(int kt, int r) { return 8 * kt + (r >> 1) + 16 * (r & 1); }
 
 // accumulator registers 8s..8s+7 -> bf16 B-operand fragment of k-step s
 __device__ __forceinline__ sv8 pack16(const fv16& x, int s) {
@@ -261,7 +282,7 @@ __device__ __forceinline__ float tile_max(const fv16 (&s)[2]) {
 
 // lazy online-softmax rescale (threshold RESCALE_THR in log2 units): called after the group's
 // previous tiles are all in O and l, before this tile is exponentiated
-__device__ __forceinline__ void rescale_if(float mt, float& m_run, float& l_run, fv16 (&o)[2]) {
+__device__ __forceinline__ void rescale_if(float mt, float& m_run, fv4& l_run, fv16 (&o)[2]) {
     if (__any(mt > m_run + RESCALE_THR)) {   // rare after the first tiles
         const float mn = fmaxf(m_run, mt);
         const float alpha = __builtin_amdgcn_exp2f(m_run - mn);
@@ -272,26 +293,47 @@ __device__ __forceinline__ void rescale_if(float mt, float& m_run, float& l_run,
     }
 }
 
-// P = exp2(S scale_log2 - m) of a full tile: row sums (four partial sums) into l_run, dropout keep
-// bits applied, packed to the bf16 B operands of O^T += V^T P^T
+// low / high 16 bits all-ones where bit j / j + 16 of a FWD keep word is set: v_lshlrev_b32 puts them
+// at bits 15 / 31, v_perm_b32 selectors 8 / 9 replicate those bits over bytes 0-1 / 2-3
+__device__ __forceinline__ uint32_t pair_mask(uint32_t w, int j) {
+    const uint32_t x = w << (15 - j), sel = 0x09090808u;
+    uint32_t m;
+    // (the builtin form made hipcc emit an illegal v_cmp against src_shared_base in the forward ring kernel)
+    asm("v_perm_b32 %0, %1, %1, %2" : "=v"(m) : "v"(x), "s"(sel));
+    return m;
+}
+
+// P = exp2(S scale_log2 - m) of a tile's NSUB subtiles, packed to the bf16 B operands of
+// O^T += V^T P^T; the row sums of the packed (undropped) P go to the matrix core (rowsum_ones), then
+// the dropout keep bits are applied to the packed pairs: the pair j = 8 kt + 4 sk + i of fragment
+// (kt, sk) has its keep bits at j and j + 16 of the FWD word, so w << (15 - j) puts them at bits 15
+// and 31, v_perm_b32 selectors 8 / 9 replicate those into the low / high 16 bits, and one v_and_b32
+// drops the pair's halves -- 3 instructions per pair instead of v_bfe_i32 + v_and_b32 per element
 template <bool DROP, int NSUB = 2>
-__device__ __forceinline__ void softmax_pack(fv16 (&s)[2], float scale_log2, float m_run, float& l_run, uint32_t mw,
-                                             sv8 (&pf)[2][2]) {
+__device__ __forceinline__ void softmax_pack(fv16 (&s)[2], float scale_log2, float m_run, fv4& l_run, uint32_t mw,
+                                             sv8 (&pf)[2][2], const sv8& ones) {
     const float mneg = -m_run;
-    float ls[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kt = 0; kt < NSUB; ++kt) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            // raw v_exp_f32: weights below 2^-126 of the stale max flush to 0
-            const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][r], scale_log2, mneg));
-            ls[r & 3] += p;
-            s[kt][r] = DROP ? keep_and(mw, 16 * kt + r, p) : p;
+        for (int r = 0; r < 16; ++r)   // raw v_exp_f32: weights below 2^-126 of the stale max flush to 0
+            s[kt][r] = __builtin_amdgcn_exp2f(fmaf(s[kt][r], scale_log2, mneg));
+#pragma unroll
+        for (int sk = 0; sk < 2; ++sk) {
+            sv8 u = pack16(s[kt], sk);
+            l_run = mfma16(ones, u, l_run);
+            if (DROP) {
+                const int j = 8 * kt + 4 * sk;
+                uint4 w = __builtin_bit_cast(uint4, u);
+                w.x &= pair_mask(mw, j);
+                w.y &= pair_mask(mw, j + 1);
+                w.z &= pair_mask(mw, j + 2);
+                w.w &= pair_mask(mw, j + 3);
+                u = __builtin_bit_cast(sv8, w);
+            }
+            pf[kt][sk] = u;
         }
-        pf[kt][0] = pack16(s[kt], 0);
-        pf[kt][1] = pack16(s[kt], 1);
     }
-    l_run += (ls[0] + ls[1]) + (ls[2] + ls[3]);
 }
 
 // O^T += V^T P^T over a 64-key tile's NSUB live subtiles (two independent chains, one per 32-dim half)
@@ -312,8 +354,8 @@ __device__ __forceinline__ void pv_tile(fv16 (&o)[2], const char* Vi, const sv8 
 // QREG: the group's Q fragments come from registers (qreg[4]) instead of the Q image.
 template <bool DROP, int NSUB, int DIAG, bool QREG = false>
 __device__ __forceinline__ void fwd_group_tile(const char* Ki, const char* Vi, const char* Qimg, int qr, int lane,
-                                               float scale_log2, float& m_run, float& l_run, fv16 (&o)[2],
-                                               uint32_t mw, const sv8* qreg = nullptr) {
+                                               float scale_log2, float& m_run, fv4& l_run, fv16 (&o)[2],
+                                               uint32_t mw, const sv8& ones, const sv8* qreg = nullptr) {
     fv16 s[2];
     s[0] = fv16{};
     s[1] = fv16{};
@@ -326,7 +368,7 @@ __device__ __forceinline__ void fwd_group_tile(const char* Ki, const char* Vi, c
     if (DIAG >= 0) mask_upper(s[DIAG], lane & 31, 0, lane, -INFINITY);   // key0 = the group's first query
     rescale_if(tile_max<NSUB>(s) * scale_log2, m_run, l_run, o);
     sv8 pf[2][2];
-    softmax_pack<DROP, NSUB>(s, scale_log2, m_run, l_run, mw, pf);
+    softmax_pack<DROP, NSUB>(s, scale_log2, m_run, l_run, mw, pf, ones);
     pv_tile<NSUB>(o, Vi, pf, lane);
 }
 
@@ -384,7 +426,9 @@ __device__ __forceinline__ void fwd_qblock(int qblk, int bh, char* smem, int64_t
     for (int g = 0; g < 2; ++g) oacc[g][0] = oacc[g][1] = fv16{};
     // running max starts at -FLT_MAX, not -inf: a -inf score then exponentiates to 0, never NaN,
     // and the first tile still always moves the max (its decision compares against -FLT_MAX + THR)
-    float m_run[2] = {-FLT_MAX, -FLT_MAX}, l_run[2] = {0.f, 0.f};
+    float m_run[2] = {-FLT_MAX, -FLT_MAX};
+    fv4 l_run[2] = {fv4{}, fv4{}};
+    const sv8 ones = rowsum_ones(lane);
     const int qlast = (Q0 + 255 < T - 1) ? Q0 + 255 : T - 1;
     const int nkv = qlast / 64 + 1;
     const int npipe = act[1] ? (qg[1] + 31) / 64 : 0;   // B's diagonal tile: first unpipelined tile
@@ -431,13 +475,13 @@ __device__ __forceinline__ void fwd_qblock(int qblk, int bh, char* smem, int64_t
         const char* Vp = smem + ps * SLOT + TILE;
         // at kv = 0, B's "previous tile" is sB = -inf against a zeroed V slot: it adds exactly 0
         qk_tile(sA, Ki, Qimg, qr[0], lane);
-        softmax_pack<DROP>(sB, scale_log2, m_run[1], l_run[1], mwBp, pfB);
+        softmax_pack<DROP>(sB, scale_log2, m_run[1], l_run[1], mwBp, pfB, ones);
         pv_tile(oacc[1], Vp, pfB, lane);
         rescale_if(tile_max(sA) * scale_log2, m_run[0], l_run[0], oacc[0]);
         stage_store1(stk, smem + ns * SLOT, tid);
         const Stage1 stv = stage_load1(vb_, ld, (int64_t)nxt * 64, tid);
         qk_tile(sB, Ki, Qimg, qr[1], lane);
-        softmax_pack<DROP>(sA, scale_log2, m_run[0], l_run[0], mw[0], pfA);
+        softmax_pack<DROP>(sA, scale_log2, m_run[0], l_run[0], mw[0], pfA, ones);
         pv_tile(oacc[0], Vi, pfA, lane);
         rescale_if(tile_max(sB) * scale_log2, m_run[1], l_run[1], oacc[1]);
         stage_store1(stv, smem + ns * SLOT + TILE, tid);
@@ -450,7 +494,7 @@ __device__ __forceinline__ void fwd_qblock(int qblk, int bh, char* smem, int64_t
         __syncthreads();
     }
     if (npipe > 0) {   // pipeline tail: B's pending tile npipe - 1 (its V still in the previous slot)
-        softmax_pack<DROP>(sB, scale_log2, m_run[1], l_run[1], mwBp, pfB);
+        softmax_pack<DROP>(sB, scale_log2, m_run[1], l_run[1], mwBp, pfB, ones);
         pv_tile(oacc[1], smem + ps * SLOT + TILE, pfB, lane);
     }
     for (; kv < nkv; ++kv) {
@@ -466,20 +510,18 @@ __device__ __forceinline__ void fwd_qblock(int qblk, int bh, char* smem, int64_t
             // subtile (qg = k0 + 32) or in its first with the second wholly masked (qg = k0)
             const int rel = __builtin_amdgcn_readfirstlane(qg[g] - k0);
             if (rel >= 64)
-                fwd_group_tile<DROP, 2, -1>(Ki, Vi, Qimg, qr[g], lane, scale_log2, m_run[g], l_run[g], oacc[g], mw[g]);
+                fwd_group_tile<DROP, 2, -1>(Ki, Vi, Qimg, qr[g], lane, scale_log2, m_run[g], l_run[g], oacc[g], mw[g], ones);
             else if (rel == 32)
-                fwd_group_tile<DROP, 2, 1>(Ki, Vi, Qimg, qr[g], lane, scale_log2, m_run[g], l_run[g], oacc[g], mw[g]);
+                fwd_group_tile<DROP, 2, 1>(Ki, Vi, Qimg, qr[g], lane, scale_log2, m_run[g], l_run[g], oacc[g], mw[g], ones);
             else
-                fwd_group_tile<DROP, 1, 0>(Ki, Vi, Qimg, qr[g], lane, scale_log2, m_run[g], l_run[g], oacc[g], mw[g]);
+                fwd_group_tile<DROP, 1, 0>(Ki, Vi, Qimg, qr[g], lane, scale_log2, m_run[g], l_run[g], oacc[g], mw[g], ones);
         }
         advance(st, mn);
     }
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
         if (!act[g]) continue;
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run[g]), __float_as_uint(l_run[g]), false,
-                                                         false);
-        const float lt = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+        const float lt = l_run[g][0];   // every accumulator register holds query lane & 31's sum
         const int64_t qa = qg[g] + (lane & 31);
         store_rows(o + (boff + qa) * ldo + hh * 64, oacc[g], dscale / lt, lane);
         if (lane < 32) lse[(int64_t)bh * T_ + qa] = (m_run[g] + __log2f(lt)) * LN2;
@@ -547,7 +589,8 @@ __device__ __forceinline__ void dq_group_tile(const char* Ki, const char* Vi, in
     for (int kt = 0; kt < 2; ++kt) {
         if (k0 + 32 * kt > qg + 31) break;   // subtile fully masked
         const bool diag = __builtin_amdgcn_readfirstlane(k0 + 32 * kt == qg);
-        fv16 s = fv16{}, dp = fv16{};
+        // dP^T starts from -delta' (its column's, lane-uniform), so the chain leaves dP - delta'
+        fv16 s = fv16{}, dp = fv16{} + dl;
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
             s = mfma32(frag_row(Ki, 32 * kt, ks, lane), qf[ks], s);
@@ -557,8 +600,8 @@ __device__ __forceinline__ void dq_group_tile(const char* Ki, const char* Vi, in
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lse2));
-            float d = dp[r] + dl;
-            if (DROP) d = keep_sel2(keep_mask(mw, 16 * kt + r), d, dl);
+            float d = dp[r];
+            if (DROP) d = keep_sel2(keep_mask(mw, fwd_bit(kt, r)), d, dl);
             s[r] = p * d;
         }
         const sv8 d0 = pack16(s, 0), d1 = pack16(s, 1);
@@ -974,7 +1017,9 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64r(int H, const bf16_t* _
     fv16 oacc[2][2];
 #pragma unroll
     for (int g = 0; g < 2; ++g) oacc[g][0] = oacc[g][1] = fv16{};
-    float m_run[2] = {-FLT_MAX, -FLT_MAX}, l_run[2] = {0.f, 0.f};
+    float m_run[2] = {-FLT_MAX, -FLT_MAX};
+    fv4 l_run[2] = {fv4{}, fv4{}};
+    const sv8 ones = rowsum_ones(lane);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         if (t) {   // tile t's DMAs (every wave's) have landed
@@ -996,21 +1041,19 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64r(int H, const bf16_t* _
             const int rel = __builtin_amdgcn_readfirstlane(qg[g] - 64 * t);
             if (rel >= 64)
                 fwd_group_tile<DROP, 2, -1, true>(Ki, Vi, nullptr, 0, lane, scale_log2, m_run[g], l_run[g], oacc[g],
-                                                  mw[g][t], qf[g]);
+                                                  mw[g][t], ones, qf[g]);
             else if (rel == 32)
                 fwd_group_tile<DROP, 2, 1, true>(Ki, Vi, nullptr, 0, lane, scale_log2, m_run[g], l_run[g], oacc[g],
-                                                 mw[g][t], qf[g]);
+                                                 mw[g][t], ones, qf[g]);
             else
                 fwd_group_tile<DROP, 1, 0, true>(Ki, Vi, nullptr, 0, lane, scale_log2, m_run[g], l_run[g], oacc[g],
-                                                 mw[g][t], qf[g]);
+                                                 mw[g][t], ones, qf[g]);
         }
     }
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
         if (!act[g]) continue;
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run[g]), __float_as_uint(l_run[g]), false,
-                                                         false);
-        const float lt = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+        const float lt = l_run[g][0];   // every accumulator register holds query lane & 31's sum
         const int64_t qa = qg[g] + (lane & 31);
         store_rows_wide(o + (boff + qa) * ldo + hh * 64, oacc[g], dscale / lt, lane);
         if (lane < 32) lse[(int64_t)bh * T + qa] = (m_run[g] + __log2f(lt)) * LN2;
@@ -1373,11 +1416,14 @@ __device__ __forceinline__ void dma_lane_offs(int64_t ldx, int wave, int lane, u
         off[i] = (uint32_t)((r * ldx + 8 * c) * 2);
     }
 }
+// img as a 32-bit LDS byte address (lds_base of the kernel's __shared__ array + an integer offset):
+// casting a generic slot pointer back to LDS per call made hipcc emit a null-pointer select -- and,
+// once the forward ring kernel ran out of SGPRs, an illegal v_cmp on src_shared_base for it
 __device__ __forceinline__ void dma_tile_s(const bf16_t* X, int64_t ldx, int64_t row0, const uint32_t (&off)[2],
-                                           char* img, int wave) {
+                                           uint32_t img, int wave) {
     const bf16_t* base = X + row0 * ldx;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) dma16s(base, off[i], img + 1024 * (2 * wave + i));
+    for (int i = 0; i < 2; ++i) dma16sl(base, off[i], img + 1024 * (2 * wave + i));
 }
 
 __device__ __forceinline__ void qk_tile_reg(fv16 (&s)[2], const char* Ki, const sv8 (&qf)[4], int lane) {
@@ -1416,6 +1462,8 @@ __device__ __forceinline__ void fwd_qblock_dma(int qblk, int bh, char* smem, int
     uint32_t doff[2];   // per-lane DMA byte offsets (K, V and Q share ld and the image layout)
     dma_lane_offs(ld, wave, lane, doff);
     auto slot = [&](int t) { return smem + R::slot_of(t) * 2 * TILE; };
+    const uint32_t lds0 = lds_base(smem);
+    auto lslot = [&](int t) { return lds0 + (uint32_t)(R::slot_of(t) * 2 * TILE); };
     // keep words of (group, key tile t) at mrow[g] + 64 t + lane (uniform bases, one lane offset); an
     // inactive group reads block 0's (unused)
     const uint32_t* mrow[2];
@@ -1444,7 +1492,7 @@ __device__ __forceinline__ void fwd_qblock_dma(int qblk, int bh, char* smem, int
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             if (Q0 + 64 * t < T) {
-                dma_tile_s(qb_, ld, Q0 + 64 * t, doff, Qimg + t * TILE, wave);
+                dma_tile_s(qb_, ld, Q0 + 64 * t, doff, lds0 + (uint32_t)(R::NSLOT * 2 * TILE + t * TILE), wave);
             } else {
                 const int r = tid >> 3, c = tid & 7;
                 *(uint4*)(Qimg + t * TILE + aoff(r, c)) = make_uint4(0, 0, 0, 0);
@@ -1455,8 +1503,8 @@ __device__ __forceinline__ void fwd_qblock_dma(int qblk, int bh, char* smem, int
 #pragma unroll
     for (int t = 0; t < AH; ++t) {
         if (t < nkv) {
-            dma_tile_s(kb_, ld, (int64_t)t * 64, doff, slot(t), wave);
-            dma_tile_s(vb_, ld, (int64_t)t * 64, doff, slot(t) + TILE, wave);
+            dma_tile_s(kb_, ld, (int64_t)t * 64, doff, lslot(t), wave);
+            dma_tile_s(vb_, ld, (int64_t)t * 64, doff, lslot(t) + TILE, wave);
         }
     }
     ring_wait<NWAIT>(AH == 2 && nkv > 1);   // the register loads, Q and tile 0 have landed
@@ -1476,7 +1524,9 @@ __device__ __forceinline__ void fwd_qblock_dma(int qblk, int bh, char* smem, int
     fv16 oacc[2][2];
 #pragma unroll
     for (int g = 0; g < 2; ++g) oacc[g][0] = oacc[g][1] = fv16{};
-    float m_run[2] = {-FLT_MAX, -FLT_MAX}, l_run[2] = {0.f, 0.f};
+    float m_run[2] = {-FLT_MAX, -FLT_MAX};
+    fv4 l_run[2] = {fv4{}, fv4{}};
+    const sv8 ones = rowsum_ones(lane);
     fv16 sA[2], sB[2] = {fv16{} - INFINITY, fv16{} - INFINITY};
     sv8 pfA[2][2], pfB[2][2];
     uint32_t mwBp = 0u;   // B's keep word of the previous tile
@@ -1489,19 +1539,19 @@ __device__ __forceinline__ void fwd_qblock_dma(int qblk, int bh, char* smem, int
         }
         const bool pf = kv + AH < nkv;
         if (pf) {
-            dma_tile_s(kb_, ld, (int64_t)(kv + AH) * 64, doff, slot(kv + AH), wave);
-            dma_tile_s(vb_, ld, (int64_t)(kv + AH) * 64, doff, slot(kv + AH) + TILE, wave);
+            dma_tile_s(kb_, ld, (int64_t)(kv + AH) * 64, doff, lslot(kv + AH), wave);
+            dma_tile_s(vb_, ld, (int64_t)(kv + AH) * 64, doff, lslot(kv + AH) + TILE, wave);
         }
         const char* Ki = slot(kv);
         const char* Vi = Ki + TILE;
         const char* Vp = slot(kv - 1) + TILE;
         // at kv = 0, B's "previous tile" is sB = -inf against the zeroed V slot: it adds exactly 0
         qk(sA, Ki, 0);
-        softmax_pack<DROP>(sB, scale_log2, m_run[1], l_run[1], mwBp, pfB);
+        softmax_pack<DROP>(sB, scale_log2, m_run[1], l_run[1], mwBp, pfB, ones);
         pv_tile(oacc[1], Vp, pfB, lane);
         rescale_if(tile_max(sA) * scale_log2, m_run[0], l_run[0], oacc[0]);
         qk(sB, Ki, 1);
-        softmax_pack<DROP>(sA, scale_log2, m_run[0], l_run[0], mw[0], pfA);
+        softmax_pack<DROP>(sA, scale_log2, m_run[0], l_run[0], mw[0], pfA, ones);
         pv_tile(oacc[0], Vi, pfA, lane);
         rescale_if(tile_max(sB) * scale_log2, m_run[1], l_run[1], oacc[1]);
         ring_wait<NWAIT>(pf);
@@ -1511,7 +1561,7 @@ __device__ __forceinline__ void fwd_qblock_dma(int qblk, int bh, char* smem, int
         mw[1] = mn[1];
     }
     if (npipe > 0) {   // pipeline tail: B's pending tile npipe - 1 (its V still in that tile's slot)
-        softmax_pack<DROP>(sB, scale_log2, m_run[1], l_run[1], mwBp, pfB);
+        softmax_pack<DROP>(sB, scale_log2, m_run[1], l_run[1], mwBp, pfB, ones);
         pv_tile(oacc[1], slot(npipe - 1) + TILE, pfB, lane);   // the tail requests kv + AH: another slot
     }
     for (; kv < nkv; ++kv) {
@@ -1524,8 +1574,8 @@ __device__ __forceinline__ void fwd_qblock_dma(int qblk, int bh, char* smem, int
         }
         const bool pf = kv + AH < nkv;
         if (pf) {
-            dma_tile_s(kb_, ld, (int64_t)(kv + AH) * 64, doff, slot(kv + AH), wave);
-            dma_tile_s(vb_, ld, (int64_t)(kv + AH) * 64, doff, slot(kv + AH) + TILE, wave);
+            dma_tile_s(kb_, ld, (int64_t)(kv + AH) * 64, doff, lslot(kv + AH), wave);
+            dma_tile_s(vb_, ld, (int64_t)(kv + AH) * 64, doff, lslot(kv + AH) + TILE, wave);
         }
         const char* Ki = slot(kv);
         const char* Vi = Ki + TILE;
@@ -1537,23 +1587,23 @@ __device__ __forceinline__ void fwd_qblock_dma(int qblk, int bh, char* smem, int
             if constexpr (QR) {
                 if (rel >= 64)
                     fwd_group_tile<DROP, 2, -1, true>(Ki, Vi, nullptr, 0, lane, scale_log2, m_run[g], l_run[g],
-                                                      oacc[g], mw[g], qf[g]);
+                                                      oacc[g], mw[g], ones, qf[g]);
                 else if (rel == 32)
                     fwd_group_tile<DROP, 2, 1, true>(Ki, Vi, nullptr, 0, lane, scale_log2, m_run[g], l_run[g],
-                                                     oacc[g], mw[g], qf[g]);
+                                                     oacc[g], mw[g], ones, qf[g]);
                 else
                     fwd_group_tile<DROP, 1, 0, true>(Ki, Vi, nullptr, 0, lane, scale_log2, m_run[g], l_run[g],
-                                                     oacc[g], mw[g], qf[g]);
+                                                     oacc[g], mw[g], ones, qf[g]);
             } else {
                 if (rel >= 64)
                     fwd_group_tile<DROP, 2, -1>(Ki, Vi, Qimg, qr[g], lane, scale_log2, m_run[g], l_run[g], oacc[g],
-                                                mw[g]);
+                                                mw[g], ones);
                 else if (rel == 32)
                     fwd_group_tile<DROP, 2, 1>(Ki, Vi, Qimg, qr[g], lane, scale_log2, m_run[g], l_run[g], oacc[g],
-                                               mw[g]);
+                                               mw[g], ones);
                 else
                     fwd_group_tile<DROP, 1, 0>(Ki, Vi, Qimg, qr[g], lane, scale_log2, m_run[g], l_run[g], oacc[g],
-                                               mw[g]);
+                                               mw[g], ones);
             }
         }
         ring_wait<NWAIT>(pf);
@@ -1564,9 +1614,7 @@ __device__ __forceinline__ void fwd_qblock_dma(int qblk, int bh, char* smem, int
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
         if (!act[g]) continue;
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run[g]), __float_as_uint(l_run[g]), false,
-                                                         false);
-        const float lt = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+        const float lt = l_run[g][0];   // every accumulator register holds query lane & 31's sum
         const int64_t qa = qg[g] + (lane & 31);
         store_rows_wide(o + (boff + qa) * ldo + hh * 64, oacc[g], dscale / lt, lane);
         if (lane < 32) lse[(int64_t)bh * T_ + qa] = (m_run[g] + __log2f(lt)) * LN2;

@@ -23,26 +23,64 @@ namespace {
 
 
 // Keep bits of the MFMA kernels (attention_common.h: FWD and BWD tiles).  One wave per 64x64
-// (query tile QT, key tile KT <= QT) region, TPW regions per wave: its four 32x32 sub-blocks
-// (qs, ks) give FWD tiles (2 QT + qs, KT) and BWD tiles (2 KT + ks, QT) whole.  Per sub-block, lane l
-// takes query 32 qb + (l & 31) and keys 32 kb + 16 (l >> 5) .. +15 -- two Philox calls, 16 decisions.
-// All of a region's Philox calls are issued first (8 independent chains), then:
-// FWD word: the lane's register keys 4h + {0-3, 8-11, 16-19, 24-27} (h = l >> 5) are nibbles of its
-// own and its lane^32 partner's decisions (v_permlane32_swap); BWD word: bit (key & 15) of the 16
-// query rows the lane's registers hold, read back from ONE wave-private LDS copy of the region's
-// decisions (one wave barrier per region instead of two per sub-block).
+// (query tile QT, key tile KT <= QT) region, DM_TPW regions per wave: its four 32x32 sub-blocks
+// (qs, ks) give FWD tiles (2 QT + qs, KT) and BWD tiles (2 KT + ks, QT) whole.  Per sub-block, lane
+// l = 32 h + i takes query 32 qs + sig(i) -- sig(i) = (i & 3) + 8 ((i >> 2) & 3) + 4 (i >> 4), a lane
+// order chosen for the BWD words below -- and keys 32 ks + 16 h .. +15: two Philox calls, 16
+// decisions, each made by one packed saturating u16 add (or subtract, thr > 2^15) whose top bit is
+// the decision and one packed shift.  A lane gathers its 32 decisions of sub-block row qs into one
+// word R (bit 8 ks + 4 (w >> 1) + 2 c + (w & 1) + 16 e for call c, Philox word w, half e), an order in
+// which
+//   FWD: the lane's own decisions already sit at their FWD bits and its lane^32 partner's sit 4 bits
+//        off: one v_permlane32_swap, one rotate and one v_bfi_b32 make the FWD word (stored at the
+//        lane of query sig(i));
+//   BWD: a 32x32 bit transpose inside each half-wave (five butterfly stages: one lane exchange, one
+//        rotate, one v_bfi_b32 each) gives lane 32 h + j the column j of R over the 32 queries in
+//        sig order, which makes every BWD lane's 16 query bits contiguous: one ds_bpermute and one
+//        v_bfe_u32 per (qs, ks).
+// (The round-2 form spent ~880 of its ~1200 instructions per region on keep8_bits compares, nibble
+// assembly and an LDS transpose; Philox itself -- 19 v_mad_u64_u32 per call -- is what remains.)
 constexpr int DM_TPW = 2;
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+// keep decisions of the two u16 halves of a Philox word as bits 0 and 16: u >= thr <=> the top bit of
+// sat(u + (2^15 - thr)) (thr <= 2^15) or of sat(u - (thr - 2^15)) (thr > 2^15)
+template <bool SUBF>
+__device__ __forceinline__ uint32_t keep2(uint32_t w, us2 k) {
+    const us2 u = __builtin_bit_cast(us2, w);
+    const us2 t = SUBF ? __builtin_elementwise_sub_sat(u, k) : __builtin_elementwise_add_sat(u, k);
+    return __builtin_bit_cast(uint32_t, (us2)(t >> (us2)15));
+}
+
+template <bool SUBF>
 __global__ __launch_bounds__(256) void k_attn_dropmask(int64_t T_, int64_t nbh, uint32_t* __restrict__ mask_f,
                                                        uint32_t* __restrict__ mask_b, DropArgs d) {
-    __shared__ __attribute__((aligned(16))) uint32_t sbits[4][2][64];   // [wave][qs][lane]: ks 0 | ks 1 << 16
     const int NB = (int)(T_ >> 5), NP = NB >> 1;
     const int64_t nreg = (int64_t)NP * (NP + 1) / 2, ntile = mask_tiles(T_);
     const int64_t total = nbh * nreg;
     const int lane = threadIdx.x & 63, h = lane >> 5, lq = lane & 31, w = threadIdx.x >> 6;
-    const int kk = lq, e = kk & 15, hk = kk >> 4;
+    const int qsig = (lq & 3) + 8 * ((lq >> 2) & 3) + 4 * (lq >> 4);
     const uint64_t stream = dropout_stream(d.rng_call, d.site);
+    const uint16_t kc = (uint16_t)(SUBF ? d.thr - 0x8000u : 0x8000u - d.thr);
+    const us2 K = us2{kc, kc};
     const int64_t first = ((int64_t)blockIdx.x * 4 + w) * DM_TPW;
     if (first >= total) return;
+    // butterfly stage j = 16 >> t: lanes with bit j clear keep the low blocks (mask m_j) and take their
+    // partner's low blocks into the high ones (rotate right by 32 - j), the others the reverse
+    uint32_t bmask[5], brot[5];
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+        const int j = 16 >> t;
+        const uint32_t m = t == 0 ? 0x0000FFFFu : t == 1 ? 0x00FF00FFu : t == 2 ? 0x0F0F0F0Fu : t == 3 ? 0x33333333u : 0x55555555u;
+        const bool lo = (lane & j) == 0;
+        bmask[t] = lo ? m : ~m;
+        brot[t] = lo ? (uint32_t)(32 - j) : (uint32_t)j;
+    }
+    // BWD gather source: column j of R (key lq of the sub-block) in half-wave lq >> 4
+    const int kk = lq;
+    const int jcol = 16 * (kk & 1) + 4 * ((kk >> 2) & 1) + 2 * ((kk >> 3) & 1) + ((kk >> 1) & 1);
+    const int src0 = 32 * (kk >> 4) + jcol;   // + 8 ks
+    const uint32_t fmask = h ? 0xF0F0F0F0u : 0x0F0F0F0Fu, frot = h ? 4u : 28u;
     uint64_t bh = (uint64_t)(first / nreg);
     const int r0 = (int)(first - (int64_t)bh * nreg);
     int QT = (int)((sqrtf(8.f * r0 + 1.f) - 1.f) * 0.5f);
@@ -59,58 +97,52 @@ __global__ __launch_bounds__(256) void k_attn_dropmask(int64_t T_, int64_t nbh, 
                 ++bh;
             }
         }
-        const bool diag = QT == KT;   // wave-uniform
-        uint32_t bits[2][2];
+        uint32_t R[2] = {0u, 0u};
+        // Philox group of (query 64 QT + 32 qs + sig, keys 64 KT + 32 ks + 16 h + 8 c ..): g0 + 4 T qs + 4 ks + c
+        const uint64_t g0 = ((bh * (uint64_t)T_ + (uint64_t)(64 * QT + qsig)) * (uint64_t)T_ + (uint64_t)(64 * KT + 16 * h)) >> 3;
 #pragma unroll
         for (int qs = 0; qs < 2; ++qs)
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
-                const uint64_t q = (uint64_t)(2 * QT + qs) * 32 + lq, key0 = (uint64_t)(2 * KT + ks) * 32 + 16 * h;
-                const uint64_t grp = ((bh * T_ + q) * T_ + key0) >> 3;
+                const uint64_t grp = g0 + (uint64_t)(4 * T_ * qs + 4 * ks);
                 // (the sub-block above the diagonal is computed too -- branch-free -- and zeroed below)
-                bits[qs][ks] = keep8_bits(philox_group(d.seed, stream, grp), d.thr) |
-                               (keep8_bits(philox_group(d.seed, stream, grp + 1), d.thr) << 8);
-            }
-        if (diag) bits[0][1] = 0u;   // sub-block wholly above the diagonal: zero bits
-        uint32_t fw[2] = {0u, 0u}, bw[2] = {0u, 0u};
 #pragma unroll
-        for (int qs = 0; qs < 2; ++qs) {
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) {
-                // v_permlane32_swap of a value with itself: [0] = lanes 0-31 own / 32-63 the lower half's,
-                // [1] = lanes 0-31 the upper half's / 32-63 own -- lane l ^ 32's decisions are [h ? 0 : 1]
-                const auto sw = __builtin_amdgcn_permlane32_swap(bits[qs][ks], bits[qs][ks], false, false);
-                const uint32_t part = h ? sw[0] : sw[1];
-                const uint32_t lo = h ? part : bits[qs][ks], hi = h ? bits[qs][ks] : part, sh = 4 * h;
-                const uint32_t f16 = ((lo >> sh) & 0xFu) | (((lo >> (8 + sh)) & 0xFu) << 4) |
-                                     (((hi >> sh) & 0xFu) << 8) | (((hi >> (8 + sh)) & 0xFu) << 12);
-                fw[qs] |= f16 << (16 * ks);
-            }
-            sbits[w][qs][lane] = bits[qs][0] | (bits[qs][1] << 16);   // lane q + 32 h': keys 16 h' .. +15 of query q
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-        for (int qs = 0; qs < 2; ++qs)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {   // query rows 4h + 8j + 0..3 of key kk: source lanes 32 hk + 4h + 8j ..
-                const uint4 v = *(const uint4*)&sbits[w][qs][32 * hk + 4 * h + 8 * j];
-#pragma unroll
-                for (int ks = 0; ks < 2; ++ks) {
-                    const int bit = 16 * ks + e;
-                    const uint32_t nib = ((v.x >> bit) & 1u) | (((v.y >> bit) & 1u) << 1) | (((v.z >> bit) & 1u) << 2) |
-                                         (((v.w >> bit) & 1u) << 3);
-                    bw[ks] |= nib << (16 * qs + 4 * j);
+                for (int c = 0; c < 2; ++c) {
+                    const u32x4 r = philox_group(d.seed, stream, grp + c);
+                    const int b0 = 8 * ks + 2 * c;
+                    R[qs] |= keep2<SUBF>(r.x, K) << b0;
+                    R[qs] |= keep2<SUBF>(r.y, K) << (b0 + 1);
+                    R[qs] |= keep2<SUBF>(r.z, K) << (b0 + 4);
+                    R[qs] |= keep2<SUBF>(r.w, K) << (b0 + 5);
                 }
             }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (QT == KT) R[0] &= 0x00FF00FFu;   // sub-block (0, 1) wholly above the diagonal: zero bits
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-            mask_f[((int64_t)bh * ntile + mask_fwd_tile(2 * QT + s2, KT)) * 64 + lane] = fw[s2];
-            mask_b[((int64_t)bh * ntile + mask_bwd_tile(2 * KT + s2, QT, NP)) * 64 + lane] = bw[s2];
+        for (int qs = 0; qs < 2; ++qs) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(R[qs], R[qs], false, false);
+            const uint32_t part = h ? sw[0] : sw[1];
+            const uint32_t rp = __builtin_amdgcn_alignbit(part, part, frot);
+            mask_f[((int64_t)bh * ntile + mask_fwd_tile(2 * QT + qs, KT)) * 64 + 32 * h + qsig] =
+                (R[qs] & fmask) | (rp & ~fmask);
+        }
+        uint32_t W[2];
+#pragma unroll
+        for (int qs = 0; qs < 2; ++qs) {
+            uint32_t x = R[qs];
+#pragma unroll
+            for (int t = 0; t < 5; ++t) {
+                const uint32_t y = (uint32_t)__shfl_xor((int)x, 16 >> t, 64);
+                const uint32_t ry = __builtin_amdgcn_alignbit(y, y, brot[t]);
+                x = (x & bmask[t]) | (ry & ~bmask[t]);
+            }
+            W[qs] = x;
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const uint32_t a = (uint32_t)__shfl((int)W[0], src0 + 8 * ks, 64);
+            const uint32_t b = (uint32_t)__shfl((int)W[1], src0 + 8 * ks, 64);
+            mask_b[((int64_t)bh * ntile + mask_bwd_tile(2 * KT + ks, QT, NP)) * 64 + lane] =
+                __builtin_amdgcn_ubfe(a, 16 * h, 16) | (__builtin_amdgcn_ubfe(b, 16 * h, 16) << 16);
         }
     }
 }
@@ -558,7 +590,10 @@ void set_masks(DropArgs& d, const uint64_t* mask, int64_t B, int64_t H, int64_t 
 void launch_dropmask(int64_t B, int64_t H, int64_t T, uint64_t* mask, const DropArgs& d, hipStream_t st) {
     const int64_t np = T / 64, regions = B * H * np * (np + 1) / 2;
     uint32_t* m = (uint32_t*)mask;
-    k_attn_dropmask<<<ceil_div(regions, 4 * DM_TPW), 256, 0, st>>>(T, B * H, m, m + B * H * mask_tiles(T) * 64, d);
+    if (d.thr > 0x8000u)
+        k_attn_dropmask<true><<<ceil_div(regions, 4 * DM_TPW), 256, 0, st>>>(T, B * H, m, m + B * H * mask_tiles(T) * 64, d);
+    else
+        k_attn_dropmask<false><<<ceil_div(regions, 4 * DM_TPW), 256, 0, st>>>(T, B * H, m, m + B * H * mask_tiles(T) * 64, d);
 }
 
 bool fast_attn_ok(int dtype, int64_t T, int64_t D, const void* a, const void* b, const void* c, int64_t ld1,

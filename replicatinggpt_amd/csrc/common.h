@@ -47,6 +47,16 @@ __device__ __forceinline__ void dma16s(const void* sbase, uint32_t voff, const v
     asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(l)
                  : "memory", "m0");
 }
+// the same with the LDS destination already a 32-bit LDS byte address (wave-uniform)
+__device__ __forceinline__ void dma16sl(const void* sbase, uint32_t voff, uint32_t lds) {
+    const uint32_t l = __builtin_amdgcn_readfirstlane(lds);
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(l)
+                 : "memory", "m0");
+}
+// LDS byte address of a pointer into a __shared__ array (fold the cast once per kernel)
+__device__ __forceinline__ uint32_t lds_base(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
 #pragma clang diagnostic pop
 }  // namespace cg
 

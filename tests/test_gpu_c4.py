@@ -81,7 +81,9 @@ def test_c4_attention_fwd_bwd_vs_fp64(p):
     # logsumexp (fp32, per (b, h, t)) of the unmasked-row softmax
     s = torch.einsum("bthd,bshd->bhts", q.detach(), k.detach()) * scale
     s = s.masked_fill(~torch.tril(torch.ones(T4, T4, dtype=torch.bool)), float("-inf"))
-    assert relerr(lse, torch.logsumexp(s, -1)) < 1e-4
+    # the bf16 kernels' row sums run on the matrix core over the bf16-rounded weights O is built from
+    # (each within 2^-8 relative), so |lse - ref| <= ln(1 + 2^-8) < 2^-8 per row
+    assert float((lse.double().cpu() - torch.logsumexp(s, -1).double().cpu()).abs().max()) < 2.0 ** -8
 
 
 def _decode_keep_bits(mask, BH, T):
@@ -96,28 +98,30 @@ def _decode_keep_bits(mask, BH, T):
     col = np.broadcast_to(lanes[None, :] & 31, (16, 64))
     out = np.zeros((2, BH, T, T), dtype=bool)
 
-    def bits(w, s):   # [BH, 64] words -> [BH, 16, 64] bits 16 s + r
-        sh = (16 * s + r).astype(np.uint32)
+    def bits(w, s, fwd):   # [BH, 64] words -> [BH, 16, 64]: FWD bit 8 s + (r >> 1) + 16 (r & 1), BWD 16 s + r
+        sh = ((8 * s + (r >> 1) + 16 * (r & 1)) if fwd else (16 * s + r)).astype(np.uint32)
         return ((w[:, None, :] >> sh[None, :, None]) & np.uint32(1)).astype(bool)
 
     for qb in range(NB):
         for kt in range(qb // 2 + 1):
             t = qb + (qb - 1) ** 2 // 4 + kt if qb else kt
             for s in range(2):
-                out[0][:, 32 * qb + col, 64 * kt + 32 * s + accrow] = bits(words[0, :, t], s)
+                out[0][:, 32 * qb + col, 64 * kt + 32 * s + accrow] = bits(words[0, :, t], s, True)
     for kb in range(NB):
         for qt in range(kb // 2, NP):
             t = kb * NP - ((kb - 1) ** 2 // 4 if kb else 0) + qt - kb // 2
             for s in range(2):
-                out[1][:, 64 * qt + 32 * s + accrow, 32 * kb + col] = bits(words[1, :, t], s)
+                out[1][:, 64 * qt + 32 * s + accrow, 32 * kb + col] = bits(words[1, :, t], s, False)
     return out
 
 
-def test_c4_dropmask_bits_match_oracle():
+@pytest.mark.parametrize("p", [0.2, 0.6])
+def test_c4_dropmask_bits_match_oracle(p):
     """cg_attn_dropmask at T=1024 (272 FWD and 272 BWD 64-row tiles per (b, h)): every keep bit of the
-    MFMA kernels' layouts equals the oracle's keep(((b H + h) T + q) T + key)."""
+    MFMA kernels' layouts equals the oracle's keep(((b H + h) T + q) T + key).  p = 0.6 takes the
+    kernel's other decision form (threshold above 2^15: saturating subtract)."""
     from replicatinggpt_amd import ops
-    B, H, T, p, seed, site = 1, 2, T4, 0.2, 0x5EED, 6
+    B, H, T, seed, site = 1, 2, T4, 0x5EED, 6
     call = torch.tensor([11], dtype=torch.int64, device=DEV)
     n = ops.attn_mask_bytes(B, H, T) // 8
     mask = torch.zeros(n, dtype=torch.int64, device=DEV)
@@ -131,7 +135,7 @@ def test_c4_dropmask_bits_match_oracle():
     assert np.array_equal(got[0], keep & tri)
     assert np.array_equal(got[1], keep & tri)
     # the measured keep rate of the 16-bit decision (p = 0.2 -> 13107 / 65536 dropped)
-    assert abs(float(keep.mean()) - (1 - 13107 / 65536)) < 2e-3
+    assert abs(float(keep.mean()) - (1 - round(p * 65536) / 65536)) < 2e-3
 
 
 def _c4_gemm_cases():

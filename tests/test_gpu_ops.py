@@ -4,6 +4,8 @@ reference (and the numpy Philox oracle for dropout masks).  Tolerances: fp32 pat
 import math
 
 import numpy as np
+import os
+
 import pytest
 
 import torch
@@ -240,10 +242,15 @@ def test_gemm_layouts(at, bt, shape, dt):
     assert relerr(out, ref) < 1e-5
 
 
-@pytest.mark.parametrize("variant,max_grid", [(1, 0), (2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (7, 0), (8, 0), (9, 0),
-                                              (9, 5), (10, 0), (10, 7), (11, 0), (11, 3), (12, 0),
-                                              (20, 0), (21, 0), (21, 3), (22, 0), (22, 5), (23, 0), (23, 7),
-                                              (24, 0), (24, 1), (25, 0), (25, 2)])
+# the product library's variants; the whole matrix when the A/B build is loaded (CHARPT_LIB=...ab.so)
+_GEMM_VARIANTS = ([(1, 0), (2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (7, 0), (8, 0), (9, 0),
+                   (9, 5), (10, 0), (10, 7), (11, 0), (11, 3), (12, 0),
+                   (20, 0), (21, 0), (21, 3), (22, 0), (22, 5), (23, 0), (23, 7),
+                   (24, 0), (24, 1), (25, 0), (25, 2)]
+                  if "_ab" in os.environ.get("CHARPT_LIB", "") else [(2, 0), (9, 0), (9, 5), (24, 0), (24, 1)])
+
+
+@pytest.mark.parametrize("variant,max_grid", _GEMM_VARIANTS)
 @pytest.mark.parametrize("at,bt", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(512, 384, 768), (512, 512, 640)])
 def test_gemm_kernel_variants(variant, max_grid, at, bt, M, N, K):
@@ -485,7 +492,9 @@ def test_attention_fast_matches_generic_bf16():
     lse = torch.empty(B, H, T, dtype=torch.float32, device=DEV)
     ops().attn_fwd(view, B, T, H, D, 0, d, 2 * d, view.stride(0), o_gen, d, lse, 0.05, 0.2, 3, call, 1, None)
     assert relerr(o_fast, o_gen) < 2e-2
-    assert relerr(lse_fast[0], lse) < 1e-4
+    # the bf16 kernels' row sums run on the matrix core over the bf16-rounded weights O is built from
+    # (each within 2^-8 relative), so |lse - ref| <= ln(1 + 2^-8) < 2^-8 per row
+    assert float((lse_fast[0].double().cpu() - lse.double().cpu()).abs().max()) < 2.0 ** -8
 
 
 @pytest.mark.parametrize("T", [64, 128, 192, 320, 512])
@@ -606,7 +615,9 @@ def test_attention_forward_rescale_branch():
     assert relerr(o, ref.reshape(B * T, d)) < 2e-2
     s = torch.einsum("bthd,bshd->bhts", q, k) * scale
     s = s.masked_fill(~torch.tril(torch.ones(T, T, dtype=torch.bool)), float("-inf"))
-    assert relerr(lse, torch.logsumexp(s, -1)) < 1e-4
+    # the bf16 kernels' row sums run on the matrix core over the bf16-rounded weights O is built from
+    # (each within 2^-8 relative), so |lse - ref| <= ln(1 + 2^-8) < 2^-8 per row
+    assert float((lse.double().cpu() - torch.logsumexp(s, -1).double().cpu()).abs().max()) < 2.0 ** -8
 
 
 def test_attention_bwd_regenerates_mask():
