@@ -200,11 +200,14 @@ __device__ __forceinline__ void store_rows(bf16_t* row, const fv16 (&acc)[2], fl
 // LDS-DMA (global_load_lds_dwordx4, common.h dma16) of one [64][64] bf16 tile -- rows row0..row0+63 of a row-major
 // matrix -- into an aoff-swizzled image: 8 wave-instructions of 1 KB, two per wave.  LDS slot s of
 // image row r holds global chunk s ^ X(r), so each lane fetches that chunk.
-__device__ __forceinline__ void dma_tile(const bf16_t* X, int64_t ldx, int64_t row0, char* img, int wave, int lane) {
+// img: 32-bit LDS byte address (lds_base of the __shared__ array + an offset), wave wave-uniform; the
+// source as a wave-uniform base + per-lane byte offset (saddr form, common.h dma16sl)
+__device__ __forceinline__ void dma_tile(const bf16_t* X, int64_t ldx, int64_t row0, uint32_t img, int wave, int lane) {
+    const bf16_t* base = X + row0 * ldx;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int ins = 2 * wave + i, r = 8 * ins + (lane >> 3), c = (lane & 7) ^ ((((r >> 1) & 1) << 2) | ((r >> 2) & 3));
-        dma16(X + (row0 + r) * ldx + 8 * c, img + 1024 * ins);
+        dma16sl(base, (uint32_t)((r * ldx + 8 * c) * 2), img + 1024u * ins);
     }
 }
 
@@ -656,11 +659,13 @@ __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t 
     // kv + AH - NS (read before an earlier barrier); NS = 4: two tiles of compute to land
     constexpr int AH = NS / 2;
     auto slot = [&](int t) { return smem + (t & (NS - 1)) * 2 * TILE; };
+    const uint32_t l0 = lds_base(smem);
+    auto lslot = [&](int t) { return l0 + (uint32_t)((t & (NS - 1)) * 2 * TILE); };
 #pragma unroll
     for (int t = 0; t < AH; ++t) {
         if (t < nkv) {
-            dma_tile(kb_, ld, (int64_t)t * 64, slot(t), wave_, lane);
-            dma_tile(vb_, ld, (int64_t)t * 64, slot(t) + TILE, wave_, lane);
+            dma_tile(kb_, ld, (int64_t)t * 64, lslot(t), wave_, lane);
+            dma_tile(vb_, ld, (int64_t)t * 64, lslot(t) + TILE, wave_, lane);
         }
     }
     ring_wait<AH == 2 ? 4 : 0>(AH == 2 && nkv > 1);   // operands and tile 0 have landed
@@ -682,8 +687,8 @@ __device__ __forceinline__ void dq_qblock(int qblk, int bh, char* smem, int64_t 
         }
         const bool pf = kv + AH < nkv;
         if (pf) {
-            dma_tile(kb_, ld, (int64_t)(kv + AH) * 64, slot(kv + AH), wave_, lane);
-            dma_tile(vb_, ld, (int64_t)(kv + AH) * 64, slot(kv + AH) + TILE, wave_, lane);
+            dma_tile(kb_, ld, (int64_t)(kv + AH) * 64, lslot(kv + AH), wave_, lane);
+            dma_tile(vb_, ld, (int64_t)(kv + AH) * 64, lslot(kv + AH) + TILE, wave_, lane);
         }
         const char* Ki = slot(kv);
         const int k0 = kv * 64;
@@ -843,14 +848,16 @@ __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_
     // compute to land.  A slot's statistics are written from hidden loads issued with its DMA.
     constexpr int AH = NS / 2;
     auto slot = [&](int it_) { return smem + (it_ & (NS - 1)) * KV_STAGE; };
+    const uint32_t l0 = lds_base(smem);
+    auto lslot = [&](int it_) { return l0 + (uint32_t)((it_ & (NS - 1)) * KV_STAGE); };
     {
         const float s0 = stat_load(qt0);
         const float s1 = (AH == 2 && qt0 + 1 < nq) ? stat_load(qt0 + 1) : 0.f;
 #pragma unroll
         for (int t = 0; t < AH; ++t) {
             if (qt0 + t < nq) {
-                dma_tile(qb_, ld, (int64_t)(qt0 + t) * 64, slot(t), wave_, lane);
-                dma_tile(ob_, ldd, (int64_t)(qt0 + t) * 64, slot(t) + TILE, wave_, lane);
+                dma_tile(qb_, ld, (int64_t)(qt0 + t) * 64, lslot(t), wave_, lane);
+                dma_tile(ob_, ldd, (int64_t)(qt0 + t) * 64, lslot(t) + TILE, wave_, lane);
                 if (tid < 128) ((float*)(slot(t) + 2 * TILE))[tid] = t ? s1 : s0;
             }
         }
@@ -873,8 +880,8 @@ __device__ __forceinline__ void dkdv_kblock(int kblk, int bh, char* smem, int64_
         }
         if (DROP && act && nxt >= qtm) gload4(mn, mcol + (nxt - qtm) * 64);
         if (pf) {
-            dma_tile(qb_, ld, (int64_t)(qt + AH) * 64, slot(it + AH), wave_, lane);
-            dma_tile(ob_, ldd, (int64_t)(qt + AH) * 64, slot(it + AH) + TILE, wave_, lane);
+            dma_tile(qb_, ld, (int64_t)(qt + AH) * 64, lslot(it + AH), wave_, lane);
+            dma_tile(ob_, ldd, (int64_t)(qt + AH) * 64, lslot(it + AH) + TILE, wave_, lane);
         }
         const char* S0 = slot(it);
         const char* Qi = S0;
@@ -993,8 +1000,8 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64r(int H, const bf16_t* _
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-        dma_tile(k + boff * ld + hh * 64, ld, 64 * t, smem + 2 * t * TILE, wave, lane);
-        dma_tile(v + boff * ld + hh * 64, ld, 64 * t, smem + (2 * t + 1) * TILE, wave, lane);
+        dma_tile(k + boff * ld + hh * 64, ld, 64 * t, lds_base(smem) + 2u * t * TILE, wave, lane);
+        dma_tile(v + boff * ld + hh * 64, ld, 64 * t, lds_base(smem) + (2u * t + 1) * TILE, wave, lane);
     }
     // the register loads and tile 0 have landed (4 DMA instructions per tile per wave stay younger)
     if constexpr (!DROP) {
@@ -1119,8 +1126,8 @@ __device__ __forceinline__ void dq_res(int bh, char* smem, int H, const bf16_t* 
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-        dma_tile(k + boff * ld + hh * 64, ld, 64 * t, smem + 2 * t * TILE, wave, lane);
-        dma_tile(v + boff * ld + hh * 64, ld, 64 * t, smem + (2 * t + 1) * TILE, wave, lane);
+        dma_tile(k + boff * ld + hh * 64, ld, 64 * t, lds_base(smem) + 2u * t * TILE, wave, lane);
+        dma_tile(v + boff * ld + hh * 64, ld, 64 * t, lds_base(smem) + (2u * t + 1) * TILE, wave, lane);
     }
     if constexpr (!DROP) {
 #pragma unroll
@@ -1258,8 +1265,8 @@ __device__ __forceinline__ void dkdv_res(int bh, char* smem, int H, const bf16_t
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-        dma_tile(q + boff * ld + hh * 64, ld, 64 * t, smem + 2 * t * TILE, wave, lane);
-        dma_tile(dout + boff * ldd + hh * 64, ldd, 64 * t, smem + (2 * t + 1) * TILE, wave, lane);
+        dma_tile(q + boff * ld + hh * 64, ld, 64 * t, lds_base(smem) + 2u * t * TILE, wave, lane);
+        dma_tile(dout + boff * ldd + hh * 64, ldd, 64 * t, lds_base(smem) + (2u * t + 1) * TILE, wave, lane);
     }
     // the second key group's K / V fragments behind the tiles (in flight until that group starts)
     sv8 kf1[4], vf1[4];

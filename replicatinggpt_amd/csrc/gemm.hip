@@ -419,6 +419,7 @@ extern int g_attn_variant;  // attention_d64.hip
 extern int g_ln_rpb;  // layernorm.hip
 extern int g_adamw_mode;  // ce_adamw.hip
 extern int g_ln_waves;  // layernorm.hip
+extern int g_ln_pf;     // layernorm.hip
 }
 
 extern "C" int cg_set_tuning(const char* key, int value) {
@@ -475,6 +476,10 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     if (!strcmp(key, "adamw_mode")) {
         CG_REQUIRE(value >= 0 && value <= 3, "cg_set_tuning: adamw_mode out of range");
         g_adamw_mode = value;
+        return CG_OK;
+    }
+    if (!strcmp(key, "ln_pf")) {
+        g_ln_pf = value;
         return CG_OK;
     }
     if (!strcmp(key, "ln_rpb")) {   // takes effect for workspaces sized after the call

@@ -39,7 +39,7 @@ struct Dma8 {
     static constexpr int PER_WAVE = INSTR / P8_WAVES;
     static_assert(PER_WAVE * P8_WAVES == INSTR, "tile/wave mismatch");
     static_assert(!TR || R >= 128, "transposed image swizzle needs >= 16 chunks per row");
-    int off[PER_WAVE];
+    uint32_t off[PER_WAVE];   // byte offsets (saddr form, gemm_pk.hip DmaP)
     int64_t kstep;
 
     __device__ __forceinline__ void init(int64_t ld, int wave, int lane) {
@@ -48,19 +48,18 @@ struct Dma8 {
             const int pos = (wave * PER_WAVE + i) * 1024 + lane * 16;
             if (!TR) {
                 const int r = pos >> 7, c = ((pos >> 4) & 7) ^ row_swz(r);
-                off[i] = (int)(r * ld) + c * 8;
+                off[i] = 2u * (uint32_t)((int)(r * ld) + c * 8);
             } else {
                 const int k = pos / (2 * R), c = ((pos % (2 * R)) >> 4) ^ col_swz(k);
-                off[i] = (int)(k * ld) + c * 8;
+                off[i] = 2u * (uint32_t)((int)(k * ld) + c * 8);
             }
         }
         kstep = TR ? (int64_t)FBK * ld : (int64_t)FBK;
     }
-    __device__ __forceinline__ void issue(const bf16_t* origin, int kt, char* img, int wave) const {
+    __device__ __forceinline__ void issue(const bf16_t* origin, int kt, uint32_t img, int wave) const {
         const bf16_t* base = origin + kt * kstep;
 #pragma unroll
-        for (int i = 0; i < PER_WAVE; ++i)
-            dma16(base + off[i], img + (wave * PER_WAVE + i) * 1024);
+        for (int i = 0; i < PER_WAVE; ++i) dma16sl(base, off[i], img + (uint32_t)((wave * PER_WAVE + i) * 1024));
     }
 };
 
@@ -98,7 +97,7 @@ void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     constexpr int EPI_OPS = (EP == P8_GENERIC || FN != 4) ? FM * FN : FM * 2;
     static_assert(NBUF >= 2 && NBUF <= 4, "ring depth");
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave % WN;
     const int tilesN = (int)(N / BN);
     const int ntiles = (int)(M / BM) * tilesN;
@@ -137,7 +136,7 @@ void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
             oa = AT ? A + kb * lda + m0 : A + m0 * lda + kb;
             ob = BT ? B + kb * ldb + n0 : B + n0 * ldb + kb;
         }
-        char* img = smem + buf * G::STAGE;
+        const uint32_t img = lds_base(smem) + (uint32_t)(buf * G::STAGE);
         da.issue(oa, ikt, img, wave);
         db.issue(ob, ikt, img + G::IMG_A, wave);
         if (++ikt == nk) {

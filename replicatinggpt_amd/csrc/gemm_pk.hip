@@ -53,7 +53,7 @@ struct DmaP {
     static constexpr int PER_WAVE = INSTR / WAVES;
     static_assert(PER_WAVE * WAVES == INSTR, "tile/wave mismatch");
     static_assert(!TR || R >= 128, "transposed image swizzle needs >= 16 chunks per row");
-    int off[PER_WAVE];  // element offset of this lane's 16-B chunk from the tile origin
+    uint32_t off[PER_WAVE];  // byte offset of this lane's 16-B chunk from the tile origin
     int64_t kstep;
 
     __device__ __forceinline__ void init(int64_t ld, int wave, int lane) {
@@ -63,23 +63,21 @@ struct DmaP {
             if (!TR) {
                 const int r = BK == 64 ? pos >> 7 : pos >> 6;
                 const int c = BK == 64 ? ((pos >> 4) & 7) ^ row_swz(r) : ((pos >> 4) & 3) ^ row_swz32(r);
-                off[i] = (int)(r * ld) + c * 8;
+                off[i] = 2u * (uint32_t)((int)(r * ld) + c * 8);
             } else {
                 const int k = pos / (2 * R), c = ((pos % (2 * R)) >> 4) ^ col_swz(k);
-                off[i] = (int)(k * ld) + c * 8;
+                off[i] = 2u * (uint32_t)((int)(k * ld) + c * 8);
             }
         }
         kstep = TR ? (int64_t)BK * ld : (int64_t)BK;
     }
-    // instruction i (0..PER_WAVE-1) of one K-tile, from that K-tile's base address
-    __device__ __forceinline__ void issue1(const bf16_t* base, int i, char* img, int wave) const {
-        dma16(base + off[i], img + (wave * PER_WAVE + i) * 1024);
-    }
-    __device__ __forceinline__ void issue(const bf16_t* origin, int kt, char* img, int wave) const {
-        const bf16_t* base = origin + kt * kstep;
-#pragma unroll
-        for (int i = 0; i < PER_WAVE; ++i)
-            dma16(base + off[i], img + (wave * PER_WAVE + i) * 1024);
+    // instruction i (0..PER_WAVE-1) of one K-tile, from that K-tile's (wave-uniform) base address into
+    // the image at 32-bit LDS address img: the saddr form (SGPR base + per-lane byte offset) and an
+    // SGPR LDS address.  With a generic image pointer and a 64-bit lane address hipcc spent ~6
+    // instructions per DMA (two 64-bit VALU adds, two v_readfirstlane, a null-pointer select) on a
+    // VALU -> SGPR -> m0 dependency chain.
+    __device__ __forceinline__ void issue1(const bf16_t* base, int i, uint32_t img, int wave) const {
+        dma16sl(base, off[i], img + (uint32_t)((wave * PER_WAVE + i) * 1024));
     }
 };
 
@@ -352,7 +350,7 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     using DB = DmaP<BT, BN, G::WAVES, BK>;
     constexpr int LPT = DA::PER_WAVE + DB::PER_WAVE;  // DMA instructions per thread per K-tile
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / G::WN, wn = wave % G::WN;
     const int tilesN = (int)(N / BN);
     const int ntiles = (int)(M / BM) * tilesN;
@@ -368,6 +366,7 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
 
     DA da;
     DB db;
+    const uint32_t lds0 = lds_base(smem);
     da.init(lda, wave, lane);
     db.init(ldb, wave, lane);
 
@@ -429,7 +428,7 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     for (int s = 0; s < NBUF - 1; ++s)
         if (s < total) {
             prep_next(true);
-            char* img = smem + s * G::STAGE;
+            const uint32_t img = lds0 + (uint32_t)(s * G::STAGE);
 #pragma unroll
             for (int i = 0; i < DA::PER_WAVE; ++i) da.issue1(na, i, img, wave);
 #pragma unroll
@@ -489,7 +488,7 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         int nb = cur + NBUF - 1;
         if (nb >= NBUF) nb -= NBUF;
         prep_next(g + NBUF - 1 < total);
-        char* dimg = smem + nb * G::STAGE;
+        const uint32_t dimg = lds0 + (uint32_t)(nb * G::STAGE);
         const char* imgA = smem + cur * G::STAGE;
         const char* imgB = imgA + G::IMG_A;
         // both 32-deep halves' fragments are read before the first MFMA (sched_barrier pins it):

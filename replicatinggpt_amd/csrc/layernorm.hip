@@ -3,6 +3,8 @@
 // floats at e = (j*64 + lane)*VEC.  Specialised shapes: C = 384 (VEC 2, NJ 3), 768 (4, 3),
 // 512 (4, 2), 1024 (4, 4), even C <= 128 (2, 1; forward); any other C <= 2048 uses (1, 32) with
 // bounds checks.
+#include <type_traits>
+
 #include "common.h"
 
 using namespace cg;
@@ -62,7 +64,7 @@ __device__ __forceinline__ void ld_vec_any<bf16_t>(const bf16_t* p, float* v, in
 // One wave per row, RPW rows per wave: every load of the wave's rows is issued before the first
 // reduction, and gamma/beta are held in registers for all of them (they were re-read after each
 // row's reductions, on the critical path).
-template <int VEC, int NJ, typename TY, int RPW>
+template <int VEC, int NJ, typename TY, int RPW, bool FULL = false>
 __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ x, const float* __restrict__ w,
                                                 const float* __restrict__ b, TY* __restrict__ y,
                                                 float* __restrict__ mean_out, float* __restrict__ rstd_out,
@@ -74,7 +76,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ x, con
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
         const int e = (j * 64 + lane) * VEC;
-        if (e < C) {
+        if (FULL || e < C) {
             VecIO<VEC>::ld(w + e, wv[j]);
             VecIO<VEC>::ld(b + e, bv[j]);
         }
@@ -88,7 +90,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ x, con
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 const int e = (j * 64 + lane) * VEC;
-                if (e < C) {
+                if (FULL || e < C) {
                     VecIO<VEC>::ld(x + r * C + e, v[i][j]);
                 } else {
 #pragma unroll
@@ -110,7 +112,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ x, con
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 const int e = (j * 64 + lane) * VEC;
-                if (e < C) {
+                if (FULL || e < C) {
 #pragma unroll
                     for (int q = 0; q < VEC; ++q) {
                         const float d = v[i][j][q] - mu;
@@ -124,7 +126,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ x, con
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 const int e = (j * 64 + lane) * VEC;
-                if (e < C) {
+                if (FULL || e < C) {
                     float o[VEC];
 #pragma unroll
                     for (int q = 0; q < VEC; ++q) o[q] = (v[i][j][q] - mu) * rs * wv[j][q] + bv[j][q];
@@ -145,6 +147,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ x, con
 namespace cg {
 int g_ln_rpb = 0;     // cg_set_tuning("ln_rpb"): rows per backward block (0 = automatic)
 int g_ln_waves = 0;   // cg_set_tuning("ln_waves"): waves per backward block, 4 or 8 (0 = automatic)
+int g_ln_pf = 0;      // cg_set_tuning("ln_pf"): 1 = next row's loads before the current row (FULL shapes)
 }  // namespace cg
 // Waves per backward block: 8, or 4 where the row kernel's registers cap a SIMD at 3 waves (the
 // VEC 4 variants, C = 512..1024: 166 VGPRs at C = 768) -- 8-wave blocks then fit once per CU (8 of
@@ -192,7 +195,7 @@ struct LnRow {
 // column sums), summed over the 8 waves in a fixed order.  Measured (tools/ln_bench.py): issuing
 // the next row's loads before reducing the current one (double-buffered rows) gained nothing at
 // C4 and lost 15-25 % at C2 (occupancy); ~4.8 TB/s at C4, 5.2 TB/s at C2 without dropout.
-template <int VEC, int NJ, typename TDY, int WAVES>
+template <int VEC, int NJ, typename TDY, int WAVES, bool FULL = false, bool PF = false>
 __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ dy, const float* __restrict__ x,
                                                            const float* __restrict__ w, const float* __restrict__ mean,
                                                            const float* __restrict__ rstd,
@@ -212,22 +215,23 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
         const int e = (j * 64 + lane) * VEC;
 #pragma unroll
         for (int q = 0; q < VEC; ++q) adw[j][q] = adb[j][q] = acs[j][q] = 0.f;
-        if (e < C) VecIO<VEC>::ld(w + e, wv[j]);
+        if (FULL || e < C) VecIO<VEC>::ld(w + e, wv[j]);
         else {
 #pragma unroll
             for (int q = 0; q < VEC; ++q) wv[j][q] = 0.f;
         }
     }
-    auto load = [&](int64_t r, LnRow<VEC, NJ>& b) {
+    auto load = [&](int64_t r, LnRow<VEC, NJ>& b, auto hr) {
+        constexpr bool HR = decltype(hr)::value;
         b.mu = mean[r];
         b.rs = rstd[r];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int e = (j * 64 + lane) * VEC;
-            if (e < C) {
+            if (FULL || e < C) {
                 VecIO<VEC>::ld(x + r * C + e, b.x[j]);
                 ld_vec_any<TDY>(dy + r * C + e, b.d[j], VEC);
-                if (dres) VecIO<VEC>::ld(dres + r * C + e, b.rv[j]);
+                if (HR) VecIO<VEC>::ld(dres + r * C + e, b.rv[j]);
             }
         }
     };
@@ -237,7 +241,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
     // element e = (64 j + lane) VEC is (j VEC) >> 3 for every lane (no carry: 8 VEC <= 64).
     constexpr int NCALL = (NJ * VEC + 7) / 8;
     const bool row_groups = (C & 7) == 0;
-    auto process = [&](int64_t r, const LnRow<VEC, NJ>& b) {
+    auto process = [&](int64_t r, const LnRow<VEC, NJ>& b, auto hr) {
+        constexpr bool HR = decltype(hr)::value;
         uint32_t kbyte[NJ];   // keep bits of the 8-group holding this lane's element e, per j
         if (lp.out && lp.thr && row_groups) {
             uint32_t kb[NCALL];
@@ -256,7 +261,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int e = (j * 64 + lane) * VEC;
-            if (e < C) {
+            if (FULL || e < C) {
 #pragma unroll
                 for (int q = 0; q < VEC; ++q) {
                     xh[j][q] = (b.x[j][q] - b.mu) * b.rs;
@@ -273,12 +278,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int e = (j * 64 + lane) * VEC;
-            if (e < C) {
+            if (FULL || e < C) {
                 float o[VEC];
 #pragma unroll
                 for (int q = 0; q < VEC; ++q) {
                     o[q] = b.rs * (g[j][q] - c1 - xh[j][q] * c2);
-                    if (dres) o[q] += b.rv[j][q];
+                    if (HR) o[q] += b.rv[j][q];
                 }
                 VecIO<VEC>::st(dx + r * C + e, o);
                 if (lp.out) {
@@ -308,19 +313,41 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
     };
     const int64_t r0 = (int64_t)blockIdx.x * rpb + (int64_t)wave * rpw;
     const int n = (int)(r0 < rows ? (rows - r0 < rpw ? rows - r0 : rpw) : 0);
+    // the residual-gradient presence as a compile-time branch of the row loop: with FULL rows (C =
+    // 64 VEC NJ, no lane guards) a row's loads are then one basic block, issued back to back
+    // PF: the next row's loads are issued before the current row is processed (two rows in flight per
+    // wave; more VGPRs -- cg_set_tuning("ln_pf"))
+    auto row_loop = [&](auto hr) {
+        if constexpr (PF) {
+            if (n > 0) {
+                LnRow<VEC, NJ> A;
+                load(r0, A, hr);
 #pragma unroll 1
-    for (int i = 0; i < n; ++i) {
-        LnRow<VEC, NJ> A;
-        load(r0 + i, A);
-        process(r0 + i, A);
-    }
+                for (int i = 0; i < n; ++i) {
+                    LnRow<VEC, NJ> Bn;
+                    if (i + 1 < n) load(r0 + i + 1, Bn, hr);
+                    process(r0 + i, A, hr);
+                    A = Bn;
+                }
+            }
+        } else {
+#pragma unroll 1
+            for (int i = 0; i < n; ++i) {
+                LnRow<VEC, NJ> A;
+                load(r0 + i, A, hr);
+                process(r0 + i, A, hr);
+            }
+        }
+    };
+    if (dres) row_loop(std::true_type{});
+    else row_loop(std::false_type{});
     // column partials of the block: waves w and w + 4 pairwise, then waves 0..3 in order
     const int NC = NP * C;
     auto put = [&](bool add) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int e = (j * 64 + lane) * VEC;
-            if (e < C) {
+            if (FULL || e < C) {
                 float* dst = red + (wave & 3) * NC + e;
 #pragma unroll
                 for (int q = 0; q < VEC; ++q) {
@@ -362,12 +389,12 @@ int launch_ln_fwd(const float* x, const float* w, const float* b, TY* y, float* 
     constexpr int RPW = 2;
     int grid = ceil_div(rows, 4 * RPW);
     grid = grid > 4096 ? 4096 : grid;
-#define LNF(V, N) k_ln_fwd<V, N, TY, RPW><<<grid, 256, 0, st>>>(x, w, b, y, mean, rstd, rows, C, eps)
-    if (C == 384 && al16) LNF(2, 3);
-    else if (C == 768 && al16) LNF(4, 3);
-    else if (C == 512 && al16) LNF(4, 2);
-    else if (C == 1024 && al16) LNF(4, 4);
-    else LNF(1, 32);
+#define LNF(V, N, F) k_ln_fwd<V, N, TY, RPW, F><<<grid, 256, 0, st>>>(x, w, b, y, mean, rstd, rows, C, eps)
+    if (C == 384 && al16) LNF(2, 3, true);   // FULL rows: C = 64 V N, no per-lane column guards
+    else if (C == 768 && al16) LNF(4, 3, true);
+    else if (C == 512 && al16) LNF(4, 2, true);
+    else if (C == 1024 && al16) LNF(4, 4, true);
+    else LNF(1, 32, false);
 #undef LNF
     return CG_OK;
 }
@@ -383,21 +410,28 @@ int launch_ln_bwd(const TDY* dy, const float* x, const float* w, const float* me
     const size_t lds = (size_t)4 * NP * C * sizeof(float);
     const int rpb = ln_bwd_rpb(rows, C);
     const int waves = ln_bwd_waves(C);
-#define LNB(V, N)                                                                                              \
+#define LNB_(V, N, F, P)                                                                                       \
     do {                                                                                                       \
         if (waves == 4)                                                                                        \
-            k_ln_bwd<V, N, TDY, 4><<<(unsigned)nblk, 256, lds, st>>>(dy, x, w, mean, rstd, dres, dx, lp, part, rows, C, \
-                                                                     rpb);                                     \
+            k_ln_bwd<V, N, TDY, 4, F, P><<<(unsigned)nblk, 256, lds, st>>>(dy, x, w, mean, rstd, dres, dx, lp, part,    \
+                                                                           rows, C, rpb);                      \
         else                                                                                                   \
-            k_ln_bwd<V, N, TDY, 8><<<(unsigned)nblk, 512, lds, st>>>(dy, x, w, mean, rstd, dres, dx, lp, part, rows, C, \
-                                                                     rpb);                                     \
+            k_ln_bwd<V, N, TDY, 8, F, P><<<(unsigned)nblk, 512, lds, st>>>(dy, x, w, mean, rstd, dres, dx, lp, part,    \
+                                                                           rows, C, rpb);                      \
     } while (0)
-    if (C == 384 && al16) LNB(2, 3);
-    else if (C == 768 && al16) LNB(4, 3);
-    else if (C == 512 && al16) LNB(4, 2);
-    else if (C == 1024 && al16) LNB(4, 4);
-    else LNB(1, 16);   // C <= 1024
+#define LNB(V, N, F)                        \
+    do {                                    \
+        if (F && g_ln_pf) LNB_(V, N, F, F); \
+        else LNB_(V, N, F, false);          \
+    } while (0)
+    // the exact shapes run FULL rows (C = 64 V N: no per-lane column guards)
+    if (C == 384 && al16) LNB(2, 3, true);
+    else if (C == 768 && al16) LNB(4, 3, true);
+    else if (C == 512 && al16) LNB(4, 2, true);
+    else if (C == 1024 && al16) LNB(4, 4, true);
+    else LNB(1, 16, false);   // C <= 1024
 #undef LNB
+#undef LNB_
     if (!defer && (dw || db || dbias))
         launch_reduce_partials3(part, nblk, NP * C, dw, db, dbias, C, accumulate, dbias_accumulate, st);
     return CG_OK;
