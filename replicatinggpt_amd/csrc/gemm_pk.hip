@@ -367,6 +367,13 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     DA da;
     DB db;
     const uint32_t lds0 = lds_base(smem);
+#ifdef CG_PK_WHATIF
+    // diagnostic build only (make whatif; tools/gemm_whatif.py): pk_flags bit 4 skips the in-loop
+    // DMAs, bit 5 the MFMAs, bit 6 the item epilogues -- wrong results, timing only
+    const bool WI_NODMA = flags & 16, WI_NOMFMA = flags & 32, WI_NOEPI = flags & 64;
+#else
+    constexpr bool WI_NODMA = false, WI_NOMFMA = false, WI_NOEPI = false;
+#endif
     da.init(lda, wave, lane);
     db.init(ldb, wave, lane);
 
@@ -512,6 +519,7 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         // 8 groups of 4 MFMAs (half s, A fragment i); the next stage's DMA instructions in between,
         // CG_PK_DPG of them after each group (1: spread over the whole step)
         auto issue_dma = [&](int t) {
+            if (WI_NODMA) return;
             if (t < DA::PER_WAVE) da.issue1(na, t, dimg, wave);
             else db.issue1(nbp, t - DA::PER_WAVE, dimg + G::IMG_A, wave);
         };
@@ -519,7 +527,8 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         for (int t = 0; t < 4 * NS; ++t) {
             const int s = t >> 2, i = t & 3;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = mfma_bf16(bf[s][j], af[s][i], acc[i][j]);
+            for (int j = 0; j < 4; ++j)
+                if (!WI_NOMFMA) acc[i][j] = mfma_bf16(bf[s][j], af[s][i], acc[i][j]);
 #pragma unroll
             for (int d = 0; d < CG_PK_DPG; ++d)
                 if (t * CG_PK_DPG + d < LPT) issue_dma(t * CG_PK_DPG + d);
@@ -546,7 +555,8 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
             int sp;
             decode(cj, m0, n0, sp);
             const int64_t mr = m0 + wm * 64 + (lane & 15), nc = n0 + wn * 64 + 4 * (lane >> 4);
-            if (EK == EK_SLAB || split_k > 1) {
+            if (WI_NOEPI) {
+            } else if (EK == EK_SLAB || split_k > 1) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
