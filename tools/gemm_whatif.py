@@ -29,7 +29,7 @@ def main():
         ts = []
         for _, fl in MODES:
             L.check(lib.cg_set_tuning(b"pk_flags", fl))
-            ts.append(graph_time(gemm_fn(m, n, k, at, bt, split)))
+            ts.append(1e3 * graph_time(gemm_fn(m, n, k, at, bt, split)))   # ms -> us
         print(f"{name:12s} " + " ".join(f"{t:12.1f}us" for t in ts), flush=True)
     L.check(lib.cg_set_tuning(b"pk_flags", 0))
     L.check(lib.cg_set_tuning(b"gemm_variant", 0))

@@ -3,7 +3,7 @@ where a persistent GEMM's cycles go -- MFMA pipe, LDS instruction issue, vector-
 issue and in-flight depth, texture-address (TA) / data (TD) pipe occupancy and the L2 read latency.
 Units: GRBM_GUI_ACTIVE / 8 = kernel cycles per XCD (MI355X_MICROARCH.md), SQ_* quad-cycle counters x 4,
 per-CU counters (TA/TD/TCP _sum) divided by 256 CUs.
-usage: python tools/pmc_gemm_table.py gpurun_out <tag> [<tag> ...]"""
+usage: python tools/pmc_gemm_table.py gpurun_out <tag> [<tag> ...] [--all: non-MFMA kernels too]"""
 import collections
 import csv
 import glob
@@ -24,12 +24,16 @@ def load(root, tag):
 
 
 def main():
-    root, tags = sys.argv[1], sys.argv[2:]
+    allk = "--all" in sys.argv
+    args = [a for a in sys.argv[1:] if a != "--all"]
+    root, tags = args[0], args[1:]
     for tag in tags:
         acc = load(root, tag)
         for k, c in acc.items():
             m = lambda n: (sum(c[n]) / len(c[n])) if c.get(n) else float("nan")  # noqa: E731
-            if not c.get("SQ_INSTS_MFMA") or m("SQ_INSTS_MFMA") == 0:
+            if not allk and (not c.get("SQ_INSTS_MFMA") or m("SQ_INSTS_MFMA") == 0):
+                continue
+            if not c.get("GRBM_GUI_ACTIVE"):
                 continue
             gui = m("GRBM_GUI_ACTIVE") / 8            # kernel cycles (per XCD)
             simd = gui * 1024                          # SIMD-cycles over the chip
