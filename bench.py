@@ -369,8 +369,9 @@ def main():
     ap.add_argument("--no-generate", action="store_true", help="skip the C5 batched-decode measurement")
     ap.add_argument("--overlap", type=int, default=None, choices=[0, 1],
                     help="force the segmented (DP-overlap) backward on/off (default: on when N > 1)")
-    ap.add_argument("--seg-layers", type=int, default=2,
-                    help="DP: blocks per backward graph segment (gradient all-reduce overlaps the next segment)")
+    ap.add_argument("--seg-layers", type=int, default=1,
+                    help="DP: blocks per backward graph segment (gradient all-reduce overlaps the next segment; "
+                         "1 = the smallest exposed last segment, block 0 + embeddings: DESIGN.md section 6)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
