@@ -46,22 +46,6 @@ __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// L2 prefetch of a future K-tile (CG_PK_PF = tiles beyond the DMA cursor, 0 = off): one lane per
-// 128-B line of the tile's A and B panels (waves 0-1: A, 2-3: B, 64 lines each), two 4-B
-// LDS-DMA reads per line (bytes 0 and 64: both halves of the line, whatever the fill granule) into
-// a 256-B scratch slot per wave that nothing reads.  No VGPR destination, so nothing can be
-// clobbered by a late return; the two instructions are counted in the main loop's vmcnt waits.
-// The second read takes its own lane offset (voff + 64), not an instruction offset: an LDS-DMA's
-// instruction offset moves its LDS destination too (M0 + inst_offset + 4 lane), past the slot.
-#ifndef CG_PK_PF
-#define CG_PK_PF 0
-#endif
-__device__ __forceinline__ void pf_lines(const void* sbase, uint32_t voff, uint32_t voff2, uint32_t lds) {
-    const uint32_t l = __builtin_amdgcn_readfirstlane(lds);
-    asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %0, %2\n\tglobal_load_lds_dword %1, %2"
-                 ::"v"(voff), "v"(voff2), "s"(sbase), "s"(l) : "memory", "m0");
-}
-
 // per-lane part of one operand's LDS-DMA sources: R rows (K-contiguous) or R columns (TR) x BK k
 template <bool TR, int R, int WAVES, int BK>
 struct DmaP {
@@ -330,8 +314,7 @@ template <int BM, int BN, int NBUF, int BK = FBK>
 struct GeoP {
     static constexpr int WM = BM / 64, WN = BN / 64, WAVES = WM * WN, THREADS = WAVES * 64;
     static constexpr int IMG_A = BM * BK * 2, IMG_B = BN * BK * 2, STAGE = IMG_A + IMG_B;
-    static constexpr int PF = (NBUF == 2 && BM == 128 && BN == 128 && BK == 64) ? CG_PK_PF : 0;
-    static constexpr int LDS = NBUF * STAGE + (PF ? 512 * WAVES : 0);   // + the prefetch scratch slots (256 B used)
+    static constexpr int LDS = NBUF * STAGE;
     static constexpr int OCC_LDS = (160 * 1024) / LDS;
     static constexpr int OCC = OCC_LDS > 4 ? 4 : (OCC_LDS < 1 ? 1 : OCC_LDS);  // resident blocks per CU (LDS-bound)
 };
@@ -442,53 +425,6 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         }
     };
 
-    // L2 prefetch cursor (G::PF tiles ahead of the DMA cursor; its own copy of prep_next's walk)
-    constexpr int PF = G::PF, NPF = PF ? 2 : 0;
-    uint32_t pf_off = 0;
-    const uint32_t pf_lds = lds0 + (uint32_t)(NBUF * G::STAGE + 512 * wave);
-    int pij = 0, pikt = 0, pink = 0, pkt = 0;   // pkt: the target's K-tile within item pij's origins
-    const bf16_t* poa = A;
-    const bf16_t* pob = B;
-    auto pf_adv = [&]() {   // the next K-tile of this block's sequence (past the last: the last again)
-        if (pij < my_items) {
-            if (pikt == 0) {
-                int64_t m0, n0;
-                int sp;
-                decode(pij, m0, n0, sp);
-                pink = split_nk(sp);
-                const int64_t kb = sp * kchunk;
-                poa = AT ? A + kb * lda + m0 : A + m0 * lda + kb;
-                pob = BT ? B + kb * ldb + n0 : B + n0 * ldb + kb;
-            }
-            pkt = pikt;
-            if (++pikt == pink) {
-                pikt = 0;
-                ++pij;
-            }
-        }
-    };
-    auto pf_issue = [&]() {   // the operand base is wave-uniform: keep it in SGPRs for the saddr form
-        const bf16_t* t = wave >= 2 ? pob + pkt * db.kstep : poa + pkt * da.kstep;
-        const uint64_t p = (uint64_t)(uintptr_t)t;
-        // (readfirstlane returns int: widen through uint32_t, or a low word >= 2^31 sign-extends)
-        const uint64_t u = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(p >> 32)) << 32) |
-                           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)p);
-        pf_lines((const void*)(uintptr_t)u, pf_off, pf_off + 64u, pf_lds);
-    };
-    if constexpr (PF > 0) {
-        const bool opb = wave >= 2;
-        const bool tr = opb ? BT : AT;
-        const int64_t ldx = opb ? ldb : lda;
-        const int i = (wave & 1) * 64 + lane;   // line i of the operand's K-tile
-        pf_off = tr ? 2u * (uint32_t)((i >> 1) * ldx) + 128u * (uint32_t)(i & 1) : 2u * (uint32_t)(i * ldx);
-        pf_adv();   // tile 0: the prologue DMA's
-#pragma unroll
-        for (int t = 1; t <= PF; ++t) {   // tiles 1..PF, issued before tile 0's DMA (the g = 0 wait drains all)
-            pf_adv();
-            pf_issue();
-        }
-    }
-
     fv4 acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -539,8 +475,6 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
             } else if constexpr (NBUF == 3) {
                 if (ahead >= 1) wait_vm<LPT + EPI_OPS>();
                 else wait_vm<EPI_OPS>();
-            } else if (PF && g > 0) {
-                wait_vm<NPF + EPI_OPS>();   // younger than tile g's DMA: step g-1's prefetch + item stores
             } else {
                 wait_vm<EPI_OPS>();
             }
@@ -551,8 +485,6 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         } else if constexpr (NBUF == 3) {
             if (ahead >= 1) wait_vm<LPT>();
             else wait_vm<0>();
-        } else if (PF && g > 0) {
-            wait_vm<NPF>();
         } else {
             wait_vm<0>();
         }
@@ -603,10 +535,6 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         }
 #pragma unroll
         for (int t = 4 * NS * CG_PK_DPG; t < LPT; ++t) issue_dma(t);
-        if constexpr (PF > 0) {   // after this step's DMAs (tile g + 1): tile g + 1 + PF into L2
-            pf_adv();
-            pf_issue();
-        }
 #pragma unroll
         for (int t = 0; t < 4 * NS; ++t) {
             __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
