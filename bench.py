@@ -240,7 +240,11 @@ def kernel_census(cfg, Bsz, T, dev):
     ws = torch.empty(ops.layernorm_bwd_workspace(M, C) // 4 + 1, device=dev)
     t2 = _time_ms(lambda: ops.layernorm_bwd(dy, x, w, mean, rstd, dres, dx, lp, dw, db, False, ws, cs, False, p, 1,
                                             call, 3))
-    for name, tt, byts in (("layernorm_fwd", t, M * C * 6), ("layernorm_bwd", t2, M * C * 16)):
+    # the row kernel alone: in the training step its column-sum reduce runs on the side stream
+    # (functional.GradLink -> layernorm_bwd_rows on the main stream, layernorm_bwd_reduce beside it)
+    t3 = _time_ms(lambda: ops.layernorm_bwd_rows(dy, x, w, mean, rstd, dres, dx, lp, ws, True, p, 1, call, 3))
+    for name, tt, byts in (("layernorm_fwd", t, M * C * 6), ("layernorm_bwd", t2, M * C * 16),
+                           ("layernorm_bwd_rows", t3, M * C * 16)):
         gbs = byts / (tt * 1e-3) / 1e9
         out[name] = {"ms": round(tt, 4), "bytes": byts, "achieved": round(gbs, 1), "unit": "GB/s",
                      "peak": PEAK_HBM_GBS, "frac": round(gbs / PEAK_HBM_GBS, 4)}
