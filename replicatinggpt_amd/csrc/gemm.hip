@@ -469,6 +469,10 @@ extern "C" int cg_set_tuning(const char* key, int value) {
         g_defer_splitk = value;
         return CG_OK;
     }
+    if (!strcmp(key, "defer_partials")) {   // queue cg_layernorm_bwd_reduce / cg_reduce_rows until cg_flush_deferred
+        g_defer_partials = value;
+        return CG_OK;
+    }
     if (!strcmp(key, "ln_waves")) {   // takes effect for workspaces sized after the call
         g_ln_waves = value;
         return CG_OK;
@@ -592,7 +596,7 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
 
 extern "C" int cg_reduce_rows(const float* part, int64_t rows, int64_t N, float* out, int accumulate, void* stream) {
     CG_REQUIRE(part && out && rows > 0 && N > 0, "cg_reduce_rows: bad arguments");
-    launch_reduce_partials(part, rows, N, out, nullptr, N, accumulate, (hipStream_t)stream);
+    reduce_partials_deferrable(part, rows, N, out, nullptr, nullptr, N, accumulate, 0, (hipStream_t)stream);
     CG_LAUNCH_CHECK("cg_reduce_rows");
     return CG_OK;
 }
@@ -638,6 +642,7 @@ static void launch_splitk_reduce_job(const RedJob& j, hipStream_t st) {
 extern "C" int cg_flush_deferred(void* stream) {
     (void)stream;   // pending jobs go out on the stream they were enqueued on
     cg::flush_pending();
+    cg::flush_partials();
     CG_LAUNCH_CHECK("cg_flush_deferred");
     return CG_OK;
 }

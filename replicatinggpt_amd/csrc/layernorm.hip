@@ -508,8 +508,8 @@ extern "C" int cg_layernorm_bwd_reduce(const void* workspace, int64_t rows, int6
     if (!dw && !db && !lp_colsum) return CG_OK;
     const int64_t nblk = ln_bwd_blocks(rows, C);
     const int NP = lp_colsum_partials ? 3 : 2;
-    launch_reduce_partials3((const float*)workspace, nblk, NP * C, dw, db, lp_colsum, C, accumulate,
-                            colsum_accumulate, (hipStream_t)stream);
+    reduce_partials_deferrable((const float*)workspace, nblk, NP * C, dw, db, lp_colsum, C, accumulate,
+                               colsum_accumulate, (hipStream_t)stream);
     CG_LAUNCH_CHECK("cg_layernorm_bwd_reduce");
     return CG_OK;
 }

@@ -118,13 +118,14 @@ extern "C" int cg_dropout_apply(const float* x, int64_t rows, int64_t C, int64_t
 // then the 64 row-lane sums added in a fixed order (deterministic).  The former 32-column blocks
 // (72 blocks at C4, 8 loads in flight per lane) ran 130 us for 9.4 MB.
 // Column n goes to out_a[n] (n < S), out_b[n - S] (n < 2S) or out_c[n - 2S]; NULL drops it.
-__global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict__ part, int64_t K, int64_t N,
-                                                         float* __restrict__ out_a, float* __restrict__ out_b,
-                                                         float* __restrict__ out_c, int64_t S, int accumulate,
-                                                         int accumulate_c) {
-    __shared__ float red[64][17];
+// One block's work (block blk of the job's ceil(N / 16)): shared by the single-job kernel and the
+// deferred multi-job one, so both give the same bits.
+__device__ __forceinline__ void reduce_partials_block(const float* __restrict__ part, int64_t K, int64_t N,
+                                                      float* __restrict__ out_a, float* __restrict__ out_b,
+                                                      float* __restrict__ out_c, int64_t S, int accumulate,
+                                                      int accumulate_c, int64_t blk, float (*red)[17]) {
     const int cq = threadIdx.x & 3, rl = threadIdx.x >> 2;
-    const int64_t n0 = (int64_t)blockIdx.x * 16 + 4 * cq;
+    const int64_t n0 = blk * 16 + 4 * cq;
     float a[4] = {0.f, 0.f, 0.f, 0.f};
     if ((N & 3) == 0 && (((uintptr_t)part) & 15) == 0) {
         if (n0 < N) {
@@ -160,7 +161,7 @@ __global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict
     __syncthreads();
     if (threadIdx.x < 16) {
         const int c = threadIdx.x;
-        const int64_t n = (int64_t)blockIdx.x * 16 + c;
+        const int64_t n = blk * 16 + c;
         if (n < N) {
             float t = 0.f;
             for (int j = 0; j < 64; ++j) t += red[j][c];
@@ -177,14 +178,118 @@ __global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict
     }
 }
 
+__global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict__ part, int64_t K, int64_t N,
+                                                         float* __restrict__ out_a, float* __restrict__ out_b,
+                                                         float* __restrict__ out_c, int64_t S, int accumulate,
+                                                         int accumulate_c) {
+    __shared__ float red[64][17];
+    reduce_partials_block(part, K, N, out_a, out_b, out_c, S, accumulate, accumulate_c, blockIdx.x, red);
+}
+
 namespace cg {
+// Deferred partial reduces (cg_set_tuning "defer_partials", owned by functional.DEFER: the caller
+// keeps every queued job's partials allocated and reads no output before cg_flush_deferred).  The
+// training backward queues its ~20 LayerNorm / bias-gradient reduces here and cg_flush_deferred
+// launches them as ONE kernel: on one hardware queue each was a ~5 us launch for ~1 us of work.
+struct PartJob {
+    const float* part;
+    int64_t K, N, S;
+    float *a, *b, *c;
+    int acc, acc_c;
+};
+constexpr int MAX_PART_JOBS = 24;
+struct PartJobs {
+    int n;
+    int start[MAX_PART_JOBS + 1];   // first block of job q; start[n] = the grid
+    PartJob j[MAX_PART_JOBS];
+};
+}  // namespace cg
+
+__global__ __launch_bounds__(256) void k_reduce_partials_multi(cg::PartJobs jobs) {
+    __shared__ float red[64][17];
+    const int b = blockIdx.x;
+    int q = 0;
+    while (q + 1 < jobs.n && b >= jobs.start[q + 1]) ++q;
+    const cg::PartJob& j = jobs.j[q];
+    reduce_partials_block(j.part, j.K, j.N, j.a, j.b, j.c, j.S, j.acc, j.acc_c, b - jobs.start[q], red);
+}
+
+namespace cg {
+int g_defer_partials = 0;
+static PartJobs g_part_pending = {};
+static hipStream_t g_part_stream = nullptr;
+static int g_part_device = -1;
+
+static int part_device() {
+    int d = -1;
+    return hipGetDevice(&d) == hipSuccess ? d : -1;
+}
+
+void flush_partials() {
+    if (!g_part_pending.n) return;
+    const int cur = part_device();
+    if (g_part_device >= 0 && cur != g_part_device) (void)hipSetDevice(g_part_device);
+    const PartJobs jobs = g_part_pending;
+    g_part_pending.n = 0;
+    k_reduce_partials_multi<<<jobs.start[jobs.n], 256, 0, g_part_stream>>>(jobs);
+    if (g_part_device >= 0 && cur >= 0 && cur != g_part_device) (void)hipSetDevice(cur);
+}
+
+// [p, p + n) of job j's outputs
+static bool overlaps(const float* p, int64_t n, const float* q, int64_t m) {
+    return p && q && n > 0 && m > 0 && p < q + m && q < p + n;
+}
+static bool job_outputs_overlap(const PartJob& x, const float* p, int64_t n) {
+    return overlaps(x.a, x.S, p, n) || overlaps(x.b, x.S, p, n) || overlaps(x.c, x.N - 2 * x.S, p, n);
+}
+// an immediate reduce / write into [p, p + n): the queued jobs that target it go first
+void flush_partials_touching(const float* p, int64_t n) {
+    for (int q = 0; q < g_part_pending.n; ++q)
+        if (job_outputs_overlap(g_part_pending.j[q], p, n)) {
+            flush_partials();
+            return;
+        }
+}
+
+static bool enqueue_partials(const PartJob& j, hipStream_t st) {
+    if (!g_defer_partials) return false;
+    const int dev = part_device();
+    bool clash = g_part_pending.n == MAX_PART_JOBS ||
+                 (g_part_pending.n && (g_part_stream != st || g_part_device != dev));
+    for (int q = 0; q < g_part_pending.n && !clash; ++q) {
+        const PartJob& x = g_part_pending.j[q];
+        clash = job_outputs_overlap(x, j.a, j.S) || job_outputs_overlap(x, j.b, j.S) ||
+                job_outputs_overlap(x, j.c, j.N - 2 * j.S);
+    }
+    if (clash) flush_partials();
+    g_part_stream = st;
+    g_part_device = dev;
+    PartJobs& P = g_part_pending;
+    if (!P.n) P.start[0] = 0;
+    P.j[P.n] = j;
+    P.start[P.n + 1] = P.start[P.n] + (int)ceil_div(j.N, 16);
+    ++P.n;
+    return true;
+}
+
 void launch_reduce_partials(const float* part, int64_t K, int64_t N, float* out_a, float* out_b, int64_t S,
                             int accumulate, hipStream_t st) {
+    flush_partials_touching(out_a, S);
+    flush_partials_touching(out_b, N - S);
     k_reduce_partials<<<ceil_div(N, 16), 256, 0, st>>>(part, K, N, out_a, out_b, nullptr, S, accumulate, 0);
 }
 void launch_reduce_partials3(const float* part, int64_t K, int64_t N, float* out_a, float* out_b, float* out_c,
                              int64_t S, int accumulate, int accumulate_c, hipStream_t st) {
+    flush_partials_touching(out_a, S);
+    flush_partials_touching(out_b, S);
+    flush_partials_touching(out_c, N - 2 * S);
     k_reduce_partials<<<ceil_div(N, 16), 256, 0, st>>>(part, K, N, out_a, out_b, out_c, S, accumulate, accumulate_c);
+}
+// the deferrable forms (cg_layernorm_bwd_reduce, cg_reduce_rows): queued while defer_partials is set
+void reduce_partials_deferrable(const float* part, int64_t K, int64_t N, float* out_a, float* out_b, float* out_c,
+                                int64_t S, int accumulate, int accumulate_c, hipStream_t st) {
+    if (enqueue_partials(PartJob{part, K, N, S, out_a, out_b, out_c, accumulate, accumulate_c}, st)) return;
+    launch_reduce_partials3(part, K, N, out_a, out_b, out_c, S, accumulate, accumulate_c, st);
 }
 }  // namespace cg
 

@@ -91,6 +91,10 @@ class DeferredReduces:
 
     def __init__(self):
         self.enabled = os.environ.get("CHARPT_DEFER_SPLITK", "1") != "0"
+        # the LayerNorm / bias-gradient column-sum reduces likewise (cg_set_tuning "defer_partials"):
+        # queued and launched as ONE multi-job kernel at the flush -- on one hardware queue each was a
+        # ~5 us launch for ~1 us of work (CHARPT_DEFER_PARTIALS=0: one launch each, for A/B)
+        self.partials_on = os.environ.get("CHARPT_DEFER_PARTIALS", "1") != "0"
         self.active = False
         self.keep = []
 
@@ -99,6 +103,22 @@ class DeferredReduces:
             L.check(L.load().cg_set_tuning(b"defer_splitk", 1), "defer_splitk")
             self.active = True
         return self
+
+    @contextlib.contextmanager
+    def partials(self, *keep):
+        """Queue the cg_layernorm_bwd_reduce / cg_reduce_rows calls made inside (their outputs must be
+        flat gradient slots, which nothing reads before DEFER closes; ``keep``: their partials,
+        held until the flush)."""
+        if not (self.active and self.partials_on):
+            yield
+            return
+        lib = L.load()
+        L.check(lib.cg_set_tuning(b"defer_partials", 1), "defer_partials")
+        try:
+            yield
+        finally:
+            L.check(lib.cg_set_tuning(b"defer_partials", 0), "defer_partials")
+        self.keep.extend(t for t in keep if t is not None)
 
     def flush(self):
         """Launch every pending reduce now, on the current stream (their outputs complete in stream order)."""
@@ -397,15 +417,22 @@ def layernorm_bwd(dy2, x2, w_reg, b_reg, mean, rstd, dres=None, want_lp=False, l
     # the column-sum reduce (LN weight/bias grads, the consumer's bias grad) only feeds the optimizer:
     # when every target is a flat gradient slot (read after SIDE.join) it runs on the side stream,
     # off the dgrad chain; otherwise (tensors handed back to autograd) in line
-    side = LN_REDUCE_SIDE and SIDE.enabled and dev.type == "cuda" and (gw is not None or gb is not None or gcs is not None) and \
+    slots_only = dev.type == "cuda" and (gw is not None or gb is not None or gcs is not None) and \
         (gw is None or gw is w_reg.slot) and (gb is None or gb is b_reg.slot) and \
         (gcs is None or gcs is link.bias.slot)
+    side = LN_REDUCE_SIDE and SIDE.enabled and slots_only
     if "skip_lnbwd" in WHATIF:
         pass
     elif side:
         ops.layernorm_bwd_rows(dy2, x2, w_reg.master, mean, rstd, dres, dx, lp, ws, gcs is not None, p, seed, rng,
                                site)
         with SIDE.run(dev, ws):
+            ops.layernorm_bwd_reduce(ws, rows, C, gcs is not None, gw, gb, gcs, bool(bw or bb), bool(bcs))
+    elif slots_only and DEFER.active and DEFER.partials_on:
+        # the reduce joins the backward's one multi-job launch at the DEFER flush
+        ops.layernorm_bwd_rows(dy2, x2, w_reg.master, mean, rstd, dres, dx, lp, ws, gcs is not None, p, seed, rng,
+                               site)
+        with DEFER.partials(ws):
             ops.layernorm_bwd_reduce(ws, rows, C, gcs is not None, gw, gb, gcs, bool(bw or bb), bool(bcs))
     else:
         ops.layernorm_bwd(dy2, x2, w_reg.master, mean, rstd, dres, dx, lp, gw, gb, bool(bw or bb), ws, gcs, bool(bcs),
@@ -646,7 +673,8 @@ class FFNSublayerFn(torch.autograd.Function):
                 linear_wgrad(dz1, a, g_w1, beta_w1, g_w1 is w1.slot)
             if g_b1 is not None:
                 if part is not None:
-                    ops.reduce_rows(part, part.shape[0], part.shape[1], g_b1, bool(beta_b1))
+                    with DEFER.partials(part) if g_b1 is b1.slot else contextlib.nullcontext():
+                        ops.reduce_rows(part, part.shape[0], part.shape[1], g_b1, bool(beta_b1))
                 else:
                     colsum_into(dz1, g_b1, beta_b1)
         da = torch.empty((B * T, C), dtype=act, device=x2.device)

@@ -791,3 +791,42 @@ def test_bf16_rounding_matches_torch():
     out = torch.empty(64, dtype=torch.bfloat16, device=DEV)
     ops().cast_bf16(nan.to(DEV), out)
     assert torch.isnan(out.cpu().float()).all()
+
+
+def test_deferred_partial_reduces_match_immediate():
+    """cg_set_tuning("defer_partials"): cg_reduce_rows / cg_layernorm_bwd_reduce calls are queued and
+    cg_flush_deferred runs them as one multi-job kernel -- the same per-job bits as the immediate
+    launches, including a second job accumulating into the first job's output (queued jobs whose
+    outputs it overlaps are flushed first) and an immediate reduce into a queued output."""
+    import ctypes
+    from replicatinggpt_amd import _lib as L
+    O = ops()
+    lib = L.load()
+    torch.manual_seed(5)
+    shapes = [(256, 1152), (256, 1536), (33, 70), (512, 384)]
+    parts = [torch.randn(r, n, device=DEV) for r, n in shapes]
+    extra = torch.randn(128, 1536, device=DEV)
+
+    def run(defer):
+        outs = [torch.full((n,), 0.5, device=DEV) for _, n in shapes]
+        if defer:
+            L.check(lib.cg_set_tuning(b"defer_partials", 1))
+        try:
+            for p, o in zip(parts, outs):
+                O.reduce_rows(p, p.shape[0], p.shape[1], o, False)
+            O.reduce_rows(extra, 128, 1536, outs[1], True)         # accumulates onto a queued output
+            ws = torch.empty(O.colsum_workspace(64, 384) // 4 + 1, device=DEV)
+            O.colsum(extra[:64, :384].contiguous(), outs[3], True, ws)   # immediate reduce, queued target
+            O.reduce_rows(parts[0], 256, 1152, outs[0], True)
+        finally:
+            if defer:
+                L.check(lib.cg_set_tuning(b"defer_partials", 0))
+        L.check(lib.cg_flush_deferred(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+        torch.cuda.synchronize()
+        return [o.cpu() for o in outs]
+
+    ref, got = run(False), run(True)
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+    want1 = parts[1].double().sum(0) + extra.double().sum(0)
+    assert relerr(got[1], want1) < 1e-5

@@ -57,16 +57,19 @@ def test_deferred_splitk_reduces_bit_identical():
     """The weight gradients' split-K reduces deferred into later GEMM launches' tails
     (functional.DEFER, csrc RedJob) give the in-line reduce's bits: C2-width model (split-K weight
     gradients at B*T = 16384), graph replay with and without deferral, eager, and the segmented
-    (DP-overlap) backward whose segments each flush their pending reduces."""
+    (DP-overlap) backward whose segments each flush their pending reduces.  The LayerNorm / b1
+    column-sum reduces queued for one multi-job launch at the flush (DEFER.partials) likewise,
+    with and without the split-K deferral."""
     from replicatinggpt_amd import functional as Fn
     from replicatinggpt_amd.engine import GradReducer, TrainStep
     cfg = _cfg(block_size=256, n_embd=384, n_head=6, n_layers=3, batch_size=64)
     runs = []
-    saved = Fn.DEFER.enabled
+    saved = Fn.DEFER.enabled, Fn.DEFER.partials_on
     try:
-        for defer, graph, overlap in ((False, True, False), (True, True, False), (True, False, False),
-                                      (True, True, True)):
-            Fn.DEFER.enabled = defer
+        for defer, partials, graph, overlap in ((False, False, True, False), (True, True, True, False),
+                                                (True, True, False, False), (True, True, True, True),
+                                                (True, False, True, False)):
+            Fn.DEFER.enabled, Fn.DEFER.partials_on = defer, partials
             m, opt, s = _setup(cfg)
             red = GradReducer(m.flat.grad) if overlap else None   # world size 1: the segmentation only
             st = TrainStep(m, opt, s, red, use_graph=graph, overlap=overlap, seg_layers=1)
@@ -75,7 +78,7 @@ def test_deferred_splitk_reduces_bit_identical():
             torch.cuda.synchronize()
             runs.append((losses, m.flat.master.detach().cpu().clone(), m.flat.grad.detach().cpu().clone()))
     finally:
-        Fn.DEFER.enabled = saved
+        Fn.DEFER.enabled, Fn.DEFER.partials_on = saved
     for r in runs[1:]:
         assert r[0] == runs[0][0]
         assert torch.equal(r[1], runs[0][1]) and torch.equal(r[2], runs[0][2])
