@@ -147,13 +147,13 @@ def gemm_census(cfg, Bsz, T, dev):
         ms = time_gemm(m, n, k, at, bt, epi, dev)
         split = Fn._wgrad_split(m, n, k, True) if epi == "wgrad" else 1
         out.append({"name": name, "M": m, "N": n, "K": k, "ms": ms, "launches": cnt, "flops": 2.0 * m * n * k,
-                    "split": split, "kernel": gemm_kernel_name(m, n, at, split, dev)})
+                    "split": split, "kernel": gemm_kernel_name(m, n, at, bt, split, dev)})
     return out
 
 
-def gemm_kernel_name(M, N, at, split, dev):
-    """The kernel cg_gemm's default dispatch picks (gemm_bf16.hip fast_gemm_launch): the 8-wave
-    256x256 tile at >= 2 such tiles per CU (no split, A not transposed), else the 128x128 one."""
+def gemm_kernel_name(M, N, at, bt, split, dev):
+    """The kernel cg_gemm's default dispatch picks (gemm_bf16.hip pick_variant): the 8-wave 256x256
+    tile at >= 2 such tiles per CU (no split, A not transposed), else the 128x128 one."""
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
     if split == 1 and not at and M % 256 == 0 and N % 256 == 0 and (M // 256) * (N // 256) >= 2 * cus:
         return "k_gemm_p8<256x256>"

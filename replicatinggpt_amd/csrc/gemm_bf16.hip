@@ -176,11 +176,14 @@ void launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, in
 }  // namespace
 
 // the kernel variant cg_gemm's bf16 dispatch runs for this problem (before any fallback)
-static int pick_variant(int at, int64_t M, int64_t N, int split_k) {
+static int pick_variant(int at, int bt, int64_t M, int64_t N, int split_k) {
     int v = g_gemm_variant;
     if (v == 0) {
         // persistent 128x128 LDS-DMA: measured best on the C2 shapes (profiles/r1_gemm_scan.txt); the
         // 8-wave 256x256 tile once there are >= 2 tiles per CU (C4 forward/dgrad: profiles/r1_gemm_scan_c4_v24.txt)
+        // (the one-block-per-CU 128x192 tile, A/B variant 18, measured slower on the C2 N = 384
+        // forwards than 128x128 tiles part-filling the two-per-CU slots: profiles/r3_gemm_128x192_ab.txt)
+        (void)bt;
         const int64_t t256 = (M / 256) * (N / 256);
         v = (!at && split_k == 1 && M % 256 == 0 && N % 256 == 0 && t256 >= 2 * (int64_t)gemm_cu_count()) ? 24 : 9;
     }
@@ -202,8 +205,7 @@ static bool colpart_ok(int v, int at, int split_k) {
 }
 
 bool gemm_colpart_supported(int at, int bt, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc) {
-    (void)bt;
-    return fast_shape_ok(M, N, K, lda, ldb, ldc, 1) && colpart_ok(pick_variant(at, M, N, 1), at, 1);
+    return fast_shape_ok(M, N, K, lda, ldb, ldc, 1) && colpart_ok(pick_variant(at, bt, M, N, 1), at, 1);
 }
 
 // CG_BITS ReLU keep bits are written / read by the same two kernels' item epilogues (64-column
@@ -213,8 +215,7 @@ static bool relu_bits_ok(int v, int at, int split_k, int64_t N) {
 }
 
 bool gemm_relu_bits_supported(int at, int bt, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc) {
-    (void)bt;
-    return fast_shape_ok(M, N, K, lda, ldb, ldc, 1) && relu_bits_ok(pick_variant(at, M, N, 1), at, 1, N);
+    return fast_shape_ok(M, N, K, lda, ldb, ldc, 1) && relu_bits_ok(pick_variant(at, bt, M, N, 1), at, 1, N);
 }
 
 bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
@@ -225,7 +226,11 @@ bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf1
     if (e.bias && (((uintptr_t)e.bias) & 15)) return false;
     if (e.resid && ((((uintptr_t)e.resid) & 15) || e.ld_resid % 4)) return false;
     if (e.aux && ((((uintptr_t)e.aux) & 15) || e.ld_aux % 8)) return false;
-    int v = pick_variant(at, M, N, split_k);
+    int v = pick_variant(at, bt, M, N, split_k);
+    // the 128x192 tile has the fixed-kind item epilogues only (no keep bits, column partials or beta)
+    if (v == 18 && (e.colpart || e.aux_dtype == CG_BITS || e.beta != 0.f || at || bt || N % 192 || split_k != 1 ||
+                    (g_pk_flags & 2)))
+        v = 9;
     if (K % (FBK * split_k)) {
         // uneven split-K (the last split shorter): only the 128x128 persistent kernel, and only when
         // every split is non-empty; otherwise the generic kernels (ceil-sized chunks) take it

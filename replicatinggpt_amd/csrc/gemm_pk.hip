@@ -314,9 +314,17 @@ template <int BM, int BN, int NBUF, int BK = FBK>
 struct GeoP {
     static constexpr int WM = BM / 64, WN = BN / 64, WAVES = WM * WN, THREADS = WAVES * 64;
     static constexpr int IMG_A = BM * BK * 2, IMG_B = BN * BK * 2, STAGE = IMG_A + IMG_B;
-    static constexpr int LDS = NBUF * STAGE;
+    // 128x192 (6 waves): one block per CU by construction -- the launch asks for 96 KB of LDS so a
+    // second block never shares the CU (the tile exists to give each CU 1.5 128x128 tiles of work
+    // where 384 of them would fill 3/4 of the 512 two-per-CU slots), and only waves 0-3 issue the
+    // A image's 16 DMA instructions (6 does not divide them)
+    static constexpr bool ONE_PER_CU = WN == 3;
+    static constexpr int AW = ONE_PER_CU ? 4 : WAVES;   // waves issuing the A image's DMAs
+    static constexpr int LDS = ONE_PER_CU ? 96 * 1024 : NBUF * STAGE;
+    static_assert(NBUF * STAGE <= LDS, "ring exceeds the launch's LDS");
     static constexpr int OCC_LDS = (160 * 1024) / LDS;
     static constexpr int OCC = OCC_LDS > 4 ? 4 : (OCC_LDS < 1 ? 1 : OCC_LDS);  // resident blocks per CU (LDS-bound)
+    static constexpr int WPE = (WAVES * OCC + 3) / 4;   // waves per SIMD
 };
 
 // EK: the item epilogue.  EK_SLAB = split-K (split_k > 1, fp32 slab stores only), 0..5 = one
@@ -339,14 +347,17 @@ template <bool AT, bool BT, int BM, int BN, int NBUF, int EK = EK_ANY, int BK = 
 // left at its default it schedules for 8+ waves/SIMD, keeps ONE A fragment register and waits
 // lgkmcnt(0) before every 4 MFMAs (LDS latency exposed 8x per K-tile)
 __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, (GeoP<BM, BN, NBUF, BK>::OCC))
-__attribute__((amdgpu_waves_per_eu(1, (BM / 64) * (BN / 64) * GeoP<BM, BN, NBUF, BK>::OCC / 4)))
+__attribute__((amdgpu_waves_per_eu(1, GeoP<BM, BN, NBUF, BK>::WPE)))
 void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
                const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype, int64_t ldc,
                EpiArgs epi, int split_k, int64_t kchunk, float* __restrict__ ws, int flags, RedJobs red) {
     static_assert(BK == 64 || BK == 32, "BK");
+    static_assert(!GeoP<BM, BN, NBUF, BK>::ONE_PER_CU || (NBUF == 2 && !AT && !BT),
+                  "128x192: uneven per-wave DMA counts need the 2-stage ring's DMA-count-free waits; "
+                  "the transposed image swizzle needs 128-multiple widths");
     constexpr int NS = BK / 32;   // 32-deep MFMA slices per K-tile
     using G = GeoP<BM, BN, NBUF, BK>;
-    using DA = DmaP<AT, BM, G::WAVES, BK>;
+    using DA = DmaP<AT, BM, G::AW, BK>;
     using DB = DmaP<BT, BN, G::WAVES, BK>;
     constexpr int LPT = DA::PER_WAVE + DB::PER_WAVE;  // DMA instructions per thread per K-tile
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -374,7 +385,7 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
 #else
     constexpr bool WI_NODMA = false, WI_NOMFMA = false, WI_NOEPI = false;
 #endif
-    da.init(lda, wave, lane);
+    da.init(lda, wave < G::AW ? wave : 0, lane);
     db.init(ldb, wave, lane);
 
     auto decode = [&](int j, int64_t& m0, int64_t& n0, int& split) {
@@ -436,8 +447,9 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         if (s < total) {
             prep_next(true);
             const uint32_t img = lds0 + (uint32_t)(s * G::STAGE);
+            if (G::AW == G::WAVES || wave < G::AW)
 #pragma unroll
-            for (int i = 0; i < DA::PER_WAVE; ++i) da.issue1(na, i, img, wave);
+                for (int i = 0; i < DA::PER_WAVE; ++i) da.issue1(na, i, img, wave);
 #pragma unroll
             for (int i = 0; i < DB::PER_WAVE; ++i) db.issue1(nbp, i, img + G::IMG_A, wave);
         }
@@ -520,8 +532,11 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         // CG_PK_DPG of them after each group (1: spread over the whole step)
         auto issue_dma = [&](int t) {
             if (WI_NODMA) return;
-            if (t < DA::PER_WAVE) da.issue1(na, t, dimg, wave);
-            else db.issue1(nbp, t - DA::PER_WAVE, dimg + G::IMG_A, wave);
+            if (t < DA::PER_WAVE) {
+                if (G::AW == G::WAVES || wave < G::AW) da.issue1(na, t, dimg, wave);
+            } else {
+                db.issue1(nbp, t - DA::PER_WAVE, dimg + G::IMG_A, wave);
+            }
         };
 #pragma unroll
         for (int t = 0; t < 4 * NS; ++t) {
@@ -637,7 +652,7 @@ void launch_ek(unsigned grid, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
         L1(EK_SLAB);
         return;
     }
-    if constexpr (!AT_ && BM == 128 && BN == 128) {
+    if constexpr (!AT_ && BM == 128 && (BN == 128 || BN == 192)) {
         const bool needs_bias = e.kind >= CG_EPI_BIAS && e.kind <= CG_EPI_BIAS_DROP_RESID;
         const bool needs_resid = e.kind == CG_EPI_BIAS_RESID || e.kind == CG_EPI_BIAS_DROP_RESID;
         if (!(g_pk_flags & 2) && e.beta == 0.f && (!needs_bias || e.bias) && (!needs_resid || e.resid)) {
@@ -657,7 +672,7 @@ void launch_ek(unsigned grid, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
 }
 
 template <int BM, int BN, int NBUF, int BK = FBK>
-void launch_p(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
+bool launch_p(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
               int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, float* ws,
               hipStream_t st) {
     using G = GeoP<BM, BN, NBUF, BK>;
@@ -667,15 +682,28 @@ void launch_p(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
     if (g_gemm_max_grid > 0 && g_gemm_max_grid < slots) slots = g_gemm_max_grid;
     const unsigned grid = (unsigned)(nitems < slots ? nitems : slots);
 #define FG(AT_, BT_) launch_ek<AT_, BT_, BM, BN, NBUF, BK>(grid, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, kchunk, ws, st)
-    // transposed LDS images need >= 128 rows (DmaP): narrower tiles serve only the layouts they can
-    if (!at && !bt) FG(false, false);
-    else if (!at && bt) {
-        if constexpr (BN >= 128) FG(false, true);
+    // transposed LDS images need a multiple of 128 rows (DmaP, col_swz): other tiles serve only the
+    // layouts they can; false = not launched
+    if (!at && !bt) {
+        FG(false, false);
+        return true;
+    } else if (!at && bt) {
+        if constexpr (BN % 128 == 0) {
+            FG(false, true);
+            return true;
+        }
     } else if (at && !bt) {
-        if constexpr (BM >= 128) FG(true, false);
+        if constexpr (BM % 128 == 0 && BN != 192) {
+            FG(true, false);
+            return true;
+        }
     } else {
-        if constexpr (BM >= 128 && BN >= 128) FG(true, true);
+        if constexpr (BM % 128 == 0 && BN % 128 == 0) {
+            FG(true, true);
+            return true;
+        }
     }
+    return false;
 #undef FG
 }
 
@@ -687,8 +715,11 @@ bool pk_gemm_launch(int v, int at, int bt, int64_t M, int64_t N, int64_t K, cons
                     const bf16_t* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k,
                     float* ws, hipStream_t st) {
     switch (v) {
-        case 9: launch_p<128, 128, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st); return true;
+        case 9: return launch_p<128, 128, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
 #ifdef CG_AB_VARIANTS   // measured-slower A/B tiles (profiles/r1_gemm_scan*.txt, r2_gemm_ring_depth_scan.txt)
+        case 18:   // 128x192, one block (6 waves) per CU, NN/NT only: r3_gemm_128x192_ab.txt
+            if (at || bt || N % 192 || split_k != 1) return false;
+            return launch_p<128, 192, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
         case 10: launch_p<128, 128, 3>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st); return true;
         case 11:
             if (M % 256) return false;

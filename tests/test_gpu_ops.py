@@ -247,6 +247,7 @@ _GEMM_VARIANTS = ([(1, 0), (2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (7, 0), (8, 0
                    (9, 5), (10, 0), (10, 7), (11, 0), (11, 3), (12, 0),
                    (20, 0), (21, 0), (21, 3), (22, 0), (22, 5), (23, 0), (23, 7),
                    (24, 0), (24, 1), (25, 0), (25, 2)]
+                  + [(18, 0), (18, 3)]
                   if "_ab" in os.environ.get("CHARPT_LIB", "") else [(2, 0), (9, 0), (9, 5), (24, 0), (24, 1)])
 
 
@@ -830,3 +831,53 @@ def test_deferred_partial_reduces_match_immediate():
         assert torch.equal(a, b)
     want1 = parts[1].double().sum(0) + extra.double().sum(0)
     assert relerr(got[1], want1) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K", [(16384, 384, 384), (16384, 384, 1536), (512, 384, 256), (1024, 768, 192)])
+def test_gemm_128x192_matches_128x128_bitwise(M, N, K):
+    """The one-block-per-CU 128x192 persistent tile (A/B build, gemm_variant 18: measured slower than
+    the 128x128 tile at the C2 projection / FFN2 forwards, profiles/r3_gemm_128x192_ab.txt) walks the same K order with the same MFMA sequence per 64x64 wave
+    sub-tile as the 128x128 one, so every fused epilogue it takes gives the same bits: plain store
+    (bf16 / fp32), bias, bias+ReLU, bias+residual, bias+dropout+residual, ReLU-backward (bf16 aux);
+    also with the grid capped (several items per block)."""
+    from replicatinggpt_amd import _lib as L
+    lib = L.load()
+    if lib.cg_set_tuning(b"gemm_variant", 18) != 0:
+        pytest.skip("gemm_variant 18 is A/B-only (not in this library build)")
+    L.check(lib.cg_set_tuning(b"gemm_variant", 0))
+    torch.manual_seed(11)
+    A = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    B = torch.randn(N, K, device=DEV).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV)
+    resid = torch.randn(M, N, device=DEV)
+    aux = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    call = torch.tensor([4], dtype=torch.int64, device=DEV)
+    cases = [(0, torch.bfloat16, False), (0, torch.float32, False), (1, torch.bfloat16, False),
+             (2, torch.bfloat16, False), (3, torch.float32, False), (4, torch.float32, True),
+             (5, torch.bfloat16, False)]
+
+    def run(variant, grid):
+        L.check(lib.cg_set_tuning(b"gemm_variant", variant))
+        L.check(lib.cg_set_tuning(b"gemm_max_grid", grid))
+        outs = []
+        try:
+            for epi, dt, drop in cases:
+                o = torch.empty(M, N, dtype=dt, device=DEV)
+                ops().gemm(A, B, o, True, False, False, M, N, K, K, K, N, epi,
+                           bias if epi in (1, 2, 3, 4) else None, resid if epi in (3, 4) else None, N,
+                           aux if epi == 5 else None, N, 0.2 if drop else 0.0, 21, call if drop else None, 2,
+                           0.0, 1, None)
+                outs.append(o)
+            torch.cuda.synchronize()
+        finally:
+            L.check(lib.cg_set_tuning(b"gemm_variant", 0))
+            L.check(lib.cg_set_tuning(b"gemm_max_grid", 0))
+        return outs
+
+    ref = run(9, 0)
+    for grid in (0, 37):
+        got = run(18, grid)
+        for (epi, dt, _), a, b in zip(cases, ref, got):
+            assert torch.equal(a, b), (epi, dt, grid)
+    want = A.double().cpu() @ B.double().cpu().t()
+    assert relerr(ref[1], want) < 1e-5
