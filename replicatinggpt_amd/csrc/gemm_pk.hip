@@ -342,15 +342,15 @@ constexpr int EK_ANY = -1, EK_SLAB = 6;
 // flight at two blocks per CU; same bits -- kchunk stays a multiple of 64, same k order.  Measured
 // 10-15 % slower on every C2 shape: 64-B row segments double the TA/TCP requests,
 // profiles/r3_gemm_bk32.txt -- no launcher instantiates it)
-template <bool AT, bool BT, int BM, int BN, int NBUF, int EK = EK_ANY, int BK = FBK>
-// amdgpu_waves_per_eu: LDS caps residency at OCC blocks, so tell the scheduler the real occupancy;
-// left at its default it schedules for 8+ waves/SIMD, keeps ONE A fragment register and waits
-// lgkmcnt(0) before every 4 MFMAs (LDS latency exposed 8x per K-tile)
-__global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, (GeoP<BM, BN, NBUF, BK>::OCC))
-__attribute__((amdgpu_waves_per_eu(1, GeoP<BM, BN, NBUF, BK>::WPE)))
-void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
-               const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype, int64_t ldc,
-               EpiArgs epi, int split_k, int64_t kchunk, float* __restrict__ ws, int flags, RedJobs red) {
+// The kernel body.  GRP: a grouped weight-gradient launch (gemm_common.h WgGroup): every item's
+// problem -- operands, leading dimensions, M / N, split, slab workspace -- comes from the group
+// table g; M ... ws and red are unused.
+template <bool AT, bool BT, int BM, int BN, int NBUF, int EK, int BK, bool GRP>
+__device__ __forceinline__ void pk_body(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
+                                        const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype,
+                                        int64_t ldc, const EpiArgs& epi, int split_k, int64_t kchunk,
+                                        float* __restrict__ ws, int flags, const RedJobs& red, const WgGroup* grp) {
+    static_assert(!GRP || (AT && BT && EK == EK_SLAB && BM == 128 && BN == 128), "grouped: weight gradients only");
     static_assert(BK == 64 || BK == 32, "BK");
     static_assert(!GeoP<BM, BN, NBUF, BK>::ONE_PER_CU || (NBUF == 2 && !AT && !BT),
                   "128x192: uneven per-wave DMA counts need the 2-stage ring's DMA-count-free waits; "
@@ -363,15 +363,22 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / G::WN, wn = wave % G::WN;
-    const int tilesN = (int)(N / BN);
-    const int ntiles = (int)(M / BM) * tilesN;
-    const int nitems = ntiles * split_k;
+    const int tilesN = GRP ? 0 : (int)(N / BN);
+    const int ntiles = GRP ? 0 : (int)(M / BM) * tilesN;
+    const int nitems = GRP ? grp->nitems : ntiles * split_k;
     // split s covers K-tiles [s*nkc, min((s+1)*nkc, nkt)): the last split may be shorter (uneven
     // split-K: any split count, not only divisors of the K-tile count)
-    const int nkt = (int)(K / BK), nkc = (int)(kchunk / BK);
+    const int nkt = GRP ? 0 : (int)(K / BK), nkc = GRP ? 0 : (int)(kchunk / BK);
     const int P = gridDim.x, b = blockIdx.x;
     const int my_items = b < nitems ? (nitems - 1 - b) / P + 1 : 0;
-    auto split_nk = [&](int sp) { return nkt - sp * nkc < nkc ? nkt - sp * nkc : nkc; };
+    auto split_nk = [&](int sp, int pr) {
+        if constexpr (GRP) {
+            const WgJob& J = grp->j[pr];
+            return J.nkt - sp * J.nkc < J.nkc ? J.nkt - sp * J.nkc : J.nkc;
+        } else {
+            return nkt - sp * nkc < nkc ? nkt - sp * nkc : nkc;
+        }
+    };
     const uint64_t stream =
         (epi.kind == CG_EPI_BIAS_DROP_RESID && epi.thr && split_k == 1) ? dropout_stream(epi.rng_call, epi.site) : 0;
 
@@ -385,27 +392,40 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
 #else
     constexpr bool WI_NODMA = false, WI_NOMFMA = false, WI_NOEPI = false;
 #endif
-    da.init(lda, wave < G::AW ? wave : 0, lane);
-    db.init(ldb, wave, lane);
+    if constexpr (!GRP) {   // grouped: (re)set whenever the DMA cursor enters another problem
+        da.init(lda, wave < G::AW ? wave : 0, lane);
+        db.init(ldb, wave, lane);
+    }
 
-    auto decode = [&](int j, int64_t& m0, int64_t& n0, int& split) {
+    auto decode = [&](int j, int64_t& m0, int64_t& n0, int& split, int& pr) {
         const int it = xcd_remap(b + j * P, nitems);
-        split = it / ntiles;
         int tm, tn;
-        tile_rc(it - split * ntiles, ntiles / tilesN, tilesN, flags >> 8, tm, tn);
+        if constexpr (GRP) {
+            pr = 0;
+            while (pr + 1 < grp->n && it >= grp->j[pr + 1].item0) ++pr;
+            const WgJob& J = grp->j[pr];
+            const int li = it - J.item0;
+            split = li / J.ntiles;
+            tile_rc(li - split * J.ntiles, J.ntiles / J.tilesN, J.tilesN, flags >> 8, tm, tn);
+        } else {
+            pr = 0;
+            split = it / ntiles;
+            tile_rc(it - split * ntiles, ntiles / tilesN, tilesN, flags >> 8, tm, tn);
+        }
         m0 = (int64_t)tm * BM;
         n0 = (int64_t)tn * BN;
     };
     int total = 0;
     for (int j = 0; j < my_items; ++j) {
         int64_t m0, n0;
-        int sp;
-        decode(j, m0, n0, sp);
-        total += split_nk(sp);
+        int sp, pr;
+        decode(j, m0, n0, sp, pr);
+        total += split_nk(sp, pr);
     }
 
     // DMA issue cursor (item ij, K-tile ikt) and its operand origins
     int ij = 0, ikt = 0, ink = 0;   // ink: K-tiles of the DMA cursor's item
+    int dpr = -1;                    // GRP: the problem the DMA lane offsets were set up for
     const bf16_t* oa = A;
     const bf16_t* ob = B;
     // The in-loop DMA is split from its address bookkeeping: prep_next() (branchy: item decode at
@@ -420,12 +440,24 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         if (real) {
             if (ikt == 0) {
                 int64_t m0, n0;
-                int sp;
-                decode(ij, m0, n0, sp);
-                ink = split_nk(sp);
-                const int64_t kb = sp * kchunk;
-                oa = AT ? A + kb * lda + m0 : A + m0 * lda + kb;
-                ob = BT ? B + kb * ldb + n0 : B + n0 * ldb + kb;
+                int sp, pr;
+                decode(ij, m0, n0, sp, pr);
+                ink = split_nk(sp, pr);
+                if constexpr (GRP) {
+                    const WgJob& J = grp->j[pr];
+                    if (pr != dpr) {
+                        da.init(J.lda, wave, lane);
+                        db.init(J.ldb, wave, lane);
+                        dpr = pr;
+                    }
+                    const int64_t kb = sp * J.kchunk;
+                    oa = J.A + kb * J.lda + m0;   // AT and BT (static_assert above)
+                    ob = J.B + kb * J.ldb + n0;
+                } else {
+                    const int64_t kb = sp * kchunk;
+                    oa = AT ? A + kb * lda + m0 : A + m0 * lda + kb;
+                    ob = BT ? B + kb * ldb + n0 : B + n0 * ldb + kb;
+                }
             }
             na = oa + ikt * da.kstep;
             nbp = ob + ikt * db.kstep;
@@ -467,9 +499,9 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     int cnk;   // K-tiles of the compute cursor's item
     {
         int64_t m0, n0;
-        int sp;
-        decode(0, m0, n0, sp);
-        cnk = my_items ? split_nk(sp) : 0;
+        int sp, pr;
+        decode(0, m0, n0, sp, pr);
+        cnk = my_items ? split_nk(sp, pr) : 0;
     }
     bool stored = false;
 #ifdef CG_PK_STAMPS
@@ -567,10 +599,17 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         if (++ckt == cnk) {
             // item done: acc[i][j][r] = C[mw + 16i + (lane&15)][nw + 16j + 4(lane>>4) + r]
             int64_t m0, n0;
-            int sp;
-            decode(cj, m0, n0, sp);
+            int sp, pr;
+            decode(cj, m0, n0, sp, pr);
             const int64_t mr = m0 + wm * 64 + (lane & 15), nc = n0 + wn * 64 + 4 * (lane >> 4);
             if (WI_NOEPI) {
+            } else if (GRP) {
+                const WgJob& J = grp->j[pr];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        *(fv4*)(J.ws + ((int64_t)sp * J.M + mr + 16 * i) * J.N + nc + 16 * j) = acc[i][j];
             } else if (EK == EK_SLAB || split_k > 1) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
@@ -594,9 +633,9 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
             ++cj;
             if (cj < my_items) {
                 int64_t m1, n1;
-                int sp1;
-                decode(cj, m1, n1, sp1);
-                cnk = split_nk(sp1);
+                int sp1, pr1;
+                decode(cj, m1, n1, sp1, pr1);
+                cnk = split_nk(sp1, pr1);
             }
             stored = true;
 #ifdef CG_PK_STAMPS
@@ -616,8 +655,33 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     }
 #endif
     wait_vm<0>();  // the dummy DMAs past the last K-tile land before the workgroup's LDS is released
-    if (red.n) red_tail(red);   // a deferred split-K reduce of an earlier launch (gemm_common.h)
+    if (!GRP && red.n) red_tail(red);   // a deferred split-K reduce of an earlier launch (gemm_common.h)
 }
+
+template <bool AT, bool BT, int BM, int BN, int NBUF, int EK = EK_ANY, int BK = FBK>
+// amdgpu_waves_per_eu: LDS caps residency at OCC blocks, so tell the scheduler the real occupancy;
+// left at its default it schedules for 8+ waves/SIMD, keeps ONE A fragment register and waits
+// lgkmcnt(0) before every 4 MFMAs (LDS latency exposed 8x per K-tile)
+__global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, (GeoP<BM, BN, NBUF, BK>::OCC))
+__attribute__((amdgpu_waves_per_eu(1, GeoP<BM, BN, NBUF, BK>::WPE)))
+void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
+               const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype, int64_t ldc,
+               EpiArgs epi, int split_k, int64_t kchunk, float* __restrict__ ws, int flags, RedJobs red) {
+    pk_body<AT, BT, BM, BN, NBUF, EK, BK, false>(M, N, K, A, lda, B, ldb, Cv, c_dtype, ldc, epi, split_k, kchunk, ws,
+                                                 flags, red, nullptr);
+}
+
+// the grouped weight-gradient launch (128x128, 2-stage ring, slab epilogue)
+__global__ __launch_bounds__(256, (GeoP<128, 128, 2, FBK>::OCC))
+__attribute__((amdgpu_waves_per_eu(1, GeoP<128, 128, 2, FBK>::WPE)))
+void k_gemm_pk_grp(WgGroup grp, int flags) {
+    const RedJobs none = {};
+    pk_body<true, true, 128, 128, 2, EK_SLAB, FBK, true>(0, 0, 0, nullptr, 0, nullptr, 0, nullptr, CG_F32, 0,
+                                                          EpiArgs{}, 1, 0, nullptr, flags, none, &grp);
+}
+
+// every grouped problem's slabs summed into its output (one launch; red_jobs = red_tail's order)
+__global__ __launch_bounds__(256) void k_red_multi(RedJobsN jobs) { red_jobs(jobs); }
 
 int cu_count() {
     static int n = 0;
@@ -710,6 +774,26 @@ bool launch_p(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
 }  // namespace
 
 int gemm_cu_count() { return cu_count(); }
+
+// the queued weight gradients as one grouped persistent launch, then one reduce over all their slabs
+bool wgrad_group_launch(const WgGroup& g, hipStream_t st) {
+    if (g.n <= 0 || g.nitems <= 0) return false;
+    using G = GeoP<128, 128, 2, FBK>;
+    int64_t slots = (int64_t)cu_count() * G::OCC;
+    if (g_gemm_max_grid > 0 && g_gemm_max_grid < slots) slots = g_gemm_max_grid;
+    const unsigned grid = (unsigned)(g.nitems < slots ? g.nitems : slots);
+    k_gemm_pk_grp<<<grid, G::THREADS, G::LDS, st>>>(g, g_pk_flags | (g_gemm_group_pk << 8));
+    RedJobsN r = {};
+    int64_t most = 0;
+    for (int q = 0; q < g.n; ++q) {
+        const WgJob& J = g.j[q];
+        r.j[r.n++] = RedJob{J.ws, J.out, J.M * J.N / 4, J.split, J.beta};
+        most = J.M * J.N / 4 > most ? J.M * J.N / 4 : most;
+    }
+    const int64_t blocks = (most + 255) / 256;
+    k_red_multi<<<(unsigned)(blocks < 2048 ? blocks : 2048), 256, 0, st>>>(r);
+    return true;
+}
 
 bool pk_gemm_launch(int v, int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda,
                     const bf16_t* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k,

@@ -881,3 +881,51 @@ def test_gemm_128x192_matches_128x128_bitwise(M, N, K):
             assert torch.equal(a, b), (epi, dt, grid)
     want = A.double().cpu() @ B.double().cpu().t()
     assert relerr(ref[1], want) < 1e-5
+
+
+def test_grouped_weight_gradients_match_single_launches():
+    """cg_set_tuning("defer_wgrad"): split-K weight-gradient products (A^T B, fp32 STORE) are queued
+    and cg_flush_deferred runs them as one grouped persistent launch plus one slab reduce -- the
+    same items and summation order as their own launches, so the same bits: C2-like shapes with
+    uneven splits, beta = 1 accumulation, a second product into a queued output, a capped grid."""
+    import ctypes
+    from replicatinggpt_amd import _lib as L
+    O = ops()
+    lib = L.load()
+    torch.manual_seed(13)
+    K = 4096
+    shapes = [(384, 384, 32, 0.0), (1152, 384, 14, 0.0), (384, 1536, 14, 1.0), (1536, 384, 13, 0.0),
+              (256, 256, 5, 0.0)]
+    dys = [torch.randn(K, m, device=DEV).to(torch.bfloat16) for m, _, _, _ in shapes]
+    xs = [torch.randn(K, n, device=DEV).to(torch.bfloat16) for _, n, _, _ in shapes]
+    init = [torch.randn(m, n, device=DEV) for m, n, _, _ in shapes]
+
+    def run(defer, grid):
+        outs = [t.clone() for t in init]
+        wss = [torch.empty(O.gemm_workspace(m, n, sp) // 4, device=DEV) for m, n, sp, _ in shapes]
+        L.check(lib.cg_set_tuning(b"gemm_max_grid", grid))
+        if defer:
+            L.check(lib.cg_set_tuning(b"defer_wgrad", 1))
+        try:
+            for (m, n, sp, beta), dy, x, o, ws in zip(shapes, dys, xs, outs, wss):
+                O.gemm(dy, x, o, True, True, True, m, n, K, m, n, n, L.EPI_STORE, None, None, 0, None, 0, 0.0, 0,
+                       None, 0, float(beta), sp, ws)
+            # a second product into the first output (beta 1): the queued first one goes out before it
+            ws2 = torch.empty(O.gemm_workspace(384, 384, 8) // 4, device=DEV)
+            O.gemm(dys[0], xs[0], outs[0], True, True, True, 384, 384, K, 384, 384, 384, L.EPI_STORE, None, None,
+                   0, None, 0, 0.0, 0, None, 0, 1.0, 8, ws2)
+        finally:
+            if defer:
+                L.check(lib.cg_set_tuning(b"defer_wgrad", 0))
+            L.check(lib.cg_set_tuning(b"gemm_max_grid", 0))
+        L.check(lib.cg_flush_deferred(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+        torch.cuda.synchronize()
+        return [o.cpu() for o in outs]
+
+    ref = run(False, 0)
+    for grid in (0, 77):
+        got = run(True, grid)
+        for a, b in zip(ref, got):
+            assert torch.equal(a, b), grid
+    want = dys[2].double().cpu().t() @ xs[2].double().cpu() + init[2].double().cpu()
+    assert relerr(ref[2], want) < 1e-5

@@ -59,17 +59,18 @@ def test_deferred_splitk_reduces_bit_identical():
     gradients at B*T = 16384), graph replay with and without deferral, eager, and the segmented
     (DP-overlap) backward whose segments each flush their pending reduces.  The LayerNorm / b1
     column-sum reduces queued for one multi-job launch at the flush (DEFER.partials) likewise,
-    with and without the split-K deferral."""
+    with and without the split-K deferral, and the weight-gradient GEMMs grouped into one persistent
+    launch (defer_wgrad)."""
     from replicatinggpt_amd import functional as Fn
     from replicatinggpt_amd.engine import GradReducer, TrainStep
     cfg = _cfg(block_size=256, n_embd=384, n_head=6, n_layers=3, batch_size=64)
     runs = []
-    saved = Fn.DEFER.enabled, Fn.DEFER.partials_on
+    saved = Fn.DEFER.enabled, Fn.DEFER.partials_on, Fn.DEFER.wgrad_on
     try:
-        for defer, partials, graph, overlap in ((False, False, True, False), (True, True, True, False),
-                                                (True, True, False, False), (True, True, True, True),
-                                                (True, False, True, False)):
-            Fn.DEFER.enabled, Fn.DEFER.partials_on = defer, partials
+        for defer, partials, wg, graph, overlap in ((False, False, False, True, False), (True, True, True, True, False),
+                                                    (True, True, True, False, False), (True, True, True, True, True),
+                                                    (True, False, False, True, False), (True, True, False, True, False)):
+            Fn.DEFER.enabled, Fn.DEFER.partials_on, Fn.DEFER.wgrad_on = defer, partials, wg
             m, opt, s = _setup(cfg)
             red = GradReducer(m.flat.grad) if overlap else None   # world size 1: the segmentation only
             st = TrainStep(m, opt, s, red, use_graph=graph, overlap=overlap, seg_layers=1)
@@ -78,7 +79,7 @@ def test_deferred_splitk_reduces_bit_identical():
             torch.cuda.synchronize()
             runs.append((losses, m.flat.master.detach().cpu().clone(), m.flat.grad.detach().cpu().clone()))
     finally:
-        Fn.DEFER.enabled, Fn.DEFER.partials_on = saved
+        Fn.DEFER.enabled, Fn.DEFER.partials_on, Fn.DEFER.wgrad_on = saved
     for r in runs[1:]:
         assert r[0] == runs[0][0]
         assert torch.equal(r[1], runs[0][1]) and torch.equal(r[2], runs[0][2])
