@@ -222,7 +222,8 @@ extern "C" int cg_head_bwd(const float* logits, const float* lse, const int64_t*
     const int nb = ceil_div(M, HEAD_ROWS);
     k_head_bwd<<<nb, 256, 0, st>>>(logits, lse, targets, g_loss, g_mult, g_logits, (int)V, M, (bf16_t*)dl, (int)ld_dl,
                                    (float*)workspace);
-    if (db) launch_reduce_partials((const float*)workspace, nb, V, db, nullptr, V, db_accumulate, st);
+    if (db)   // queued while defer_partials is set (functional.DEFER, db a flat gradient slot)
+        reduce_partials_deferrable((const float*)workspace, nb, V, db, nullptr, nullptr, V, db_accumulate, 0, st);
     CG_LAUNCH_CHECK("cg_head_bwd");
     return CG_OK;
 }

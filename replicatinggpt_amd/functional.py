@@ -801,8 +801,10 @@ class HeadLossFn(torch.autograd.Function):
         gl = None if g_logits is None else g_logits.reshape(M, V).float().contiguous()
         if g_loss is None:
             t1 = None
-        ops.head_bwd(logits, lse, t1, None if g_loss is None else g_loss.reshape(1).float().contiguous(), 1.0 / M,
-                     gl, dl, gb, bool(beta_b), ws)
+        # the lm_head bias gradient's column-sum reduce joins DEFER's multi-job flush when it targets the slot
+        with DEFER.partials(ws) if (gb is not None and gb is lm_b.slot) else contextlib.nullcontext():
+            ops.head_bwd(logits, lse, t1, None if g_loss is None else g_loss.reshape(1).float().contiguous(), 1.0 / M,
+                         gl, dl, gb, bool(beta_b), ws)
         g, beta, f_lw = lm_w.grad_target()
         if g is not None:
             if g.data_ptr() == lm_w.slot.data_ptr():

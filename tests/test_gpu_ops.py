@@ -638,12 +638,14 @@ def test_attention_bwd_regenerates_mask():
     assert torch.equal(g1, g2)
 
 
-def test_embedding_fwd_bwd():
+@pytest.mark.parametrize("V,T,C,B", [(65, 40, 126, 3), (65, 256, 384, 64), (65, 100, 200, 5)])
+def test_embedding_fwd_bwd(V, T, C, B):
+    """Token + position embeddings and their deterministic backward (the token gradient's 4-wave
+    partial histograms, added in wave then chunk order) against fp64, ragged and C2-sized."""
     Fn = F()
-    V, T, C, B = 65, 40, 126, 3
     torch.manual_seed(6)
     wte = torch.randn(V, C)
-    wpe = torch.randn(64, C)
+    wpe = torch.randn(max(64, T), C)
     idx = torch.randint(0, V, (B, T))
     x = torch.empty(B, T, C, device=DEV)
     ops().embed_fwd(idx.to(DEV), wte.to(DEV), wpe.to(DEV), x)
@@ -651,12 +653,12 @@ def test_embedding_fwd_bwd():
     assert relerr(x, ref) < 1e-6
     dx = torch.randn(B, T, C)
     dwte = torch.empty(V, C, device=DEV)
-    dwpe = torch.empty(64, C, device=DEV)
+    dwpe = torch.empty(max(64, T), C, device=DEV)
     ws = torch.empty(ops().embed_bwd_workspace(B, T, C, V) // 4 + 1, device=DEV)
     ops().embed_bwd(idx.to(DEV), dx.to(DEV), dwte, dwpe[:T], False, ws)
     want_te = torch.zeros(V, C, dtype=torch.float64).index_add_(0, idx.reshape(-1), dx.reshape(-1, C).double())
-    assert relerr(dwte, want_te) < 1e-6
-    assert relerr(dwpe[:T], dx.double().sum(0)) < 1e-6
+    assert relerr(dwte, want_te) < 2e-6
+    assert relerr(dwpe[:T], dx.double().sum(0)) < 2e-6
 
 
 def test_cross_entropy():
