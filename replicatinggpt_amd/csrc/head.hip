@@ -28,6 +28,10 @@ __global__ __launch_bounds__(256) void k_head_fwd(const bf16_t* __restrict__ a, 
                                                   int V, const int64_t* __restrict__ tgt, float* __restrict__ logits,
                                                   float* __restrict__ lse, float* __restrict__ loss_part, int64_t M) {
     __shared__ float red[4];
+    // the wave's 16 logit rows staged in LDS in their [row][V] memory order, then written as one
+    // contiguous 16 V-float run with float4 stores (lane-per-row scalar stores touched 16 rows per
+    // instruction: 16.6 us per C2 step for a 4.3 MB write)
+    __shared__ __attribute__((aligned(16))) float stage[4][16 * 16 * VT];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t m0 = (int64_t)blockIdx.x * HEAD_ROWS + wave * 16;
     float my_loss = 0.f;
@@ -86,7 +90,7 @@ __global__ __launch_bounds__(256) void k_head_fwd(const bf16_t* __restrict__ a, 
                 const int n = 16 * t + nb + r;
                 if (n < V) {
                     s += __expf(acc[t][r] - mx);
-                    logits[row * V + n] = acc[t][r];
+                    stage[wave][(lane & 15) * V + n] = acc[t][r];
                     if (n == tr) xt = acc[t][r];
                 }
             }
@@ -94,6 +98,23 @@ __global__ __launch_bounds__(256) void k_head_fwd(const bf16_t* __restrict__ a, 
         s += __shfl_xor(s, 32, 64);
         xt += __shfl_xor(xt, 16, 64);
         xt += __shfl_xor(xt, 32, 64);
+        // every lane's stage writes land before any lane of the wave reads them back
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        {
+            const int64_t nrow = M - m0 < 16 ? M - m0 : 16;
+            const int64_t cnt = nrow * V;           // floats of rows m0 .. m0 + nrow - 1, contiguous
+            float* dst = logits + m0 * V;
+            const float* src = stage[wave];
+            if ((((uintptr_t)dst) & 15) == 0) {
+                const int64_t c4 = cnt >> 2;
+                for (int64_t i = lane; i < c4; i += 64) ((float4*)dst)[i] = ((const float4*)src)[i];
+                for (int64_t i = 4 * c4 + lane; i < cnt; i += 64) dst[i] = src[i];
+            } else {
+                for (int64_t i = lane; i < cnt; i += 64) dst[i] = src[i];
+            }
+        }
         const float l = mx + __logf(s);
         if (lane < 16) {
             lse[row] = l;
