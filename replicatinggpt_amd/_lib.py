@@ -37,6 +37,7 @@ _SIGS = {
     "cg_sum_f32": (c_int, [P, c_i64, c_flt, P, P, P]),
     "cg_cast_f32_bf16": (c_int, [P, P, c_i64, P]),
     "cg_gather_batch": (c_int, [P, c_int, P, P, P, c_i64, c_i64, P]),
+    "cg_gather_batch_ring": (c_int, [P, c_int, P, c_i64, P, P, P, P, P, c_i64, c_i64, P]),
     "cg_embed_fwd": (c_int, [P, P, P, P, c_i64, c_i64, c_i64, c_i64, P]),
     "cg_embed_bwd_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
     "cg_embed_bwd": (c_int, [P, P, P, P, c_i64, c_i64, c_i64, c_i64, c_int, P, P]),
@@ -78,6 +79,7 @@ _SIGS = {
                                P]),
     "cg_decode_sample": (c_int, [P, c_i64, c_i64, c_i64, c_int, P, P, P, c_i64, P]),
     "cg_adamw": (c_int, [P, P, P, P, P, c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, P, P]),
+    "cg_adamw_step": (c_int, [P, P, P, P, P, c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, P, P]),
 }
 
 _lib = None

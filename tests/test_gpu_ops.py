@@ -774,6 +774,35 @@ def test_adamw_matches_torch():
     assert torch.equal(sh.cpu(), pd.cpu().to(torch.bfloat16))
 
 
+@pytest.mark.parametrize("n,off", [(1000, 0), (1003, 1), (1 << 23, 0)])
+def test_adamw_step_advances_its_own_counter(n, off):
+    """cg_adamw_step (the training path's launch: the step count advanced by the launch's last block,
+    optim.py) equals counter_add + cg_adamw bit for bit over 4 steps, leaves {step, ticket} =
+    {4, 0}; a misaligned slice (element-wise path) and an 8192-block grid included."""
+    torch.manual_seed(9)
+    p0 = torch.randn(n + off, device=DEV)
+    outs = []
+    for fused in (False, True):
+        p = p0.clone()[off:]
+        m = torch.zeros(n + off, device=DEV)[off:]
+        v = torch.zeros(n + off, device=DEV)[off:]
+        sh = torch.empty(n + off, dtype=torch.bfloat16, device=DEV)[off:]
+        ctl = torch.zeros(2, dtype=torch.int64, device=DEV)
+        gen = torch.Generator(device=DEV).manual_seed(4)
+        for _ in range(4):
+            g = torch.randn(n + off, device=DEV, generator=gen)[off:]
+            if fused:
+                ops().adamw_step(p, g, m, v, sh, 2e-4, 0.9, 0.999, 1e-8, 1e-2, ctl)
+            else:
+                ops().counter_add(ctl[:1], 1)
+                ops().adamw(p, g, m, v, sh, 2e-4, 0.9, 0.999, 1e-8, 1e-2, ctl[:1])
+        torch.cuda.synchronize()
+        outs.append((p.cpu(), m.cpu(), v.cpu(), sh.cpu(), ctl.cpu()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert outs[1][4].tolist() == [4, 0]
+
+
 def test_bf16_rounding_matches_torch():
     """Every bf16 the kernels write goes through gfx950's v_cvt_pk_bf16_f32 (csrc/common.h
     f2bf / pack_bf2): round-to-nearest-even, bit-identical to torch's float -> bfloat16 cast,
