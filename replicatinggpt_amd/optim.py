@@ -5,10 +5,16 @@ GEMMs read.  The step count lives on the device, so the whole optimizer step is 
 hipGraph.  Numerics follow torch/optim/adam.py ``_single_tensor_adam`` (decoupled weight decay,
 bias-corrected moments, same fp32 operation order).
 """
+import os
+
 import torch
 
 from . import functional as Fn
 from . import ops
+
+# CHARPT_ADAMW_FUSED_STEP=1: the flat launch advances the step count itself (cg_adamw_step, one launch
+# instead of counter_add + adamw); off by default until measured on the MI355X
+FUSED_STEP = os.environ.get("CHARPT_ADAMW_FUSED_STEP", "0") == "1"
 
 
 class AdamW(torch.optim.Optimizer):
@@ -92,7 +98,11 @@ class AdamW(torch.optim.Optimizer):
         args = (float(grp["lr"]), float(b1), float(b2), float(grp["eps"]), float(grp["weight_decay"]))
         if not missing and self._psteps is None:
             # the training path: every parameter has a gradient, one launch over the flat buffers
-            ops.adamw_step(st.master, st.grad, self._m, self._v, st.shadow, *args, self._step_ctl)
+            if FUSED_STEP:
+                ops.adamw_step(st.master, st.grad, self._m, self._v, st.shadow, *args, self._step_ctl)
+            else:
+                ops.counter_add(self._step_t, 1)
+                ops.adamw(st.master, st.grad, self._m, self._v, st.shadow, *args, self._step_t)
         else:
             # torch.optim.AdamW skips parameters whose .grad is None (no decay, no moment update,
             # no step count): per-parameter launches over the flat slices, per-parameter step counts
