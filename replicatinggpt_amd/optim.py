@@ -13,7 +13,7 @@ from . import functional as Fn
 from . import ops
 
 # CHARPT_ADAMW_FUSED_STEP=1: the flat launch advances the step count itself (cg_adamw_step, one launch
-# instead of counter_add + adamw); off by default until measured on the MI355X
+# instead of counter_add + adamw); off by default: measured slower
 FUSED_STEP = os.environ.get("CHARPT_ADAMW_FUSED_STEP", "0") == "1"
 
 
