@@ -90,22 +90,75 @@ def cpu_baseline(cfg, seconds=12.0, batch=16):
                       f"{cfg.n_layers}L/{cfg.n_head}H/{cfg.n_embd}d (the bench workload's shape)"}
 
 
-def time_gemm(M, N, K, at, bt, epi, dev, reps=30):
-    """Average duration (ms) of one charpt bf16 GEMM launch of this shape: reps back-to-back
-    launches replayed from one hipGraph, HIP events on the replay stream."""
+def census_op(name, M, N, K, at, bt, kind, dev, p=0.2):
+    """Operands and a launch closure for one census GEMM with the epilogue the training step uses
+    (functional.py AttnSublayerFn / FFNSublayerFn): "store" (bf16 output), "bias_resid" (fp32
+    output = x + o W^T + b: the attention projection), "bias_relu_bits" (bf16 relu(a W1^T + b1) and
+    its ReLU keep bits), "bias_drop_resid" (fp32 x + dropout(h W2^T + b2)), "relu_bwd_colpart"
+    (bf16 relu'(h) (dz2 W2) from the keep bits, with the b1 column partials), "wgrad" (fp32,
+    deterministic split-K: the GEMM and its slab reduce).  Returns (run, kernels per call)."""
     from replicatinggpt_amd import functional as Fn, ops
     A = torch.randn((K, M) if at else (M, K), device=dev).to(torch.bfloat16)
     B = torch.randn((K, N) if bt else (N, K), device=dev).to(torch.bfloat16)
-    out = torch.empty(M, N, dtype=torch.bfloat16 if epi != "wgrad" else torch.float32, device=dev)
-    split, ws = 1, None
-    if epi == "wgrad":
+    fp32_out = kind in ("wgrad", "bias_resid", "bias_drop_resid")
+    out = torch.empty(M, N, dtype=torch.float32 if fp32_out else torch.bfloat16, device=dev)
+    lda, ldb = A.shape[1], B.shape[1]
+    if kind == "wgrad":
         split = Fn._wgrad_split(M, N, K, True)
-        if split > 1:
-            ws = torch.empty(ops.gemm_workspace(M, N, split) // 4, dtype=torch.float32, device=dev)
+        ws = torch.empty(ops.gemm_workspace(M, N, split) // 4, dtype=torch.float32, device=dev) if split > 1 else None
 
-    def run():
-        ops.gemm(A, B, out, True, bool(at), bool(bt), M, N, K, A.shape[1], B.shape[1], N, 0, None, None, 0, None, 0,
-                 0.0, 0, None, 0, 0.0, split, ws)
+        def run():
+            ops.gemm(A, B, out, True, bool(at), bool(bt), M, N, K, lda, ldb, N, 0, None, None, 0, None, 0,
+                     0.0, 0, None, 0, 0.0, split, ws)
+        return run, 2 if split > 1 else 1
+    if kind == "store":
+        def run():
+            ops.gemm(A, B, out, True, bool(at), bool(bt), M, N, K, lda, ldb, N, 0, None, None, 0, None, 0,
+                     0.0, 0, None, 0, 0.0, 1, None)
+        return run, 1
+    bias = torch.randn(N, device=dev) * 0.1
+    if kind in ("bias_resid", "bias_drop_resid"):
+        resid = torch.randn(M, N, device=dev)
+        drop = kind == "bias_drop_resid"
+        call = torch.zeros(1, dtype=torch.int64, device=dev)
+        epi = Fn.EPI["bias_drop_resid" if drop else "bias_resid"]
+
+        def run():
+            ops.gemm(A, B, out, True, bool(at), bool(bt), M, N, K, lda, ldb, N, epi, bias, resid, N, None, 0,
+                     p if drop else 0.0, 4919 if drop else 0, call if drop else None, 3 if drop else 0, 0.0, 1, None)
+        return run, 1
+    from replicatinggpt_amd import _lib as L
+    bits = torch.randint(-2 ** 31, 2 ** 31 - 1, (M, N // 32), dtype=torch.int32, device=dev)
+    lib = L.load()
+    if kind == "bias_relu_bits":
+        if not lib.cg_gemm_relu_bits_supported(0, 0, M, N, K, lda, ldb, N):   # the step's fallback
+            def run():
+                ops.gemm(A, B, out, True, False, False, M, N, K, lda, ldb, N, Fn.EPI["bias_relu"], bias, None, 0,
+                         None, 0, 0.0, 0, None, 0, 0.0, 1, None)
+            return run, 1
+
+        def run():
+            ops.gemm_bias_relu_bits(A, B, out, M, N, K, lda, ldb, N, bias, bits, bits.stride(0))
+        return run, 1
+    if kind == "relu_bwd_colpart":
+        part = torch.empty((M // 64, N), dtype=torch.float32, device=dev)
+        if not lib.cg_gemm_colpart_supported(0, 1, M, N, K, lda, ldb, N):   # the step's fallback (no partials)
+            def run():
+                ops.gemm(A, B, out, True, False, True, M, N, K, lda, ldb, N, Fn.EPI["relu_bwd"], None, None, 0,
+                         bits, bits.stride(0), 0.0, 0, None, 0, 0.0, 1, None)
+            return run, 1
+
+        def run():
+            ops.gemm_relu_bwd_colpart(A, B, out, M, N, K, lda, ldb, N, bits, bits.stride(0), part)
+        return run, 1
+    raise ValueError(kind)
+
+
+def time_gemm(name, M, N, K, at, bt, kind, dev, reps=30):
+    """Average duration (ms) of one charpt bf16 GEMM launch of this shape with the step's epilogue
+    (census_op): reps back-to-back launches replayed from one hipGraph, HIP events on the replay
+    stream."""
+    run, _ = census_op(name, M, N, K, at, bt, kind, dev)
     for _ in range(3):
         run()
     # the reps launches replayed from a hipGraph, as in the training step: eagerly, the smallest
@@ -118,7 +171,7 @@ def time_gemm(M, N, K, at, bt, epi, dev, reps=30):
             run()
     g.replay()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
+    s.record()   # the replay runs on the current stream
     g.replay()
     e.record()
     e.synchronize()
@@ -126,28 +179,32 @@ def time_gemm(M, N, K, at, bt, epi, dev, reps=30):
 
 
 def census_shapes(cfg, Bsz, T):
-    """Every bf16 GEMM of one training step: (name, M, N, K, a_trans, b_trans, kind, launches/step)."""
+    """Every bf16 GEMM of one training step with the epilogue the step gives it:
+    (name, M, N, K, a_trans, b_trans, epilogue kind (census_op), launches/step)."""
     M, d, L = Bsz * T, cfg.n_embd, cfg.n_layers
     F4 = 4 * d
     return [
-        ("qkv_fwd", M, 3 * d, d, 0, 0, "fwd", L), ("proj_fwd", M, d, d, 0, 0, "fwd", L),
-        ("ffn1_fwd", M, F4, d, 0, 0, "fwd", L), ("ffn2_fwd", M, d, F4, 0, 0, "fwd", L),
-        ("proj_dgrad", M, d, d, 0, 1, "fwd", L), ("qkv_dgrad", M, d, 3 * d, 0, 1, "fwd", L),
-        ("ffn2_dgrad", M, F4, d, 0, 1, "fwd", L), ("ffn1_dgrad", M, d, F4, 0, 1, "fwd", L),
+        ("qkv_fwd", M, 3 * d, d, 0, 0, "store", L), ("proj_fwd", M, d, d, 0, 0, "bias_resid", L),
+        ("ffn1_fwd", M, F4, d, 0, 0, "bias_relu_bits", L), ("ffn2_fwd", M, d, F4, 0, 0, "bias_drop_resid", L),
+        ("proj_dgrad", M, d, d, 0, 1, "store", L), ("qkv_dgrad", M, d, 3 * d, 0, 1, "store", L),
+        ("ffn2_dgrad", M, F4, d, 0, 1, "relu_bwd_colpart", L), ("ffn1_dgrad", M, d, F4, 0, 1, "store", L),
         ("proj_wgrad", d, d, M, 1, 1, "wgrad", L), ("qkv_wgrad", 3 * d, d, M, 1, 1, "wgrad", L),
         ("ffn2_wgrad", d, F4, M, 1, 1, "wgrad", L), ("ffn1_wgrad", F4, d, M, 1, 1, "wgrad", L),
     ]
 
 
 def gemm_census(cfg, Bsz, T, dev):
-    """Average launch time of every GEMM shape of one training step (HIP events, time_gemm)."""
+    """Average launch time of every GEMM of one training step, each with its step epilogue (HIP
+    events, time_gemm)."""
     from replicatinggpt_amd import functional as Fn
     out = []
-    for name, m, n, k, at, bt, epi, cnt in census_shapes(cfg, Bsz, T):
-        ms = time_gemm(m, n, k, at, bt, epi, dev)
-        split = Fn._wgrad_split(m, n, k, True) if epi == "wgrad" else 1
-        out.append({"name": name, "M": m, "N": n, "K": k, "ms": ms, "launches": cnt, "flops": 2.0 * m * n * k,
-                    "split": split, "kernel": gemm_kernel_name(m, n, at, bt, split, dev)})
+    for name, m, n, k, at, bt, kind, cnt in census_shapes(cfg, Bsz, T):
+        ms = time_gemm(name, m, n, k, at, bt, kind, dev)
+        split = Fn._wgrad_split(m, n, k, True) if kind == "wgrad" else 1
+        out.append({"name": name, "M": m, "N": n, "K": k, "epilogue": kind, "ms": ms, "launches": cnt,
+                    "flops": 2.0 * m * n * k, "split": split,
+                    "kernel": gemm_kernel_name(m, n, at, bt, split, dev)})
+        torch.cuda.empty_cache()
     return out
 
 
@@ -281,16 +338,21 @@ def gemm_family(census):
 
 def pmc_traffic(config, dom):
     """HBM (L2-miss) bytes per launch of the dominant op from the committed rocprofv3 PMC passes
-    (tools/pmc_gemm_traffic.sh + tools/pmc_gemm.py -> profiles/r2_pmc_gemm_traffic_<config>.json,
-    the latest round's file first); None when no file covers this exact shape and split."""
-    for rnd in ("r2", "r1"):
+    (tools/pmc_gemm_traffic.sh + tools/pmc_gemm.py -> profiles/r<N>_pmc_gemm_traffic_<config>.json,
+    the latest round's file first); None when no file covers this exact shape, split and epilogue
+    (files before round 4 timed every forward / dgrad with a plain store: they match only the
+    plain-store and weight-gradient ops)."""
+    for rnd in ("r4", "r3", "r2", "r1"):
         path = os.path.join(ROOT, "profiles", f"{rnd}_pmc_gemm_traffic_{config}.json")
         try:
             op = json.load(open(path))["ops"][dom["name"]]
         except (OSError, KeyError, ValueError):
             continue
-        if (op["M"], op["N"], op["K"], op["split"]) == (dom["M"], dom["N"], dom["K"], dom["split"]):
-            return op["hbm_bytes"]
+        epi = op.get("epilogue", "wgrad" if op["split"] > 1 or dom["name"].endswith("wgrad") else "store")
+        if (op["M"], op["N"], op["K"], op["split"], epi) == (dom["M"], dom["N"], dom["K"], dom["split"],
+                                                             dom["epilogue"]):
+            return {"bytes": op["hbm_bytes"], "algorithmic_bytes": op.get("algorithmic_bytes"),
+                    "source": os.path.relpath(path, ROOT)}
     return None
 
 
@@ -441,11 +503,14 @@ def main():
             dom = max(census, key=lambda c: c["ms"] * c["launches"])
             achieved = dom["flops"] / (dom["ms"] * 1e-3) / 1e12
             roofline = {"bound": "mfma", "kernel": f"cg_gemm bf16 {dom['name']} M={dom['M']} N={dom['N']} K={dom['K']}"
-                                                  f" ({dom['kernel']}, split {dom['split']})",
+                                                  f" ({dom['kernel']}, split {dom['split']}, epilogue {dom['epilogue']})",
                         "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
-                        "traffic": pmc_traffic(args.config, dom), "avg_launch_ms": round(dom["ms"], 5),
+                        "traffic": None, "avg_launch_ms": round(dom["ms"], 5),
                         "gemm_family": gemm_family(census)}
+            pt = pmc_traffic(args.config, dom)
+            if pt is not None:
+                roofline["traffic"], roofline["traffic_source"] = pt["bytes"], pt["source"]
         result = {
             "metric": "train tokens/sec at 1/2/4/8 MI355X + MFMA util, char-GPT block 256",
             "value": round(value, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,

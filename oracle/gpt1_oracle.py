@@ -134,7 +134,7 @@ def site_stream(call, site):
 def _dropout(x, p, seed, stream, idx_of_element):
     keep = philox.keep_mask(seed, stream, idx_of_element, p)
     scale = np.float32(1.0 / (1.0 - p))
-    return x * torch.from_numpy(keep.reshape(x.shape)).to(x.dtype) * float(scale)
+    return x * torch.from_numpy(keep.reshape(x.shape)).to(device=x.device, dtype=x.dtype) * float(scale)
 
 
 def layer_norm(x, w, b, eps=1e-5):                        # nn.LayerNorm, GPT1.py:159-160,173
@@ -146,7 +146,7 @@ def attention(xn, P, prefix, cfg, train, seed, stream, scale_dim=None):
     B, T, C = xn.shape
     H, hs = cfg.n_head, cfg.head_size
     scale = (scale_dim or C) ** -0.5                      # Q1: C ** -0.5 with C = n_embd, GPT1.py:114
-    causal = torch.tril(torch.ones(T, T, dtype=torch.bool))
+    causal = torch.tril(torch.ones(T, T, dtype=torch.bool, device=xn.device))
     outs = []
     for h in range(H):
         hp = f"{prefix}sa_heads.heads.{h}."
@@ -185,7 +185,7 @@ def forward(P, idx, cfg, targets=None, train=False, seed=0, call=0):
     """BigramLanguageModel.forward (GPT1.py:176-194). Returns (logits, loss) with the same
     shapes: logits (B*T, V) when targets are given, (B, T, V) otherwise."""
     B, T = idx.shape
-    x = P["token_embedding_table.weight"][idx] + P["position_embedding_table.weight"][torch.arange(T)]
+    x = P["token_embedding_table.weight"][idx] + P["position_embedding_table.weight"][torch.arange(T, device=idx.device)]
     for l in range(cfg.n_layers):                         # Block.forward, GPT1.py:162-165
         pre = f"blocks.{l}."
         x = x + attention(layer_norm(x, P[pre + "ln1.weight"], P[pre + "ln1.bias"]), P, pre, cfg, train,

@@ -291,13 +291,19 @@ def test_c2_full_size_bf16_step_close_to_fp32():
 
 
 def test_c2_full_size_bf16_step_matches_oracle():
-    """the benchmarked configuration itself (C2: B=64, T=256, d=384, H=6, L=6 --
-    BASELINE configs[1]) on the bf16 path, in training mode at dropout 0.2, against the CPU oracle
-    (fp32 restatement of GPT1.py:176-194 with the same Philox masks) from the same seeded init: one
-    forward / backward.  Loss within 1e-4 relative (measured 2.5e-6); every parameter's gradient
-    within 5e-2 by norm and cosine > 0.999 (measured: median 1.1 %, worst 3.9 % -- the LayerNorm-2 and
-    FFN-1 weight gradients, which sum bf16-rounded activations over all 16 384 tokens;
-    tools/parity_probe.py, profiles/r3_parity_probe.txt)."""
+    """the benchmarked configuration itself (C2: B=64, T=256, d=384,
+    H=6, L=6 -- BASELINE configs[1]) on the bf16 path, in training mode at dropout 0.2, against the
+    CPU oracle (fp32 restatement of GPT1.py:176-194 with the same Philox masks) from the same seeded
+    init: one forward / backward.  Loss within 1e-4 relative.  Gradients, per parameter, against a
+    bound CALIBRATED on torch's own bf16 path: the oracle's forward run under
+    torch.autocast(bfloat16) on the same GPU, inputs, init and masks gives each parameter's
+    torch-bf16 error e_t (by norm, vs the fp32 oracle); charpt's error must be within
+    max(2e-2, 1.25 e_t) by norm, with cosine > 0.999.  Where e_t itself is under 2e-2 this is the
+    north_star's 2e-2 bar.  The LayerNorm-2 / FFN-1 weights are the parameters above it (torch bf16
+    3.5-4.4 %, charpt 3.4-3.9 %): their gradient sums relu'(z) over 16 384 tokens, and bf16 forward
+    rounding of the FFN input flips 0.075 % of the ReLU decisions, whose contributions add as a
+    random walk (error ~ sqrt(flip fraction)) -- an fp32-kept dz1 changes it by 0.2 % (DESIGN §2,
+    tools/bf16_calib.py)."""
     from replicatinggpt_amd import BigramLanguageModel, PRESETS
     cfg = PRESETS["c2"].with_(dtype="bf16")
     ocfg = O.OracleConfig(block_size=256, n_embd=384, n_head=6, n_layers=6, dropout=cfg.dropout)
@@ -313,10 +319,21 @@ def test_c2_full_size_bf16_step_matches_oracle():
     P = O.init_params(ocfg)
     _, rl, rg = O.loss_and_grads(P, idx, tgt, ocfg, train=True, seed=cfg.dropout_seed, call=0)
     assert abs(float(loss.detach()) - float(rl)) < 1e-4 * float(rl)
+    # torch's bf16 path on the same GPU: the oracle's functional forward under autocast
+    Pd = {k: v.to(DEV) for k, v in P.items()}
+    with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+        _, tl, tg = O.loss_and_grads(Pd, idx.to(DEV), tgt.to(DEV), ocfg, train=True, seed=cfg.dropout_seed, call=0)
+    rows = []
     for name, prm in m.named_parameters():
         a, b = prm.grad.double().cpu().flatten(), rg[name].double().flatten()
-        assert float((a - b).norm() / b.norm()) < 5e-2, name
+        e_c = float((a - b).norm() / b.norm())
+        e_t = float((tg[name].double().cpu().flatten() - b).norm() / b.norm())
+        rows.append((name, e_c, e_t))
+        assert e_c < max(2e-2, 1.25 * e_t), (name, e_c, e_t)
         assert float(torch.nn.functional.cosine_similarity(a, b, dim=0)) > 0.999, name
+    worst = max(rows, key=lambda r: r[1])
+    print(f"charpt worst {worst}; torch-bf16 worst {max(rows, key=lambda r: r[2])}; "
+          f"params above 2e-2: charpt {sum(r[1] > 2e-2 for r in rows)}, torch {sum(r[2] > 2e-2 for r in rows)}")
 
 
 def test_adamw_skips_params_without_grad_like_torch():

@@ -461,8 +461,11 @@ def test_attention_fwd_bwd(B, T, H, D, p, dt):
     qkv_d = qkv.to(DEV)
     o = torch.empty(B * T, d, dtype=dt, device=DEV)
     lse, mask = Fn.attention_fwd(qkv_d, B, T, H, D, o, scale, p, 11, call, 7)
-    tol = 1e-5 if dt == torch.float32 else 2e-2
-    assert relerr(o, ref.reshape(B * T, d)) < tol
+    if dt == torch.float32:
+        assert relerr(o, ref.reshape(B * T, d)) < 1e-5
+    else:   # the bf16 bar element by element (conftest.bf16_close), as for dq / dk / dv below
+        ok, st = bf16_close(o, ref.reshape(B * T, d))
+        assert ok, ("o", st)
     dqkv = Fn.attention_bwd(qkv_d, B, T, H, D, o, dout.reshape(B * T, d).to(DEV), lse, scale, p, 11, call, 7, mask)
     dq, dk, dv = dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:]
     if dt == torch.float32:

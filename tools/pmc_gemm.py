@@ -6,7 +6,8 @@ pass, MI355X_MICROARCH.md 'rocprofv3 PMC slots'):
     rocprofv3 --pmc WRITE_SIZE -d <dir> -o write -- python3 tools/pmc_gemm.py run [c2]
     python tools/pmc_gemm.py parse <fetch counter csv> <write counter csv> <out.json> [c2]
 
-`run` launches each census op REPS times back to back, in census order, after all operands exist
+`run` launches each census op (bench.census_op: the step's fused epilogue) REPS times back to back,
+in census order, after all operands exist
 (so the charpt dispatches in the trace are exactly that sequence); an op is one cg_gemm call: the
 GEMM kernel plus, for split-K weight gradients, its reduce kernel.  `parse` walks the charpt
 dispatches in order, assigns them to ops, and reports per-launch bytes averaged over launches 2..REPS
@@ -33,29 +34,41 @@ def plan(config):
     ops = []
     for name, m, n, k, at, bt, kind, _cnt in bench.census_shapes(cfg, cfg.batch_size, cfg.block_size):
         split = Fn._wgrad_split(m, n, k, True) if kind == "wgrad" else 1
-        ops.append({"name": name, "M": m, "N": n, "K": k, "at": at, "bt": bt, "split": split,
+        ops.append({"name": name, "M": m, "N": n, "K": k, "at": at, "bt": bt, "split": split, "epilogue": kind,
                     "kernels": 2 if split > 1 else 1})
     return ops
 
 
+def algorithmic_bytes(op):
+    """Operands read once + output written once + the epilogue's own operands (bench.census_op)."""
+    M, N, K, kind = op["M"], op["N"], op["K"], op["epilogue"]
+    b = 2 * (M * K + N * K)
+    if kind == "wgrad":
+        return b + 4 * M * N
+    if kind == "store":
+        return b + 2 * M * N
+    if kind in ("bias_resid", "bias_drop_resid"):
+        return b + 4 * N + 4 * M * N + 4 * M * N          # bias, fp32 residual read, fp32 output
+    if kind == "bias_relu_bits":
+        return b + 4 * N + 2 * M * N + M * N // 8        # bias, bf16 output, keep bits
+    if kind == "relu_bwd_colpart":
+        return b + M * N // 8 + 2 * M * N + 4 * (M // 64) * N   # keep bits, bf16 output, column partials
+    raise ValueError(kind)
+
+
 def run(config):
     import torch
-    from replicatinggpt_amd import ops as O
+    import bench
     dev = torch.device("cuda")
     todo = []
     for op in plan(config):
-        m, n, k, at, bt, split = op["M"], op["N"], op["K"], op["at"], op["bt"], op["split"]
-        A = torch.randn((k, m) if at else (m, k), device=dev).to(torch.bfloat16)
-        B = torch.randn((k, n) if bt else (n, k), device=dev).to(torch.bfloat16)
-        out = torch.empty(m, n, dtype=torch.float32 if op["kernels"] == 2 or at else torch.bfloat16, device=dev)
-        ws = torch.empty(max(1, O.gemm_workspace(m, n, split) // 4), dtype=torch.float32, device=dev)
-        todo.append((op, A, B, out, ws))
+        fn, nk = bench.census_op(op["name"], op["M"], op["N"], op["K"], op["at"], op["bt"], op["epilogue"], dev)
+        assert nk == op["kernels"]
+        todo.append(fn)
     torch.cuda.synchronize()
-    for op, A, B, out, ws in todo:
+    for fn in todo:
         for _ in range(REPS):
-            O.gemm(A, B, out, True, bool(op["at"]), bool(op["bt"]), op["M"], op["N"], op["K"], A.shape[1],
-                   B.shape[1], op["N"], 0, None, None, 0, None, 0, 0.0, 0, None, 0, 0.0, op["split"],
-                   ws if op["split"] > 1 else None)
+            fn()
     torch.cuda.synchronize()
 
 
@@ -85,11 +98,11 @@ def parse(fetch_csv, write_csv, out_json, config):
         w = [sum(write[i + r * nk:i + (r + 1) * nk]) for r in range(REPS)]
         i += nk * REPS
         fb, wb = sum(f[1:]) / (REPS - 1), sum(w[1:]) / (REPS - 1)
-        alg = 2 * (op["M"] * op["K"] + op["N"] * op["K"]) + (4 if op["kernels"] == 2 or op["at"] else 2) * op["M"] * op["N"]
-        res[op["name"]] = {"M": op["M"], "N": op["N"], "K": op["K"], "split": op["split"],
+        alg = algorithmic_bytes(op)
+        res[op["name"]] = {"M": op["M"], "N": op["N"], "K": op["K"], "split": op["split"], "epilogue": op["epilogue"],
                            "fetch_bytes": round(fb), "write_bytes": round(wb), "hbm_bytes": round(fb + wb),
                            "algorithmic_bytes": alg, "cold_first_launch_bytes": round(f[0] + w[0])}
-        print(f"{op['name']:11s} split {op['split']:2d}  hbm {(fb + wb) / 1e6:8.2f} MB/launch  "
+        print(f"{op['name']:11s} {op['epilogue']:16s} split {op['split']:2d}  hbm {(fb + wb) / 1e6:8.2f} MB/launch  "
               f"(algorithmic {alg / 1e6:7.2f} MB, cold {(f[0] + w[0]) / 1e6:8.2f} MB)")
     json.dump({"config": config, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of "
                "tools/pmc_gemm.py run; FETCH_SIZE x2 (gfx950); mean of launches 2..%d per op" % REPS,

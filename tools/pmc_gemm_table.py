@@ -17,8 +17,8 @@ def load(root, tag):
         for path in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
             with open(path) as f:
                 for r in csv.DictReader(f):
-                    k = re.sub(r"\(.*$", "", r["Kernel_Name"]).replace("void ", "").replace("cg::", "")
-                    k = k.replace("(anonymous namespace)::", "").strip()
+                    k = r["Kernel_Name"].replace("(anonymous namespace)::", "")
+                    k = re.sub(r"\(.*$", "", k).replace("void ", "").replace("cg::", "").strip()
                     acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return acc
 
@@ -51,8 +51,8 @@ def main():
                 ("TCP pending stall (per CU)", m("TCP_PENDING_STALL_CYCLES_sum") / cu),
                 ("SQ->TA addr FIFO full (x4 / SIMD cycles)", 4 * m("SQ_VMEM_TA_ADDR_FIFO_FULL") / simd),
                 ("LDS data FIFO full (x4 / SIMD cycles)", 4 * m("SQ_LDS_DATA_FIFO_FULL") / simd),
-                ("wave wait for any (of wave cycles)", m("SQ_WAIT_ANY") / m("SQ_WAVE_CYCLES")),
-                ("wave wait on s_waitcnt (of wave cycles)", m("SQ_WAIT_INST_ANY") / m("SQ_WAVE_CYCLES")),
+                ("waves parked: s_waitcnt / barrier (SQ_WAIT_ANY)", m("SQ_WAIT_ANY") / m("SQ_WAVE_CYCLES")),
+                ("issue stalls: dependency / pipe (SQ_WAIT_INST_ANY)", m("SQ_WAIT_INST_ANY") / m("SQ_WAVE_CYCLES")),
             ]
             print(f"== {tag}: {k[:70]}  ({len(c.get('SQ_INSTS_MFMA', []))} launches, "
                   f"{gui / 2.1e3:.1f} us at 2.1 GHz)")
