@@ -430,9 +430,6 @@ def main():
     ap.add_argument("--config", default="c2", choices=["c2", "c4", "c1"])
     ap.add_argument("--batch", type=int, default=None, help="sequences per GPU (default: config)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--ring", action="store_true",
-                    help="offsets ring gathered inside the step graph instead of the per-step get_batch "
-                         "(H2D offsets copy + gather outside the graph)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-census", action="store_true")
     ap.add_argument("--no-generate", action="store_true", help="skip the C5 batched-decode measurement")
@@ -466,7 +463,7 @@ def main():
                            generator=torch.Generator().manual_seed(cfg.seed))
     reducer = GradReducer(model.flat.grad) if (world > 1 or args.overlap) else None
     step = TrainStep(model, opt, sampler, reducer, use_graph=not args.no_graph, seg_layers=args.seg_layers,
-                     overlap=None if args.overlap is None else bool(args.overlap), ring=args.ring)
+                     overlap=None if args.overlap is None else bool(args.overlap))
     step.capture()
     _log("captured; warmup")
     for _ in range(args.warmup):

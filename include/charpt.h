@@ -13,6 +13,13 @@
  *     owns every buffer; the library never allocates, frees or synchronises the host.
  *   - every function is stream-ordered on `stream` (a hipStream_t, passed as void*), so it is
  *     capturable into a hipGraph.
+ *   - state: the library keeps no per-call state, with two process-wide exceptions -- the
+ *     cg_set_tuning knobs and the deferred-work queues they enable ("defer_splitk": a split-K
+ *     weight-gradient reduce left for the next persistent GEMM on the same stream or
+ *     cg_flush_deferred; "defer_partials": column-sum reduces queued for one launch at
+ *     cg_flush_deferred).  Those are not thread-safe: set knobs, enable deferral and make the
+ *     calls it affects from one host thread.  Every other entry point is
+ *     reentrant; cg_last_error_string() is per thread.
  *   - return CG_OK (0) or an error code; cg_last_error_string() gives the message.
  *   - dtype codes: CG_F32 = 0 (float), CG_BF16 = 1 (bfloat16 bits, RNE rounding).
  *   - dropout: Philox4x32-10 counter RNG, spec in oracle/philox.py and DESIGN.md; the stream id
@@ -92,12 +99,6 @@ int cg_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, void* stream);
 /* x[b,t] = data[ix[b]+t], y[b,t] = data[ix[b]+t+1]; data is the token stream (int64 or uint8) */
 int cg_gather_batch(const void* data, int data_is_u8, const int64_t* ix, int64_t* x, int64_t* y,
                     int64_t B, int64_t T, void* stream);
-/* same, offsets read from an HBM ring: ix = ring[(ctl[0] % slots)*B ..]; advances ctl[0] by one
-   (ctl[1] is a block ticket, zero between launches) and, when rng_counter is non-NULL, also does
-   cg_rng_snapshot(rng_counter, rng_snap) -- one launch per graph-replayed step (GPT1.py:227)     */
-int cg_gather_batch_ring(const void* data, int data_is_u8, const int64_t* ring, int64_t slots, int64_t* ctl,
-                         uint64_t* rng_counter, uint64_t* rng_snap, int64_t* x, int64_t* y, int64_t B,
-                         int64_t T, void* stream);
 
 /* ---- embeddings (GPT1.py:179-181) ------------------------------------------------------ */
 /* x[b,t,:] = wte[idx[b,t],:] + wpe[t,:]  (fp32)                                          */
@@ -251,11 +252,6 @@ int cg_decode_sample(const float* logits, int64_t ldl, int64_t V, int64_t B, int
    p_bf16: optional bf16 shadow written after the update (GEMM operands).                    */
 int cg_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, double lr, double beta1,
              double beta2, double eps, double weight_decay, const int64_t* step_ptr, void* stream);
-/* same with the step count advanced by the launch itself (torch.optim.AdamW's state['step'] += 1,
-   optim.py:92 ahead of cg_adamw otherwise): step_ctl = {step count, block ticket (0 between
-   launches)}; the update uses step_ctl[0] + 1 and leaves it there.  n > 0.                      */
-int cg_adamw_step(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, double lr,
-                  double beta1, double beta2, double eps, double weight_decay, int64_t* step_ctl, void* stream);
 
 #ifdef __cplusplus
 }

@@ -37,7 +37,6 @@ _SIGS = {
     "cg_sum_f32": (c_int, [P, c_i64, c_flt, P, P, P]),
     "cg_cast_f32_bf16": (c_int, [P, P, c_i64, P]),
     "cg_gather_batch": (c_int, [P, c_int, P, P, P, c_i64, c_i64, P]),
-    "cg_gather_batch_ring": (c_int, [P, c_int, P, c_i64, P, P, P, P, P, c_i64, c_i64, P]),
     "cg_embed_fwd": (c_int, [P, P, P, P, c_i64, c_i64, c_i64, c_i64, P]),
     "cg_embed_bwd_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
     "cg_embed_bwd": (c_int, [P, P, P, P, c_i64, c_i64, c_i64, c_i64, c_int, P, P]),
@@ -79,7 +78,6 @@ _SIGS = {
                                P]),
     "cg_decode_sample": (c_int, [P, c_i64, c_i64, c_i64, c_int, P, P, P, c_i64, P]),
     "cg_adamw": (c_int, [P, P, P, P, P, c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, P, P]),
-    "cg_adamw_step": (c_int, [P, P, P, P, P, c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, P, P]),
 }
 
 _lib = None
@@ -107,13 +105,13 @@ def load():
         fn.argtypes = args
     _lib = lib
     # CHARPT_TUNING="key=value,key=value": kernel-selection knobs for measurement runs (cg_set_tuning)
-    # defer_splitk / defer_partials / defer_wgrad are owned by functional.DEFER (it keeps the slab / partial
+    # defer_splitk / defer_partials are owned by functional.DEFER (it keeps the slab / partial
     # workspaces alive while a reduce is pending), so they cannot be set from here; skip_splitk_reduce (wrong gradients, timing only)
     # additionally needs CHARPT_WHATIF to name it.
     for kv in filter(None, os.environ.get("CHARPT_TUNING", "").split(",")):
         key, _, val = kv.partition("=")
         key = key.strip()
-        if key in ("defer_splitk", "defer_partials", "defer_wgrad") or (key == "skip_splitk_reduce" and
+        if key in ("defer_splitk", "defer_partials") or (key == "skip_splitk_reduce" and
                                      "skip_splitk_reduce" not in os.environ.get("CHARPT_WHATIF", "")):
             raise RuntimeError(f"charpt: CHARPT_TUNING may not set {key}")
         check(lib.cg_set_tuning(key.encode(), int(val)), f"cg_set_tuning({key})")

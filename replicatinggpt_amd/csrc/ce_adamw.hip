@@ -122,12 +122,8 @@ template <bool VEC, bool NT, int U>
 __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const float* __restrict__ g,
                                                float* __restrict__ m, float* __restrict__ v, bf16_t* __restrict__ pb,
                                                int64_t n, double lr, double beta1, double beta2, double eps,
-                                               double wd, int64_t* __restrict__ step_ptr, int inc) {
-    // inc: this launch is step *step_ptr + 1 and advances the counter itself -- every block reads it
-    // here, the last block to finish (behind all those reads, step_ptr[1] is its ticket) writes it
-    const int64_t t_old = inc ? __hip_atomic_load(step_ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-    int64_t t_now = inc ? t_old + 1 : 0;
-    const AdamScalars s = adam_scalars(lr, beta1, beta2, eps, wd, inc ? &t_now : step_ptr);
+                                               double wd, const int64_t* __restrict__ step_ptr) {
+    const AdamScalars s = adam_scalars(lr, beta1, beta2, eps, wd, step_ptr);
     const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
     int64_t i = i0;
@@ -182,16 +178,6 @@ __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const floa
             }
         }
     }
-    if (inc) {
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __threadfence();
-            if (atomicAdd((unsigned long long*)(step_ptr + 1), 1ull) == (unsigned long long)gridDim.x - 1) {
-                step_ptr[0] = t_old + 1;
-                step_ptr[1] = 0;
-            }
-        }
-    }
 }
 
 namespace cg {
@@ -204,7 +190,7 @@ int g_adamw_mode = 0;
 }
 
 static int adamw_launch(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, double lr,
-                        double beta1, double beta2, double eps, double weight_decay, int64_t* step_ptr, int inc,
+                        double beta1, double beta2, double eps, double weight_decay, const int64_t* step_ptr,
                         void* stream) {
     CG_REQUIRE(n >= 0, "cg_adamw: n < 0");
     if (n == 0) return CG_OK;
@@ -217,7 +203,7 @@ static int adamw_launch(float* p, const float* g, float* m, float* v, uint16_t* 
     hipStream_t st = (hipStream_t)stream;
 #define ADAMW(VEC_, NT_, U_)                                                                                \
     k_adamw<VEC_, NT_, U_><<<grid, 256, 0, st>>>(p, g, m, v, (bf16_t*)p_bf16, n, lr, beta1, beta2, eps, \
-                                                 weight_decay, step_ptr, inc)
+                                                 weight_decay, step_ptr)
     const int mode = g_adamw_mode ? g_adamw_mode : (n >= (int64_t)1 << 25 ? 2 : 1);
     if (!vec) ADAMW(false, false, 1);
     else if (mode == 2) ADAMW(true, true, 2);
@@ -231,12 +217,5 @@ static int adamw_launch(float* p, const float* g, float* m, float* v, uint16_t* 
 extern "C" int cg_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, double lr,
                         double beta1, double beta2, double eps, double weight_decay, const int64_t* step_ptr,
                         void* stream) {
-    return adamw_launch(p, g, m, v, p_bf16, n, lr, beta1, beta2, eps, weight_decay, (int64_t*)step_ptr, 0, stream);
-}
-
-extern "C" int cg_adamw_step(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, double lr,
-                             double beta1, double beta2, double eps, double weight_decay, int64_t* step_ctl,
-                             void* stream) {
-    CG_REQUIRE(n > 0, "cg_adamw_step: n <= 0 (the launch advances the step counter)");
-    return adamw_launch(p, g, m, v, p_bf16, n, lr, beta1, beta2, eps, weight_decay, step_ctl, 1, stream);
+    return adamw_launch(p, g, m, v, p_bf16, n, lr, beta1, beta2, eps, weight_decay, step_ptr, stream);
 }

@@ -164,6 +164,19 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 
+// sum over the 16 lanes of each DPP row (lanes 16r .. 16r + 15) with no LDS round trip: the quad
+// butterflies and two row rotations of wave_sum_dpp.  Every lane ends with its row's sum; the
+// association depends on the lane's quad (fixed run to run), so read one fixed lane per row.  Every
+// lane of the wave must be active.  (__shfl_xor over 1, 2, 4, 8 compiled to four ds_bpermute_b32:
+// LDS-pipe instructions with LDS latency in a dependent chain.)
+__device__ __forceinline__ float row16_sum_dpp(float v) {
+    v += dpp_f<0xB1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v += dpp_f<0x4E, 0xf>(v);   // quad_perm [2,3,0,1]
+    v += dpp_f<0x124, 0xf>(v);  // row_ror:4
+    v += dpp_f<0x128, 0xf>(v);  // row_ror:8
+    return v;
+}
+
 // ---------------------------------------------------------------------------------------
 // Philox4x32-10 counter-based dropout RNG (spec: oracle/philox.py; DESIGN.md "Dropout").
 // 16-bit keep decisions, 8 consecutive elements per Philox call:

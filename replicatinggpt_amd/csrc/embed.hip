@@ -122,16 +122,21 @@ __global__ void k_embed_bwd_pos(const float* __restrict__ dx, float* __restrict_
 }
 
 // per row-chunk partial histogram-sum: part[chunk][v][c] = sum_{rows in chunk, idx=v} dx[row][c].
-// A block takes 64 columns of a 128-row chunk; its 4 waves walk rows 32w .. 32w+31 of the chunk in
-// order into their own LDS histograms (lane = column: deterministic, no atomics), which are then
-// added in wave order.  (The former 2-wave blocks walked all 128 rows per lane: 768 waves in flight
-// for a 25 MB read, 20 us per C2 step.)
+// A block takes 64 columns of a 128-row chunk; its EMB_WAVES waves walk rows 128/W w .. of the chunk
+// in order into their own LDS histograms (lane = column: deterministic, no atomics), which are then
+// added in wave order.  4 waves (the 65-character vocabulary: 66.5 KB of histograms; the former
+// 2-wave blocks walked twice the rows per lane, 20 us per C2 step against 14.6) while
+// 4 V 64 4 B fits the LDS, then 2 (V <= 320) and 1 (V <= 640): fewer waves, same per-V bits for
+// a given wave count.
 constexpr int EMB_CHUNK = 128;
-constexpr int EMB_COLS = 64, EMB_WAVES = 4, EMB_RPW = EMB_CHUNK / EMB_WAVES;
+constexpr int EMB_COLS = 64;
 
-__global__ __launch_bounds__(256) void k_embed_bwd_tok_partial(const int64_t* __restrict__ idx,
-                                                               const float* __restrict__ dx, float* __restrict__ part,
-                                                               int64_t rows, int64_t C, int64_t V) {
+template <int EMB_WAVES>
+__global__ __launch_bounds__(64 * EMB_WAVES) void k_embed_bwd_tok_partial(const int64_t* __restrict__ idx,
+                                                                          const float* __restrict__ dx,
+                                                                          float* __restrict__ part, int64_t rows,
+                                                                          int64_t C, int64_t V) {
+    constexpr int EMB_RPW = EMB_CHUNK / EMB_WAVES;
     extern __shared__ __attribute__((aligned(16))) float acc[];  // [EMB_WAVES][V][EMB_COLS]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t c = (int64_t)blockIdx.x * EMB_COLS + lane;
@@ -161,10 +166,10 @@ __global__ __launch_bounds__(256) void k_embed_bwd_tok_partial(const int64_t* __
         }
     }
     __syncthreads();
-    // the chunk's partial: ((w0 + w1) + w2) + w3 per (v, column), all 256 threads over V x 64 entries
+    // the chunk's partial: ((w0 + w1) + w2) + w3 per (v, column), all threads over V x 64 entries
     const int64_t n = V * EMB_COLS;
     float* out = part + chunk * V * C;
-    for (int64_t i = threadIdx.x; i < n; i += 256) {
+    for (int64_t i = threadIdx.x; i < n; i += 64 * EMB_WAVES) {
         const int64_t v = i / EMB_COLS, cc = (int64_t)blockIdx.x * EMB_COLS + (i % EMB_COLS);
         if (cc < C) {
             float t = acc[i];
@@ -200,8 +205,9 @@ extern "C" int64_t cg_embed_bwd_workspace(int64_t B, int64_t T, int64_t C, int64
 extern "C" int cg_embed_bwd(const int64_t* idx, const float* dx, float* dwte, float* dwpe, int64_t B, int64_t T,
                             int64_t C, int64_t V, int accumulate, void* workspace, void* stream) {
     CG_REQUIRE(B > 0 && T > 0 && C > 0 && V > 0, "cg_embed_bwd: bad shape");
-    CG_REQUIRE(EMB_WAVES * V * EMB_COLS * 4 <= 160 * 1024, "cg_embed_bwd: vocab %lld too large for the LDS histogram",
+    CG_REQUIRE(V * EMB_COLS * 4 <= 160 * 1024, "cg_embed_bwd: vocab %lld too large for the LDS histogram",
                (long long)V);
+    const int waves = 4 * V * EMB_COLS * 4 <= 160 * 1024 ? 4 : (2 * V * EMB_COLS * 4 <= 160 * 1024 ? 2 : 1);
     hipStream_t st = (hipStream_t)stream;
     const int64_t rows = B * T;
     if (dwpe) {
@@ -213,8 +219,13 @@ extern "C" int cg_embed_bwd(const int64_t* idx, const float* dx, float* dwte, fl
     if (dwte) {
         const int64_t nchunk = (rows + EMB_CHUNK - 1) / EMB_CHUNK;
         dim3 grid(ceil_div(C, EMB_COLS), (unsigned)nchunk);
-        size_t lds = (size_t)EMB_WAVES * V * EMB_COLS * sizeof(float);
-        k_embed_bwd_tok_partial<<<grid, 256, lds, st>>>(idx, dx, (float*)workspace, rows, C, V);
+        const size_t lds = (size_t)waves * V * EMB_COLS * sizeof(float);
+        if (waves == 4)
+            k_embed_bwd_tok_partial<4><<<grid, 256, lds, st>>>(idx, dx, (float*)workspace, rows, C, V);
+        else if (waves == 2)
+            k_embed_bwd_tok_partial<2><<<grid, 128, lds, st>>>(idx, dx, (float*)workspace, rows, C, V);
+        else
+            k_embed_bwd_tok_partial<1><<<grid, 64, lds, st>>>(idx, dx, (float*)workspace, rows, C, V);
         k_embed_bwd_tok_reduce<<<ceil_div(V * C, 64), 64, 0, st>>>((const float*)workspace, dwte, nchunk, V * C,
                                                                     accumulate);
     }

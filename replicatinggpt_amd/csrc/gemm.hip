@@ -414,52 +414,6 @@ static void flush_pending() {
     if (g_red_device >= 0 && cur >= 0 && cur != g_red_device) (void)hipSetDevice(cur);
 }
 
-// grouped weight gradients (gemm_common.h WgGroup): cg_set_tuning("defer_wgrad"), owned by DEFER
-int g_defer_wgrad = 0;
-int g_wg_max = MAX_WG;   // cg_set_tuning("wgrad_group"): products per grouped launch (1..MAX_WG)
-static WgGroup g_wg_pending = {};
-static hipStream_t g_wg_stream = nullptr;
-static int g_wg_device = -1;
-
-static void flush_wgrads() {
-    if (!g_wg_pending.n) return;
-    const int cur = current_device();
-    if (g_wg_device >= 0 && cur != g_wg_device) (void)hipSetDevice(g_wg_device);
-    const WgGroup g = g_wg_pending;
-    g_wg_pending.n = 0;
-    g_wg_pending.nitems = 0;
-    (void)wgrad_group_launch(g, g_wg_stream);
-    if (g_wg_device >= 0 && cur >= 0 && cur != g_wg_device) (void)hipSetDevice(cur);
-}
-
-// queue a dW = A^T B split-K product (bf16, fp32 STORE into a contiguous [M, N], workspace of
-// split slabs) for the next grouped launch; false = run it now as usual
-static bool enqueue_wgrad(int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
-                          int64_t ldb, float* C, int64_t ldc, float beta, int split, float* ws, hipStream_t st) {
-    if (!g_defer_wgrad || split < 2 || !ws || st == nullptr) return false;
-    if (M % 128 || N % 128 || K % 64 || ldc != N || lda % 8 || ldb % 8) return false;
-    if ((((uintptr_t)A) | ((uintptr_t)B) | ((uintptr_t)C) | ((uintptr_t)ws)) & 15) return false;
-    const int64_t nkt = K / 64, nkc = (nkt + split - 1) / split;   // 64-deep K-tiles (gemm_tile.h FBK)
-    if ((split - 1) * nkc >= nkt) return false;   // an empty last split
-    const int64_t tiles = (M / 128) * (N / 128);
-    const int dev = current_device();
-    if (g_wg_pending.n >= g_wg_max || (g_wg_pending.n && (g_wg_stream != st || g_wg_device != dev)) ||
-        (int64_t)g_wg_pending.nitems + tiles * split > (int64_t)1 << 30)
-        flush_wgrads();
-    for (int q = 0; q < g_wg_pending.n; ++q)   // a second product into a queued output: keep the order
-        if (g_wg_pending.j[q].out == C) {
-            flush_wgrads();
-            break;
-        }
-    g_wg_stream = st;
-    g_wg_device = dev;
-    WgJob& J = g_wg_pending.j[g_wg_pending.n++];
-    J = WgJob{A, B, ws, C, lda, ldb, M, N, nkc * 64, g_wg_pending.nitems, (int)(N / 128), (int)tiles, (int)nkt,
-              (int)nkc, split, beta};
-    g_wg_pending.nitems += (int)(tiles * split);
-    return true;
-}
-
 int g_skip_splitk_reduce = 0;  // measurement knob (WRONG results): time a step without the split-K reduce
 extern int g_attn_variant;  // attention_d64.hip
 extern int g_ln_rpb;  // layernorm.hip
@@ -515,15 +469,6 @@ extern "C" int cg_set_tuning(const char* key, int value) {
         g_defer_splitk = value;
         return CG_OK;
     }
-    if (!strcmp(key, "defer_wgrad")) {   // queue weight-gradient GEMMs for one grouped launch at cg_flush_deferred
-        g_defer_wgrad = value;
-        return CG_OK;
-    }
-    if (!strcmp(key, "wgrad_group")) {
-        CG_REQUIRE(value >= 1 && value <= MAX_WG, "cg_set_tuning: wgrad_group must be 1..%d", MAX_WG);
-        g_wg_max = value;
-        return CG_OK;
-    }
     if (!strcmp(key, "defer_partials")) {   // queue cg_layernorm_bwd_reduce / cg_reduce_rows until cg_flush_deferred
         g_defer_partials = value;
         return CG_OK;
@@ -575,11 +520,6 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
     EpiArgs e = make_epi(epi);
     CG_REQUIRE(split_k == 1 || e.kind == CG_EPI_STORE || e.kind == CG_EPI_BIAS || e.kind == CG_EPI_BIAS_RESID,
                "cg_gemm: split-K supports STORE/BIAS/BIAS_RESID epilogues only");
-    if (op_dtype == CG_BF16 && a_trans && b_trans && c_dtype == CG_F32 && e.kind == CG_EPI_STORE && !e.bias &&
-        !g_skip_splitk_reduce && g_gemm_variant == 0 &&
-        enqueue_wgrad(M, N, K, (const bf16_t*)A, lda, (const bf16_t*)B, ldb, (float*)C, ldc, e.beta, split_k,
-                      (float*)workspace, st))
-        return CG_OK;   // grouped with the other queued weight gradients at cg_flush_deferred
     bool fast = false;
     if (op_dtype == CG_BF16 && fast_gemm_launch(a_trans, b_trans, M, N, K, (const bf16_t*)A, lda,
                                                 (const bf16_t*)B, ldb, C, c_dtype, ldc, e, split_k,
@@ -701,7 +641,6 @@ static void launch_splitk_reduce_job(const RedJob& j, hipStream_t st) {
 
 extern "C" int cg_flush_deferred(void* stream) {
     (void)stream;   // pending jobs go out on the stream they were enqueued on
-    cg::flush_wgrads();   // first: the grouped launch's reduces complete its outputs in stream order
     cg::flush_pending();
     cg::flush_partials();
     CG_LAUNCH_CHECK("cg_flush_deferred");

@@ -83,40 +83,8 @@ struct RedJobs {
 };
 RedJobs take_pending_reduces(hipStream_t st);   // gemm.hip: pending jobs (cleared) for a launch on st
 
-template <typename JOBS>
-__device__ __forceinline__ void red_jobs(const JOBS& r);
-__device__ __forceinline__ void red_tail(const RedJobs& r) { red_jobs(r); }
-
-// The training backward's weight-gradient GEMMs grouped into ONE persistent launch
-// (cg_set_tuning("defer_wgrad", 1), owned by functional.DEFER): each split-K dW = dY^T X call
-// (bf16, both operands transposed, fp32 STORE output, split > 1) is queued with its own split and
-// workspace; cg_flush_deferred (or a full queue) launches k_gemm_pk over the items of every queued
-// problem -- item i of the group belongs to the problem with item0 <= i < next item0, and is that
-// problem's (split, tile) item exactly as its own launch would number it -- then one reduce kernel
-// sums every problem's slabs (red_jobs: slab 0, 1, ... then beta, the bits of k_splitk_reduce4).
-// On one hardware queue the 25 launches each paid a ramp, a tail and a part-filled last round.
-struct WgJob {
-    const bf16_t* A;
-    const bf16_t* B;
-    float* ws;
-    float* out;
-    int64_t lda, ldb, M, N, kchunk;
-    int item0, tilesN, ntiles, nkt, nkc, split;
-    float beta;
-};
-constexpr int MAX_WG = 16;
-struct WgGroup {
-    int n, nitems;
-    WgJob j[MAX_WG];
-};
-constexpr int MAX_REDN = 2 * MAX_WG;
-struct RedJobsN {
-    RedJob j[MAX_REDN];
-    int n;
-};
-// red_tail's loop over any job list: thread t sums float4 chunks t, t + threads, ... of every job
-template <typename JOBS>
-__device__ __forceinline__ void red_jobs(const JOBS& r) {
+// thread t sums float4 chunks t, t + threads, ... of every job
+__device__ __forceinline__ void red_tail(const RedJobs& r) {
     const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
     const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (int q = 0; q < r.n; ++q) {
@@ -133,7 +101,6 @@ __device__ __forceinline__ void red_jobs(const JOBS& r) {
         }
     }
 }
-bool wgrad_group_launch(const WgGroup& g, hipStream_t st);   // gemm_pk.hip
 
 // tuning knob (cg_set_tuning("gemm_variant", v)); 0 = automatic choice
 extern int g_gemm_variant;

@@ -237,7 +237,7 @@ void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
             if constexpr (COLPART) {
                 // ReLU backward (bf16 ReLU output as the mask, beta 0: checked on the host) with the
                 // consumer's bias gradient fused: column sums of the bf16-rounded outputs per 64-row
-                // block (the layout of k_gemm_pk's colpart), 4 rows per lane then a butterfly over the
+                // block (the layout of k_gemm_pk's colpart), 4 rows per lane then a DPP row sum over the
                 // column group's 16 lanes.  The partial stores go before the item's FM x FN output
                 // stores, which stay the youngest EPI_OPS vector-memory operations.
                 if constexpr (EP == P8_CP_BITS) {   // ReLU keep bits: one word pair per row (FN == 4)
@@ -274,13 +274,9 @@ void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
                         fv4 t;
 #pragma unroll
                         for (int q = 0; q < 4; ++q) {
-                            float sum = ((acc[4 * ib][j][q] + acc[4 * ib + 1][j][q]) + acc[4 * ib + 2][j][q]) +
-                                        acc[4 * ib + 3][j][q];
-                            sum += __shfl_xor(sum, 1);
-                            sum += __shfl_xor(sum, 2);
-                            sum += __shfl_xor(sum, 4);
-                            sum += __shfl_xor(sum, 8);
-                            t[q] = sum;
+                            const float sum = ((acc[4 * ib][j][q] + acc[4 * ib + 1][j][q]) + acc[4 * ib + 2][j][q]) +
+                                              acc[4 * ib + 3][j][q];
+                            t[q] = row16_sum_dpp(sum);   // the 16 lanes of the column group = one DPP row
                         }
                         if ((lane & 15) == 0) *(fv4*)(cp + 16 * j) = t;
                     }

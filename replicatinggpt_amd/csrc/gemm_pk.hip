@@ -149,6 +149,11 @@ template <int EK>
 __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t nc, int64_t N, void* Cv, int c_dtype,
                                          int64_t ldc, const EpiArgs& epi, uint64_t stream) {
     const int kind = EK >= 0 ? EK : epi.kind;
+    // the fixed kinds' output dtype (launch_ek dispatches them only with it): no per-fragment branch
+    constexpr int OUT = (EK == CG_EPI_BIAS_RESID || EK == CG_EPI_BIAS_DROP_RESID) ? CG_F32
+                        : (EK == CG_EPI_BIAS_RELU || EK == CG_EPI_RELU_BWD)   ? CG_BF16
+                                                                              : -1;
+    if constexpr (OUT >= 0) c_dtype = OUT;
     constexpr bool WIDE = EK == CG_EPI_STORE || EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_RELU_BWD;
     if (EK < 0 && epi.beta != 0.f) {
 #pragma unroll
@@ -195,7 +200,7 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
             if (epi.colpart) {
                 // the consumer's bias gradient, fused: column sums of this wave's 64 rows (rows
                 // 16i + lane&15 of each column 16j + 4(lane>>4) + q: 4 rows per lane, then a
-                // butterfly over the 16 lanes of the column group), lane r = 0 of each group writes.
+                // DPP row sum over the 16 lanes of the column group), lane r = 0 of each group writes.
                 // These stores precede the item's 16 output stores, which stay the youngest
                 // EPI_OPS vector-memory operations the main loop's wait counts assume.
                 const int lane = threadIdx.x & 63;
@@ -207,12 +212,8 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
                     for (int q = 0; q < 4; ++q) {
                         // the bf16-rounded values the stores below write (the precision cg_colsum
                         // and the W1 weight gradient see), summed in fp32
-                        float s = ((rbf(acc[0][j][q]) + rbf(acc[1][j][q])) + rbf(acc[2][j][q])) + rbf(acc[3][j][q]);
-                        s += __shfl_xor(s, 1);
-                        s += __shfl_xor(s, 2);
-                        s += __shfl_xor(s, 4);
-                        s += __shfl_xor(s, 8);
-                        t[q] = s;
+                        const float s = ((rbf(acc[0][j][q]) + rbf(acc[1][j][q])) + rbf(acc[2][j][q])) + rbf(acc[3][j][q]);
+                        t[q] = row16_sum_dpp(s);   // the 16 lanes of the column group = one DPP row
                     }
                     if ((lane & 15) == 0) *(fv4*)(cp + 16 * j) = t;
                 }
@@ -251,7 +252,7 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) r[i][j] = *(const float4*)(epi.resid + (mr + 16 * i) * epi.ld_resid + nc + 16 * j);
-        const bool drop = kind == CG_EPI_BIAS_DROP_RESID && epi.thr;
+        const bool drop = kind == CG_EPI_BIAS_DROP_RESID && (EK == CG_EPI_BIAS_DROP_RESID || epi.thr);
         uint32_t nib[4][4];
         if (drop) drop_nibbles(epi, stream, mr, nc, N, nib);
 #pragma unroll
@@ -314,14 +315,7 @@ template <int BM, int BN, int NBUF, int BK = FBK>
 struct GeoP {
     static constexpr int WM = BM / 64, WN = BN / 64, WAVES = WM * WN, THREADS = WAVES * 64;
     static constexpr int IMG_A = BM * BK * 2, IMG_B = BN * BK * 2, STAGE = IMG_A + IMG_B;
-    // 128x192 (6 waves): one block per CU by construction -- the launch asks for 96 KB of LDS so a
-    // second block never shares the CU (the tile exists to give each CU 1.5 128x128 tiles of work
-    // where 384 of them would fill 3/4 of the 512 two-per-CU slots), and only waves 0-3 issue the
-    // A image's 16 DMA instructions (6 does not divide them)
-    static constexpr bool ONE_PER_CU = WN == 3;
-    static constexpr int AW = ONE_PER_CU ? 4 : WAVES;   // waves issuing the A image's DMAs
-    static constexpr int LDS = ONE_PER_CU ? 96 * 1024 : NBUF * STAGE;
-    static_assert(NBUF * STAGE <= LDS, "ring exceeds the launch's LDS");
+    static constexpr int LDS = NBUF * STAGE;
     static constexpr int OCC_LDS = (160 * 1024) / LDS;
     static constexpr int OCC = OCC_LDS > 4 ? 4 : (OCC_LDS < 1 ? 1 : OCC_LDS);  // resident blocks per CU (LDS-bound)
     static constexpr int WPE = (WAVES * OCC + 3) / 4;   // waves per SIMD
@@ -342,43 +336,33 @@ constexpr int EK_ANY = -1, EK_SLAB = 6;
 // flight at two blocks per CU; same bits -- kchunk stays a multiple of 64, same k order.  Measured
 // 10-15 % slower on every C2 shape: 64-B row segments double the TA/TCP requests,
 // profiles/r3_gemm_bk32.txt -- no launcher instantiates it)
-// The kernel body.  GRP: a grouped weight-gradient launch (gemm_common.h WgGroup): every item's
-// problem -- operands, leading dimensions, M / N, split, slab workspace -- comes from the group
-// table g; M ... ws and red are unused.
-template <bool AT, bool BT, int BM, int BN, int NBUF, int EK, int BK, bool GRP>
-__device__ __forceinline__ void pk_body(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
-                                        const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype,
-                                        int64_t ldc, const EpiArgs& epi, int split_k, int64_t kchunk,
-                                        float* __restrict__ ws, int flags, const RedJobs& red, const WgGroup* grp) {
-    static_assert(!GRP || (AT && BT && EK == EK_SLAB && BM == 128 && BN == 128), "grouped: weight gradients only");
+// amdgpu_waves_per_eu: LDS caps residency at OCC blocks, so tell the scheduler the real occupancy;
+// left at its default it schedules for 8+ waves/SIMD, keeps ONE A fragment register and waits
+// lgkmcnt(0) before every 4 MFMAs (LDS latency exposed 8x per K-tile)
+template <bool AT, bool BT, int BM, int BN, int NBUF, int EK, int BK>
+__global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, (GeoP<BM, BN, NBUF, BK>::OCC))
+__attribute__((amdgpu_waves_per_eu(1, GeoP<BM, BN, NBUF, BK>::WPE)))
+void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
+               const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype, int64_t ldc,
+               EpiArgs epi, int split_k, int64_t kchunk, float* __restrict__ ws, int flags, RedJobs red) {
     static_assert(BK == 64 || BK == 32, "BK");
-    static_assert(!GeoP<BM, BN, NBUF, BK>::ONE_PER_CU || (NBUF == 2 && !AT && !BT),
-                  "128x192: uneven per-wave DMA counts need the 2-stage ring's DMA-count-free waits; "
-                  "the transposed image swizzle needs 128-multiple widths");
     constexpr int NS = BK / 32;   // 32-deep MFMA slices per K-tile
     using G = GeoP<BM, BN, NBUF, BK>;
-    using DA = DmaP<AT, BM, G::AW, BK>;
+    using DA = DmaP<AT, BM, G::WAVES, BK>;
     using DB = DmaP<BT, BN, G::WAVES, BK>;
     constexpr int LPT = DA::PER_WAVE + DB::PER_WAVE;  // DMA instructions per thread per K-tile
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / G::WN, wn = wave % G::WN;
-    const int tilesN = GRP ? 0 : (int)(N / BN);
-    const int ntiles = GRP ? 0 : (int)(M / BM) * tilesN;
-    const int nitems = GRP ? grp->nitems : ntiles * split_k;
+    const int tilesN = (int)(N / BN);
+    const int ntiles = (int)(M / BM) * tilesN;
+    const int nitems = ntiles * split_k;
     // split s covers K-tiles [s*nkc, min((s+1)*nkc, nkt)): the last split may be shorter (uneven
     // split-K: any split count, not only divisors of the K-tile count)
-    const int nkt = GRP ? 0 : (int)(K / BK), nkc = GRP ? 0 : (int)(kchunk / BK);
+    const int nkt = (int)(K / BK), nkc = (int)(kchunk / BK);
     const int P = gridDim.x, b = blockIdx.x;
     const int my_items = b < nitems ? (nitems - 1 - b) / P + 1 : 0;
-    auto split_nk = [&](int sp, int pr) {
-        if constexpr (GRP) {
-            const WgJob& J = grp->j[pr];
-            return J.nkt - sp * J.nkc < J.nkc ? J.nkt - sp * J.nkc : J.nkc;
-        } else {
-            return nkt - sp * nkc < nkc ? nkt - sp * nkc : nkc;
-        }
-    };
+    auto split_nk = [&](int sp) { return nkt - sp * nkc < nkc ? nkt - sp * nkc : nkc; };
     const uint64_t stream =
         (epi.kind == CG_EPI_BIAS_DROP_RESID && epi.thr && split_k == 1) ? dropout_stream(epi.rng_call, epi.site) : 0;
 
@@ -392,40 +376,27 @@ __device__ __forceinline__ void pk_body(int64_t M, int64_t N, int64_t K, const b
 #else
     constexpr bool WI_NODMA = false, WI_NOMFMA = false, WI_NOEPI = false;
 #endif
-    if constexpr (!GRP) {   // grouped: (re)set whenever the DMA cursor enters another problem
-        da.init(lda, wave < G::AW ? wave : 0, lane);
-        db.init(ldb, wave, lane);
-    }
+    da.init(lda, wave, lane);
+    db.init(ldb, wave, lane);
 
-    auto decode = [&](int j, int64_t& m0, int64_t& n0, int& split, int& pr) {
+    auto decode = [&](int j, int64_t& m0, int64_t& n0, int& split) {
         const int it = xcd_remap(b + j * P, nitems);
         int tm, tn;
-        if constexpr (GRP) {
-            pr = 0;
-            while (pr + 1 < grp->n && it >= grp->j[pr + 1].item0) ++pr;
-            const WgJob& J = grp->j[pr];
-            const int li = it - J.item0;
-            split = li / J.ntiles;
-            tile_rc(li - split * J.ntiles, J.ntiles / J.tilesN, J.tilesN, flags >> 8, tm, tn);
-        } else {
-            pr = 0;
-            split = it / ntiles;
-            tile_rc(it - split * ntiles, ntiles / tilesN, tilesN, flags >> 8, tm, tn);
-        }
+        split = it / ntiles;
+        tile_rc(it - split * ntiles, ntiles / tilesN, tilesN, flags >> 8, tm, tn);
         m0 = (int64_t)tm * BM;
         n0 = (int64_t)tn * BN;
     };
     int total = 0;
     for (int j = 0; j < my_items; ++j) {
         int64_t m0, n0;
-        int sp, pr;
-        decode(j, m0, n0, sp, pr);
-        total += split_nk(sp, pr);
+        int sp;
+        decode(j, m0, n0, sp);
+        total += split_nk(sp);
     }
 
     // DMA issue cursor (item ij, K-tile ikt) and its operand origins
     int ij = 0, ikt = 0, ink = 0;   // ink: K-tiles of the DMA cursor's item
-    int dpr = -1;                    // GRP: the problem the DMA lane offsets were set up for
     const bf16_t* oa = A;
     const bf16_t* ob = B;
     // The in-loop DMA is split from its address bookkeeping: prep_next() (branchy: item decode at
@@ -440,24 +411,12 @@ __device__ __forceinline__ void pk_body(int64_t M, int64_t N, int64_t K, const b
         if (real) {
             if (ikt == 0) {
                 int64_t m0, n0;
-                int sp, pr;
-                decode(ij, m0, n0, sp, pr);
-                ink = split_nk(sp, pr);
-                if constexpr (GRP) {
-                    const WgJob& J = grp->j[pr];
-                    if (pr != dpr) {
-                        da.init(J.lda, wave, lane);
-                        db.init(J.ldb, wave, lane);
-                        dpr = pr;
-                    }
-                    const int64_t kb = sp * J.kchunk;
-                    oa = J.A + kb * J.lda + m0;   // AT and BT (static_assert above)
-                    ob = J.B + kb * J.ldb + n0;
-                } else {
-                    const int64_t kb = sp * kchunk;
-                    oa = AT ? A + kb * lda + m0 : A + m0 * lda + kb;
-                    ob = BT ? B + kb * ldb + n0 : B + n0 * ldb + kb;
-                }
+                int sp;
+                decode(ij, m0, n0, sp);
+                ink = split_nk(sp);
+                const int64_t kb = sp * kchunk;
+                oa = AT ? A + kb * lda + m0 : A + m0 * lda + kb;
+                ob = BT ? B + kb * ldb + n0 : B + n0 * ldb + kb;
             }
             na = oa + ikt * da.kstep;
             nbp = ob + ikt * db.kstep;
@@ -479,9 +438,8 @@ __device__ __forceinline__ void pk_body(int64_t M, int64_t N, int64_t K, const b
         if (s < total) {
             prep_next(true);
             const uint32_t img = lds0 + (uint32_t)(s * G::STAGE);
-            if (G::AW == G::WAVES || wave < G::AW)
 #pragma unroll
-                for (int i = 0; i < DA::PER_WAVE; ++i) da.issue1(na, i, img, wave);
+            for (int i = 0; i < DA::PER_WAVE; ++i) da.issue1(na, i, img, wave);
 #pragma unroll
             for (int i = 0; i < DB::PER_WAVE; ++i) db.issue1(nbp, i, img + G::IMG_A, wave);
         }
@@ -499,9 +457,9 @@ __device__ __forceinline__ void pk_body(int64_t M, int64_t N, int64_t K, const b
     int cnk;   // K-tiles of the compute cursor's item
     {
         int64_t m0, n0;
-        int sp, pr;
-        decode(0, m0, n0, sp, pr);
-        cnk = my_items ? split_nk(sp, pr) : 0;
+        int sp;
+        decode(0, m0, n0, sp);
+        cnk = my_items ? split_nk(sp) : 0;
     }
     bool stored = false;
 #ifdef CG_PK_STAMPS
@@ -565,7 +523,7 @@ __device__ __forceinline__ void pk_body(int64_t M, int64_t N, int64_t K, const b
         auto issue_dma = [&](int t) {
             if (WI_NODMA) return;
             if (t < DA::PER_WAVE) {
-                if (G::AW == G::WAVES || wave < G::AW) da.issue1(na, t, dimg, wave);
+                da.issue1(na, t, dimg, wave);
             } else {
                 db.issue1(nbp, t - DA::PER_WAVE, dimg + G::IMG_A, wave);
             }
@@ -599,17 +557,10 @@ __device__ __forceinline__ void pk_body(int64_t M, int64_t N, int64_t K, const b
         if (++ckt == cnk) {
             // item done: acc[i][j][r] = C[mw + 16i + (lane&15)][nw + 16j + 4(lane>>4) + r]
             int64_t m0, n0;
-            int sp, pr;
-            decode(cj, m0, n0, sp, pr);
+            int sp;
+            decode(cj, m0, n0, sp);
             const int64_t mr = m0 + wm * 64 + (lane & 15), nc = n0 + wn * 64 + 4 * (lane >> 4);
             if (WI_NOEPI) {
-            } else if (GRP) {
-                const WgJob& J = grp->j[pr];
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        *(fv4*)(J.ws + ((int64_t)sp * J.M + mr + 16 * i) * J.N + nc + 16 * j) = acc[i][j];
             } else if (EK == EK_SLAB || split_k > 1) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
@@ -633,9 +584,9 @@ __device__ __forceinline__ void pk_body(int64_t M, int64_t N, int64_t K, const b
             ++cj;
             if (cj < my_items) {
                 int64_t m1, n1;
-                int sp1, pr1;
-                decode(cj, m1, n1, sp1, pr1);
-                cnk = split_nk(sp1, pr1);
+                int sp1;
+                decode(cj, m1, n1, sp1);
+                cnk = split_nk(sp1);
             }
             stored = true;
 #ifdef CG_PK_STAMPS
@@ -655,33 +606,9 @@ __device__ __forceinline__ void pk_body(int64_t M, int64_t N, int64_t K, const b
     }
 #endif
     wait_vm<0>();  // the dummy DMAs past the last K-tile land before the workgroup's LDS is released
-    if (!GRP && red.n) red_tail(red);   // a deferred split-K reduce of an earlier launch (gemm_common.h)
+    if (red.n) red_tail(red);   // a deferred split-K reduce of an earlier launch (gemm_common.h)
 }
 
-template <bool AT, bool BT, int BM, int BN, int NBUF, int EK = EK_ANY, int BK = FBK>
-// amdgpu_waves_per_eu: LDS caps residency at OCC blocks, so tell the scheduler the real occupancy;
-// left at its default it schedules for 8+ waves/SIMD, keeps ONE A fragment register and waits
-// lgkmcnt(0) before every 4 MFMAs (LDS latency exposed 8x per K-tile)
-__global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, (GeoP<BM, BN, NBUF, BK>::OCC))
-__attribute__((amdgpu_waves_per_eu(1, GeoP<BM, BN, NBUF, BK>::WPE)))
-void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
-               const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype, int64_t ldc,
-               EpiArgs epi, int split_k, int64_t kchunk, float* __restrict__ ws, int flags, RedJobs red) {
-    pk_body<AT, BT, BM, BN, NBUF, EK, BK, false>(M, N, K, A, lda, B, ldb, Cv, c_dtype, ldc, epi, split_k, kchunk, ws,
-                                                 flags, red, nullptr);
-}
-
-// the grouped weight-gradient launch (128x128, 2-stage ring, slab epilogue)
-__global__ __launch_bounds__(256, (GeoP<128, 128, 2, FBK>::OCC))
-__attribute__((amdgpu_waves_per_eu(1, GeoP<128, 128, 2, FBK>::WPE)))
-void k_gemm_pk_grp(WgGroup grp, int flags) {
-    const RedJobs none = {};
-    pk_body<true, true, 128, 128, 2, EK_SLAB, FBK, true>(0, 0, 0, nullptr, 0, nullptr, 0, nullptr, CG_F32, 0,
-                                                          EpiArgs{}, 1, 0, nullptr, flags, none, &grp);
-}
-
-// every grouped problem's slabs summed into its output (one launch; red_jobs = red_tail's order)
-__global__ __launch_bounds__(256) void k_red_multi(RedJobsN jobs) { red_jobs(jobs); }
 
 int cu_count() {
     static int n = 0;
@@ -716,17 +643,29 @@ void launch_ek(unsigned grid, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
         L1(EK_SLAB);
         return;
     }
-    if constexpr (!AT_ && BM == 128 && (BN == 128 || BN == 192)) {
+    if constexpr (!AT_ && BM == 128 && BN == 128) {
         const bool needs_bias = e.kind >= CG_EPI_BIAS && e.kind <= CG_EPI_BIAS_DROP_RESID;
         const bool needs_resid = e.kind == CG_EPI_BIAS_RESID || e.kind == CG_EPI_BIAS_DROP_RESID;
+        // the residual kinds write fp32, BIAS_RELU / RELU_BWD bf16 (epi_item's OUT); other dtypes take
+        // the run-time epilogue.  Dropout at p = 0 is the bias + residual epilogue (same arithmetic).
+        const bool f32 = c_dtype == CG_F32, b16 = c_dtype == CG_BF16;
         if (!(g_pk_flags & 2) && e.beta == 0.f && (!needs_bias || e.bias) && (!needs_resid || e.resid)) {
             switch (e.kind) {
                 case CG_EPI_STORE: L1(CG_EPI_STORE); return;
                 case CG_EPI_BIAS: L1(CG_EPI_BIAS); return;
-                case CG_EPI_BIAS_RELU: L1(CG_EPI_BIAS_RELU); return;
-                case CG_EPI_BIAS_RESID: L1(CG_EPI_BIAS_RESID); return;
-                case CG_EPI_BIAS_DROP_RESID: L1(CG_EPI_BIAS_DROP_RESID); return;
-                case CG_EPI_RELU_BWD: L1(CG_EPI_RELU_BWD); return;
+                case CG_EPI_BIAS_RELU:
+                    if (b16) { L1(CG_EPI_BIAS_RELU); return; }
+                    break;
+                case CG_EPI_BIAS_RESID:
+                    if (f32) { L1(CG_EPI_BIAS_RESID); return; }
+                    break;
+                case CG_EPI_BIAS_DROP_RESID:
+                    if (f32 && e.thr) { L1(CG_EPI_BIAS_DROP_RESID); return; }
+                    if (f32) { L1(CG_EPI_BIAS_RESID); return; }
+                    break;
+                case CG_EPI_RELU_BWD:
+                    if (b16) { L1(CG_EPI_RELU_BWD); return; }
+                    break;
                 default: break;
             }
         }
@@ -757,7 +696,7 @@ bool launch_p(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
             return true;
         }
     } else if (at && !bt) {
-        if constexpr (BM % 128 == 0 && BN != 192) {
+        if constexpr (BM % 128 == 0) {
             FG(true, false);
             return true;
         }
@@ -775,35 +714,12 @@ bool launch_p(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
 
 int gemm_cu_count() { return cu_count(); }
 
-// the queued weight gradients as one grouped persistent launch, then one reduce over all their slabs
-bool wgrad_group_launch(const WgGroup& g, hipStream_t st) {
-    if (g.n <= 0 || g.nitems <= 0) return false;
-    using G = GeoP<128, 128, 2, FBK>;
-    int64_t slots = (int64_t)cu_count() * G::OCC;
-    if (g_gemm_max_grid > 0 && g_gemm_max_grid < slots) slots = g_gemm_max_grid;
-    const unsigned grid = (unsigned)(g.nitems < slots ? g.nitems : slots);
-    k_gemm_pk_grp<<<grid, G::THREADS, G::LDS, st>>>(g, g_pk_flags | (g_gemm_group_pk << 8));
-    RedJobsN r = {};
-    int64_t most = 0;
-    for (int q = 0; q < g.n; ++q) {
-        const WgJob& J = g.j[q];
-        r.j[r.n++] = RedJob{J.ws, J.out, J.M * J.N / 4, J.split, J.beta};
-        most = J.M * J.N / 4 > most ? J.M * J.N / 4 : most;
-    }
-    const int64_t blocks = (most + 255) / 256;
-    k_red_multi<<<(unsigned)(blocks < 2048 ? blocks : 2048), 256, 0, st>>>(r);
-    return true;
-}
-
 bool pk_gemm_launch(int v, int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda,
                     const bf16_t* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k,
                     float* ws, hipStream_t st) {
     switch (v) {
         case 9: return launch_p<128, 128, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
 #ifdef CG_AB_VARIANTS   // measured-slower A/B tiles (profiles/r1_gemm_scan*.txt, r2_gemm_ring_depth_scan.txt)
-        case 18:   // 128x192, one block (6 waves) per CU, NN/NT only: r3_gemm_128x192_ab.txt
-            if (at || bt || N % 192 || split_k != 1) return false;
-            return launch_p<128, 192, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
         case 10: launch_p<128, 128, 3>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st); return true;
         case 11:
             if (M % 256) return false;

@@ -376,56 +376,3 @@ extern "C" int cg_gather_batch(const void* data, int data_is_u8, const int64_t* 
     CG_LAUNCH_CHECK("cg_gather_batch");
     return CG_OK;
 }
-
-// The graph-replayed form: the offsets of the next `slots` steps sit in an HBM ring the host refills
-// a half at a time (data.BatchSampler.ring_prepare), so a replayed step needs no per-step H2D copy
-// and no launch outside its graph.  ctl = {ring position, block ticket}: every block reads the
-// position, the last block to finish advances it (all reads are behind its ticket) and, when given,
-// takes the step's dropout-call snapshot (what cg_rng_snapshot would have done in its own launch).
-template <typename D>
-__global__ void k_gather_batch_ring(const D* data, const int64_t* ring, int64_t slots, int64_t* ctl,
-                                    uint64_t* rng_counter, uint64_t* rng_snap, int64_t* x, int64_t* y, int64_t B,
-                                    int64_t T) {
-    __shared__ int64_t s_base;
-    const int64_t b = blockIdx.y;
-    int64_t pos = 0;
-    if (threadIdx.x == 0) {
-        pos = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_base = ring[(pos % slots) * B + b];
-    }
-    __syncthreads();
-    const int64_t base = s_base;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < T; t += (int64_t)gridDim.x * blockDim.x) {
-        x[b * T + t] = (int64_t)data[base + t];
-        y[b * T + t] = (int64_t)data[base + t + 1];
-    }
-    if (threadIdx.x == 0) {
-        __threadfence();
-        const unsigned long long nb = (unsigned long long)gridDim.x * gridDim.y;
-        if (atomicAdd((unsigned long long*)(ctl + 1), 1ull) == nb - 1) {
-            ctl[0] = pos + 1;
-            ctl[1] = 0;
-            if (rng_counter) {
-                const uint64_t v = *rng_counter;
-                *rng_snap = v;
-                *rng_counter = v + 1;
-            }
-        }
-    }
-}
-
-extern "C" int cg_gather_batch_ring(const void* data, int data_is_u8, const int64_t* ring, int64_t slots,
-                                    int64_t* ctl, uint64_t* rng_counter, uint64_t* rng_snap, int64_t* x, int64_t* y,
-                                    int64_t B, int64_t T, void* stream) {
-    CG_REQUIRE(B > 0 && T > 0 && B < 65536 && slots > 0, "cg_gather_batch_ring: bad shape");
-    CG_REQUIRE((rng_counter == nullptr) == (rng_snap == nullptr), "cg_gather_batch_ring: rng_counter/rng_snap");
-    dim3 grid(ceil_div(T, 256), (unsigned)B);
-    if (data_is_u8)
-        k_gather_batch_ring<uint8_t><<<grid, 256, 0, (hipStream_t)stream>>>((const uint8_t*)data, ring, slots, ctl,
-                                                                            rng_counter, rng_snap, x, y, B, T);
-    else
-        k_gather_batch_ring<int64_t><<<grid, 256, 0, (hipStream_t)stream>>>((const int64_t*)data, ring, slots, ctl,
-                                                                            rng_counter, rng_snap, x, y, B, T);
-    CG_LAUNCH_CHECK("cg_gather_batch_ring");
-    return CG_OK;
-}

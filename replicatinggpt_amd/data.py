@@ -117,47 +117,3 @@ class BatchSampler:
             x, y = out
         ops.gather_batch(data, ix_dev, x, y)
         return x, y
-
-    # -- offsets ring for graph-replayed training steps ---------------------------------------
-    def ring_init(self, dev, half=32):
-        """An HBM ring of 2*half steps' offsets plus its control word {position, ticket}.  The
-        replayed step gathers from slot position % (2*half) (``ring_gather``, captured in the step
-        graph) instead of copying its offsets H2D outside the graph.  ``ring_prepare(s)`` draws the
-        offsets of step s (and the rest of its half) on the host generator in step order -- the same
-        ``draw_ix`` calls ``get_batch`` makes -- so the index stream is unchanged as long as nothing
-        else draws from the generator between training steps (estimate_loss does in GPT1.py:88-93:
-        the GPT1 driver keeps the per-step get_batch)."""
-        self._rh = half
-        self.ring = torch.empty((2 * half, self.B), dtype=torch.int64, device=dev)
-        self.ring_ctl = torch.zeros(2, dtype=torch.int64, device=dev)
-        self._ring_stage = [[torch.empty((half, self.B), dtype=torch.int64, pin_memory=True), None] for _ in range(2)]
-        self._ring_drawn = 0      # host steps whose offsets are in the ring
-
-    def ring_prepare(self, s):
-        """Make step s's offsets resident: when s reaches the drawn end, draw steps s .. the end of
-        s's half and copy them (stream-ordered behind every step that last read those slots)."""
-        if s < self._ring_drawn:
-            return
-        H = self._rh
-        end = (s // H + 1) * H
-        h = (s // H) % 2
-        stage = self._ring_stage[h]
-        if stage[1] is not None:
-            stage[1].synchronize()            # the pinned half's previous copy has been consumed
-        buf = stage[0]
-        for k in range(end - s):
-            buf[k].copy_(self.draw_ix("train"))
-        lo = s % (2 * H)
-        self.ring[lo:lo + end - s].copy_(buf[:end - s], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        stage[1] = ev
-        self._ring_drawn = end
-
-    def ring_gather(self, out, rng=None):
-        """Launch the ring gather into out=(x, y) (capturable); rng=(counter, snap) folds the step's
-        dropout-call snapshot into the same launch."""
-        x, y = out
-        ctr, snap = rng if rng is not None else (None, None)
-        ops.gather_batch_ring(self.s.train_dev, self.ring, self.ring_ctl, x, y, ctr, snap)
-        return x, y

@@ -79,17 +79,8 @@ def segment_plan(model, seg_layers):
 
 
 class TrainStep:
-    def __init__(self, model, optimizer, sampler, reducer=None, use_graph=True, overlap=None, seg_layers=2,
-                 ring=False):
-        """ring=True (graph mode): the replayed step gathers its batch from an HBM ring of offsets
-        drawn ahead on the host (data.BatchSampler.ring_init) inside its graph, with the dropout
-        snapshot folded into that launch -- no per-step H2D copy or launch outside the graph.  Only
-        for loops where nothing else draws from the sampler's generator between steps.  An int
-        sets the steps per ring half (True = 32)."""
+    def __init__(self, model, optimizer, sampler, reducer=None, use_graph=True, overlap=None, seg_layers=2):
         self.model, self.opt, self.sampler, self.reducer = model, optimizer, sampler, reducer
-        self.ring = 32 if ring is True else int(ring)   # steps per ring half
-        self._ring_pos = 0
-        self._snap = None
         dev = model.flat.master.device
         B, T = sampler.B, sampler.T
         self.x = torch.empty((B, T), dtype=torch.int64, device=dev)
@@ -209,26 +200,8 @@ class TrainStep:
             torch.set_rng_state(s["rng"])
         torch.cuda.synchronize()
 
-    def _batch_in_graph(self):
-        """The ring gather at the head of the captured step (ring mode; no-op otherwise)."""
-        if not self.ring:
-            return
-        m = self.model
-        if m.training and m.config.dropout > 0:
-            self.sampler.ring_gather((self.x, self.y), rng=(m._rng_counter, self._snap))
-            m._ext_rng_snap = self._snap
-        else:
-            self.sampler.ring_gather((self.x, self.y))
-
     def _capture(self, warmup):
-        if self.ring:
-            self.sampler.ring_init(self.x.device, half=self.ring)
-            self._ring_pos = 0
-            self._snap = torch.empty(1, dtype=torch.int64, device=self.x.device)
-        try:
-            self._capture_graphs(warmup)
-        finally:
-            self.model._ext_rng_snap = None
+        self._capture_graphs(warmup)
 
     def _capture_graphs(self, warmup):
         s = torch.cuda.Stream()
@@ -249,12 +222,10 @@ class TrainStep:
         self.g_fb = torch.cuda.CUDAGraph()
         if self.reducer is None:
             with torch.cuda.graph(self.g_fb):
-                self._batch_in_graph()
                 self.loss = self._fwd_bwd()
                 self.opt.step()
         else:
             with torch.cuda.graph(self.g_fb):
-                self._batch_in_graph()
                 self.loss = self._fwd_bwd()
             self.g_opt = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_opt, pool=self.g_fb.pool()):
@@ -264,7 +235,6 @@ class TrainStep:
     def _capture_segmented(self):
         g0 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g0):
-            self._batch_in_graph()
             loss, xs = self._forward_with_cuts()
             self.opt.zero_grad(set_to_none=True)
             self._segment(0, loss, xs)
@@ -283,11 +253,7 @@ class TrainStep:
 
     # -- one training step ----------------------------------------------------------------
     def step(self):
-        if self.ring and (self.g_fb is not None or self.g_seg):
-            self.sampler.ring_prepare(self._ring_pos)           # GPT1.py:227, gathered in the graph
-            self._ring_pos += 1
-        else:
-            self.sampler.get_batch("train", out=(self.x, self.y))   # GPT1.py:227
+        self.sampler.get_batch("train", out=(self.x, self.y))   # GPT1.py:227
         if self.g_seg:
             works = []
             for i, g in enumerate(self.g_seg):

@@ -95,13 +95,6 @@ class DeferredReduces:
         # queued and launched as ONE multi-job kernel at the flush -- on one hardware queue each was a
         # ~5 us launch for ~1 us of work (CHARPT_DEFER_PARTIALS=0: one launch each, for A/B)
         self.partials_on = os.environ.get("CHARPT_DEFER_PARTIALS", "1") != "0"
-        # and the split-K weight-gradient GEMMs themselves (cg_set_tuning "defer_wgrad"): queued with
-        # their own splits and workspaces and run as ONE grouped persistent launch + one slab reduce at
-        # the flush -- same items, same bits.  OFF by default (CHARPT_DEFER_WGRAD=1 turns it on): it
-        # measured slower -- C2 3.06 -> 3.09-3.21 ms/step by group size, C4 54.4 -> 56.3 -- the
-        # products lose their inputs' cache warmth and the slab reduces leave the dgrad GEMMs' tails
-        # (profiles/r3_grouped_wgrad_ab.txt)
-        self.wgrad_on = os.environ.get("CHARPT_DEFER_WGRAD", "0") == "1"
         self.active = False
         self.keep = []
 
@@ -109,8 +102,6 @@ class DeferredReduces:
         if self.enabled and torch.cuda.is_available():
             lib = L.load()
             L.check(lib.cg_set_tuning(b"defer_splitk", 1), "defer_splitk")
-            if self.wgrad_on:
-                L.check(lib.cg_set_tuning(b"defer_wgrad", 1), "defer_wgrad")
             self.active = True
         return self
 
@@ -140,7 +131,6 @@ class DeferredReduces:
             lib = L.load()
             self.flush()
             L.check(lib.cg_set_tuning(b"defer_splitk", 0), "defer_splitk")
-            L.check(lib.cg_set_tuning(b"defer_wgrad", 0), "defer_wgrad")
             if SIDE.enabled:   # the flush runs on the stream its reduces were enqueued on: join it
                 dev = torch.device("cuda", torch.cuda.current_device())
                 torch.cuda.current_stream(dev).wait_stream(SIDE.stream(dev))
@@ -332,7 +322,7 @@ def linear_wgrad(dy2, x2, out, beta, into_slot=False):
     if split > 1:
         ws = torch.empty(ops.gemm_workspace(N, K, split) // 4, dtype=torch.float32, device=dy2.device)
         if defer:
-            # its reduce -- and with defer_wgrad the product itself -- may run after this call returns
+            # its reduce may run after this call returns
             DEFER.keep.extend((ws, dy2, x2))
     ops.gemm(dy2, x2, out, _is_bf16(dy2.dtype), True, True, N, K, M, N, K, out.stride(0), L.EPI_STORE, None, None, 0,
              None, 0, 0.0, 0, None, 0, float(beta), split, ws)

@@ -451,11 +451,8 @@ class BigramLanguageModel(nn.Module):
         R = self._store.regions
         p = cfg.dropout if self.training else 0.0
         if p > 0:
-            snap = getattr(self, "_ext_rng_snap", None)
-            if snap is None:
-                snap = torch.empty(1, dtype=torch.int64, device=idx.device)
-                ops.rng_snapshot(self._rng_counter, snap)
-            # else: the graph-replayed step's ring gather took the snapshot (engine.TrainStep)
+            snap = torch.empty(1, dtype=torch.int64, device=idx.device)
+            ops.rng_snapshot(self._rng_counter, snap)
             self._fwd_rng = snap
             hs = cfg.n_embd // cfg.n_head
             if Fn.SIDE.premask and Fn.premask_ok(act, T, hs) and self.blocks[0].sa_heads.heads[0].dropout.p > 0:

@@ -65,17 +65,6 @@ def gather_batch(data: Tensor, ix: Tensor, x: Tensor, y: Tensor) -> None:
                                      T, _s(x)), "gather_batch")
 
 
-@_op("gather_batch_ring", ("ctl", "x", "y", "rng_counter", "rng_snap"))
-def gather_batch_ring(data: Tensor, ring: Tensor, ctl: Tensor, x: Tensor, y: Tensor, rng_counter: Optional[Tensor],
-                      rng_snap: Optional[Tensor]) -> None:
-    B, T = x.shape
-    if ring.dim() != 2 or ring.shape[1] != B or ctl.numel() != 2 or ctl.dtype != torch.int64:
-        raise ValueError("gather_batch_ring: ring must be [slots, B] and ctl int64[2]")
-    L.check(L.load().cg_gather_batch_ring(L.ptr(data), int(data.dtype == torch.uint8), L.ptr(ring), ring.shape[0],
-                                          L.ptr(ctl), L.ptr(rng_counter), L.ptr(rng_snap), L.ptr(x), L.ptr(y), B, T,
-                                          _s(x)), "gather_batch_ring")
-
-
 # ---------------------------------------------------------------------------------------
 @_op("embed_fwd", ("x",))
 def embed_fwd(idx: Tensor, wte: Tensor, wpe: Tensor, x: Tensor) -> None:
@@ -334,15 +323,6 @@ def adamw(p: Tensor, g: Tensor, m: Tensor, v: Tensor, p_bf16: Optional[Tensor], 
           eps: float, weight_decay: float, step: Tensor) -> None:
     L.check(L.load().cg_adamw(L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), L.ptr(p_bf16), p.numel(), lr, beta1, beta2, eps,
                               weight_decay, L.ptr(step), _s(p)), "adamw")
-
-
-@_op("adamw_step", ("p", "m", "v", "p_bf16", "step_ctl"))
-def adamw_step(p: Tensor, g: Tensor, m: Tensor, v: Tensor, p_bf16: Optional[Tensor], lr: float, beta1: float,
-               beta2: float, eps: float, weight_decay: float, step_ctl: Tensor) -> None:
-    if step_ctl.numel() != 2 or step_ctl.dtype != torch.int64:
-        raise ValueError("adamw_step: step_ctl must be int64[2] = {step, ticket}")
-    L.check(L.load().cg_adamw_step(L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), L.ptr(p_bf16), p.numel(), lr, beta1, beta2,
-                                   eps, weight_decay, L.ptr(step_ctl), _s(p)), "adamw_step")
 
 
 # ---------------------------------------------------------------------------------------

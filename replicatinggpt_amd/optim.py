@@ -5,16 +5,10 @@ GEMMs read.  The step count lives on the device, so the whole optimizer step is 
 hipGraph.  Numerics follow torch/optim/adam.py ``_single_tensor_adam`` (decoupled weight decay,
 bias-corrected moments, same fp32 operation order).
 """
-import os
-
 import torch
 
 from . import functional as Fn
 from . import ops
-
-# CHARPT_ADAMW_FUSED_STEP=1: the flat launch advances the step count itself (cg_adamw_step, one launch
-# instead of counter_add + adamw); off by default: measured slower (DESIGN.md section 8)
-FUSED_STEP = os.environ.get("CHARPT_ADAMW_FUSED_STEP", "0") == "1"
 
 
 class AdamW(torch.optim.Optimizer):
@@ -48,9 +42,7 @@ class AdamW(torch.optim.Optimizer):
         self._store = st
         self._m = torch.zeros_like(st.master)
         self._v = torch.zeros_like(st.master)
-        # {step count, block ticket}: the flat launch advances the count itself (cg_adamw_step)
-        self._step_ctl = torch.zeros(2, dtype=torch.int64, device=st.master.device)
-        self._step_t = self._step_ctl[:1]
+        self._step_t = torch.zeros(1, dtype=torch.int64, device=st.master.device)
         self._psteps = None
         return self
 
@@ -61,8 +53,7 @@ class AdamW(torch.optim.Optimizer):
         if self._m.device != st.master.device:
             self._m = self._m.to(st.master.device)
             self._v = self._v.to(st.master.device)
-            self._step_ctl = self._step_ctl.to(st.master.device)
-            self._step_t = self._step_ctl[:1]
+            self._step_t = self._step_t.to(st.master.device)
             if self._psteps is not None:
                 self._psteps = self._psteps.to(st.master.device)
 
@@ -98,11 +89,8 @@ class AdamW(torch.optim.Optimizer):
         args = (float(grp["lr"]), float(b1), float(b2), float(grp["eps"]), float(grp["weight_decay"]))
         if not missing and self._psteps is None:
             # the training path: every parameter has a gradient, one launch over the flat buffers
-            if FUSED_STEP:
-                ops.adamw_step(st.master, st.grad, self._m, self._v, st.shadow, *args, self._step_ctl)
-            else:
-                ops.counter_add(self._step_t, 1)
-                ops.adamw(st.master, st.grad, self._m, self._v, st.shadow, *args, self._step_t)
+            ops.counter_add(self._step_t, 1)
+            ops.adamw(st.master, st.grad, self._m, self._v, st.shadow, *args, self._step_t)
         else:
             # torch.optim.AdamW skips parameters whose .grad is None (no decay, no moment update,
             # no step count): per-parameter launches over the flat slices, per-parameter step counts

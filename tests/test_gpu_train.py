@@ -53,51 +53,23 @@ def test_capture_rollback_matches_eager():
     assert torch.equal(runs[0][1], runs[1][1])
 
 
-@pytest.mark.parametrize("overlap,dropout", [(False, 0.2), (True, 0.2), (False, 0.0)])
-def test_offsets_ring_matches_per_step_get_batch(overlap, dropout):
-    """TrainStep(ring=...): the offsets drawn ahead into the HBM ring (refilled a half at a time,
-    ring half = 3 steps so 8 steps cross 2 refills and a wrap) and gathered inside the step graph,
-    with the dropout snapshot taken by that launch, give the per-step get_batch loop's losses,
-    weights, dropout counter and last batch bit for bit -- single graph and segmented backward."""
-    from replicatinggpt_amd.engine import GradReducer, TrainStep
-    cfg = _cfg(dropout=dropout)
-    runs = []
-    for ring in (0, 3):
-        m, opt, s = _setup(cfg)
-        s.generator = torch.Generator().manual_seed(7)
-        red = GradReducer(m.flat.grad) if overlap else None
-        st = TrainStep(m, opt, s, red, use_graph=True, overlap=overlap, seg_layers=1, ring=ring)
-        st.capture(restore=True)
-        losses = [float(st.step().detach()) for _ in range(8)]
-        torch.cuda.synchronize()
-        if ring:
-            assert int(s.ring_ctl[0]) == 8 and int(s.ring_ctl[1]) == 0
-        x_last = st.x.detach().cpu().clone()
-        runs.append((losses, m.flat.master.detach().cpu().clone(), int(m._rng_counter), x_last))
-    assert runs[0][0] == runs[1][0]
-    assert torch.equal(runs[0][1], runs[1][1])
-    assert runs[0][2] == runs[1][2]
-    assert torch.equal(runs[0][3], runs[1][3])
-
-
 def test_deferred_splitk_reduces_bit_identical():
     """The weight gradients' split-K reduces deferred into later GEMM launches' tails
     (functional.DEFER, csrc RedJob) give the in-line reduce's bits: C2-width model (split-K weight
     gradients at B*T = 16384), graph replay with and without deferral, eager, and the segmented
     (DP-overlap) backward whose segments each flush their pending reduces.  The LayerNorm / b1
     column-sum reduces queued for one multi-job launch at the flush (DEFER.partials) likewise,
-    with and without the split-K deferral, and the weight-gradient GEMMs grouped into one persistent
-    launch (defer_wgrad)."""
+    with and without the split-K deferral."""
     from replicatinggpt_amd import functional as Fn
     from replicatinggpt_amd.engine import GradReducer, TrainStep
     cfg = _cfg(block_size=256, n_embd=384, n_head=6, n_layers=3, batch_size=64)
     runs = []
-    saved = Fn.DEFER.enabled, Fn.DEFER.partials_on, Fn.DEFER.wgrad_on
+    saved = Fn.DEFER.enabled, Fn.DEFER.partials_on
     try:
-        for defer, partials, wg, graph, overlap in ((False, False, False, True, False), (True, True, True, True, False),
-                                                    (True, True, True, False, False), (True, True, True, True, True),
-                                                    (True, False, False, True, False), (True, True, False, True, False)):
-            Fn.DEFER.enabled, Fn.DEFER.partials_on, Fn.DEFER.wgrad_on = defer, partials, wg
+        for defer, partials, graph, overlap in ((False, False, True, False), (True, True, True, False),
+                                                (True, True, False, False), (True, True, True, True),
+                                                (True, False, True, False)):
+            Fn.DEFER.enabled, Fn.DEFER.partials_on = defer, partials
             m, opt, s = _setup(cfg)
             red = GradReducer(m.flat.grad) if overlap else None   # world size 1: the segmentation only
             st = TrainStep(m, opt, s, red, use_graph=graph, overlap=overlap, seg_layers=1)
@@ -106,7 +78,7 @@ def test_deferred_splitk_reduces_bit_identical():
             torch.cuda.synchronize()
             runs.append((losses, m.flat.master.detach().cpu().clone(), m.flat.grad.detach().cpu().clone()))
     finally:
-        Fn.DEFER.enabled, Fn.DEFER.partials_on, Fn.DEFER.wgrad_on = saved
+        Fn.DEFER.enabled, Fn.DEFER.partials_on = saved
     for r in runs[1:]:
         assert r[0] == runs[0][0]
         assert torch.equal(r[1], runs[0][1]) and torch.equal(r[2], runs[0][2])
