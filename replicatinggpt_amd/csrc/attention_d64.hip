@@ -26,6 +26,36 @@
 namespace cg {
 int g_attn_variant = 0;
 
+#ifdef CG_ATTN_STAMPS
+// Diagnostic build only (make attnstamps; tools/attn_stamps.py): per workgroup of the resident
+// kernels, {start, operands landed (the prologue's wait), end} in s_memrealtime ticks (100 MHz) and
+// {kind << 48 | XCC << 40 | HW_ID} -- written by lane 0 of wave 0 with a plain vector store into a
+// buffer no other code reads.  Never in the product library.
+constexpr int ATTN_STAMP_WG = 4096;
+__device__ unsigned long long g_attn_stamps[ATTN_STAMP_WG * 4];
+extern "C" int cg_debug_attn_stamps(unsigned long long* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_stamps), (size_t)n * 4 * sizeof(unsigned long long)) ==
+                   hipSuccess ? 0 : 1;
+}
+__device__ __forceinline__ void attn_stamp(int slot, unsigned long long v) {
+    const int wg = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    if (threadIdx.x == 0 && wg < ATTN_STAMP_WG) {
+        volatile unsigned long long* p = g_attn_stamps + 4 * wg + slot + (threadIdx.x & 63);
+        *p = v;
+    }
+}
+__device__ __forceinline__ unsigned long long attn_now() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ unsigned long long attn_where(int kind) {
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    return ((unsigned long long)kind << 48) | ((unsigned long long)(xcc & 0xff) << 40) | hw;
+}
+#define ATTN_STAMP(slot, v) attn_stamp(slot, v)
+#else
+#define ATTN_STAMP(slot, v)
+#endif
+
 namespace {
 
 typedef float fv16 __attribute__((ext_vector_type(16)));
@@ -974,6 +1004,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64r(int H, const bf16_t* _
                                                           const uint32_t* __restrict__ mask, float dscale) {
     constexpr int T = 64 * NT;
     __shared__ __attribute__((aligned(16))) char smem[NT * 2 * TILE];   // K, V images of tile t at 2 t TILE
+    ATTN_STAMP(0, attn_now());
     int x, bh;
     block_coords<false>(x, bh);
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1013,6 +1044,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64r(int H, const bf16_t* _
     // then every destination is named "+v" by an (ordered, volatile) empty statement after the wait,
     // so nothing reads it earlier
     asm volatile("s_waitcnt vmcnt(%c0)\n\ts_barrier" ::"i"(4 * (NT - 1)) : "memory");
+    ATTN_STAMP(1, attn_now());
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
 #pragma unroll
@@ -1065,6 +1097,8 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64r(int H, const bf16_t* _
         store_rows_wide(o + (boff + qa) * ldo + hh * 64, oacc[g], dscale / lt, lane);
         if (lane < 32) lse[(int64_t)bh * T + qa] = (m_run[g] + __log2f(lt)) * LN2;
     }
+    ATTN_STAMP(2, attn_now());
+    ATTN_STAMP(3, attn_where(2));
 }
 
 // tile t > 0 of a resident kernel: this wave's DMAs of tiles 0..t have landed (4 DMA instructions per
@@ -1136,6 +1170,7 @@ __device__ __forceinline__ void dq_res(int bh, char* smem, int H, const bf16_t* 
             for (int t = 0; t < NT; ++t) mw[g][t] = 0u;
     }
     asm volatile("s_waitcnt vmcnt(%c0)\n\ts_barrier" ::"i"(4 * (NT - 1)) : "memory");
+    ATTN_STAMP(1, attn_now());
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
 #pragma unroll
@@ -1325,6 +1360,7 @@ __device__ __forceinline__ void dkdv_res(int bh, char* smem, int H, const bf16_t
     }
     // the row statistics are visible to every wave, and tile 0 has landed for every wave
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    ATTN_STAMP(1, attn_now());
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
         const int kq = kqs[p], key = kq + (lane & 31);
@@ -1385,6 +1421,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_d64r(int H, const bf16_t* _
                                                           const uint32_t* __restrict__ mask_fwd,
                                                           const uint32_t* __restrict__ mask_bwd, float dscale) {
     __shared__ __attribute__((aligned(16))) char smem[NT * 2 * TILE + 2 * 64 * NT * 4];
+    ATTN_STAMP(0, attn_now());
     int x, id;
     block_coords<false>(x, id);
     if (id & 1)
@@ -1393,6 +1430,8 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_d64r(int H, const bf16_t* _
     else
         dq_res<DROP, NT>(id >> 1, smem, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale, mask_fwd,
                          dscale);
+    ATTN_STAMP(2, attn_now());
+    ATTN_STAMP(3, attn_where(id & 1));
 }
 
 // =====================================================================================

@@ -34,6 +34,26 @@ extern "C" int cg_debug_pk_stamps_reset() {
 #define PK_STAMP(v)
 #endif
 
+#ifdef CG_PK_BOUNDS
+// Diagnostic build only (make bounds; tools/gemm_bounds.py): every LDS-DMA source chunk of k_gemm_pk
+// (the past-the-end reloads included) is checked against its operand's extent, every item's output
+// tile / split-K slab against the problem, and -- check-only, nothing issued -- the address stream of
+// round 3's L2-prefetch trial (commit db80795: one 128-B line per lane of K-tile g + 1 + PF, bytes 0
+// and 64), for PF = 1..3.  Counts: [0] A DMA, [1] B DMA, [2] item tile / slab, [3..5] prefetch PF = 1..3.
+// Violations are added by the offending lanes (vector atomics); never in the product library.
+__device__ unsigned long long g_pk_bounds[8];
+extern "C" int cg_debug_pk_bounds(unsigned long long* host8) {
+    return hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_pk_bounds), 8 * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
+}
+extern "C" int cg_debug_pk_bounds_reset() {
+    unsigned long long z[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_pk_bounds), z, sizeof(z)) == hipSuccess ? 0 : 1;
+}
+__device__ __forceinline__ void bounds_chk(const void* p, int bytes, const void* lo, const void* hi, int slot) {
+    if ((const char*)p < (const char*)lo || (const char*)p + bytes > (const char*)hi) atomicAdd(&g_pk_bounds[slot], 1ull);
+}
+#endif
+
 namespace cg {
 int g_pk_flags = 0;  // cg_set_tuning("pk_flags"): bit 0 = drain epilogue stores each step, bit 1 = per-fragment epilogue
 namespace {
@@ -55,6 +75,11 @@ struct DmaP {
     static_assert(!TR || R >= 128, "transposed image swizzle needs >= 16 chunks per row");
     uint32_t off[PER_WAVE];  // byte offset of this lane's 16-B chunk from the tile origin
     int64_t kstep;
+#ifdef CG_PK_BOUNDS
+    const void* lo = nullptr;
+    const void* hi = nullptr;
+    int slot = 0;
+#endif
 
     __device__ __forceinline__ void init(int64_t ld, int wave, int lane) {
 #pragma unroll
@@ -77,6 +102,9 @@ struct DmaP {
     // instructions per DMA (two 64-bit VALU adds, two v_readfirstlane, a null-pointer select) on a
     // VALU -> SGPR -> m0 dependency chain.
     __device__ __forceinline__ void issue1(const bf16_t* base, int i, uint32_t img, int wave) const {
+#ifdef CG_PK_BOUNDS
+        bounds_chk((const char*)base + off[i], 16, lo, hi, slot);
+#endif
         dma16sl(base, off[i], img + (uint32_t)((wave * PER_WAVE + i) * 1024));
     }
 };
@@ -394,6 +422,59 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         decode(j, m0, n0, sp);
         total += split_nk(sp);
     }
+#ifdef CG_PK_BOUNDS
+    da.lo = A;
+    da.hi = A + (AT ? K * lda : M * lda);
+    da.slot = 0;
+    db.lo = B;
+    db.hi = B + (BT ? K * ldb : N * ldb);
+    db.slot = 1;
+    if (flags & 128) {   // positive control (tools/gemm_bounds.py): windows 1 KB short, so in-range chunks count
+        da.hi = (const char*)da.hi - 1024;
+        db.hi = (const char*)db.hi - 1024;
+    }
+    // the L2-prefetch trial's cursors (db80795), one per distance PF = 1..3: tile j + PF of this
+    // block's K-tile sequence when the DMA cursor is at tile j (clamped to the last tile)
+    int pij[3] = {0, 0, 0}, pikt[3] = {0, 0, 0}, pink[3] = {0, 0, 0}, pkt[3] = {0, 0, 0};
+    const bf16_t* poa[3] = {A, A, A};
+    const bf16_t* pob[3] = {B, B, B};
+    auto pf_adv = [&](int q) {
+        if (pij[q] < my_items) {
+            if (pikt[q] == 0) {
+                int64_t m0, n0;
+                int sp;
+                decode(pij[q], m0, n0, sp);
+                pink[q] = split_nk(sp);
+                const int64_t kb = sp * kchunk;
+                poa[q] = AT ? A + kb * lda + m0 : A + m0 * lda + kb;
+                pob[q] = BT ? B + kb * ldb + n0 : B + n0 * ldb + kb;
+            }
+            pkt[q] = pikt[q];
+            if (++pikt[q] == pink[q]) {
+                pikt[q] = 0;
+                ++pij[q];
+            }
+        }
+    };
+    auto pf_check = [&](int q) {   // lines 0..127 of the A (waves 0-1) or B (waves 2-3) K-tile
+        const bool opb = wave >= 2;
+        const bool tr = opb ? BT : AT;
+        const int64_t ldx = opb ? ldb : lda;
+        const int i = (wave & 1) * 64 + lane;
+        const uint32_t off = tr ? 2u * (uint32_t)((i >> 1) * ldx) + 128u * (uint32_t)(i & 1) : 2u * (uint32_t)(i * ldx);
+        const char* t = opb ? (const char*)(pob[q] + pkt[q] * db.kstep) : (const char*)(poa[q] + pkt[q] * da.kstep);
+        bounds_chk(t + off, 4, opb ? db.lo : da.lo, opb ? db.hi : da.hi, 3 + q);
+        bounds_chk(t + off + 64, 4, opb ? db.lo : da.lo, opb ? db.hi : da.hi, 3 + q);
+    };
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        pf_adv(q);
+        for (int t = 1; t <= q + 1; ++t) {
+            pf_adv(q);
+            pf_check(q);
+        }
+    }
+#endif
 
     // DMA issue cursor (item ij, K-tile ikt) and its operand origins
     int ij = 0, ikt = 0, ink = 0;   // ink: K-tiles of the DMA cursor's item
@@ -497,6 +578,13 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         int nb = cur + NBUF - 1;
         if (nb >= NBUF) nb -= NBUF;
         prep_next(g + NBUF - 1 < total);
+#ifdef CG_PK_BOUNDS
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {   // the trial issued tile g + 1 + PF after this step's DMAs
+            pf_adv(q);
+            pf_check(q);
+        }
+#endif
         const uint32_t dimg = lds0 + (uint32_t)(nb * G::STAGE);
         const char* imgA = smem + cur * G::STAGE;
         const char* imgB = imgA + G::IMG_A;
@@ -560,6 +648,10 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
             int sp;
             decode(cj, m0, n0, sp);
             const int64_t mr = m0 + wm * 64 + (lane & 15), nc = n0 + wn * 64 + 4 * (lane >> 4);
+#ifdef CG_PK_BOUNDS
+            if (m0 < 0 || m0 + BM > M || n0 < 0 || n0 + BN > N || sp < 0 || sp >= split_k)
+                atomicAdd(&g_pk_bounds[2], 1ull);
+#endif
             if (WI_NOEPI) {
             } else if (EK == EK_SLAB || split_k > 1) {
 #pragma unroll

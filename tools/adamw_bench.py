@@ -20,7 +20,7 @@ def main():
         base[3].abs_()
         step = torch.full((1,), 3, dtype=torch.int64, device=dev)
         ref = None
-        for mode in (0, 2, 3, 0, 2, 3):
+        for mode in ((0, 2, 3, 4, 5, 0, 2, 3, 4, 5) if name == "c4" else (0, 1, 3, 5, 0, 1, 3, 5)):
             _lib.check(lib.cg_set_tuning(b"adamw_mode", mode), "tuning")
             p, g, m, v = (t.clone() for t in base)
             p16 = torch.empty(n, dtype=torch.bfloat16, device=dev)

@@ -1,7 +1,8 @@
 """Where the persistent 128x128 GEMM's K-steps spend their cycles: loads the stamp-instrumented
 diagnostic library (make -C replicatinggpt_amd/csrc stamps; gemm_pk.hip CG_PK_STAMPS) and prints,
 per shape, the per-wave s_memtime cycles of each K-step's head wait (vmcnt + barrier) and of its
-fragment reads + MFMA/DMA issue, the epilogue cycles per item and the clock the waves ran at.
+fragment reads + MFMA/DMA issue, the epilogue cycles per item and the clock the waves ran at --
+every op of the training census with the step's fused epilogue (bench.census_op).
 GPU only.  usage: python tools/gemm_stamps.py [c2|c4]"""
 import ctypes
 import os
@@ -13,21 +14,22 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import torch  # noqa: E402
 
-from gemm_scan import gemm_fn  # noqa: E402
+import bench  # noqa: E402
+from replicatinggpt_amd import PRESETS  # noqa: E402
 from replicatinggpt_amd import _lib as L  # noqa: E402
+from replicatinggpt_amd import functional as Fn  # noqa: E402
 
 
 def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
     lib = L.load()
     lib.cg_debug_pk_stamps.argtypes = [ctypes.c_void_p]
-    d, M = (384, 16384) if cfg == "c2" else (768, 65536)
-    shapes = [("qkv_fwd", M, 3 * d, d, 0, 0, 1), ("ffn1_fwd", M, 4 * d, d, 0, 0, 1), ("ffn2_fwd", M, d, 4 * d, 0, 0, 1),
-              ("ffn2_dgrad", M, 4 * d, d, 0, 1, 1), ("ffn2_wgrad", d, 4 * d, M, 1, 1, 14 if cfg == "c2" else 7)]
+    c = PRESETS[cfg]
     L.check(lib.cg_set_tuning(b"gemm_variant", 9))
     buf = (ctypes.c_ulonglong * 8)()
-    for name, m, n, k, at, bt, split in shapes:
-        fn = gemm_fn(m, n, k, at, bt, split)
+    for name, m, n, k, at, bt, kind, _ in bench.census_shapes(c, c.batch_size, c.block_size):
+        split = Fn._wgrad_split(m, n, k, True) if kind == "wgrad" else 1
+        fn, _ = bench.census_op(name, m, n, k, at, bt, kind, torch.device("cuda"))
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
@@ -42,7 +44,7 @@ def main():
         waves = max(waves, 1)
         items = m // 128 * (n // 128) * split
         clk = wall / max(real, 1) * 100.0   # MHz
-        print(f"{cfg} {name:11s} M={m:6d} N={n:5d} K={k:6d} split {split:2d}: {a.elapsed_time(b) * 1e3:7.1f} us | "
+        print(f"{cfg} {name:11s} {kind:16s} M={m:6d} N={n:5d} K={k:6d} split {split:2d}: {a.elapsed_time(b) * 1e3:7.1f} us | "
               f"per wave {wall / waves:8.0f} cyc @ {clk:5.0f} MHz, {steps / waves:5.1f} K-steps: "
               f"head wait {sw / steps:6.0f} cyc/step, reads+MFMA {sm / steps:6.0f} cyc/step, "
               f"epilogue {se / max(1, items * 4):6.0f} cyc/item-wave, other {(wall - sw - sm - se) / waves:7.0f} cyc/wave",

@@ -36,6 +36,7 @@ def run(M, C, p):
 if __name__ == "__main__":
     lib = L.load()
     L.check(lib.cg_set_tuning(b"ln_pf", int(os.environ.get("LN_PF", "0"))), "tuning")   # next-row prefetch A/B
+    L.check(lib.cg_set_tuning(b"ln_nt", int(os.environ.get("LN_NT", "-1"))), "tuning")   # non-temporal streams A/B
     rpbs = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0]
     waves = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0]
     for M, C in ((16384, 384), (65536, 768)):
