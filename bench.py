@@ -217,11 +217,11 @@ def gemm_kernel_name(M, N, at, bt, split, dev):
     return "k_gemm_pk<128x128>" + (" + k_splitk_reduce4" if split > 1 else "")
 
 
-def _time_ms(fn, reps=20):
+def _time_ms(fn, reps=20, warm=3):
     """Average duration (ms) of fn() over reps back-to-back calls replayed from one hipGraph (as in
     the training step; eagerly the small LayerNorm launches are host-bound), HIP events on the
-    replay stream (the stream every charpt op launches on)."""
-    for _ in range(3):
+    replay stream (the stream every charpt op launches on), after ``warm`` eager calls."""
+    for _ in range(warm):
         fn()
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
@@ -312,7 +312,9 @@ def kernel_census(cfg, Bsz, T, dev):
     v.abs_()
     p16 = torch.empty(n, dtype=torch.bfloat16, device=dev)
     step_t = torch.ones(1, dtype=torch.int64, device=dev)
-    t = _time_ms(lambda: ops.adamw(pp, g, m, v, p16, 1e-3, 0.9, 0.999, 1e-8, 0.01, step_t))
+    # steady state: the step's optimizer buffers are long-lived; on freshly allocated ones the first
+    # launches ran up to 20 % slower (profiles/r4_adamw_ab.txt)
+    t = _time_ms(lambda: ops.adamw(pp, g, m, v, p16, 1e-3, 0.9, 0.999, 1e-8, 0.01, step_t), warm=20)
     gbs = 30 * n / (t * 1e-3) / 1e9
     out["adamw"] = {"ms": round(t, 4), "params": n, "bytes": 30 * n, "achieved": round(gbs, 1), "unit": "GB/s",
                     "peak": PEAK_HBM_GBS, "frac": round(gbs / PEAK_HBM_GBS, 4)}

@@ -185,7 +185,8 @@ namespace cg {
 // thread in flight once the 30 B/param stream is far past the 256 MB Infinity Cache (n >= 32 M: C4
 // 86 M params, -2.4 % same-box interleaved A/B), plain loads/stores below (C2 10.8 M: the NT form is
 // 16 % slower there, the gradients just written by the backward are still partly cache-resident);
-// 1 plain, 2 NT + 2 groups, 3 plain + 2 groups (A/B: profiles/r3_adamw_ab.txt)
+// 1 plain, 2 NT + 2 groups, 3 plain + 2 groups (A/B: profiles/r3_adamw_ab.txt), 4 NT + 4 groups,
+// 5 plain + 4 groups
 int g_adamw_mode = 0;
 }
 
@@ -208,6 +209,8 @@ static int adamw_launch(float* p, const float* g, float* m, float* v, uint16_t* 
     if (!vec) ADAMW(false, false, 1);
     else if (mode == 2) ADAMW(true, true, 2);
     else if (mode == 3) ADAMW(true, false, 2);
+    else if (mode == 4) ADAMW(true, true, 4);    // A/B: four groups in flight per thread
+    else if (mode == 5) ADAMW(true, false, 4);
     else ADAMW(true, false, 1);
 #undef ADAMW
     CG_LAUNCH_CHECK("cg_adamw");

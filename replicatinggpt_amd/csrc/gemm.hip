@@ -420,6 +420,7 @@ extern int g_ln_rpb;  // layernorm.hip
 extern int g_adamw_mode;  // ce_adamw.hip
 extern int g_ln_waves;  // layernorm.hip
 extern int g_ln_pf;     // layernorm.hip
+extern int g_ln_nt;     // layernorm.hip
 }
 
 extern "C" int cg_set_tuning(const char* key, int value) {
@@ -478,8 +479,12 @@ extern "C" int cg_set_tuning(const char* key, int value) {
         return CG_OK;
     }
     if (!strcmp(key, "adamw_mode")) {
-        CG_REQUIRE(value >= 0 && value <= 3, "cg_set_tuning: adamw_mode out of range");
+        CG_REQUIRE(value >= 0 && value <= 5, "cg_set_tuning: adamw_mode out of range");
         g_adamw_mode = value;
+        return CG_OK;
+    }
+    if (!strcmp(key, "ln_nt")) {   // the LayerNorm backward's non-temporal streams (-1 automatic, 0..3)
+        g_ln_nt = value;
         return CG_OK;
     }
     if (!strcmp(key, "ln_pf")) {

@@ -46,6 +46,23 @@ struct VecIO<4> {
     }
 };
 
+// non-temporal VEC-float load / store (VEC 2 or 4): the stream bypasses the caches' allocation
+template <int VEC>
+__device__ __forceinline__ void ld_nt(const float* p, float* v) {
+    typedef float nfv __attribute__((ext_vector_type(VEC)));
+    const nfv t = __builtin_nontemporal_load((const nfv*)p);
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) v[q] = t[q];
+}
+template <int VEC>
+__device__ __forceinline__ void st_nt(float* p, const float* v) {
+    typedef float nfv __attribute__((ext_vector_type(VEC)));
+    nfv t;
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) t[q] = v[q];
+    __builtin_nontemporal_store(t, (nfv*)p);
+}
+
 template <typename T>
 __device__ __forceinline__ void ld_vec_any(const T* p, float* v, int n);
 template <>
@@ -148,6 +165,10 @@ namespace cg {
 int g_ln_rpb = 0;     // cg_set_tuning("ln_rpb"): rows per backward block (0 = automatic)
 int g_ln_waves = 0;   // cg_set_tuning("ln_waves"): waves per backward block, 4 or 8 (0 = automatic)
 int g_ln_pf = 0;      // cg_set_tuning("ln_pf"): 1 = next row's loads before the current row (FULL shapes)
+// cg_set_tuning("ln_nt"): the backward's non-temporal streams (k_ln_bwd NTM) for the FULL C = 384 / 768
+// rows; -1 (default) = 3 at C = 768 (C4 rows kernel 172 -> 133 us, 4.7 -> 6.0 TB/s:
+// profiles/r4_ln_nt_ab.txt), 0 at C = 384
+int g_ln_nt = -1;
 }  // namespace cg
 // Waves per backward block: 8, or 4 where the row kernel's registers cap a SIMD at 3 waves (the
 // VEC 4 variants, C = 512..1024: 166 VGPRs at C = 768) -- 8-wave blocks then fit once per CU (8 of
@@ -195,7 +216,8 @@ struct LnRow {
 // column sums), summed over the 8 waves in a fixed order.  Measured (tools/ln_bench.py): issuing
 // the next row's loads before reducing the current one (double-buffered rows) gained nothing at
 // C4 and lost 15-25 % at C2 (occupancy); ~4.8 TB/s at C4, 5.2 TB/s at C2 without dropout.
-template <int VEC, int NJ, typename TDY, int WAVES, bool FULL = false, bool PF = false>
+// NTM (VEC 2 / 4): 1 the residual gradient read non-temporally, 2 also x, 3 also the dx store
+template <int VEC, int NJ, typename TDY, int WAVES, bool FULL = false, bool PF = false, int NTM = 0>
 __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ dy, const float* __restrict__ x,
                                                            const float* __restrict__ w, const float* __restrict__ mean,
                                                            const float* __restrict__ rstd,
@@ -229,9 +251,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
         for (int j = 0; j < NJ; ++j) {
             const int e = (j * 64 + lane) * VEC;
             if (FULL || e < C) {
-                VecIO<VEC>::ld(x + r * C + e, b.x[j]);
+                if constexpr (NTM >= 2 && VEC >= 2) ld_nt<VEC>(x + r * C + e, b.x[j]);
+                else VecIO<VEC>::ld(x + r * C + e, b.x[j]);
                 ld_vec_any<TDY>(dy + r * C + e, b.d[j], VEC);
-                if (HR) VecIO<VEC>::ld(dres + r * C + e, b.rv[j]);
+                if constexpr (HR && NTM >= 1 && VEC >= 2) ld_nt<VEC>(dres + r * C + e, b.rv[j]);
+                else if (HR) VecIO<VEC>::ld(dres + r * C + e, b.rv[j]);
             }
         }
     };
@@ -285,7 +309,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
                     o[q] = b.rs * (g[j][q] - c1 - xh[j][q] * c2);
                     if (HR) o[q] += b.rv[j][q];
                 }
-                VecIO<VEC>::st(dx + r * C + e, o);
+                if constexpr (NTM >= 3 && VEC >= 2) st_nt<VEC>(dx + r * C + e, o);
+                else VecIO<VEC>::st(dx + r * C + e, o);
                 if (lp.out) {
                     float z[VEC];
                     if (lp.thr && row_groups) {
@@ -419,19 +444,37 @@ int launch_ln_bwd(const TDY* dy, const float* x, const float* w, const float* me
             k_ln_bwd<V, N, TDY, 8, F, P><<<(unsigned)nblk, 512, lds, st>>>(dy, x, w, mean, rstd, dres, dx, lp, part,    \
                                                                            rows, C, rpb);                      \
     } while (0)
+#define LNB_NT(V, N, M_)                                                                                       \
+    do {                                                                                                       \
+        if (waves == 4)                                                                                        \
+            k_ln_bwd<V, N, TDY, 4, true, false, M_><<<(unsigned)nblk, 256, lds, st>>>(dy, x, w, mean, rstd, dres, dx, \
+                                                                                      lp, part, rows, C, rpb); \
+        else                                                                                                   \
+            k_ln_bwd<V, N, TDY, 8, true, false, M_><<<(unsigned)nblk, 512, lds, st>>>(dy, x, w, mean, rstd, dres, dx, \
+                                                                                      lp, part, rows, C, rpb); \
+    } while (0)
 #define LNB(V, N, F)                        \
     do {                                    \
         if (F && g_ln_pf) LNB_(V, N, F, F); \
         else LNB_(V, N, F, false);          \
     } while (0)
     // the exact shapes run FULL rows (C = 64 V N: no per-lane column guards)
-    if (C == 384 && al16) LNB(2, 3, true);
+    const int ntm = g_ln_nt >= 0 ? g_ln_nt : (C == 768 ? 3 : 0);
+    const bool nt_ok = al16 && !g_ln_pf && (C == 384 || C == 768);
+    if (nt_ok && ntm == 1 && C == 384) LNB_NT(2, 3, 1);
+    else if (nt_ok && ntm == 2 && C == 384) LNB_NT(2, 3, 2);
+    else if (nt_ok && ntm == 3 && C == 384) LNB_NT(2, 3, 3);
+    else if (nt_ok && ntm == 1 && C == 768) LNB_NT(4, 3, 1);
+    else if (nt_ok && ntm == 2 && C == 768) LNB_NT(4, 3, 2);
+    else if (nt_ok && ntm == 3 && C == 768) LNB_NT(4, 3, 3);
+    else if (C == 384 && al16) LNB(2, 3, true);
     else if (C == 768 && al16) LNB(4, 3, true);
     else if (C == 512 && al16) LNB(4, 2, true);
     else if (C == 1024 && al16) LNB(4, 4, true);
     else LNB(1, 16, false);   // C <= 1024
 #undef LNB
 #undef LNB_
+#undef LNB_NT
     if (!defer && (dw || db || dbias))
         launch_reduce_partials3(part, nblk, NP * C, dw, db, dbias, C, accumulate, dbias_accumulate, st);
     return CG_OK;
