@@ -166,8 +166,10 @@ int g_ln_rpb = 0;     // cg_set_tuning("ln_rpb"): rows per backward block (0 = a
 int g_ln_waves = 0;   // cg_set_tuning("ln_waves"): waves per backward block, 4 or 8 (0 = automatic)
 int g_ln_pf = 0;      // cg_set_tuning("ln_pf"): 1 = next row's loads before the current row (FULL shapes)
 // cg_set_tuning("ln_nt"): the backward's non-temporal streams (k_ln_bwd NTM) for the FULL C = 384 / 768
-// rows; -1 (default) = 3 at C = 768 (C4 rows kernel 172 -> 133 us, 4.7 -> 6.0 TB/s:
-// profiles/r4_ln_nt_ab.txt), 0 at C = 384
+// rows; -1 (default) = 3: the residual gradient and x read and dx written non-temporally.  dx is read
+// again only by the next LayerNorm backward, after the sublayer's GEMMs and attention, so caching it
+// only evicts their operands: C4 rows kernel 172 -> 133 us (4.7 -> 6.0 TB/s), C4 step 54.0 -> 53.6 ms,
+// C2 step 3.045 -> 3.038 ms (the C2 kernel alone 18.0 -> 18.4 us) -- profiles/r4_ln_nt_ab.txt
 int g_ln_nt = -1;
 }  // namespace cg
 // Waves per backward block: 8, or 4 where the row kernel's registers cap a SIMD at 3 waves (the
@@ -459,7 +461,7 @@ int launch_ln_bwd(const TDY* dy, const float* x, const float* w, const float* me
         else LNB_(V, N, F, false);          \
     } while (0)
     // the exact shapes run FULL rows (C = 64 V N: no per-lane column guards)
-    const int ntm = g_ln_nt >= 0 ? g_ln_nt : (C == 768 ? 3 : 0);
+    const int ntm = g_ln_nt >= 0 ? g_ln_nt : 3;
     const bool nt_ok = al16 && !g_ln_pf && (C == 384 || C == 768);
     if (nt_ok && ntm == 1 && C == 384) LNB_NT(2, 3, 1);
     else if (nt_ok && ntm == 2 && C == 384) LNB_NT(2, 3, 2);
