@@ -203,17 +203,31 @@ def gemm_census(cfg, Bsz, T, dev):
         split = Fn._wgrad_split(m, n, k, True) if kind == "wgrad" else 1
         out.append({"name": name, "M": m, "N": n, "K": k, "epilogue": kind, "ms": ms, "launches": cnt,
                     "flops": 2.0 * m * n * k, "split": split,
-                    "kernel": gemm_kernel_name(m, n, at, bt, split, dev)})
+                    "kernel": gemm_kernel_name(m, n, at, bt, split, dev, kind)})
         torch.cuda.empty_cache()
     return out
 
 
-def gemm_kernel_name(M, N, at, bt, split, dev):
-    """The kernel cg_gemm's default dispatch picks (gemm_bf16.hip pick_variant): the 8-wave 256x256
-    tile at >= 2 such tiles per CU (no split, A not transposed), else the 128x128 one."""
+def gemm_kernel_name(M, N, at, bt, split, dev, kind="store"):
+    """The kernel cg_gemm's default dispatch picks (gemm_bf16.hip pick_variant, gemm_pk.hip
+    launch_n96): the 8-wave 256x256 tile at >= 2 such tiles per CU (no split, A not transposed);
+    128x96 tiles for the fp32 residual forwards where they shorten the busiest slot's work (rounds
+    of items x tile width; cg_set_tuning gemm_n96); else 128x128."""
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
     if split == 1 and not at and M % 256 == 0 and N % 256 == 0 and (M // 256) * (N // 256) >= 2 * cus:
         return "k_gemm_p8<256x256>"
+    n96 = 1
+    for kv in filter(None, os.environ.get("CHARPT_TUNING", "").split(",")):
+        k, _, v = kv.partition("=")
+        if k.strip() == "gemm_n96":
+            n96 = int(v)
+    if (n96 and split == 1 and not at and not bt and kind in ("bias_resid", "bias_drop_resid") and M % 128 == 0
+            and N % 96 == 0):
+        slots = 2 * cus
+        crit96 = -(-(M // 128) * (N // 96) // slots) * 96
+        crit128 = -(-(M // 128) * (N // 128) // slots) * 128 if N % 128 == 0 else float("inf")
+        if crit96 < crit128:
+            return "k_gemm_pk<128x96>"
     return "k_gemm_pk<128x128>" + (" + k_splitk_reduce4" if split > 1 else "")
 
 

@@ -378,6 +378,7 @@ int g_gemm_variant = 0;
 int g_gemm_max_grid = 0;
 int g_gemm_group_p8 = 0;   // persistent-kernel tile order (gemm_tile.h tile_rc), cg_set_tuning knobs
 int g_gemm_group_pk = 0;
+int g_gemm_n96 = 1;       // cg_set_tuning("gemm_n96"): 128x96 tiles for the part-filling fp32 residual forwards (gemm_pk.hip launch_n96)
 int g_defer_splitk = 0;   // cg_set_tuning("defer_splitk"): split-K reduces of fp32 STORE outputs deferred
 RedJobs g_red_pending = {};
 hipStream_t g_red_stream = nullptr;   // the stream the pending jobs were enqueued on
@@ -448,6 +449,10 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     if (!strcmp(key, "gemm_group_pk")) {
         CG_REQUIRE(value >= 0 && value < 256, "cg_set_tuning: gemm_group_pk out of range");
         g_gemm_group_pk = value;
+        return CG_OK;
+    }
+    if (!strcmp(key, "gemm_n96")) {
+        g_gemm_n96 = value;
         return CG_OK;
     }
     if (!strcmp(key, "pk_flags")) {

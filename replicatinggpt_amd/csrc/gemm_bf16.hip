@@ -227,10 +227,6 @@ bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf1
     if (e.resid && ((((uintptr_t)e.resid) & 15) || e.ld_resid % 4)) return false;
     if (e.aux && ((((uintptr_t)e.aux) & 15) || e.ld_aux % 8)) return false;
     int v = pick_variant(at, bt, M, N, split_k);
-    // the 128x192 tile has the fixed-kind item epilogues only (no keep bits, column partials or beta)
-    if (v == 18 && (e.colpart || e.aux_dtype == CG_BITS || e.beta != 0.f || at || bt || N % 192 || split_k != 1 ||
-                    (g_pk_flags & 2)))
-        v = 9;
     if (K % (FBK * split_k)) {
         // uneven split-K (the last split shorter): only the 128x128 persistent kernel, and only when
         // every split is non-empty; otherwise the generic kernels (ceil-sized chunks) take it

@@ -108,6 +108,7 @@ extern int g_gemm_variant;
 extern int g_gemm_max_grid;
 extern int g_gemm_group_p8;
 extern int g_gemm_group_pk;
+extern int g_gemm_n96;
 // test knob (cg_set_tuning("pk_flags", f)) for the persistent kernel's epilogue (gemm_pk.hip)
 extern int g_pk_flags;
 int gemm_cu_count();  // compute units of the current device (cached; gemm_pk.hip)

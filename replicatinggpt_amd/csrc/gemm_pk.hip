@@ -339,9 +339,75 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
     store_item<WIDE>(acc, mr, nc, Cv, c_dtype, ldc);
 }
 
+// Dropout keep nibbles of a wave's 64 x 16NJ item fragment for any NJ: as drop_nibbles, lanes l and
+// l ^ 16 hold the two 4-column halves of one 8-column Philox group, but the pair splits the work by
+// rows -- lane half odd = (lane >> 4) & 1 evaluates rows i = 2 odd, 2 odd + 1 for every j -- and
+// trades one word per j.  Same bits.
+template <int NJ>
+__device__ __forceinline__ void drop_nibbles_rows(const EpiArgs& epi, uint64_t stream, int64_t mr, int64_t nc, int64_t N,
+                                                  uint32_t (&nib)[4][NJ]) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t odd = (lane >> 4) & 1;
+    const int64_t c8 = nc & ~(int64_t)7;
+    uint32_t mine[NJ], other[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        mine[j] = 0u;
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii) {
+            const uint64_t idx = (uint64_t)(mr + 16 * (2 * odd + ii)) * (uint64_t)N + (uint64_t)(c8 + 16 * j);
+            mine[j] |= keep8_bits(philox_group(epi.seed, stream, idx >> 3), epi.thr) << (8 * ii);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) other[j] = (uint32_t)__shfl_xor((int)mine[j], 16, 64);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const uint32_t w = ((uint32_t)(i >> 1) == odd) ? mine[j] : other[j];
+            nib[i][j] = (w >> (8 * (i & 1) + 4 * odd)) & 0xfu;
+        }
+}
+
+// The fp32 residual epilogues (CG_EPI_BIAS_RESID, CG_EPI_BIAS_DROP_RESID) of a 64 x 16NJ wave tile:
+// epi_item's arithmetic and order (bias, dropout, residual), operands loaded before the first store.
+template <int EK, int NJ>
+__device__ __forceinline__ void epi_resid_nj(fv4 (&acc)[4][NJ], int64_t mr, int64_t nc, int64_t N, float* C, int64_t ldc,
+                                             const EpiArgs& epi, uint64_t stream) {
+    static_assert(EK == CG_EPI_BIAS_RESID || EK == CG_EPI_BIAS_DROP_RESID, "residual kinds only");
+    float4 bv[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bv[j] = *(const float4*)(epi.bias + nc + 16 * j);
+    float4 r[4][NJ];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) r[i][j] = *(const float4*)(epi.resid + (mr + 16 * i) * epi.ld_resid + nc + 16 * j);
+    uint32_t nib[4][NJ];
+    if constexpr (EK == CG_EPI_BIAS_DROP_RESID) drop_nibbles_rows<NJ>(epi, stream, mr, nc, N, nib);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            fv4 v = acc[i][j];
+            v[0] += bv[j].x; v[1] += bv[j].y; v[2] += bv[j].z; v[3] += bv[j].w;
+            if constexpr (EK == CG_EPI_BIAS_DROP_RESID) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = ((nib[i][j] >> q) & 1u) ? v[q] * epi.dscale : 0.f;
+            }
+            v[0] = r[i][j].x + v[0]; v[1] = r[i][j].y + v[1]; v[2] = r[i][j].z + v[2]; v[3] = r[i][j].w + v[3];
+            *(float4*)(C + (mr + 16 * i) * ldc + nc + 16 * j) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+}
+
+// Wave grid: 64 x 64 wave tiles, except BN = 96 (two 64 x 48 wave tiles per 64-row band: NJ = 3
+// fragments of 16 columns instead of 4).
 template <int BM, int BN, int NBUF, int BK = FBK>
 struct GeoP {
-    static constexpr int WM = BM / 64, WN = BN / 64, WAVES = WM * WN, THREADS = WAVES * 64;
+    static constexpr int WM = BM / 64, WN = BN == 96 ? 2 : BN / 64, WAVES = WM * WN, THREADS = WAVES * 64;
+    static constexpr int WTN = BN / WN, NJ = WTN / 16;   // wave tile columns, 16-column fragments per wave
+    static_assert(WTN == 64 || WTN == 48, "wave tile");
     static constexpr int IMG_A = BM * BK * 2, IMG_B = BN * BK * 2, STAGE = IMG_A + IMG_B;
     static constexpr int LDS = NBUF * STAGE;
     static constexpr int OCC_LDS = (160 * 1024) / LDS;
@@ -368,7 +434,7 @@ constexpr int EK_ANY = -1, EK_SLAB = 6;
 // left at its default it schedules for 8+ waves/SIMD, keeps ONE A fragment register and waits
 // lgkmcnt(0) before every 4 MFMAs (LDS latency exposed 8x per K-tile)
 template <bool AT, bool BT, int BM, int BN, int NBUF, int EK, int BK>
-__global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, (GeoP<BM, BN, NBUF, BK>::OCC))
+__global__ __launch_bounds__((GeoP<BM, BN, NBUF, BK>::THREADS), (GeoP<BM, BN, NBUF, BK>::OCC))
 __attribute__((amdgpu_waves_per_eu(1, GeoP<BM, BN, NBUF, BK>::WPE)))
 void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
                const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype, int64_t ldc,
@@ -376,6 +442,9 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     static_assert(BK == 64 || BK == 32, "BK");
     constexpr int NS = BK / 32;   // 32-deep MFMA slices per K-tile
     using G = GeoP<BM, BN, NBUF, BK>;
+    constexpr int NJ = G::NJ, WTN = G::WTN;
+    static_assert(NJ == 4 || (!BT && (EK == CG_EPI_BIAS_RESID || EK == CG_EPI_BIAS_DROP_RESID)),
+                  "48-column wave tiles: the fp32 residual kinds with a K-contiguous B only");
     using DA = DmaP<AT, BM, G::WAVES, BK>;
     using DB = DmaP<BT, BN, G::WAVES, BK>;
     constexpr int LPT = DA::PER_WAVE + DB::PER_WAVE;  // DMA instructions per thread per K-tile
@@ -508,11 +577,11 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         }
     };
 
-    fv4 acc[4][4];
+    fv4 acc[4][NJ];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NJ; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
     for (int s = 0; s < NBUF - 1; ++s)
@@ -532,8 +601,10 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     // issue order).
     // (8 for the fixed kinds whose bf16 output goes out as 16-B row segments -- store_item: with an
     // fp32 output they issue 16, more than counted, which only makes the wait conservative)
+    // (4 NJ = 12 for the 48-column wave tiles, whose residual kinds store each fragment on its own)
     constexpr int EPI_OPS =
-        (EK == CG_EPI_STORE || EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_RELU_BWD) ? 8 : 16;
+        NJ != 4 ? 4 * NJ
+                : (EK == CG_EPI_STORE || EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_RELU_BWD) ? 8 : 16;
     int cur = 0, cj = 0, ckt = 0;
     int cnk;   // K-tiles of the compute cursor's item
     {
@@ -590,17 +661,17 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         const char* imgB = imgA + G::IMG_A;
         // both 32-deep halves' fragments are read before the first MFMA (sched_barrier pins it):
         // otherwise the scheduler sinks each A read next to its 4 MFMAs and waits lgkmcnt(0) on it
-        sv8 af[NS][4], bf[NS][4];
+        sv8 af[NS][4], bf[NS][NJ];
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             if constexpr (BK == 64) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) bf[s][j] = frag<BT, BN>(imgB, wn * 64 + j * 16, s, lane);
+                for (int j = 0; j < NJ; ++j) bf[s][j] = frag<BT, BN>(imgB, wn * WTN + j * 16, s, lane);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) af[s][i] = frag<AT, BM>(imgA, wm * 64 + i * 16, s, lane);
             } else {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) bf[s][j] = frag32<BT, BN>(imgB, wn * 64 + j * 16, lane);
+                for (int j = 0; j < NJ; ++j) bf[s][j] = frag32<BT, BN>(imgB, wn * WTN + j * 16, lane);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) af[s][i] = frag32<AT, BM>(imgA, wm * 64 + i * 16, lane);
             }
@@ -620,7 +691,7 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         for (int t = 0; t < 4 * NS; ++t) {
             const int s = t >> 2, i = t & 3;
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < NJ; ++j)
                 if (!WI_NOMFMA) acc[i][j] = mfma_bf16(bf[s][j], af[s][i], acc[i][j]);
 #pragma unroll
             for (int d = 0; d < CG_PK_DPG; ++d)
@@ -630,7 +701,7 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
         for (int t = 4 * NS * CG_PK_DPG; t < LPT; ++t) issue_dma(t);
 #pragma unroll
         for (int t = 0; t < 4 * NS; ++t) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, NJ, 0);
 #pragma unroll
             for (int d = 0; d < CG_PK_DPG; ++d)
                 if (t * CG_PK_DPG + d < LPT) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
@@ -647,7 +718,7 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
             int64_t m0, n0;
             int sp;
             decode(cj, m0, n0, sp);
-            const int64_t mr = m0 + wm * 64 + (lane & 15), nc = n0 + wn * 64 + 4 * (lane >> 4);
+            const int64_t mr = m0 + wm * 64 + (lane & 15), nc = n0 + wn * WTN + 4 * (lane >> 4);
 #ifdef CG_PK_BOUNDS
             if (m0 < 0 || m0 + BM > M || n0 < 0 || n0 + BN > N || sp < 0 || sp >= split_k)
                 atomicAdd(&g_pk_bounds[2], 1ull);
@@ -657,21 +728,23 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) *(fv4*)(ws + ((int64_t)sp * M + mr + 16 * i) * N + nc + 16 * j) = acc[i][j];
+                    for (int j = 0; j < NJ; ++j) *(fv4*)(ws + ((int64_t)sp * M + mr + 16 * i) * N + nc + 16 * j) = acc[i][j];
             } else if constexpr (EK == EK_SLAB) {
             } else if (EK < 0 && (flags & 2)) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
+                    for (int j = 0; j < NJ; ++j)
                         epi_store4(acc[i][j], mr + 16 * i, nc + 16 * j, N, Cv, c_dtype, ldc, epi, stream);
-            } else {
+            } else if constexpr (NJ == 4) {
                 epi_item<EK < 0 ? EK_ANY : EK>(acc, mr, nc, N, Cv, c_dtype, ldc, epi, stream);
+            } else {
+                epi_resid_nj<EK, NJ>(acc, mr, nc, N, (float*)Cv, ldc, epi, stream);
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
+                for (int j = 0; j < NJ; ++j) acc[i][j] = fv4{0.f, 0.f, 0.f, 0.f};
             ckt = 0;
             ++cj;
             if (cj < my_items) {
@@ -802,6 +875,35 @@ bool launch_p(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
 #undef FG
 }
 
+// 128 x 96 tiles for the fp32 residual forwards (projection + residual, FFN2 + dropout + residual)
+// where they shorten the busiest resident slot's work (rounds of items x tile width): at C2
+// (M = 16384, N = 384) 384 tiles of 128 x 128 fill 3/4 of the 512 two-per-CU slots -- half the CUs
+// run two, half one, and the launch waits for the former -- while 512 tiles of 128 x 96 put two on
+// every CU: a quarter fewer MFMAs and an eighth fewer operand bytes on the busiest CU (proj 19.4 ->
+// 16.6 us, FFN2 36.7 -> 31.5 us).  Same K order per output element as 128 x 128: bitwise equal.  The
+// plain-store products measured no gain or a loss (QKV forward, transposed-B input gradients:
+// profiles/r4_gemm_n96_ab.txt).  cg_set_tuning("gemm_n96", 0) turns it off (A/B).
+bool launch_n96(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
+                int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, hipStream_t st) {
+    if (!g_gemm_n96 || at || bt || split_k != 1 || e.beta != 0.f || e.colpart || (g_pk_flags & 2)) return false;
+    if ((e.kind != CG_EPI_BIAS_RESID && e.kind != CG_EPI_BIAS_DROP_RESID) || !e.bias || !e.resid || c_dtype != CG_F32)
+        return false;
+    if (M % 128 || N % 96 || K % FBK) return false;
+    using G = GeoP<128, 96, 2>;
+    int64_t slots = (int64_t)cu_count() * G::OCC;
+    if (g_gemm_max_grid > 0 && g_gemm_max_grid < slots) slots = g_gemm_max_grid;
+    // the busiest slot's output columns: rounds of items x tile width
+    const int64_t t96 = (M / 128) * (N / 96), t128 = (M / 128) * (N / 128);
+    const int64_t crit96 = (t96 + slots - 1) / slots * 96, crit128 = N % 128 ? INT64_MAX : (t128 + slots - 1) / slots * 128;
+    if (crit96 >= crit128) return false;
+    const unsigned grid = (unsigned)(t96 < slots ? t96 : slots);
+#define L96(EK_) launch_1<false, false, 128, 96, 2, EK_, FBK>(grid, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, 1, K, nullptr, st)
+    if (e.kind == CG_EPI_BIAS_DROP_RESID && e.thr) L96(CG_EPI_BIAS_DROP_RESID);
+    else L96(CG_EPI_BIAS_RESID);   // dropout at p = 0 is the bias + residual epilogue
+#undef L96
+    return true;
+}
+
 }  // namespace
 
 int gemm_cu_count() { return cu_count(); }
@@ -810,7 +912,9 @@ bool pk_gemm_launch(int v, int at, int bt, int64_t M, int64_t N, int64_t K, cons
                     const bf16_t* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k,
                     float* ws, hipStream_t st) {
     switch (v) {
-        case 9: return launch_p<128, 128, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
+        case 9:
+            if (launch_n96(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, st)) return true;
+            return launch_p<128, 128, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
 #ifdef CG_AB_VARIANTS   // measured-slower A/B tiles (profiles/r1_gemm_scan*.txt, r2_gemm_ring_depth_scan.txt)
         case 10: launch_p<128, 128, 3>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st); return true;
         case 11:

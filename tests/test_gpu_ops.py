@@ -427,6 +427,39 @@ def test_gemm_epilogues(dt, M, N, K):
     assert relerr(g, acc * (aux.double() > 0)) < tol
 
 
+@pytest.mark.parametrize("M,K", [(16384, 384), (16384, 1536), (256, 128), (1024, 640)])
+@pytest.mark.parametrize("kind", ["bias_resid", "bias_drop_resid"])
+def test_gemm_n96_matches_128x128_bitwise(M, K, kind):
+    """The 128x96 tiles of the part-filling fp32 residual forwards (gemm_pk.hip launch_n96: the C2
+    projection and FFN2 forwards, GPT1.py:136,145-147) against the 128x128 tiles (cg_set_tuning
+    gemm_n96 = 0; their dropout mask is the oracle's, test_gemm_epilogues): same K order per output
+    element, so equal bit for bit, dropout included."""
+    from replicatinggpt_amd import _lib as L
+    Fn, lib = F(), L.load()
+    N = 384
+    torch.manual_seed(11)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV)
+    resid = torch.randn(M, N, device=DEV)
+    call = torch.tensor([4], dtype=torch.int64, device=DEV)
+    outs = []
+    try:
+        for n96 in (1, 0):
+            L.check(lib.cg_set_tuning(b"gemm_n96", n96))
+            o = torch.full((M, N), float("nan"), device=DEV)
+            kw = dict(dropout_p=0.2, seed=5, rng_call=call, site=3) if kind == "bias_drop_resid" else {}
+            Fn.linear_fwd(x, w, o, kind, bias=bias, resid=resid, **kw)
+            outs.append(o)
+    finally:
+        L.check(lib.cg_set_tuning(b"gemm_n96", 1))
+    torch.cuda.synchronize()
+    assert not torch.isnan(outs[0]).any()
+    assert torch.equal(outs[0], outs[1])
+    ref = (x.double() @ w.double().t() + bias.double())
+    if kind == "bias_resid":
+        assert relerr(outs[0], ref + resid.double()) < 1e-5
+
 def _attn_ref(q, k, v, scale, p=0.0, seed=0, stream=0):
     """q,k,v [B,T,H,D] float64; reference softmax attention with the oracle dropout mask."""
     B, T, H, D = q.shape
