@@ -90,75 +90,87 @@ def cpu_baseline(cfg, seconds=12.0, batch=16):
                       f"{cfg.n_layers}L/{cfg.n_head}H/{cfg.n_embd}d (the bench workload's shape)"}
 
 
-def census_op(name, M, N, K, at, bt, kind, dev, p=0.2):
+COLD_BYTES = 1 << 29   # census operand sets cycle through >= 512 MB: twice the 256 MB Infinity Cache
+
+
+def census_op(name, M, N, K, at, bt, kind, dev, p=0.2, cold=False):
     """Operands and a launch closure for one census GEMM with the epilogue the training step uses
     (functional.py AttnSublayerFn / FFNSublayerFn): "store" (bf16 output), "bias_resid" (fp32
     output = x + o W^T + b: the attention projection), "bias_relu_bits" (bf16 relu(a W1^T + b1) and
     its ReLU keep bits), "bias_drop_resid" (fp32 x + dropout(h W2^T + b2)), "relu_bwd_colpart"
     (bf16 relu'(h) (dz2 W2) from the keep bits, with the b1 column partials), "wgrad" (fp32,
-    deterministic split-K: the GEMM and its slab reduce).  Returns (run, kernels per call)."""
+    deterministic split-K: the GEMM and its slab reduce).  cold: successive calls cycle through as
+    many operand sets as make >= COLD_BYTES, so no call finds its operands in the Infinity Cache
+    (in the training step every activation operand was last touched a whole sublayer or more
+    earlier).  Returns (run, kernels per call)."""
     from replicatinggpt_amd import functional as Fn, ops
-    A = torch.randn((K, M) if at else (M, K), device=dev).to(torch.bfloat16)
-    B = torch.randn((K, N) if bt else (N, K), device=dev).to(torch.bfloat16)
+    from replicatinggpt_amd import _lib as L
+    lib = L.load()
     fp32_out = kind in ("wgrad", "bias_resid", "bias_drop_resid")
-    out = torch.empty(M, N, dtype=torch.float32 if fp32_out else torch.bfloat16, device=dev)
-    lda, ldb = A.shape[1], B.shape[1]
-    if kind == "wgrad":
-        split = Fn._wgrad_split(M, N, K, True)
-        ws = torch.empty(ops.gemm_workspace(M, N, split) // 4, dtype=torch.float32, device=dev) if split > 1 else None
+    split = Fn._wgrad_split(M, N, K, True) if kind == "wgrad" else 1
+    lda, ldb = (M if at else K), (N if bt else K)
+    relu_bits = kind == "bias_relu_bits" and lib.cg_gemm_relu_bits_supported(0, 0, M, N, K, lda, ldb, N)
+    colpart = kind == "relu_bwd_colpart" and lib.cg_gemm_colpart_supported(0, 1, M, N, K, lda, ldb, N)
 
-        def run():
+    def make_set():
+        st = {"A": torch.randn((K, M) if at else (M, K), device=dev).to(torch.bfloat16),
+              "B": torch.randn((K, N) if bt else (N, K), device=dev).to(torch.bfloat16),
+              "out": torch.empty(M, N, dtype=torch.float32 if fp32_out else torch.bfloat16, device=dev)}
+        if kind == "wgrad" and split > 1:
+            st["ws"] = torch.empty(ops.gemm_workspace(M, N, split) // 4, dtype=torch.float32, device=dev)
+        if kind in ("bias_resid", "bias_drop_resid"):
+            st["resid"] = torch.randn(M, N, device=dev)
+        if kind in ("bias_relu_bits", "relu_bwd_colpart"):
+            st["bits"] = torch.randint(-2 ** 31, 2 ** 31 - 1, (M, N // 32), dtype=torch.int32, device=dev)
+        if colpart:
+            st["part"] = torch.empty((M // 64, N), dtype=torch.float32, device=dev)
+        return st
+
+    first = make_set()
+    nbytes = sum(t.numel() * t.element_size() for t in first.values())
+    sets = [first] + [make_set() for _ in range(max(1, -(-COLD_BYTES // max(1, nbytes))) - 1)] if cold else [first]
+    bias = torch.randn(N, device=dev) * 0.1
+    call = torch.zeros(1, dtype=torch.int64, device=dev)
+    ctr = [0]
+
+    def run():
+        st = sets[ctr[0] % len(sets)]
+        ctr[0] += 1
+        A, B, out = st["A"], st["B"], st["out"]
+        if kind == "wgrad":
             ops.gemm(A, B, out, True, bool(at), bool(bt), M, N, K, lda, ldb, N, 0, None, None, 0, None, 0,
-                     0.0, 0, None, 0, 0.0, split, ws)
-        return run, 2 if split > 1 else 1
-    if kind == "store":
-        def run():
+                     0.0, 0, None, 0, 0.0, split, st.get("ws"))
+        elif kind == "store":
             ops.gemm(A, B, out, True, bool(at), bool(bt), M, N, K, lda, ldb, N, 0, None, None, 0, None, 0,
                      0.0, 0, None, 0, 0.0, 1, None)
-        return run, 1
-    bias = torch.randn(N, device=dev) * 0.1
-    if kind in ("bias_resid", "bias_drop_resid"):
-        resid = torch.randn(M, N, device=dev)
-        drop = kind == "bias_drop_resid"
-        call = torch.zeros(1, dtype=torch.int64, device=dev)
-        epi = Fn.EPI["bias_drop_resid" if drop else "bias_resid"]
-
-        def run():
-            ops.gemm(A, B, out, True, bool(at), bool(bt), M, N, K, lda, ldb, N, epi, bias, resid, N, None, 0,
+        elif kind in ("bias_resid", "bias_drop_resid"):
+            drop = kind == "bias_drop_resid"
+            epi = Fn.EPI["bias_drop_resid" if drop else "bias_resid"]
+            ops.gemm(A, B, out, True, bool(at), bool(bt), M, N, K, lda, ldb, N, epi, bias, st["resid"], N, None, 0,
                      p if drop else 0.0, 4919 if drop else 0, call if drop else None, 3 if drop else 0, 0.0, 1, None)
-        return run, 1
-    from replicatinggpt_amd import _lib as L
-    bits = torch.randint(-2 ** 31, 2 ** 31 - 1, (M, N // 32), dtype=torch.int32, device=dev)
-    lib = L.load()
-    if kind == "bias_relu_bits":
-        if not lib.cg_gemm_relu_bits_supported(0, 0, M, N, K, lda, ldb, N):   # the step's fallback
-            def run():
+        elif kind == "bias_relu_bits":
+            if relu_bits:
+                ops.gemm_bias_relu_bits(A, B, out, M, N, K, lda, ldb, N, bias, st["bits"], st["bits"].stride(0))
+            else:   # the step's fallback
                 ops.gemm(A, B, out, True, False, False, M, N, K, lda, ldb, N, Fn.EPI["bias_relu"], bias, None, 0,
                          None, 0, 0.0, 0, None, 0, 0.0, 1, None)
-            return run, 1
-
-        def run():
-            ops.gemm_bias_relu_bits(A, B, out, M, N, K, lda, ldb, N, bias, bits, bits.stride(0))
-        return run, 1
-    if kind == "relu_bwd_colpart":
-        part = torch.empty((M // 64, N), dtype=torch.float32, device=dev)
-        if not lib.cg_gemm_colpart_supported(0, 1, M, N, K, lda, ldb, N):   # the step's fallback (no partials)
-            def run():
+        elif kind == "relu_bwd_colpart":
+            if colpart:
+                ops.gemm_relu_bwd_colpart(A, B, out, M, N, K, lda, ldb, N, st["bits"], st["bits"].stride(0),
+                                          st["part"])
+            else:   # the step's fallback (no partials)
                 ops.gemm(A, B, out, True, False, True, M, N, K, lda, ldb, N, Fn.EPI["relu_bwd"], None, None, 0,
-                         bits, bits.stride(0), 0.0, 0, None, 0, 0.0, 1, None)
-            return run, 1
-
-        def run():
-            ops.gemm_relu_bwd_colpart(A, B, out, M, N, K, lda, ldb, N, bits, bits.stride(0), part)
-        return run, 1
-    raise ValueError(kind)
+                         st["bits"], st["bits"].stride(0), 0.0, 0, None, 0, 0.0, 1, None)
+        else:
+            raise ValueError(kind)
+    return run, (2 if split > 1 else 1)
 
 
-def time_gemm(name, M, N, K, at, bt, kind, dev, reps=30):
+def time_gemm(name, M, N, K, at, bt, kind, dev, reps=30, cold=False):
     """Average duration (ms) of one charpt bf16 GEMM launch of this shape with the step's epilogue
-    (census_op): reps back-to-back launches replayed from one hipGraph, HIP events on the replay
-    stream."""
-    run, _ = census_op(name, M, N, K, at, bt, kind, dev)
+    (census_op; cold: operands cycled past the Infinity Cache): reps back-to-back launches replayed
+    from one hipGraph, HIP events on the replay stream."""
+    run, _ = census_op(name, M, N, K, at, bt, kind, dev, cold=cold)
     for _ in range(3):
         run()
     # the reps launches replayed from a hipGraph, as in the training step: eagerly, the smallest
@@ -193,13 +205,13 @@ def census_shapes(cfg, Bsz, T):
     ]
 
 
-def gemm_census(cfg, Bsz, T, dev):
+def gemm_census(cfg, Bsz, T, dev, cold=False):
     """Average launch time of every GEMM of one training step, each with its step epilogue (HIP
-    events, time_gemm)."""
+    events, time_gemm; cold: operands cycled past the Infinity Cache)."""
     from replicatinggpt_amd import functional as Fn
     out = []
     for name, m, n, k, at, bt, kind, cnt in census_shapes(cfg, Bsz, T):
-        ms = time_gemm(name, m, n, k, at, bt, kind, dev)
+        ms = time_gemm(name, m, n, k, at, bt, kind, dev, cold=cold)
         split = Fn._wgrad_split(m, n, k, True) if kind == "wgrad" else 1
         out.append({"name": name, "M": m, "N": n, "K": k, "epilogue": kind, "ms": ms, "launches": cnt,
                     "flops": 2.0 * m * n * k, "split": split,

@@ -187,6 +187,15 @@ int cg_attn_fwd_premasked(int dtype, int64_t B, int64_t T, int64_t H, int64_t D,
 /* fill the MFMA path's keep-bit buffer for one attention call (0 < p < 1, T % 64 == 0)          */
 int cg_attn_dropmask(int64_t B, int64_t H, int64_t T, double dropout_p, uint64_t seed, const uint64_t* rng_call,
                      int site, uint64_t* mask, void* stream);
+/* one launch for a sublayer's LayerNorm forward (cg_layernorm_fwd arguments, GPT1.py:163 ln1) and
+   the keep bits of the attention it feeds (cg_attn_dropmask arguments): the two are independent and
+   the launch runs them side by side on the CUs (Philox VALU work under the LayerNorm's memory time).
+   Results identical to cg_layernorm_fwd followed by cg_attn_dropmask; shapes without a fused form
+   (y not bf16, C not 384 / 768, unaligned) take those two launches.                             */
+int cg_layernorm_fwd_attn_dropmask(const float* x, const float* w, const float* b, void* y, int y_dtype, float* mean,
+                                   float* rstd, int64_t rows, int64_t C, float eps, int64_t B, int64_t H, int64_t T,
+                                   double dropout_p, uint64_t seed, const uint64_t* rng_call, int site,
+                                   uint64_t* mask, void* stream);
 /* keep-bit buffer for dropout on the MFMA (bf16, head_size 64) path: the forward fills it from the
    Philox stream (cg_attn_fwd `mask`, may be NULL on the generic path or with p = 0) and the
    backward reads it (cg_attn_bwd `mask`; NULL -> regenerated inside the workspace).  Layout

@@ -62,6 +62,8 @@ _SIGS = {
     "cg_attn_fwd_premasked": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, P, P, P, c_i64, P, c_i64, P, c_flt, c_dbl,
                                       c_u64, P, c_int, P, P]),
     "cg_attn_dropmask": (c_int, [c_i64, c_i64, c_i64, c_dbl, c_u64, P, c_int, P, P]),
+    "cg_layernorm_fwd_attn_dropmask": (c_int, [P, P, P, P, c_int, P, P, c_i64, c_i64, c_flt, c_i64, c_i64, c_i64,
+                                               c_dbl, c_u64, P, c_int, P, P]),
     "cg_attn_mask_bytes": (c_i64, [c_i64, c_i64, c_i64]),
     "cg_attn_bwd_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
     "cg_attn_bwd": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, P, P, P, c_i64, P, c_i64, P, c_i64, P, P, P, P, c_i64,

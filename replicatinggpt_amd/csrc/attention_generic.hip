@@ -16,6 +16,7 @@
 #include <math.h>
 
 #include "attention_common.h"
+#include "ln_fwd.h"
 
 using namespace cg;
 
@@ -52,9 +53,10 @@ __device__ __forceinline__ uint32_t keep2(uint32_t w, us2 k) {
     return __builtin_bit_cast(uint32_t, (us2)(t >> (us2)15));
 }
 
+// block `bid` (256 threads) of the keep-bit generation: regions (bid * 4 + wave) * DM_TPW ..
 template <bool SUBF>
-__global__ __launch_bounds__(256) void k_attn_dropmask(int64_t T_, int64_t nbh, uint32_t* __restrict__ mask_f,
-                                                       uint32_t* __restrict__ mask_b, DropArgs d) {
+__device__ __forceinline__ void dropmask_block(int64_t T_, int64_t nbh, uint32_t* __restrict__ mask_f,
+                                               uint32_t* __restrict__ mask_b, const DropArgs& d, int bid) {
     const int NB = (int)(T_ >> 5), NP = NB >> 1;
     const int64_t nreg = (int64_t)NP * (NP + 1) / 2, ntile = mask_tiles(T_);
     const int64_t total = nbh * nreg;
@@ -63,7 +65,7 @@ __global__ __launch_bounds__(256) void k_attn_dropmask(int64_t T_, int64_t nbh, 
     const uint64_t stream = dropout_stream(d.rng_call, d.site);
     const uint16_t kc = (uint16_t)(SUBF ? d.thr - 0x8000u : 0x8000u - d.thr);
     const us2 K = us2{kc, kc};
-    const int64_t first = ((int64_t)blockIdx.x * 4 + w) * DM_TPW;
+    const int64_t first = ((int64_t)bid * 4 + w) * DM_TPW;
     if (first >= total) return;
     // butterfly stage j = 16 >> t: lanes with bit j clear keep the low blocks (mask m_j) and take their
     // partner's low blocks into the high ones (rotate right by 32 - j), the others the reverse
@@ -145,6 +147,31 @@ __global__ __launch_bounds__(256) void k_attn_dropmask(int64_t T_, int64_t nbh, 
                 __builtin_amdgcn_ubfe(a, 16 * h, 16) | (__builtin_amdgcn_ubfe(b, 16 * h, 16) << 16);
         }
     }
+}
+
+template <bool SUBF>
+__global__ __launch_bounds__(256) void k_attn_dropmask(int64_t T_, int64_t nbh, uint32_t* __restrict__ mask_f,
+                                                       uint32_t* __restrict__ mask_b, DropArgs d) {
+    dropmask_block<SUBF>(T_, nbh, mask_f, mask_b, d, (int)blockIdx.x);
+}
+
+// One launch for a sublayer's LayerNorm forward and its attention's keep bits (the two are
+// independent: LN1 feeds the QKV GEMM, the bits the attention after it).  Blocks 0..n_dm-1 generate
+// keep bits (Philox: VALU-bound), the rest run LayerNorm rows (HBM-bound) -- co-resident on the CUs,
+// so the Philox arithmetic hides under the LayerNorm's memory time instead of running as its own
+// 7.8 us launch at C2.  Bits and rows are exactly those of k_attn_dropmask and k_ln_fwd.
+template <bool SUBF, int VEC, int NJ>
+__global__ __launch_bounds__(256) void k_ln_fwd_dropmask(const float* __restrict__ x, const float* __restrict__ w,
+                                                         const float* __restrict__ b, bf16_t* __restrict__ y,
+                                                         float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                         int64_t rows, int C, float eps, int n_ln, int64_t T_,
+                                                         int64_t nbh, uint32_t* __restrict__ mask_f,
+                                                         uint32_t* __restrict__ mask_b, DropArgs d, int n_dm) {
+    const int bid = (int)blockIdx.x;
+    if (bid < n_dm)
+        dropmask_block<SUBF>(T_, nbh, mask_f, mask_b, d, bid);
+    else
+        ln_fwd_rows<VEC, NJ, bf16_t, 2, true>(x, w, b, y, mean_out, rstd_out, rows, C, eps, bid - n_dm, n_ln);
 }
 
 __device__ __forceinline__ bool keep_elem(const DropArgs& d, uint64_t stream, uint64_t idx) {
@@ -638,6 +665,44 @@ extern "C" int cg_attn_dropmask(int64_t B, int64_t H, int64_t T, double dropout_
     DropArgs d = make_drop(dropout_p, seed, rng_call, site);
     launch_dropmask(B, H, T, mask, d, (hipStream_t)stream);
     CG_LAUNCH_CHECK("cg_attn_dropmask");
+    return CG_OK;
+}
+
+extern "C" int cg_layernorm_fwd_attn_dropmask(const float* x, const float* w, const float* b, void* y, int y_dtype,
+                                              float* mean, float* rstd, int64_t rows, int64_t C, float eps, int64_t B,
+                                              int64_t H, int64_t T, double dropout_p, uint64_t seed,
+                                              const uint64_t* rng_call, int site, uint64_t* mask, void* stream) {
+    CG_REQUIRE(B > 0 && H > 0 && T > 0 && T % 64 == 0, "cg_layernorm_fwd_attn_dropmask: bad shape (T %% 64 == 0 required)");
+    CG_REQUIRE(dropout_p > 0 && dropout_p < 1 && mask, "cg_layernorm_fwd_attn_dropmask: needs 0 < p < 1 and a mask buffer");
+    CG_REQUIRE(rows > 0 && C > 0 && C <= 2048, "cg_layernorm_fwd_attn_dropmask: need 0 < C <= 2048");
+    hipStream_t st = (hipStream_t)stream;
+    const DropArgs d = make_drop(dropout_p, seed, rng_call, site);
+    const bool al16 = (((uintptr_t)x | (uintptr_t)w | (uintptr_t)b) & 15) == 0;
+    if (y_dtype != CG_BF16 || !al16 || (C != 384 && C != 768)) {   // the shapes without a fused form: two launches
+        const int rc = cg_layernorm_fwd(x, w, b, y, y_dtype, mean, rstd, rows, C, eps, stream);
+        if (rc != CG_OK) return rc;
+        launch_dropmask(B, H, T, mask, d, st);
+        CG_LAUNCH_CHECK("cg_layernorm_fwd_attn_dropmask");
+        return CG_OK;
+    }
+    const int64_t np = T / 64, regions = B * H * np * (np + 1) / 2;
+    const int n_dm = (int)ceil_div(regions, 4 * DM_TPW);
+    int n_ln = (int)ceil_div(rows, 8);   // k_ln_fwd's grid: 4 waves x 2 rows per block
+    n_ln = n_ln > 4096 ? 4096 : n_ln;
+    uint32_t* mf = (uint32_t*)mask;
+    uint32_t* mb = mf + B * H * mask_tiles(T) * 64;
+#define LDM(SUBF_, V_)                                                                                                \
+    k_ln_fwd_dropmask<SUBF_, V_, 3><<<n_dm + n_ln, 256, 0, st>>>(x, w, b, (bf16_t*)y, mean, rstd, rows, (int)C, eps, \
+                                                               n_ln, T, B * H, mf, mb, d, n_dm)
+    if (d.thr > 0x8000u) {
+        if (C == 384) LDM(true, 2);
+        else LDM(true, 4);
+    } else {
+        if (C == 384) LDM(false, 2);
+        else LDM(false, 4);
+    }
+#undef LDM
+    CG_LAUNCH_CHECK("cg_layernorm_fwd_attn_dropmask");
     return CG_OK;
 }
 

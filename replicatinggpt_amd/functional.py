@@ -372,6 +372,25 @@ def layernorm(x2, w, b, out_dtype, eps=1e-5):
     return y, mean, rstd
 
 
+# CHARPT_LN_MASK=0: the attention keep bits in their own launch (A/B of layernorm_attn_mask)
+LN_MASK = os.environ.get("CHARPT_LN_MASK", "1") != "0"
+
+
+def layernorm_attn_mask(x2, w, b, out_dtype, B, H, T, p, seed, rng_call, site, eps=1e-5):
+    """layernorm() and the dropout keep bits of the attention it feeds (cg_attn_dropmask) in one
+    launch: the Philox work runs beside the LayerNorm's memory traffic.  Returns (y, mean, rstd,
+    mask); same values as the two launches."""
+    rows, C = x2.shape
+    dev = x2.device
+    y = torch.empty((rows, C), dtype=out_dtype, device=dev)
+    mean = torch.empty(rows, dtype=torch.float32, device=dev)
+    rstd = torch.empty(rows, dtype=torch.float32, device=dev)
+    mask = torch.empty(ops.attn_mask_bytes(B, H, T) // 8, dtype=torch.int64, device=dev)
+    ops.layernorm_fwd_attn_dropmask(x2, w, b, y, mean, rstd, float(eps), B, H, T, float(p), int(seed), rng_call,
+                                    int(site), mask)
+    return y, mean, rstd, mask
+
+
 class GradLink:
     """What a sublayer's backward wants for its incoming residual-stream gradient (GPT1.py:163-164:
     the gradient of x + f(x) arrives at f as-is): a bf16 copy with the sublayer's output dropout
@@ -449,14 +468,15 @@ def layernorm_bwd(dy2, x2, w_reg, b_reg, mean, rstd, dres=None, want_lp=False, l
 def attention_fwd(qkv, B, T, H, D, out, scale, p, seed, rng_call, site, premask=None):
     """Returns (lse, mask): mask holds the dropout keep bits of the MFMA path (None when p == 0
     or when the generic kernels, which regenerate Philox in place, are used).  ``premask`` =
-    (mask, event): keep bits already generated on the side stream (the main stream waits on the
-    event instead of generating them)."""
+    (mask, event): keep bits already generated -- on the side stream (the main stream waits on the
+    event instead of generating them) or, event None, earlier on this stream (layernorm_attn_mask)."""
     d = H * D
     lse = torch.empty((B, H, T), dtype=torch.float32, device=qkv.device)
     mask, ready = None, False
     if p > 0 and premask is not None:
         mask, ev = premask
-        torch.cuda.current_stream(qkv.device).wait_event(ev)
+        if ev is not None:
+            torch.cuda.current_stream(qkv.device).wait_event(ev)
         ready = True
     elif p > 0 and T % 16 == 0:
         mask = torch.empty(ops.attn_mask_bytes(B, H, T) // 8, dtype=torch.int64, device=qkv.device)
@@ -554,12 +574,18 @@ class AttnSublayerFn(torch.autograd.Function):
         B, T, C = x.shape
         x2 = x.reshape(B * T, C)
         act = lc.act
-        a, mean, rstd = layernorm(x2, ln_w.master, ln_b.master, act)
+        pm = lc.premask
+        if pm is None and lc.p > 0 and LN_MASK and premask_ok(act, T, lc.head_size):
+            a, mean, rstd, mask = layernorm_attn_mask(x2, ln_w.master, ln_b.master, act, B, lc.n_head, T, lc.p,
+                                                      lc.seed, lc.rng_call, lc.site)
+            pm = (mask, None)
+        else:
+            a, mean, rstd = layernorm(x2, ln_w.master, ln_b.master, act)
         qkv = torch.empty((B * T, 3 * C), dtype=act, device=x.device)
         linear_fwd(a, qkv_w.operand(act), qkv)
         o = torch.empty((B * T, C), dtype=act, device=x.device)
         lse, ctx.mask = attention_fwd(qkv, B, T, lc.n_head, lc.head_size, o, lc.scale, lc.p, lc.seed, lc.rng_call,
-                                      lc.site, lc.premask)
+                                      lc.site, pm)
         out = torch.empty((B * T, C), dtype=torch.float32, device=x.device)
         linear_fwd(o, proj_w.operand(act), out, "bias_resid", bias=proj_b.master, resid=x2)
         ctx.save_for_backward(x2, a, mean, rstd, qkv, o, lse)

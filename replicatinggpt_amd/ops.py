@@ -96,6 +96,20 @@ def layernorm_fwd(x: Tensor, w: Tensor, b: Tensor, y: Tensor, mean: Tensor, rstd
                                       L.ptr(rstd), rows, C, eps, _s(x)), "layernorm_fwd")
 
 
+@_op("layernorm_fwd_attn_dropmask", ("y", "mean", "rstd", "mask"))
+def layernorm_fwd_attn_dropmask(x: Tensor, w: Tensor, b: Tensor, y: Tensor, mean: Tensor, rstd: Tensor, eps: float,
+                                B: int, H: int, T: int, dropout_p: float, seed: int, rng_call: Optional[Tensor],
+                                site: int, mask: Tensor) -> None:
+    """layernorm_fwd and attn_dropmask (the keep bits of the attention the LayerNorm feeds) in one
+    launch; same results as the two ops."""
+    C = x.shape[-1]
+    rows = x.numel() // C
+    L.check(L.load().cg_layernorm_fwd_attn_dropmask(L.ptr(x), L.ptr(w), L.ptr(b), L.ptr(y), L.dtype_code(y.dtype),
+                                                    L.ptr(mean), L.ptr(rstd), rows, C, eps, B, H, T, dropout_p, seed,
+                                                    L.ptr(rng_call), site, L.ptr(mask), _s(x)),
+            "layernorm_fwd_attn_dropmask")
+
+
 @_op("layernorm_bwd", ("dx", "dx_lp", "dw", "db", "ws", "lp_colsum"))
 def layernorm_bwd(dy: Tensor, x: Tensor, w: Tensor, mean: Tensor, rstd: Tensor, dres: Optional[Tensor], dx: Tensor,
                   dx_lp: Optional[Tensor], dw: Optional[Tensor], db: Optional[Tensor], accumulate: bool,

@@ -91,6 +91,37 @@ def test_layernorm(C, out_dtype):
     assert relerr(grads[1], br2.grad) < 1e-5
 
 
+@pytest.mark.parametrize("C,B,H,T", [(384, 64, 6, 256), (768, 4, 12, 1024), (126, 2, 6, 256), (384, 3, 6, 64)])
+@pytest.mark.parametrize("p", [0.2, 0.6])
+def test_layernorm_fwd_attn_dropmask_matches_separate_launches(C, B, H, T, p):
+    """cg_layernorm_fwd_attn_dropmask (ln1 forward + the attention keep bits in one launch,
+    GPT1.py:163,117) == cg_layernorm_fwd then cg_attn_dropmask, bit for bit: y, mean, rstd and every
+    mask word (p = 0.6 takes the thr > 2^15 Philox compare).  C = 126: the two-launch fallback."""
+    O = ops()
+    torch.manual_seed(5)
+    rows = B * T
+    x = (torch.randn(rows, C, device=DEV) * 2 + 0.5)
+    w = torch.randn(C, device=DEV) * 0.1 + 1
+    b = torch.randn(C, device=DEV) * 0.1
+    call = torch.tensor([3], dtype=torch.int64, device=DEV)
+    n = O.attn_mask_bytes(B, H, T) // 8
+    outs = []
+    for fused in (True, False):
+        y = torch.full((rows, C), float("nan"), device=DEV).to(torch.bfloat16)
+        mean, rstd = torch.full((rows,), float("nan"), device=DEV), torch.full((rows,), float("nan"), device=DEV)
+        mask = torch.full((n,), -1, dtype=torch.int64, device=DEV)
+        if fused:
+            O.layernorm_fwd_attn_dropmask(x, w, b, y, mean, rstd, 1e-5, B, H, T, p, 77, call, 2, mask)
+        else:
+            O.layernorm_fwd(x, w, b, y, mean, rstd, 1e-5)
+            O.attn_dropmask(B, H, T, p, 77, call, 2, mask)
+        torch.cuda.synchronize()
+        outs.append((y.view(torch.int16), mean, rstd, mask))
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)
+    assert not torch.isnan(outs[0][1]).any()
+
+
 @pytest.mark.parametrize("C", [384, 768, 126])
 @pytest.mark.parametrize("with_link", [False, True])
 def test_layernorm_bwd_rows_then_reduce_is_bitwise_ex(C, with_link):
