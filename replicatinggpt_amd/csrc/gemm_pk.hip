@@ -791,9 +791,15 @@ void launch_1(unsigned grid, int64_t M, int64_t N, int64_t K, const bf16_t* A, i
               void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, int64_t kchunk, float* ws,
               hipStream_t st) {
     using G = GeoP<BM, BN, NBUF, BK>;
+    // tile order (gemm_tile.h tile_rc): row-major -- consecutive items, which run on one XCD, share
+    // the A row panel and walk the B panels -- unless there are more B panels than A panels (the FFN2
+    // weight gradient dW2 = dz2^T h: 6 x 24 tiles at C4), where column-major makes them share the
+    // B panel (h, 403 MB at C4: read by one XCD instead of up to all eight) and walk the few A panels.
+    // cg_set_tuning("gemm_group_pk", g): g row panels per group (1 = row-major); 0 = this choice.
+    const int64_t tM = M / BM, tN = N / BN;
+    const int gm = g_gemm_group_pk > 0 ? g_gemm_group_pk : (tN > tM ? (int)tM : 0);
     k_gemm_pk<AT_, BT_, BM, BN, NBUF, EK, BK><<<grid, G::THREADS, G::LDS, st>>>(M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e,
-                                                                         split_k, kchunk, ws,
-                                                                         g_pk_flags | (g_gemm_group_pk << 8),
+                                                                         split_k, kchunk, ws, g_pk_flags | (gm << 8),
                                                                          take_pending_reduces(st));
 }
 

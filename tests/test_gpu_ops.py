@@ -398,6 +398,34 @@ def test_gemm_uneven_splitk_wgrad_shapes(M, N, K, split):
     assert relerr(out, ref) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K,split", [(384, 1536, 16384, 14), (768, 3072, 65536, 7), (256, 2048, 4096, 4),
+                                         (1536, 384, 16384, 14)])
+def test_gemm_tile_order_is_bitwise_invariant(M, N, K, split):
+    """The persistent kernel's automatic tile order (column-major where B panels outnumber A panels:
+    the FFN2 weight gradient dW2 = dz2^T h, GPT1.py:145 backward) against forced row-major
+    (cg_set_tuning gemm_group_pk = 1) and a 3-row grouping: the order only moves items between
+    blocks, so the output is equal bit for bit."""
+    from replicatinggpt_amd import _lib as L
+    lib = L.load()
+    torch.manual_seed(13)
+    A = (torch.randn(K, M, device=DEV) * 0.5).to(torch.bfloat16)
+    B = (torch.randn(K, N, device=DEV) * 0.5).to(torch.bfloat16)
+    ws = torch.empty(ops().gemm_workspace(M, N, split) // 4, dtype=torch.float32, device=DEV)
+    outs = []
+    try:
+        for g in (0, 1, 3):
+            L.check(lib.cg_set_tuning(b"gemm_group_pk", g))
+            out = torch.full((M, N), float("nan"), device=DEV)
+            ops().gemm(A, B, out, True, True, True, M, N, K, M, N, N, 0, None, None, 0, None, 0, 0.0, 0, None, 0,
+                       0.0, split, ws)
+            outs.append(out)
+    finally:
+        L.check(lib.cg_set_tuning(b"gemm_group_pk", 0))
+    torch.cuda.synchronize()
+    assert not torch.isnan(outs[0]).any()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
 @pytest.mark.parametrize("c_dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("beta", [0.0, 1.0])
 def test_gemm_splitk_reduce_vec_matches_scalar(c_dt, beta):
