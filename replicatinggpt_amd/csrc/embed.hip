@@ -180,6 +180,77 @@ __global__ __launch_bounds__(64 * EMB_WAVES) void k_embed_bwd_tok_partial(const 
     }
 }
 
+// Both gradients from one read of dx (the C2 step: B 64, T 256): block (column block, chunk) takes
+// the TS = 128 / B positions t0 .. t0 + TS - 1 of every sequence -- wave w the sequences
+// [w B / 4, (w + 1) B / 4), rows in (t, b) order -- into its LDS token histogram (as
+// k_embed_bwd_tok_partial, the chunk's partial in wave order) and, per position, a register sum
+// over its sequences; dwpe[t] = ((s0 + s1) + s2) + s3 over the waves.  Replaces the separate
+// position kernel's second 25 MB read of dx.  Deterministic (fixed orders), not the separate
+// kernels' bits.
+template <int TS>
+__global__ __launch_bounds__(256) void k_embed_bwd_fused(const int64_t* __restrict__ idx, const float* __restrict__ dx,
+                                                         float* __restrict__ part, float* __restrict__ dwpe,
+                                                         int64_t B, int64_t T, int64_t C, int64_t V, int accumulate) {
+    extern __shared__ __attribute__((aligned(16))) float acc[];  // [4][V][EMB_COLS], then pos [4][TS][EMB_COLS]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t c = (int64_t)blockIdx.x * EMB_COLS + lane;
+    const int64_t chunk = blockIdx.y, t0 = chunk * TS;
+    float* my = acc + (int64_t)wave * V * EMB_COLS;
+    float* pos = acc + 4 * V * EMB_COLS;
+    for (int64_t v = 0; v < V; ++v) my[v * EMB_COLS + lane] = 0.f;
+    const int64_t nb = B / 4, b0 = wave * nb;
+    if (c < C) {
+#pragma unroll
+        for (int ti = 0; ti < TS; ++ti) {
+            const int64_t t = t0 + ti;
+            float ps = 0.f;
+            int64_t b = b0;
+            for (; b + 8 <= b0 + nb; b += 8) {   // 8 rows of loads in flight; sums stay in b order
+                int64_t tk[8];
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int64_t r = (b + j) * T + t;
+                    const int64_t tt = idx[r];
+                    tk[j] = tt < 0 ? 0 : (tt >= V ? V - 1 : tt);
+                    v[j] = dx[r * C + c];
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    my[tk[j] * EMB_COLS + lane] += v[j];
+                    ps += v[j];
+                }
+            }
+            for (; b < b0 + nb; ++b) {
+                const int64_t r = b * T + t;
+                int64_t tok = idx[r];
+                tok = tok < 0 ? 0 : (tok >= V ? V - 1 : tok);
+                const float v = dx[r * C + c];
+                my[tok * EMB_COLS + lane] += v;
+                ps += v;
+            }
+            pos[(wave * TS + ti) * EMB_COLS + lane] = ps;
+        }
+    }
+    __syncthreads();
+    const int64_t n = V * EMB_COLS;
+    float* out = part + chunk * V * C;
+    for (int64_t i = threadIdx.x; i < n; i += 256) {
+        const int64_t v = i / EMB_COLS, cc = (int64_t)blockIdx.x * EMB_COLS + (i % EMB_COLS);
+        if (cc < C) out[v * C + cc] = ((acc[i] + acc[n + i]) + acc[2 * n + i]) + acc[3 * n + i];
+    }
+    for (int i = threadIdx.x; i < TS * EMB_COLS; i += 256) {
+        const int ti = i / EMB_COLS, l = i % EMB_COLS;
+        const int64_t cc = (int64_t)blockIdx.x * EMB_COLS + l;
+        if (cc < C) {
+            const float s = ((pos[ti * EMB_COLS + l] + pos[(TS + ti) * EMB_COLS + l]) + pos[(2 * TS + ti) * EMB_COLS + l]) +
+                            pos[(3 * TS + ti) * EMB_COLS + l];
+            float* o = dwpe + (t0 + ti) * C + cc;
+            *o = accumulate ? *o + s : s;
+        }
+    }
+}
+
 __global__ void k_embed_bwd_tok_reduce(const float* __restrict__ part, float* __restrict__ dwte, int64_t nchunk,
                                        int64_t VC, int accumulate) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -210,6 +281,27 @@ extern "C" int cg_embed_bwd(const int64_t* idx, const float* dx, float* dwte, fl
     const int waves = 4 * V * EMB_COLS * 4 <= 160 * 1024 ? 4 : (2 * V * EMB_COLS * 4 <= 160 * 1024 ? 2 : 1);
     hipStream_t st = (hipStream_t)stream;
     const int64_t rows = B * T;
+    // both gradients, one accumulate flag, a 4-wave histogram and B a divisor or multiple of 128
+    // (TS = 128 / B positions per chunk -- the same chunk count as the row chunks): the fused kernel
+    const int64_t ts = B >= 128 ? 1 : 128 / B;
+    const bool fused = dwte && dwpe && waves == 4 && B % 4 == 0 && (B >= 128 ? B % 128 == 0 : 128 % B == 0) &&
+                       T % ts == 0 && (ts == 1 || ts == 2 || ts == 4 || ts == 8) &&
+                       (4 * V + 4 * ts) * EMB_COLS * 4 <= 160 * 1024;
+    if (fused) {
+        const int64_t nchunk = T / ts;
+        dim3 grid(ceil_div(C, EMB_COLS), (unsigned)nchunk);
+        const size_t lds = (size_t)(4 * V + 4 * ts) * EMB_COLS * sizeof(float);
+#define EBF(TS_) k_embed_bwd_fused<TS_><<<grid, 256, lds, st>>>(idx, dx, (float*)workspace, dwpe, B, T, C, V, accumulate)
+        if (ts == 1) EBF(1);
+        else if (ts == 2) EBF(2);
+        else if (ts == 4) EBF(4);
+        else EBF(8);
+#undef EBF
+        k_embed_bwd_tok_reduce<<<ceil_div(V * C, 64), 64, 0, st>>>((const float*)workspace, dwte, nchunk, V * C,
+                                                                    accumulate);
+        CG_LAUNCH_CHECK("cg_embed_bwd");
+        return CG_OK;
+    }
     if (dwpe) {
         if ((T * C) % 4 == 0 && ((((uintptr_t)dx) | ((uintptr_t)dwpe)) & 15) == 0)
             k_embed_bwd_pos4<<<ceil_div(T * C / 4, 64), 64, 0, st>>>(dx, dwpe, B, T * C, accumulate);

@@ -733,11 +733,12 @@ def test_attention_bwd_regenerates_mask():
 
 
 @pytest.mark.parametrize("V,T,C,B", [(65, 40, 126, 3), (65, 256, 384, 64), (65, 100, 200, 5), (200, 64, 128, 4),
-                                     (600, 64, 96, 3)])
+                                     (600, 64, 96, 3), (65, 64, 384, 16), (65, 32, 192, 128), (65, 1024, 768, 64)])
 def test_embedding_fwd_bwd(V, T, C, B):
     """Token + position embeddings and their deterministic backward (the token gradient's 4-wave
     partial histograms, added in wave then chunk order) against fp64, ragged and C2-sized; larger
-    vocabularies take the 2- and 1-wave histogram blocks (V 200, 600)."""
+    vocabularies take the 2- and 1-wave histogram blocks (V 200, 600).  B = 64 / 16 / 128 take the
+    fused pass (both gradients from one read of dx, 2 / 8 / 1 positions per chunk)."""
     Fn = F()
     torch.manual_seed(6)
     wte = torch.randn(V, C)
