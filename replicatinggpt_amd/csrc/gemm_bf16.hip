@@ -195,8 +195,12 @@ static bool fast_shape_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t 
            ldc % 8 == 0;
 }
 
-// the 128x128 persistent kernel (gemm_pk.hip)
+// the 128x128 persistent kernel (gemm_pk.hip); the A/B build also its 3- and 4-stage rings
+#ifdef CG_AB_VARIANTS
+static bool pk128(int v) { return v == 9 || v == 10 || v == 12; }
+#else
 static bool pk128(int v) { return v == 9; }
+#endif
 
 // column partials come from the 128x128 persistent kernel's per-item ReLU-backward epilogue (not its
 // pk_flags bit-1 per-fragment form) and from the 8-wave 256x256 persistent kernel
