@@ -49,7 +49,12 @@ enum {
     CG_EPI_BIAS_RELU = 2,    /* out = relu(acc + bias[n])               (GPT1.py:143-144)       */
     CG_EPI_BIAS_RESID = 3,   /* out = resid[m,n] + acc + bias[n]  (resid NULL: no add; :136,163) */
     CG_EPI_BIAS_DROP_RESID = 4, /* out = resid + dropout(acc + bias)    (GPT1.py:145-146,164)   */
-    CG_EPI_RELU_BWD = 5      /* out = acc * (aux[m,n] > 0)              (ReLU backward, :144)   */
+    CG_EPI_RELU_BWD = 5,     /* out = acc * (aux[m,n] > 0)              (ReLU backward, :144)   */
+    /* 6 unused.  out = acc (bf16), and the attention backward's delta = rowsum(dO * O) per head from
+       the written values: colpart[((m / T) * (N / 64) + n / 64) * T + m % T] = sum over the head's 64
+       columns of bf16(acc) * aux[m, n]  (aux = the attention output O, bf16, stride ld_aux;
+       T = ld_resid, M % T == 0).  Only where cg_gemm_rowdot_supported() says so.               */
+    CG_EPI_STORE_ROWDOT = 7
 };
 
 typedef struct {
@@ -156,6 +161,10 @@ int cg_gemm_colpart_supported(int a_trans, int b_trans, int64_t M, int64_t N, in
    FeedForward uses them when both its W1 forward and its W2 dgrad products say yes.           */
 int cg_gemm_relu_bits_supported(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                                 int64_t ldc);
+/* 1 if cg_gemm can run CG_EPI_STORE_ROWDOT (bf16 output, split 1, beta 0, N % 64 == 0) for this
+   problem under the current dispatch, else 0 -- the attention backward then computes delta itself. */
+int cg_gemm_rowdot_supported(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
+                             int64_t ldc);
 /* cg_set_tuning("defer_splitk", 1): a split-K cg_gemm with an fp32 CG_EPI_STORE output (the weight
    gradients) leaves its slab reduce pending -- its workspace must stay allocated -- and the next
    persistent bf16 GEMM launch on the stream performs it in its tail (same summation order, same
@@ -209,6 +218,14 @@ int cg_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const voi
                 const float* lse, void* dq, void* dk, void* dv, int64_t ld_dqkv, float scale, double dropout_p,
                 uint64_t seed, const uint64_t* rng_call, int site, const uint64_t* mask, void* workspace,
                 void* stream);
+/* cg_attn_bwd with delta = rowsum(dO * O) already computed (fp32 [B][H][T], e.g. by the dO GEMM's
+   CG_EPI_STORE_ROWDOT epilogue); the sequence-resident kernels (T <= 256) read it instead of
+   loading O, other paths recompute it in the workspace.  NULL delta: exactly cg_attn_bwd.         */
+int cg_attn_bwd_delta(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const void* q, const void* k,
+                      const void* v, int64_t ld_qkv, const void* o, int64_t ld_o, const void* dout, int64_t ld_do,
+                      const float* lse, const float* delta, void* dq, void* dk, void* dv, int64_t ld_dqkv,
+                      float scale, double dropout_p, uint64_t seed, const uint64_t* rng_call, int site,
+                      const uint64_t* mask, void* workspace, void* stream);
 
 /* ---- cross entropy over the char vocabulary (F.cross_entropy, GPT1.py:189-192) ----------
    logits fp32 [rows, V] (row stride ld); loss_rows[r] = lse_r - logit[r, tgt_r]; lse saved.

@@ -15,6 +15,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "charpt.h")
 
 CG_F32, CG_BF16, CG_BITS = 0, 1, 2
 EPI_STORE, EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_RESID, EPI_BIAS_DROP_RESID, EPI_RELU_BWD = range(6)
+EPI_STORE_ROWDOT = 7
 
 c_i64, c_int, c_dbl, c_flt, c_u64, P = ctypes.c_int64, ctypes.c_int, ctypes.c_double, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p
 
@@ -51,6 +52,7 @@ _SIGS = {
     "cg_gemm_workspace": (c_i64, [c_i64, c_i64, c_int]),
     "cg_gemm_colpart_supported": (c_int, [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64]),
     "cg_gemm_relu_bits_supported": (c_int, [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64]),
+    "cg_gemm_rowdot_supported": (c_int, [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64]),
     "cg_flush_deferred": (c_int, [P]),
     "cg_reduce_rows": (c_int, [P, c_i64, c_i64, P, c_int, P]),
     "cg_gemm": (c_int, [c_int, c_int, c_int, c_i64, c_i64, c_i64, P, c_i64, P, c_i64, P, c_int, c_i64,
@@ -68,6 +70,8 @@ _SIGS = {
     "cg_attn_bwd_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
     "cg_attn_bwd": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, P, P, P, c_i64, P, c_i64, P, c_i64, P, P, P, P, c_i64,
                             c_flt, c_dbl, c_u64, P, c_int, P, P, P]),
+    "cg_attn_bwd_delta": (c_int, [c_int, c_i64, c_i64, c_i64, c_i64, P, P, P, c_i64, P, c_i64, P, c_i64, P, P, P, P,
+                                  P, c_i64, c_flt, c_dbl, c_u64, P, c_int, P, P, P]),
     "cg_ce_fwd": (c_int, [P, c_i64, c_i64, c_i64, P, P, P, P]),
     "cg_ce_bwd": (c_int, [P, c_i64, c_i64, c_i64, P, P, P, c_flt, P, c_i64, P, P]),
     "cg_head_workspace": (c_i64, [c_i64, c_i64]),

@@ -53,10 +53,12 @@ void launch_fwd_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* 
 void launch_dq_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                    const bf16_t* o, int64_t ldo, const bf16_t* dout, int64_t ldd, const float* lse, float* delta,
                    bf16_t* dq, int64_t lddq, float scale, const DropArgs& d, hipStream_t st);
-// dQ then dK/dV (T <= 256: one merged launch)
+// dQ then dK/dV (T <= 256: one merged launch, bwd_merged(T)); delta_ready (merged launch only):
+// `delta` already holds rowsum(dO * O) and is read, not computed
+bool bwd_merged(int64_t T);
 void launch_bwd_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                     const bf16_t* o, int64_t ldo, const bf16_t* dout, int64_t ldd, const float* lse, float* delta,
-                    bf16_t* dq, int64_t lddq, bf16_t* dk, bf16_t* dv, int64_t lddkv, float scale, const DropArgs& d,
+                    bool delta_ready, bf16_t* dq, int64_t lddq, bf16_t* dk, bf16_t* dv, int64_t lddkv, float scale, const DropArgs& d,
                     hipStream_t st);
 void launch_dkdv_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                      const bf16_t* dout, int64_t ldd, const float* lse, const float* delta, bf16_t* dk, bf16_t* dv,

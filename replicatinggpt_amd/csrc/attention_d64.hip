@@ -1121,7 +1121,7 @@ __device__ __forceinline__ void res_tile_wait(int t) {
 // by hidden register loads first, then the K/V tiles by LDS-DMA in tile order; tile t waits only
 // for tiles 0..t (as k_attn_fwd_d64r).  Per-group setup (delta in dq_group_setup's summation order)
 // and per-tile arithmetic as the ring kernel.
-template <bool DROP, int NT>
+template <bool DROP, int NT, bool DIN = false>
 __device__ __forceinline__ void dq_res(int bh, char* smem, int H, const bf16_t* __restrict__ q,
                                        const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, int64_t ld,
                                        const bf16_t* __restrict__ o, int64_t ldo, const bf16_t* __restrict__ dout,
@@ -1137,7 +1137,7 @@ __device__ __forceinline__ void dq_res(int bh, char* smem, int H, const bf16_t* 
     const int qg[2] = {32 * (7 - wave), 32 * wave};
     const bool act[2] = {qg[0] < T, qg[1] < T};
     sv8 qf[2][4], df[2][4], of[2][4];
-    uint32_t lsew[2], mw[2][NT];
+    uint32_t lsew[2], delw[2] = {0u, 0u}, mw[2][NT];
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
         const int64_t qa = (act[g] ? qg[g] : 0) + (lane & 31);   // inactive groups: a valid row, unused
@@ -1146,9 +1146,10 @@ __device__ __forceinline__ void dq_res(int bh, char* smem, int H, const bf16_t* 
             const int col = hh * 64 + 16 * ks + 8 * (lane >> 5);
             gload16(qf[g][ks], q + (boff + qa) * ld + col);
             gload16(df[g][ks], dout + (boff + qa) * ldd + col);
-            gload16(of[g][ks], o + (boff + qa) * ldo + col);
+            if constexpr (!DIN) gload16(of[g][ks], o + (boff + qa) * ldo + col);
         }
         gload4(lsew[g], lse + (int64_t)bh * T + qa);
+        if constexpr (DIN) gload4(delw[g], delta + (int64_t)bh * T + qa);
         if constexpr (DROP) {
             const int qb = act[g] ? qg[g] >> 5 : 0;
 #pragma unroll
@@ -1177,9 +1178,9 @@ __device__ __forceinline__ void dq_res(int bh, char* smem, int H, const bf16_t* 
         for (int ks = 0; ks < 4; ++ks) {
             asm volatile("" : "+v"(qf[g][ks]));
             asm volatile("" : "+v"(df[g][ks]));
-            asm volatile("" : "+v"(of[g][ks]));
+            if constexpr (!DIN) asm volatile("" : "+v"(of[g][ks]));
         }
-        asm volatile("" : "+v"(lsew[g]));
+        asm volatile("" : "+v"(lsew[g]), "+v"(delw[g]));
 #pragma unroll
         for (int t = 0; t < NT; ++t) asm volatile("" : "+v"(mw[g][t]));
     }
@@ -1187,15 +1188,19 @@ __device__ __forceinline__ void dq_res(int bh, char* smem, int H, const bf16_t* 
 #pragma unroll
     for (int g = 0; g < 2; ++g) {   // dq_group_setup's arithmetic on the loaded fragments
         float dsum = 0.f;
+        if constexpr (DIN) {
+            dsum = act[g] ? __uint_as_float(delw[g]) : 0.f;
+        } else {
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
+            for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) dsum += bf2f((bf16_t)of[g][ks][j]) * bf2f((bf16_t)df[g][ks][j]);
-        if (!act[g]) dsum = 0.f;
-        dsum += __shfl_xor(dsum, 32, 64);
+                for (int j = 0; j < 8; ++j) dsum += bf2f((bf16_t)of[g][ks][j]) * bf2f((bf16_t)df[g][ks][j]);
+            if (!act[g]) dsum = 0.f;
+            dsum += __shfl_xor(dsum, 32, 64);
+        }
         dl[g] = -dsum / dscale;
         lse2[g] = act[g] ? __uint_as_float(lsew[g]) * LOG2E : 0.f;
-        if (act[g] && lane < 32) delta[(int64_t)bh * T + qg[g] + (lane & 31)] = dsum;
+        if (!DIN && act[g] && lane < 32) delta[(int64_t)bh * T + qg[g] + (lane & 31)] = dsum;
     }
     fv16 dqa[2][2];
 #pragma unroll
@@ -1406,11 +1411,12 @@ __global__ __launch_bounds__(256, 2) void k_attn_dkdv_d64r(int H, const bf16_t* 
 }
 
 // The whole T <= 256 backward in one launch: workgroup 2i computes dQ of (b, h) = i, 2i + 1 its
-// dK/dV (with delta from O and dO itself, so the two do not depend on each other).  768
+// dK/dV (with delta from O and dO itself, so the two do not depend on each other; DIN: both read
+// delta, precomputed by the dO GEMM's epilogue, and neither loads O).  768
 // workgroups fill the 512 slots and the second wave of them starts as slots free up, where the
 // two separate 384-workgroup launches each ran 3/4 full and back to back.  The pair of one (b, h)
 // stays on one XCD (block_coords: consecutive logical ids), sharing its K/V/Q/dO lines in L2.
-template <bool DROP, int NT>
+template <bool DROP, int NT, bool DIN>
 __global__ __launch_bounds__(256, 2) void k_attn_bwd_d64r(int H, const bf16_t* __restrict__ q,
                                                           const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
                                                           int64_t ld, const bf16_t* __restrict__ o, int64_t ldo,
@@ -1425,11 +1431,11 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_d64r(int H, const bf16_t* _
     int x, id;
     block_coords<false>(x, id);
     if (id & 1)
-        dkdv_res<DROP, NT, true>(id >> 1, smem, H, q, k, v, ld, dout, ldd, lse, delta, o, ldo, dk, dv, lddkv, scale, mask_bwd,
-                           dscale);
+        dkdv_res<DROP, NT, !DIN>(id >> 1, smem, H, q, k, v, ld, dout, ldd, lse, delta, o, ldo, dk, dv, lddkv, scale,
+                                 mask_bwd, dscale);
     else
-        dq_res<DROP, NT>(id >> 1, smem, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale, mask_fwd,
-                         dscale);
+        dq_res<DROP, NT, DIN>(id >> 1, smem, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale, mask_fwd,
+                              dscale);
     ATTN_STAMP(2, attn_now());
     ATTN_STAMP(3, attn_where(id & 1));
 }
@@ -1769,18 +1775,27 @@ void launch_dq_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k
     DQ(4);
 #undef DQ
 }
+bool bwd_merged(int64_t T) { return resident(T) && g_attn_variant != 2; }   // 2: the two resident kernels (A/B)
+
 void launch_bwd_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* k, const bf16_t* v, int64_t ld,
                     const bf16_t* o, int64_t ldo, const bf16_t* dout, int64_t ldd, const float* lse, float* delta,
-                    bf16_t* dq, int64_t lddq, bf16_t* dk, bf16_t* dv, int64_t lddkv, float scale, const DropArgs& d,
-                    hipStream_t st) {
-    if (resident(T) && g_attn_variant != 2) {   // 2: the two resident kernels back to back (A/B)
+                    bool delta_ready, bf16_t* dq, int64_t lddq, bf16_t* dk, bf16_t* dv, int64_t lddkv, float scale,
+                    const DropArgs& d, hipStream_t st) {
+    if (bwd_merged(T)) {
         const dim3 grid(1, (unsigned)(2 * B * H));
-        RES_SWITCH(T, if (d.mask) k_attn_bwd_d64r<true, NT_><<<grid, 256, 0, st>>>(
-                              H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, dk, dv, lddkv, scale, d.mask,
-                              d.mask_bwd, d.dscale);
-                   else k_attn_bwd_d64r<false, NT_><<<grid, 256, 0, st>>>(
-                              H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, dk, dv, lddkv, scale, nullptr,
-                              nullptr, 1.f));
+#define BWDR(DIN_)                                                                                                 \
+    RES_SWITCH(T, if (d.mask) k_attn_bwd_d64r<true, NT_, DIN_><<<grid, 256, 0, st>>>(                            \
+                          H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, dk, dv, lddkv, scale, d.mask,    \
+                          d.mask_bwd, d.dscale);                                                                    \
+               else k_attn_bwd_d64r<false, NT_, DIN_><<<grid, 256, 0, st>>>(                                     \
+                          H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, dk, dv, lddkv, scale, nullptr,   \
+                          nullptr, 1.f))
+        if (delta_ready) {
+            BWDR(true);
+        } else {
+            BWDR(false);
+        }
+#undef BWDR
         return;
     }
     launch_dq_d64(B, T, H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, scale, d, st);

@@ -756,11 +756,13 @@ extern "C" int64_t cg_attn_bwd_workspace(int64_t B, int64_t T, int64_t H, int64_
     return delta + mask_bytes(B, H, T);
 }
 
-extern "C" int cg_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const void* q, const void* k,
-                           const void* v, int64_t ld_qkv, const void* o, int64_t ld_o, const void* dout, int64_t ld_do,
-                           const float* lse, void* dq, void* dk, void* dv, int64_t ld_dqkv, float scale,
-                           double dropout_p, uint64_t seed, const uint64_t* rng_call, int site, const uint64_t* mask,
-                           void* workspace, void* stream) {
+namespace {
+// delta_in: rowsum(dO * O) precomputed (cg_attn_bwd_delta), read only by the merged resident kernel
+int attn_bwd_impl(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const void* q, const void* k,
+                  const void* v, int64_t ld_qkv, const void* o, int64_t ld_o, const void* dout, int64_t ld_do,
+                  const float* lse, const float* delta_in, void* dq, void* dk, void* dv, int64_t ld_dqkv, float scale,
+                  double dropout_p, uint64_t seed, const uint64_t* rng_call, int site, const uint64_t* mask,
+                  void* workspace, void* stream) {
     CG_REQUIRE(B > 0 && T > 0 && H > 0 && D > 0 && D <= 128, "cg_attn_bwd: bad shape (D must be <= 128)");
     CG_REQUIRE(workspace, "cg_attn_bwd: workspace required");
     hipStream_t st = (hipStream_t)stream;
@@ -787,8 +789,10 @@ extern "C" int cg_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D
             set_masks(d, mask, B, H, T);
         }
         const bf16_t *Q = (const bf16_t*)q, *K = (const bf16_t*)k, *V = (const bf16_t*)v, *DO = (const bf16_t*)dout;
-        attn::launch_bwd_d64(B, T, (int)H, Q, K, V, ld_qkv, (const bf16_t*)o, ld_o, DO, ld_do, lse, delta,
-                             (bf16_t*)dq, ld_dqkv, (bf16_t*)dk, (bf16_t*)dv, ld_dqkv, scale, d, st);
+        const bool din = delta_in && attn::bwd_merged(T);
+        attn::launch_bwd_d64(B, T, (int)H, Q, K, V, ld_qkv, (const bf16_t*)o, ld_o, DO, ld_do, lse,
+                             din ? (float*)delta_in : delta, din, (bf16_t*)dq, ld_dqkv, (bf16_t*)dk, (bf16_t*)dv,
+                             ld_dqkv, scale, d, st);
     } else {
         dim3 grid(ceil_div(T, GB), (unsigned)(B * H));
         const size_t lds_dq = generic_lds<float>((int)D, 4, 1);
@@ -813,4 +817,25 @@ extern "C" int cg_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D
     }
     CG_LAUNCH_CHECK("cg_attn_bwd");
     return CG_OK;
+}
+}  // namespace
+
+extern "C" int cg_attn_bwd(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const void* q, const void* k,
+                           const void* v, int64_t ld_qkv, const void* o, int64_t ld_o, const void* dout, int64_t ld_do,
+                           const float* lse, void* dq, void* dk, void* dv, int64_t ld_dqkv, float scale,
+                           double dropout_p, uint64_t seed, const uint64_t* rng_call, int site, const uint64_t* mask,
+                           void* workspace, void* stream) {
+    return attn_bwd_impl(dtype, B, T, H, D, q, k, v, ld_qkv, o, ld_o, dout, ld_do, lse, nullptr, dq, dk, dv, ld_dqkv,
+                         scale, dropout_p, seed, rng_call, site, mask, workspace, stream);
+}
+
+extern "C" int cg_attn_bwd_delta(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const void* q, const void* k,
+                                 const void* v, int64_t ld_qkv, const void* o, int64_t ld_o, const void* dout,
+                                 int64_t ld_do, const float* lse, const float* delta, void* dq, void* dk, void* dv,
+                                 int64_t ld_dqkv, float scale, double dropout_p, uint64_t seed,
+                                 const uint64_t* rng_call, int site, const uint64_t* mask, void* workspace,
+                                 void* stream) {
+    CG_REQUIRE(!delta || (((uintptr_t)delta) & 3) == 0, "cg_attn_bwd_delta: delta must be 4-byte aligned");
+    return attn_bwd_impl(dtype, B, T, H, D, q, k, v, ld_qkv, o, ld_o, dout, ld_do, lse, delta, dq, dk, dv, ld_dqkv,
+                         scale, dropout_p, seed, rng_call, site, mask, workspace, stream);
 }

@@ -514,6 +514,11 @@ extern "C" int cg_gemm_relu_bits_supported(int a_trans, int b_trans, int64_t M, 
     return gemm_relu_bits_supported(a_trans, b_trans, M, N, K, lda, ldb, ldc) ? 1 : 0;
 }
 
+extern "C" int cg_gemm_rowdot_supported(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, int64_t lda,
+                                        int64_t ldb, int64_t ldc) {
+    return gemm_rowdot_supported(a_trans, b_trans, M, N, K, lda, ldb, ldc) ? 1 : 0;
+}
+
 extern "C" int64_t cg_gemm_workspace(int64_t M, int64_t N, int split_k) {
     return split_k > 1 ? (int64_t)split_k * M * N * (int64_t)sizeof(float) : 0;
 }
@@ -537,6 +542,10 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
         fast = true;
     } else if (e.aux_dtype == CG_BITS) {
         set_error("cg_gemm: CG_BITS ReLU keep bits need a persistent bf16 kernel (cg_gemm_relu_bits_supported)");
+        return CG_EINVAL;
+    } else if (e.kind == CG_EPI_STORE_ROWDOT) {
+        set_error("cg_gemm: CG_EPI_STORE_ROWDOT needs the 128x128 persistent bf16 kernel (cg_gemm_rowdot_supported; "
+                  "bf16 aux, colpart, ld_resid = T dividing M)");
         return CG_EINVAL;
     } else if (e.colpart) {
         set_error("cg_gemm: colpart needs a persistent bf16 kernel (bf16 operands and output, NT/NN, beta 0, "

@@ -222,6 +222,16 @@ bool gemm_relu_bits_supported(int at, int bt, int64_t M, int64_t N, int64_t K, i
     return fast_shape_ok(M, N, K, lda, ldb, ldc, 1) && relu_bits_ok(pick_variant(at, bt, M, N, 1), at, 1, N);
 }
 
+// the attention-delta epilogue (CG_EPI_STORE_ROWDOT) is the 128x128 persistent kernel's fixed kind:
+// one wave's 64 output columns are one head
+static bool rowdot_ok(int v, int at, int split_k, int64_t N) {
+    return pk128(v) && !(g_pk_flags & 2) && split_k == 1 && !at && N % 64 == 0;
+}
+
+bool gemm_rowdot_supported(int at, int bt, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc) {
+    return fast_shape_ok(M, N, K, lda, ldb, ldc, 1) && rowdot_ok(pick_variant(at, bt, M, N, 1), at, 1, N);
+}
+
 bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
                       int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, float* ws,
                       hipStream_t st) {
@@ -237,7 +247,11 @@ bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf1
         const int64_t nkt = K / FBK, nkc = (nkt + split_k - 1) / split_k;
         if (!pk128(v) || (split_k - 1) * nkc >= nkt) return false;
     }
-    if (e.colpart && (!colpart_ok(v, at, split_k) || e.kind != CG_EPI_RELU_BWD ||
+    if (e.kind == CG_EPI_STORE_ROWDOT &&
+        (!rowdot_ok(v, at, split_k, N) || !e.aux || e.aux_dtype != CG_BF16 || !e.colpart || e.ld_resid <= 0 ||
+         M % e.ld_resid || e.beta != 0.f || c_dtype != CG_BF16 || (((uintptr_t)e.colpart) & 3)))
+        return false;
+    if (e.colpart && e.kind != CG_EPI_STORE_ROWDOT && (!colpart_ok(v, at, split_k) || e.kind != CG_EPI_RELU_BWD ||
                       (e.aux_dtype != CG_BF16 && e.aux_dtype != CG_BITS) || e.beta != 0.f || c_dtype != CG_BF16))
         return false;
     if (e.aux_dtype == CG_BITS &&

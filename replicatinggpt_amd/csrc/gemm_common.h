@@ -18,7 +18,7 @@ struct EpiArgs {
     const uint64_t* rng_call;
     int site;
     float beta;
-    float* colpart;  // RELU_BWD: per-64-row-block column sums (k_gemm_pk only)
+    float* colpart;  // RELU_BWD: per-64-row-block column sums; STORE_ROWDOT: per-head row dots (k_gemm_pk only)
 };
 
 __device__ __forceinline__ float aux_at(const EpiArgs& e, int64_t m, int64_t n) {
@@ -120,6 +120,7 @@ bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf1
 // whether cg_gemm (bf16, split 1, CG_EPI_RELU_BWD with bf16 aux, beta 0) can write column partials
 bool gemm_colpart_supported(int at, int bt, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
 // whether cg_gemm can write / read CG_BITS ReLU keep bits for this problem (bf16, split 1, beta 0)
+bool gemm_rowdot_supported(int at, int bt, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
 bool gemm_relu_bits_supported(int at, int bt, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
 // LDS-DMA (global_load_lds) kernels, variant >= 5 (gemm_glds.hip); false if the variant/shape does not apply
 bool glds_gemm_launch(int variant, int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda,

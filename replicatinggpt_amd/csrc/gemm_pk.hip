@@ -183,6 +183,45 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
                                                                               : -1;
     if constexpr (OUT >= 0) c_dtype = OUT;
     constexpr bool WIDE = EK == CG_EPI_STORE || EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_RELU_BWD;
+    if constexpr (EK == CG_EPI_STORE_ROWDOT) {
+        // bf16(acc) stored, and per row the dot of those rounded values with O's row over this wave's
+        // 64 columns (one head): lane l holds columns 16j + 4(l >> 4) + q of rows 16i + (l & 15), so
+        // 16 products per lane, then the 4 lane quarters (xor 16, 32); quarter 0 writes 4 rows' delta.
+        // These 4 stores precede the item's 8 output stores (EPI_OPS = 12).
+        const int lane = threadIdx.x & 63;
+        uint2 o[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[i][j] = *(const uint2*)((const bf16_t*)epi.aux + (mr + 16 * i) * epi.ld_aux + nc + 16 * j);
+        float dsum[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float s = 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const fv4& v = acc[i][j];
+                s += rbf(v[0]) * __uint_as_float(o[i][j].x << 16);
+                s += rbf(v[1]) * __uint_as_float(o[i][j].x & 0xffff0000u);
+                s += rbf(v[2]) * __uint_as_float(o[i][j].y << 16);
+                s += rbf(v[3]) * __uint_as_float(o[i][j].y & 0xffff0000u);
+            }
+            s += __shfl_xor(s, 16, 64);
+            s += __shfl_xor(s, 32, 64);
+            dsum[i] = s;
+        }
+        const int64_t T = epi.ld_resid, H = N >> 6, h = (nc - 4 * (lane >> 4)) >> 6;
+        if (lane < 16) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int64_t m = mr + 16 * i, b = m / T;
+                epi.colpart[(b * H + h) * T + (m - b * T)] = dsum[i];
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        store_item<true>(acc, mr, nc, Cv, CG_BF16, ldc);
+        return;
+    }
     if (EK < 0 && epi.beta != 0.f) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -601,10 +640,12 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     // issue order).
     // (8 for the fixed kinds whose bf16 output goes out as 16-B row segments -- store_item: with an
     // fp32 output they issue 16, more than counted, which only makes the wait conservative)
-    // (4 NJ = 12 for the 48-column wave tiles, whose residual kinds store each fragment on its own)
+    // (4 NJ = 12 for the 48-column wave tiles, whose residual kinds store each fragment on its own;
+    // 4 + 8 for STORE_ROWDOT: its delta stores, then the 16-B row segments)
     constexpr int EPI_OPS =
         NJ != 4 ? 4 * NJ
-                : (EK == CG_EPI_STORE || EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_RELU_BWD) ? 8 : 16;
+        : EK == CG_EPI_STORE_ROWDOT ? 12
+        : (EK == CG_EPI_STORE || EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_RELU_BWD) ? 8 : 16;
     int cur = 0, cj = 0, ckt = 0;
     int cnk;   // K-tiles of the compute cursor's item
     {
@@ -837,6 +878,9 @@ void launch_ek(unsigned grid, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
                 case CG_EPI_RELU_BWD:
                     if (b16) { L1(CG_EPI_RELU_BWD); return; }
                     break;
+                case CG_EPI_STORE_ROWDOT:   // fast_gemm_launch admits it only here (rowdot_ok)
+                    L1(CG_EPI_STORE_ROWDOT);
+                    return;
                 default: break;
             }
         }

@@ -492,14 +492,35 @@ def premask_ok(act, T, D):
     return act == torch.bfloat16 and D == 64 and T % 64 == 0
 
 
-def attention_bwd(qkv, B, T, H, D, o, do, lse, scale, p, seed, rng_call, site, mask=None):
+# CHARPT_ROWDOT=0: the attention backward computes delta = rowsum(dO * O) itself (A/B of the proj
+# dgrad's CG_EPI_STORE_ROWDOT epilogue)
+ROWDOT = os.environ.get("CHARPT_ROWDOT", "1") != "0"
+
+
+def rowdot_ok(dy2, w, o, T, D):
+    """Whether the attention-output gradient dO = dy2 @ w can come out of cg_gemm together with the
+    attention backward's delta (CG_EPI_STORE_ROWDOT) -- only where the sequence-resident attention
+    backward (T <= 256, head_size 64) reads it; asked from the library (cg_gemm_rowdot_supported)."""
+    if not (ROWDOT and D == 64 and T <= 256 and T % 64 == 0 and _is_bf16(dy2.dtype) and _is_bf16(o.dtype)
+            and dy2.is_cuda):
+        return False
+    if dy2.stride(1) != 1 or w.stride(1) != 1 or o.stride(1) != 1 or o.stride(0) % 8:
+        return False
+    if any(t.data_ptr() % 16 for t in (dy2, w, o)):
+        return False
+    M, K = dy2.shape
+    N = w.shape[1]
+    return M % T == 0 and ops.gemm_rowdot_supported(M, N, K, dy2.stride(0), w.stride(0), N)
+
+
+def attention_bwd(qkv, B, T, H, D, o, do, lse, scale, p, seed, rng_call, site, mask=None, delta=None):
     d = H * D
     dqkv = torch.empty_like(qkv)
     ws = torch.empty(ops.attn_bwd_workspace(B, T, H, D) // 4 + 1, dtype=torch.float32, device=qkv.device)
     if "skip_attn" in WHATIF:
         return dqkv
     ops.attn_bwd(qkv, B, T, H, D, 0, d, 2 * d, qkv.stride(0), o, o.stride(0), do, do.stride(0), lse, dqkv,
-                 dqkv.stride(0), float(scale), float(p), int(seed), rng_call, int(site), mask, ws)
+                 dqkv.stride(0), float(scale), float(p), int(seed), rng_call, int(site), mask, ws, delta)
     return dqkv
 
 
@@ -617,9 +638,18 @@ class AttnSublayerFn(torch.autograd.Function):
             if g_pb is not None and not bias_done:
                 colsum_into(dy, g_pb, beta_pb)
         do = torch.empty((B * T, C), dtype=act, device=x2.device)
-        linear_dgrad(dy, proj_w.operand(act), do)
+        wp = proj_w.operand(act)
+        delta = None
+        if rowdot_ok(dy, wp, o, T, lc.head_size):
+            # dO and the attention backward's delta = rowsum(dO * O) from one epilogue (the attention
+            # kernel then loads neither O nor computes the row dots)
+            delta = torch.empty((B, lc.n_head, T), dtype=torch.float32, device=dev)
+            ops.gemm_store_rowdot(dy, wp, do, B * T, C, C, dy.stride(0), wp.stride(0), do.stride(0), o, o.stride(0),
+                                  T, delta)
+        else:
+            linear_dgrad(dy, wp, do)
         dqkv = attention_bwd(qkv, B, T, lc.n_head, lc.head_size, o, do, lse, lc.scale, lc.p, lc.seed, lc.rng_call,
-                             lc.site, ctx.mask)
+                             lc.site, ctx.mask, delta)
         g, beta, f_qkv = qkv_w.grad_target()
         if g is not None:
             with SIDE.run(dev, dqkv, a):

@@ -190,6 +190,22 @@ def gemm_relu_bwd_colpart(a: Tensor, b: Tensor, out: Tensor, M: int, N: int, K: 
                              L.dtype_code(out.dtype), ldc, e, 1, None, _s(out)), "gemm_relu_bwd_colpart")
 
 
+@_op("gemm_store_rowdot", ("out", "delta"))
+def gemm_store_rowdot(a: Tensor, b: Tensor, out: Tensor, M: int, N: int, K: int, lda: int, ldb: int, ldc: int,
+                      o: Tensor, ld_o: int, T: int, delta: Tensor) -> None:
+    """out = bf16(a[M,K] @ b[N,K]^T) (the attention-output gradient dO) and the attention backward's
+    delta[b, h, t] = sum_e out[b*T + t, 64h + e] * o[b*T + t, 64h + e] (fp32 [M/T, N/64, T]) from
+    the rounded values.  Fails (CG_EINVAL) unless cg_gemm_rowdot_supported."""
+    e = L.Epilogue(L.EPI_STORE_ROWDOT, None, None, T, L.ptr(o), L.dtype_code(o.dtype), ld_o, 0.0, 0, None, 0, 0.0,
+                   L.ptr(delta))
+    L.check(L.load().cg_gemm(L.CG_BF16, 0, 1, M, N, K, L.ptr(a), lda, L.ptr(b), ldb, L.ptr(out),
+                             L.dtype_code(out.dtype), ldc, e, 1, None, _s(out)), "gemm_store_rowdot")
+
+
+def gemm_rowdot_supported(M, N, K, lda, ldb, ldc):
+    return bool(L.load().cg_gemm_rowdot_supported(0, 1, M, N, K, lda, ldb, ldc))
+
+
 @_op("reduce_rows", ("out",))
 def reduce_rows(part: Tensor, rows: int, N: int, out: Tensor, accumulate: bool) -> None:
     L.check(L.load().cg_reduce_rows(L.ptr(part), rows, N, L.ptr(out), int(accumulate), _s(out)), "reduce_rows")
@@ -239,13 +255,15 @@ def attn_mask_bytes(B, H, T):
 def attn_bwd(qkv: Tensor, B: int, T: int, H: int, D: int, q_off: int, k_off: int, v_off: int, ld: int, o: Tensor,
              ld_o: int, dout: Tensor, ld_do: int, lse: Tensor, dqkv: Tensor, ld_d: int, scale: float,
              dropout_p: float, seed: int, rng_call: Optional[Tensor], site: int, mask: Optional[Tensor],
-             ws: Tensor) -> None:
+             ws: Tensor, delta: Optional[Tensor] = None) -> None:
+    """delta: rowsum(dO * O) precomputed (gemm_store_rowdot), fp32 [B, H, T]; None: computed here."""
     es = qkv.element_size()
     base, dbase = qkv.data_ptr(), dqkv.data_ptr()
-    L.check(L.load().cg_attn_bwd(L.dtype_code(qkv.dtype), B, T, H, D, base + q_off * es, base + k_off * es,
-                                 base + v_off * es, ld, L.ptr(o), ld_o, L.ptr(dout), ld_do, L.ptr(lse),
-                                 dbase + q_off * es, dbase + k_off * es, dbase + v_off * es, ld_d, scale, dropout_p,
-                                 seed, L.ptr(rng_call), site, L.ptr(mask), L.ptr(ws), _s(qkv)), "attn_bwd")
+    L.check(L.load().cg_attn_bwd_delta(L.dtype_code(qkv.dtype), B, T, H, D, base + q_off * es, base + k_off * es,
+                                       base + v_off * es, ld, L.ptr(o), ld_o, L.ptr(dout), ld_do, L.ptr(lse),
+                                       L.ptr(delta), dbase + q_off * es, dbase + k_off * es, dbase + v_off * es, ld_d,
+                                       scale, dropout_p, seed, L.ptr(rng_call), site, L.ptr(mask), L.ptr(ws),
+                                       _s(qkv)), "attn_bwd")
 
 
 def attn_bwd_workspace(B, T, H, D):

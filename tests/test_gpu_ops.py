@@ -519,6 +519,89 @@ def test_gemm_n96_matches_128x128_bitwise(M, K, kind):
     if kind == "bias_resid":
         assert relerr(outs[0], ref + resid.double()) < 1e-5
 
+@pytest.mark.parametrize("M,C,T", [(16384, 384, 256), (2048, 768, 128), (1024, 384, 64), (512, 128, 256)])
+def test_gemm_store_rowdot(M, C, T):
+    """CG_EPI_STORE_ROWDOT (the projection dgrad dO = dy W, GPT1.py:136, with the attention backward's
+    delta = rowsum(dO * O) per head): dO bit-equal to the plain dgrad, delta within fp32 summation
+    order of the fp64 row dots of the written bf16 dO and O."""
+    from replicatinggpt_amd import _lib as L
+    Fn, O = F(), ops()
+    torch.manual_seed(17)
+    dy = torch.randn(M, C, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(C, C, device=DEV) * C ** -0.5).to(torch.bfloat16)
+    o = torch.randn(M, C, device=DEV).to(torch.bfloat16)
+    assert O.gemm_rowdot_supported(M, C, C, C, C, C)
+    ref = torch.full((M, C), float("nan"), device=DEV).to(torch.bfloat16)
+    Fn.linear_dgrad(dy, w, ref)
+    do = torch.full((M, C), float("nan"), device=DEV).to(torch.bfloat16)
+    H, B = C // 64, M // T
+    delta = torch.full((B, H, T), float("nan"), device=DEV)
+    O.gemm_store_rowdot(dy, w, do, M, C, C, C, C, C, o, C, T, delta)
+    torch.cuda.synchronize()
+    assert torch.equal(do.view(torch.int16), ref.view(torch.int16))
+    exp = (do.double() * o.double()).view(B, T, H, 64).sum(-1).permute(0, 2, 1)
+    assert not torch.isnan(delta).any()
+    err = (delta.double() - exp).abs().max().item()
+    assert err <= 1e-5 * max(1.0, exp.abs().max().item()), err
+    # outside the persistent kernel's shapes the call fails instead of silently skipping delta
+    assert not O.gemm_rowdot_supported(1000, C, C, C, C, C)
+    with pytest.raises(RuntimeError):
+        O.gemm_store_rowdot(dy[:1000], w, do[:1000], 1000, C, C, C, C, C, o[:1000], C, 200, delta)
+
+
+@pytest.mark.parametrize("T", [256, 192, 64])
+@pytest.mark.parametrize("p", [0.0, 0.2])
+def test_attention_bwd_precomputed_delta(T, p):
+    """cg_attn_bwd_delta: the merged resident backward reading delta instead of loading O.  Given the
+    delta the dQ kernel itself computes (the two-launch variant leaves it in the workspace), dQ / dK /
+    dV equal the default launch's bit for bit; given the projection dgrad's delta
+    (gemm_store_rowdot, another fp32 summation order) they agree to bf16 rounding."""
+    from replicatinggpt_amd import _lib as L
+    O, lib = ops(), L.load()
+    B, H, D = 4, 6, 64   # B T % 128 == 0: the dO GEMM's persistent tiles
+    torch.manual_seed(90 + T)
+    d = H * D
+    qkv = (torch.randn(B * T, 3 * d) * 0.7).to(torch.bfloat16).to(DEV)
+    dout = torch.randn(B * T, d).to(torch.bfloat16).to(DEV)
+    call = torch.tensor([5], dtype=torch.int64, device=DEV)
+    scale = (3.0 * D) ** -0.5
+    o = torch.empty(B * T, d, dtype=torch.bfloat16, device=DEV)
+    lse, mask = F().attention_fwd(qkv, B, T, H, D, o, scale, p, 21, call, 4)
+    nws = O.attn_bwd_workspace(B, T, H, D) // 4 + 1
+
+    def bwd(delta=None):
+        ws = torch.zeros(nws, device=DEV)
+        dqkv = torch.full_like(qkv, float("nan"))
+        O.attn_bwd(qkv, B, T, H, D, 0, d, 2 * d, qkv.stride(0), o, d, dout, d, lse, dqkv, 3 * d, scale, p, 21, call,
+                   4, mask, ws, delta)
+        return dqkv, ws
+
+    base, _ = bwd()
+    try:
+        L.check(lib.cg_set_tuning(b"attn_variant", 2))
+        two, ws = bwd()
+    finally:
+        L.check(lib.cg_set_tuning(b"attn_variant", 0))
+    own = ws[:B * H * T].view(B, H, T).clone()
+    din, _ = bwd(own)
+    torch.cuda.synchronize()
+    assert torch.equal(base.view(torch.int16), two.view(torch.int16))
+    assert torch.equal(base.view(torch.int16), din.view(torch.int16))
+    # delta from the dO GEMM's epilogue
+    dy = torch.randn(B * T, d, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(d, d, device=DEV) * d ** -0.5).to(torch.bfloat16)
+    do = torch.empty(B * T, d, dtype=torch.bfloat16, device=DEV)
+    delta = torch.empty(B, H, T, device=DEV)
+    O.gemm_store_rowdot(dy, w, do, B * T, d, d, d, d, d, o, d, T, delta)
+    dout.copy_(do)
+    ref, _ = bwd()
+    got, _ = bwd(delta)
+    torch.cuda.synchronize()
+    assert not torch.isnan(got.float()).any()
+    diff = (got.float() - ref.float()).abs().max().item()
+    assert diff <= 2 ** -7 * ref.float().abs().max().item(), diff
+
+
 def _attn_ref(q, k, v, scale, p=0.0, seed=0, stream=0):
     """q,k,v [B,T,H,D] float64; reference softmax attention with the oracle dropout mask."""
     B, T, H, D = q.shape
