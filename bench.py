@@ -98,8 +98,9 @@ def census_op(name, M, N, K, at, bt, kind, dev, p=0.2, cold=False):
     (functional.py AttnSublayerFn / FFNSublayerFn): "store" (bf16 output), "bias_resid" (fp32
     output = x + o W^T + b: the attention projection), "bias_relu_bits" (bf16 relu(a W1^T + b1) and
     its ReLU keep bits), "bias_drop_resid" (fp32 x + dropout(h W2^T + b2)), "relu_bwd_colpart"
-    (bf16 relu'(h) (dz2 W2) from the keep bits, with the b1 column partials), "wgrad" (fp32,
-    deterministic split-K: the GEMM and its slab reduce).  cold: successive calls cycle through as
+    (bf16 relu'(h) (dz2 W2) from the keep bits, with the b1 column partials), "store_rowdot" (bf16
+    dO = dy Wp and the attention backward's delta = rowsum(dO * O) per head, T = 256), "wgrad" (fp32,
+    deterministic split-K through bf16 slabs as in the step: the GEMM and its slab reduce).  cold: successive calls cycle through as
     many operand sets as make >= COLD_BYTES, so no call finds its operands in the Infinity Cache
     (in the training step every activation operand was last touched a whole sublayer or more
     earlier).  Returns (run, kernels per call)."""
@@ -111,6 +112,8 @@ def census_op(name, M, N, K, at, bt, kind, dev, p=0.2, cold=False):
     lda, ldb = (M if at else K), (N if bt else K)
     relu_bits = kind == "bias_relu_bits" and lib.cg_gemm_relu_bits_supported(0, 0, M, N, K, lda, ldb, N)
     colpart = kind == "relu_bwd_colpart" and lib.cg_gemm_colpart_supported(0, 1, M, N, K, lda, ldb, N)
+    rowdot_T = 256 if M % 256 == 0 else 128
+    rowdot = kind == "store_rowdot" and lib.cg_gemm_rowdot_supported(0, 1, M, N, K, lda, ldb, N)
 
     def make_set():
         st = {"A": torch.randn((K, M) if at else (M, K), device=dev).to(torch.bfloat16),
@@ -124,6 +127,9 @@ def census_op(name, M, N, K, at, bt, kind, dev, p=0.2, cold=False):
             st["bits"] = torch.randint(-2 ** 31, 2 ** 31 - 1, (M, N // 32), dtype=torch.int32, device=dev)
         if colpart:
             st["part"] = torch.empty((M // 64, N), dtype=torch.float32, device=dev)
+        if rowdot:
+            st["o"] = torch.randn(M, N, device=dev).to(torch.bfloat16)
+            st["delta"] = torch.empty(M * N // 64, dtype=torch.float32, device=dev)
         return st
 
     first = make_set()
@@ -137,10 +143,19 @@ def census_op(name, M, N, K, at, bt, kind, dev, p=0.2, cold=False):
         st = sets[ctr[0] % len(sets)]
         ctr[0] += 1
         A, B, out = st["A"], st["B"], st["out"]
-        if kind == "wgrad":
-            ops.gemm(A, B, out, True, bool(at), bool(bt), M, N, K, lda, ldb, N, 0, None, None, 0, None, 0,
-                     0.0, 0, None, 0, 0.0, split, st.get("ws"))
-        elif kind == "store":
+        if kind == "wgrad":   # the step's slot weight gradients: bf16 split-K slabs (functional.linear_wgrad)
+            slab16 = Fn.SLAB_BF16 and split > 1
+            if slab16:
+                L.check(lib.cg_set_tuning(b"slab_bf16", 1), "slab_bf16")
+            try:
+                ops.gemm(A, B, out, True, bool(at), bool(bt), M, N, K, lda, ldb, N, 0, None, None, 0, None, 0,
+                         0.0, 0, None, 0, 0.0, split, st.get("ws"))
+            finally:
+                if slab16:
+                    L.check(lib.cg_set_tuning(b"slab_bf16", 0), "slab_bf16")
+        elif kind == "store_rowdot" and rowdot:
+            ops.gemm_store_rowdot(A, B, out, M, N, K, lda, ldb, N, st["o"], N, rowdot_T, st["delta"])
+        elif kind in ("store", "store_rowdot"):   # store_rowdot unsupported: the step's plain dgrad
             ops.gemm(A, B, out, True, bool(at), bool(bt), M, N, K, lda, ldb, N, 0, None, None, 0, None, 0,
                      0.0, 0, None, 0, 0.0, 1, None)
         elif kind in ("bias_resid", "bias_drop_resid"):
@@ -198,7 +213,8 @@ def census_shapes(cfg, Bsz, T):
     return [
         ("qkv_fwd", M, 3 * d, d, 0, 0, "store", L), ("proj_fwd", M, d, d, 0, 0, "bias_resid", L),
         ("ffn1_fwd", M, F4, d, 0, 0, "bias_relu_bits", L), ("ffn2_fwd", M, d, F4, 0, 0, "bias_drop_resid", L),
-        ("proj_dgrad", M, d, d, 0, 1, "store", L), ("qkv_dgrad", M, d, 3 * d, 0, 1, "store", L),
+        ("proj_dgrad", M, d, d, 0, 1, "store_rowdot" if T <= 256 and d % 64 == 0 else "store", L),
+        ("qkv_dgrad", M, d, 3 * d, 0, 1, "store", L),
         ("ffn2_dgrad", M, F4, d, 0, 1, "relu_bwd_colpart", L), ("ffn1_dgrad", M, d, F4, 0, 1, "store", L),
         ("proj_wgrad", d, d, M, 1, 1, "wgrad", L), ("qkv_wgrad", 3 * d, d, M, 1, 1, "wgrad", L),
         ("ffn2_wgrad", d, F4, M, 1, 1, "wgrad", L), ("ffn1_wgrad", F4, d, M, 1, 1, "wgrad", L),
@@ -240,7 +256,10 @@ def gemm_kernel_name(M, N, at, bt, split, dev, kind="store"):
         crit128 = -(-(M // 128) * (N // 128) // slots) * 128 if N % 128 == 0 else float("inf")
         if crit96 < crit128:
             return "k_gemm_pk<128x96>"
-    return "k_gemm_pk<128x128>" + (" + k_splitk_reduce4" if split > 1 else "")
+    if split > 1:
+        from replicatinggpt_amd import functional as Fn
+        return "k_gemm_pk<128x128>" + (" + k_slab16_reduce8 (bf16 slabs)" if Fn.SLAB_BF16 else " + k_splitk_reduce4")
+    return "k_gemm_pk<128x128>"
 
 
 def _time_ms(fn, reps=20, warm=3):

@@ -111,13 +111,13 @@ def load():
         fn.argtypes = args
     _lib = lib
     # CHARPT_TUNING="key=value,key=value": kernel-selection knobs for measurement runs (cg_set_tuning)
-    # defer_splitk / defer_partials are owned by functional.DEFER (it keeps the slab / partial
+    # defer_splitk / defer_partials / slab_bf16 are owned by functional.DEFER (it keeps the slab / partial
     # workspaces alive while a reduce is pending), so they cannot be set from here; skip_splitk_reduce (wrong gradients, timing only)
     # additionally needs CHARPT_WHATIF to name it.
     for kv in filter(None, os.environ.get("CHARPT_TUNING", "").split(",")):
         key, _, val = kv.partition("=")
         key = key.strip()
-        if key in ("defer_splitk", "defer_partials") or (key == "skip_splitk_reduce" and
+        if key in ("defer_splitk", "defer_partials", "slab_bf16") or (key == "skip_splitk_reduce" and
                                      "skip_splitk_reduce" not in os.environ.get("CHARPT_WHATIF", "")):
             raise RuntimeError(f"charpt: CHARPT_TUNING may not set {key}")
         check(lib.cg_set_tuning(key.encode(), int(val)), f"cg_set_tuning({key})")

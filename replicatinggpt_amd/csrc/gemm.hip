@@ -243,6 +243,13 @@ __global__ void k_splitk_reduce(const float* __restrict__ ws, int split_k, int64
 // bitwise those of the scalar form.
 // S > 0: compile-time split, every slab's float4 loaded before the first add (S loads in flight per
 // thread instead of 4); the adds still run k = 0..S-1 in order.
+// bf16 slabs of an fp32 STORE output (cg_set_tuning "slab_bf16"): 8 outputs per thread
+__global__ __launch_bounds__(256) void k_slab16_reduce8(const void* __restrict__ ws, int S, int64_t n8,
+                                                        float* __restrict__ out, float beta) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n8) slab16_chunk8(ws, S, 8 * n8, i, out, beta);
+}
+
 template <typename TC, int S>
 __global__ __launch_bounds__(256) void k_splitk_reduce4(const float* __restrict__ ws, int split_k, int M, int N,
                                                         TC* __restrict__ C, int64_t ldc, EpiArgs epi) {
@@ -250,39 +257,31 @@ __global__ __launch_bounds__(256) void k_splitk_reduce4(const float* __restrict_
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= M * n4) return;
     const int m = i / n4, n = (i - m * n4) * 4;
-    const int64_t slab = (int64_t)M * N;
-    const float* p = ws + (int64_t)m * N + n;
-    float4 s;
+    const int64_t slab = (int64_t)M * N, p = (int64_t)m * N + n;
+    const bool sb = epi.slab_bf16;   // bf16 slabs (cg_set_tuning "slab_bf16"): same order, widened exactly
+    fv4 s;
     int k = 1;
     if constexpr (S > 0) {
-        float4 a[S];
+        fv4 a[S];
 #pragma unroll
-        for (int j = 0; j < S; ++j) {
-            const fv4 t = __builtin_nontemporal_load((const fv4*)(p + j * slab));  // slabs are read once
-            a[j] = make_float4(t[0], t[1], t[2], t[3]);
-        }
+        for (int j = 0; j < S; ++j) a[j] = ld_slab4(ws, p + j * slab, sb);   // slabs are read once
         s = a[0];
 #pragma unroll
-        for (int j = 1; j < S; ++j) {
-            s.x += a[j].x; s.y += a[j].y; s.z += a[j].z; s.w += a[j].w;
-        }
+        for (int j = 1; j < S; ++j) s += a[j];
         k = split_k;
     } else {
-        s = *(const float4*)p;
+        s = ld_slab4(ws, p, sb);
     }
     for (; k + 4 <= split_k; k += 4) {
-        const float4 a = *(const float4*)(p + k * slab), b = *(const float4*)(p + (k + 1) * slab);
-        const float4 c = *(const float4*)(p + (k + 2) * slab), d = *(const float4*)(p + (k + 3) * slab);
-        s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
-        s.x += b.x; s.y += b.y; s.z += b.z; s.w += b.w;
-        s.x += c.x; s.y += c.y; s.z += c.z; s.w += c.w;
-        s.x += d.x; s.y += d.y; s.z += d.z; s.w += d.w;
+        const fv4 a = ld_slab4(ws, p + k * slab, sb), b = ld_slab4(ws, p + (k + 1) * slab, sb);
+        const fv4 c = ld_slab4(ws, p + (k + 2) * slab, sb), d = ld_slab4(ws, p + (k + 3) * slab, sb);
+        s += a;
+        s += b;
+        s += c;
+        s += d;
     }
-    for (; k < split_k; ++k) {
-        const float4 a = *(const float4*)(p + k * slab);
-        s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
-    }
-    float v[4] = {s.x, s.y, s.z, s.w};
+    for (; k < split_k; ++k) s += ld_slab4(ws, p + k * slab, sb);
+    float v[4] = {s[0], s[1], s[2], s[3]};
     if (epi.kind != CG_EPI_STORE && epi.bias) {
         const float4 b = *(const float4*)(epi.bias + n);
         v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
@@ -380,6 +379,7 @@ int g_gemm_group_p8 = 0;   // persistent-kernel tile order (gemm_tile.h tile_rc)
 int g_gemm_group_pk = 0;
 int g_gemm_n96 = 1;       // cg_set_tuning("gemm_n96"): 128x96 tiles for the part-filling fp32 residual forwards (gemm_pk.hip launch_n96)
 int g_defer_splitk = 0;   // cg_set_tuning("defer_splitk"): split-K reduces of fp32 STORE outputs deferred
+int g_slab_bf16 = 0;      // cg_set_tuning("slab_bf16"): split-K partial sums of fp32 STORE outputs as bf16 slabs
 RedJobs g_red_pending = {};
 hipStream_t g_red_stream = nullptr;   // the stream the pending jobs were enqueued on
 int g_red_device = -1;                // ... and that stream's device (stream handles repeat across devices)
@@ -475,6 +475,10 @@ extern "C" int cg_set_tuning(const char* key, int value) {
         g_defer_splitk = value;
         return CG_OK;
     }
+    if (!strcmp(key, "slab_bf16")) {   // split-K fp32 STORE products on the 128x128 persistent kernel
+        g_slab_bf16 = value;
+        return CG_OK;
+    }
     if (!strcmp(key, "defer_partials")) {   // queue cg_layernorm_bwd_reduce / cg_reduce_rows until cg_flush_deferred
         g_defer_partials = value;
         return CG_OK;
@@ -535,10 +539,24 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
     EpiArgs e = make_epi(epi);
     CG_REQUIRE(split_k == 1 || e.kind == CG_EPI_STORE || e.kind == CG_EPI_BIAS || e.kind == CG_EPI_BIAS_RESID,
                "cg_gemm: split-K supports STORE/BIAS/BIAS_RESID epilogues only");
+    const bool vec4 = N % 4 == 0 && ldc % 4 == 0 && M * N < (int64_t)1 << 31 &&
+                      (((uintptr_t)C | (uintptr_t)workspace | (uintptr_t)(e.bias ? e.bias : (const float*)C) |
+                        (uintptr_t)(e.resid ? e.resid : (const float*)C)) & 15) == 0 &&
+                      (!e.resid || e.ld_resid % 4 == 0);
     bool fast = false;
-    if (op_dtype == CG_BF16 && fast_gemm_launch(a_trans, b_trans, M, N, K, (const bf16_t*)A, lda,
-                                                (const bf16_t*)B, ldb, C, c_dtype, ldc, e, split_k,
-                                                (float*)workspace, st)) {
+    // bf16 slabs: only the 128x128 persistent kernel writes them (fast_gemm_launch declines otherwise,
+    // nothing launched) and only the vectorised reduces read them
+    e.slab_bf16 = g_slab_bf16 && split_k > 1 && op_dtype == CG_BF16 && e.kind == CG_EPI_STORE &&
+                  c_dtype == CG_F32 && vec4 && ldc == N && (M * N) % 8 == 0 && !g_skip_splitk_reduce;
+    if (e.slab_bf16) {
+        fast = fast_gemm_launch(a_trans, b_trans, M, N, K, (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, c_dtype,
+                                ldc, e, split_k, (float*)workspace, st);
+        if (!fast) e.slab_bf16 = 0;
+    }
+    if (fast) {
+    } else if (op_dtype == CG_BF16 && fast_gemm_launch(a_trans, b_trans, M, N, K, (const bf16_t*)A, lda,
+                                                       (const bf16_t*)B, ldb, C, c_dtype, ldc, e, split_k,
+                                                       (float*)workspace, st)) {
         fast = true;
     } else if (e.aux_dtype == CG_BITS) {
         set_error("cg_gemm: CG_BITS ReLU keep bits need a persistent bf16 kernel (cg_gemm_relu_bits_supported)");
@@ -561,10 +579,6 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
         launch_generic<float, float>(a_trans, b_trans, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k,
                                      workspace, st);
     }
-    const bool vec4 = N % 4 == 0 && ldc % 4 == 0 && M * N < (int64_t)1 << 31 &&
-                      (((uintptr_t)C | (uintptr_t)workspace | (uintptr_t)(e.bias ? e.bias : (const float*)C) |
-                        (uintptr_t)(e.resid ? e.resid : (const float*)C)) & 15) == 0 &&
-                      (!e.resid || e.ld_resid % 4 == 0);
     // (slab sets above 40 MB -- the C4 FFN / QKV weight gradients -- keep their own reduce kernel: in
     // the next 256x256 GEMM's tail they measured no gain, C4 58.2 vs 57.9 ms/step)
     if (split_k > 1 && vec4 && !g_skip_splitk_reduce && g_defer_splitk && fast && e.kind == CG_EPI_STORE &&
@@ -576,7 +590,10 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
             flush_pending();
         g_red_stream = st;
         g_red_device = dev;
-        g_red_pending.j[g_red_pending.n++] = RedJob{(const float*)workspace, (float*)C, M * N / 4, split_k, e.beta};
+        g_red_pending.j[g_red_pending.n++] = RedJob{(const float*)workspace, (float*)C, M * N / 4, split_k, e.beta, e.slab_bf16};
+    } else if (split_k > 1 && e.slab_bf16) {
+        const int64_t n8 = M * N / 8;
+        k_slab16_reduce8<<<ceil_div(n8, 256), 256, 0, st>>>(workspace, split_k, n8, (float*)C, e.beta);
     } else if (split_k > 1 && vec4 && !g_skip_splitk_reduce) {
         const int n4 = (int)(M * N / 4);
 #define SKR(TC_, S_)                                                                                  \
@@ -641,8 +658,13 @@ extern "C" int cg_colsum(const void* X, int x_dtype, int64_t rows, int64_t N, in
 
 namespace cg {
 static void launch_splitk_reduce_job(const RedJob& j, hipStream_t st) {
+    if (j.bf16 && (j.n4 & 1) == 0) {   // red_tail's bf16 form, standalone
+        k_slab16_reduce8<<<ceil_div(j.n4 / 2, 256), 256, 0, st>>>(j.ws, j.S, j.n4 / 2, j.out, j.beta);
+        return;
+    }
     EpiArgs e = make_epi(nullptr);
     e.beta = j.beta;
+    e.slab_bf16 = j.bf16;
     const int64_t n = 4 * j.n4;
     const int n4 = (int)j.n4;
     // one row of n elements: the same kernel and summation order as the in-line reduce

@@ -241,6 +241,7 @@ bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf1
     if (e.resid && ((((uintptr_t)e.resid) & 15) || e.ld_resid % 4)) return false;
     if (e.aux && ((((uintptr_t)e.aux) & 15) || e.ld_aux % 8)) return false;
     int v = pick_variant(at, bt, M, N, split_k);
+    if (e.slab_bf16 && (!pk128(v) || split_k < 2 || e.kind != CG_EPI_STORE)) return false;
     if (K % (FBK * split_k)) {
         // uneven split-K (the last split shorter): only the 128x128 persistent kernel, and only when
         // every split is non-empty; otherwise the generic kernels (ceil-sized chunks) take it

@@ -19,7 +19,19 @@ struct EpiArgs {
     int site;
     float beta;
     float* colpart;  // RELU_BWD: per-64-row-block column sums; STORE_ROWDOT: per-head row dots (k_gemm_pk only)
+    int slab_bf16;   // split-K: the per-split partial sums stored as bf16 slabs (cg_set_tuning "slab_bf16")
 };
+
+// four consecutive slab elements as fp32 (bf16 slabs: one 8-B load, exact widening)
+typedef unsigned slab_u2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ fv4 ld_slab4(const void* ws, int64_t idx, bool bf16) {
+    if (bf16) {
+        const slab_u2 w = __builtin_nontemporal_load((const slab_u2*)((const bf16_t*)ws + idx));
+        return fv4{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u), __uint_as_float(w.y << 16),
+                   __uint_as_float(w.y & 0xffff0000u)};
+    }
+    return __builtin_nontemporal_load((const fv4*)((const float*)ws + idx));
+}
 
 __device__ __forceinline__ float aux_at(const EpiArgs& e, int64_t m, int64_t n) {
     return e.aux_dtype == CG_BF16 ? bf2f(((const bf16_t*)e.aux)[m * e.ld_aux + n])
@@ -70,11 +82,12 @@ __device__ __forceinline__ void store_out(TC* C, int64_t off, float v, float bet
 // chunks once its block's own items are done) or by cg_flush_deferred.  Slab 0 first, then 1, ...:
 // k_splitk_reduce4's order, so the same bits.
 struct RedJob {
-    const float* ws;
+    const float* ws;   // fp32 slabs, or bf16 ones (bf16 != 0)
     float* out;
     int64_t n4;
     int S;
     float beta;
+    int bf16;
 };
 constexpr int MAX_RED = 2;
 struct RedJobs {
@@ -83,6 +96,35 @@ struct RedJobs {
 };
 RedJobs take_pending_reduces(hipStream_t st);   // gemm.hip: pending jobs (cleared) for a launch on st
 
+// out[8i .. 8i+7] = sum over slabs k = 0..S-1 (in order, fp32) of bf16 slab elements (one 16-B load
+// per slab), (+ beta out): the deferred tail and the standalone reduce of bf16 slabs (same bits)
+__device__ __forceinline__ void slab16_chunk8(const void* ws, int S, int64_t slab, int64_t i, float* out, float beta) {
+    typedef unsigned u4v __attribute__((ext_vector_type(4)));
+    fv4 lo = fv4{0.f, 0.f, 0.f, 0.f}, hi = lo;
+#pragma unroll 8
+    for (int k = 0; k < S; ++k) {
+        const u4v w = __builtin_nontemporal_load((const u4v*)((const bf16_t*)ws + 8 * i + k * slab));
+        const fv4 a = {__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u), __uint_as_float(w.y << 16),
+                       __uint_as_float(w.y & 0xffff0000u)};
+        const fv4 b = {__uint_as_float(w.z << 16), __uint_as_float(w.z & 0xffff0000u), __uint_as_float(w.w << 16),
+                       __uint_as_float(w.w & 0xffff0000u)};
+        if (k == 0) {
+            lo = a;
+            hi = b;
+        } else {
+            lo += a;
+            hi += b;
+        }
+    }
+    fv4* o = (fv4*)(out + 8 * i);
+    if (beta != 0.f) {
+        lo += beta * o[0];
+        hi += beta * o[1];
+    }
+    o[0] = lo;
+    o[1] = hi;
+}
+
 // thread t sums float4 chunks t, t + threads, ... of every job
 __device__ __forceinline__ void red_tail(const RedJobs& r) {
     const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
@@ -90,11 +132,14 @@ __device__ __forceinline__ void red_tail(const RedJobs& r) {
     for (int q = 0; q < r.n; ++q) {
         const RedJob& J = r.j[q];
         const int64_t slab = 4 * J.n4;
+        if (J.bf16 && (J.n4 & 1) == 0) {   // bf16 slabs: 8 elements (one 16-B load) per slab per chunk
+            for (int64_t i = t0; i < J.n4 / 2; i += nthr) slab16_chunk8(J.ws, J.S, slab, i, J.out, J.beta);
+            continue;
+        }
         for (int64_t i = t0; i < J.n4; i += nthr) {
-            const float* p = J.ws + 4 * i;
-            fv4 s = __builtin_nontemporal_load((const fv4*)p);
+            fv4 s = ld_slab4(J.ws, 4 * i, J.bf16);
 #pragma unroll 8
-            for (int k = 1; k < J.S; ++k) s += __builtin_nontemporal_load((const fv4*)(p + k * slab));
+            for (int k = 1; k < J.S; ++k) s += ld_slab4(J.ws, 4 * i + k * slab, J.bf16);
             fv4* o = (fv4*)(J.out + 4 * i);
             if (J.beta != 0.f) s += J.beta * *o;
             *o = s;
@@ -109,6 +154,7 @@ extern int g_gemm_max_grid;
 extern int g_gemm_group_p8;
 extern int g_gemm_group_pk;
 extern int g_gemm_n96;
+extern int g_slab_bf16;
 // test knob (cg_set_tuning("pk_flags", f)) for the persistent kernel's epilogue (gemm_pk.hip)
 extern int g_pk_flags;
 int gemm_cu_count();  // compute units of the current device (cached; gemm_pk.hip)

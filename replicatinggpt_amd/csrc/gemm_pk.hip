@@ -464,7 +464,7 @@ struct GeoP {
 #ifndef CG_PK_DPG
 #define CG_PK_DPG 1   // next-stage DMA instructions issued per group of 4 MFMAs
 #endif
-constexpr int EK_ANY = -1, EK_SLAB = 6;
+constexpr int EK_ANY = -1, EK_SLAB = 6, EK_SLAB16 = 8;   // 7: CG_EPI_STORE_ROWDOT
 // BK: K depth of one LDS stage, 64 or 32 (32: the same 64 KB per block holds 4 stages, 3 K-tiles in
 // flight at two blocks per CU; same bits -- kchunk stays a multiple of 64, same k order.  Measured
 // 10-15 % slower on every C2 shape: 64-B row segments double the TA/TCP requests,
@@ -645,6 +645,7 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     constexpr int EPI_OPS =
         NJ != 4 ? 4 * NJ
         : EK == CG_EPI_STORE_ROWDOT ? 12
+        : EK == EK_SLAB16 ? 8
         : (EK == CG_EPI_STORE || EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_RELU_BWD) ? 8 : 16;
     int cur = 0, cj = 0, ckt = 0;
     int cnk;   // K-tiles of the compute cursor's item
@@ -765,6 +766,8 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
                 atomicAdd(&g_pk_bounds[2], 1ull);
 #endif
             if (WI_NOEPI) {
+            } else if constexpr (EK == EK_SLAB16) {   // bf16 slab: 16-B row segments, as a bf16 output
+                store_item<true>(acc, mr, nc, (bf16_t*)ws + (int64_t)sp * M * N, CG_BF16, N);
             } else if (EK == EK_SLAB || split_k > 1) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
@@ -852,7 +855,8 @@ void launch_ek(unsigned grid, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
                hipStream_t st) {
 #define L1(EK_) launch_1<AT_, BT_, BM, BN, NBUF, EK_, BK>(grid, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, kchunk, ws, st)
     if (split_k > 1) {
-        L1(EK_SLAB);
+        if (e.slab_bf16) L1(EK_SLAB16);
+        else L1(EK_SLAB);
         return;
     }
     if constexpr (!AT_ && BM == 128 && BN == 128) {

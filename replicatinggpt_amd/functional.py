@@ -304,13 +304,20 @@ def _wgrad_split(M, N, K, fast):
     return split
 
 
+# The training path's weight gradients (flat gradient slots) take their split-K partial sums through
+# bf16 slabs (cg_set_tuning "slab_bf16": half the slab bytes written and read back; each per-split
+# partial rounded once to bf16, the sum over splits in fp32 -- torch's bf16 path rounds the whole
+# gradient to bf16).  Temporaries (charpt::linear's backward) keep fp32 slabs.  CHARPT_SLAB_BF16=0: A/B.
+SLAB_BF16 = os.environ.get("CHARPT_SLAB_BF16", "1") != "0"
+
+
 def linear_wgrad(dy2, x2, out, beta, into_slot=False):
     """out[N,K] (+)= dy2[M,N]^T @ x2[M,K]   (fp32, deterministic split-K).
 
     into_slot: ``out`` is a region's flat gradient slot, which nothing reads before DEFER closes,
     so inside ``with DEFER:`` its split-K reduce may stay pending past this call.  Any other
     output (a temporary, a tensor handed to autograd) gets its pending reduces flushed right after
-    the GEMM, so it is complete when this returns."""
+    the GEMM, so it is complete when this returns.  Slot outputs use bf16 split-K slabs (SLAB_BF16)."""
     if "skip_wgrad" in WHATIF:
         return out
     M, N = dy2.shape
@@ -324,8 +331,15 @@ def linear_wgrad(dy2, x2, out, beta, into_slot=False):
         if defer:
             # its reduce may run after this call returns
             DEFER.keep.extend((ws, dy2, x2))
-    ops.gemm(dy2, x2, out, _is_bf16(dy2.dtype), True, True, N, K, M, N, K, out.stride(0), L.EPI_STORE, None, None, 0,
-             None, 0, 0.0, 0, None, 0, float(beta), split, ws)
+    slab16 = SLAB_BF16 and into_slot and split > 1 and dy2.is_cuda
+    if slab16:
+        L.check(L.load().cg_set_tuning(b"slab_bf16", 1), "slab_bf16")
+    try:
+        ops.gemm(dy2, x2, out, _is_bf16(dy2.dtype), True, True, N, K, M, N, K, out.stride(0), L.EPI_STORE, None,
+                 None, 0, None, 0, 0.0, 0, None, 0, float(beta), split, ws)
+    finally:
+        if slab16:
+            L.check(L.load().cg_set_tuning(b"slab_bf16", 0), "slab_bf16")
     if DEFER.active and not defer and split > 1:
         DEFER.flush()
     return out

@@ -426,6 +426,53 @@ def test_gemm_tile_order_is_bitwise_invariant(M, N, K, split):
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
 
 
+@pytest.mark.parametrize("M,N,K,split", [(1152, 384, 16384, 16), (384, 1536, 16384, 14), (384, 384, 16384, 24),
+                                         (256, 2048, 4096, 4)])
+@pytest.mark.parametrize("defer", [False, True])
+def test_gemm_bf16_slabs(M, N, K, split, defer):
+    """cg_set_tuning("slab_bf16") (the training backward's weight gradients, GPT1.py:232 backward):
+    the split-K partial sums go through bf16 slabs.  The output is exactly the fp32 sum, in split
+    order, of each split's fp32 partial (a split-1 GEMM over that K chunk: same MFMA order) rounded
+    to bf16 -- bit for bit, with the reduce in line or deferred into the next GEMM's tail / the
+    flush -- and within bf16 rounding of the fp64 product."""
+    from replicatinggpt_amd import _lib as L
+    lib = L.load()
+    torch.manual_seed(19)
+    A = (torch.randn(K, M, device=DEV) * 0.5).to(torch.bfloat16)
+    B = (torch.randn(K, N, device=DEV) * 0.5).to(torch.bfloat16)
+    ws = torch.empty(ops().gemm_workspace(M, N, split) // 4, dtype=torch.float32, device=DEV)
+    out = torch.full((M, N), float("nan"), device=DEV)
+    try:
+        L.check(lib.cg_set_tuning(b"slab_bf16", 1))
+        L.check(lib.cg_set_tuning(b"defer_splitk", int(defer)))
+        ops().gemm(A, B, out, True, True, True, M, N, K, M, N, N, 0, None, None, 0, None, 0, 0.0, 0, None, 0, 0.0,
+                   split, ws)
+        if defer:   # a later persistent launch on the stream takes the pending reduce in its tail
+            x = torch.randn(256, 128, device=DEV).to(torch.bfloat16)
+            y = torch.empty(256, 128, dtype=torch.bfloat16, device=DEV)
+            ops().gemm(x, x[:128], y, True, False, False, 256, 128, 128, 128, 128, 128, 0, None, None, 0, None, 0,
+                       0.0, 0, None, 0, 0.0, 1, None)
+            L.check(lib.cg_flush_deferred(L.ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    finally:
+        L.check(lib.cg_set_tuning(b"slab_bf16", 0))
+        L.check(lib.cg_set_tuning(b"defer_splitk", 0))
+    kc = -(-(K // 64) // split) * 64
+    want = None
+    for sp in range(split):
+        k0, k1 = sp * kc, min(K, (sp + 1) * kc)
+        part = torch.empty(M, N, device=DEV)
+        Ak, Bk = A[k0:k1], B[k0:k1]
+        ops().gemm(Ak, Bk, part, True, True, True, M, N, k1 - k0, M, N, N, 0, None, None, 0, None, 0, 0.0, 0, None, 0,
+                   0.0, 1, None)
+        p16 = part.to(torch.bfloat16).float()
+        want = p16 if want is None else want + p16
+    torch.cuda.synchronize()
+    assert not torch.isnan(out).any()
+    assert torch.equal(out, want)
+    ref = A.double().t() @ B.double()
+    assert relerr(out, ref) < 2 ** -8   # each partial rounded once to bf16 (2^-9 relative)
+
+
 @pytest.mark.parametrize("c_dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("beta", [0.0, 1.0])
 def test_gemm_splitk_reduce_vec_matches_scalar(c_dt, beta):

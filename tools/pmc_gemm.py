@@ -47,6 +47,8 @@ def algorithmic_bytes(op):
         return b + 4 * M * N
     if kind == "store":
         return b + 2 * M * N
+    if kind == "store_rowdot":
+        return b + 2 * M * N + 2 * M * N + 4 * (M * N // 64)   # bf16 dO, O read, delta
     if kind in ("bias_resid", "bias_drop_resid"):
         return b + 4 * N + 4 * M * N + 4 * M * N          # bias, fp32 residual read, fp32 output
     if kind == "bias_relu_bits":
@@ -77,7 +79,7 @@ def _dispatches(path, counter):
     with open(path) as f:
         for r in csv.DictReader(f):
             name = r["Kernel_Name"]
-            if r["Counter_Name"] != counter or not ("k_gemm" in name or "k_splitk_reduce" in name):
+            if r["Counter_Name"] != counter or not ("k_gemm" in name or "k_splitk_reduce" in name or "k_slab16_reduce" in name):
                 continue
             key = int(r.get("Dispatch_Id") or r["Correlation_Id"])
             rows[key] = rows.get(key, 0.0) + float(r["Counter_Value"]) * 1024.0   # KiB -> bytes
