@@ -380,6 +380,7 @@ int g_gemm_group_pk = 0;
 int g_gemm_n96 = 1;       // cg_set_tuning("gemm_n96"): 128x96 tiles for the part-filling fp32 residual forwards (gemm_pk.hip launch_n96)
 int g_defer_splitk = 0;   // cg_set_tuning("defer_splitk"): split-K reduces of fp32 STORE outputs deferred
 int g_slab_bf16 = 0;      // cg_set_tuning("slab_bf16"): split-K partial sums of fp32 STORE outputs as bf16 slabs
+int g_red_side = 1;       // cg_set_tuning("red_side"): a part-filling persistent launch takes a pending reduce on extra blocks
 RedJobs g_red_pending = {};
 hipStream_t g_red_stream = nullptr;   // the stream the pending jobs were enqueued on
 int g_red_device = -1;                // ... and that stream's device (stream handles repeat across devices)
@@ -399,6 +400,10 @@ RedJobs take_pending_reduces(hipStream_t st) {
         g_red_pending.n = 0;
     }
     return r;
+}
+
+bool has_pending_reduces(hipStream_t st) {
+    return g_red_pending.n && st == g_red_stream && current_device() == g_red_device;
 }
 
 static void launch_splitk_reduce_job(const RedJob& j, hipStream_t st);
@@ -473,6 +478,10 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     }
     if (!strcmp(key, "defer_splitk")) {   // off: pending reduces are flushed on the caller's next cg_flush_deferred
         g_defer_splitk = value;
+        return CG_OK;
+    }
+    if (!strcmp(key, "red_side")) {
+        g_red_side = value;
         return CG_OK;
     }
     if (!strcmp(key, "slab_bf16")) {   // split-K fp32 STORE products on the 128x128 persistent kernel

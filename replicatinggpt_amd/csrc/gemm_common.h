@@ -95,6 +95,7 @@ struct RedJobs {
     int n;
 };
 RedJobs take_pending_reduces(hipStream_t st);   // gemm.hip: pending jobs (cleared) for a launch on st
+bool has_pending_reduces(hipStream_t st);       // gemm.hip: whether a launch on st would take some
 
 // out[8i .. 8i+7] = sum over slabs k = 0..S-1 (in order, fp32) of bf16 slab elements (one 16-B load
 // per slab), (+ beta out): the deferred tail and the standalone reduce of bf16 slabs (same bits)
@@ -125,10 +126,13 @@ __device__ __forceinline__ void slab16_chunk8(const void* ws, int S, int64_t sla
     o[1] = hi;
 }
 
-// thread t sums float4 chunks t, t + threads, ... of every job
-__device__ __forceinline__ void red_tail(const RedJobs& r) {
-    const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
-    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// thread t sums float4 chunks t, t + threads, ... of every job.  first > 0: only blocks first ..
+// grid - 1 take part -- the blocks a part-filling GEMM launch was given beyond its items, which run
+// the reduce beside the items instead of after them
+__device__ __forceinline__ void red_tail(const RedJobs& r, int first = 0) {
+    if ((int)blockIdx.x < first) return;
+    const int64_t nthr = (int64_t)(gridDim.x - first) * blockDim.x;
+    const int64_t t0 = (int64_t)(blockIdx.x - first) * blockDim.x + threadIdx.x;
     for (int q = 0; q < r.n; ++q) {
         const RedJob& J = r.j[q];
         const int64_t slab = 4 * J.n4;
@@ -155,6 +159,7 @@ extern int g_gemm_group_p8;
 extern int g_gemm_group_pk;
 extern int g_gemm_n96;
 extern int g_slab_bf16;
+extern int g_red_side;
 // test knob (cg_set_tuning("pk_flags", f)) for the persistent kernel's epilogue (gemm_pk.hip)
 extern int g_pk_flags;
 int gemm_cu_count();  // compute units of the current device (cached; gemm_pk.hip)

@@ -815,7 +815,9 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     }
 #endif
     wait_vm<0>();  // the dummy DMAs past the last K-tile land before the workgroup's LDS is released
-    if (red.n) red_tail(red);   // a deferred split-K reduce of an earlier launch (gemm_common.h)
+    // a deferred split-K reduce of an earlier launch (gemm_common.h): on the blocks beyond the items
+    // when the launch has them (launch_p), else in every block's tail
+    if (red.n) red_tail(red, P > nitems ? nitems : 0);
 }
 
 
@@ -902,7 +904,10 @@ bool launch_p(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
     const int64_t nitems = (M / BM) * (N / BN) * split_k;
     int64_t slots = (int64_t)cu_count() * G::OCC;
     if (g_gemm_max_grid > 0 && g_gemm_max_grid < slots) slots = g_gemm_max_grid;
-    const unsigned grid = (unsigned)(nitems < slots ? nitems : slots);
+    // a part-filling launch that will take a pending split-K reduce gets the free slots too: those
+    // blocks have no items and run the reduce beside the items (red_tail's `first`)
+    const bool side = g_red_side && nitems < slots && has_pending_reduces(st);
+    const unsigned grid = (unsigned)(nitems < slots && !side ? nitems : slots);
 #define FG(AT_, BT_) launch_ek<AT_, BT_, BM, BN, NBUF, BK>(grid, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, kchunk, ws, st)
     // transposed LDS images need a multiple of 128 rows (DmaP, col_swz): other tiles serve only the
     // layouts they can; false = not launched
