@@ -55,13 +55,23 @@ def _train(world, rank, batch, kind="small", p=0.0):
     return losses, model.flat.master.detach().cpu().clone(), len(step.g_seg), model.config.dropout_seed, keep, init
 
 
+def _by_value(x):
+    """Tensors cross the queue as numpy arrays (pickled by value): torch's shared-fd form needs the
+    sending process alive until the parent unpickles, and the worker exits right after put."""
+    return ("__tensor__", x.numpy()) if isinstance(x, torch.Tensor) else x
+
+
+def _from_value(x):
+    return torch.from_numpy(x[1]) if isinstance(x, tuple) and len(x) == 2 and x[0] == "__tensor__" else x
+
+
 def _worker(rank, port, q, kind="small", p=0.0):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
     try:
         torch.cuda.set_device(0)
-        q.put((rank,) + _train(WORLD, rank, B_RANK, kind, p))
+        q.put(tuple(_by_value(v) for v in (rank,) + _train(WORLD, rank, B_RANK, kind, p)))
     finally:
         dist.destroy_process_group()
 
@@ -76,7 +86,7 @@ def _run_ranks(kind="small", p=0.0):
     res = {}
     try:
         for _ in range(WORLD):
-            r, *rest = q.get(timeout=300)
+            r, *rest = (_from_value(v) for v in q.get(timeout=300))
             res[r] = rest
     finally:
         for pr in procs:
@@ -132,7 +142,7 @@ def test_dp_two_ranks_equal_one_rank_on_concatenated_batch():
     res = {}
     try:
         for _ in range(WORLD):
-            r, losses, master, nseg, seed, _, _ = q.get(timeout=300)
+            r, losses, master, nseg, seed, _, _ = (_from_value(v) for v in q.get(timeout=300))
             res[r] = (losses, master, nseg, seed)
     finally:
         for p in procs:
