@@ -17,7 +17,8 @@
  *     cg_set_tuning knobs and the deferred-work queues they enable ("defer_splitk": a split-K
  *     weight-gradient reduce left for the next persistent GEMM on the same stream or
  *     cg_flush_deferred; "defer_partials": column-sum reduces queued for one launch at
- *     cg_flush_deferred).  Those are not thread-safe: set knobs, enable deferral and make the
+ *     cg_flush_deferred; cg_adamw_defer: AdamW region updates queued for the free blocks of a
+ *     later part-filling GEMM launch or cg_flush_deferred).  Those are not thread-safe: set knobs, enable deferral and make the
  *     calls it affects from one host thread.  Every other entry point is
  *     reentrant; cg_last_error_string() is per thread.
  *   - return CG_OK (0) or an error code; cg_last_error_string() gives the message.
@@ -278,6 +279,19 @@ int cg_decode_sample(const float* logits, int64_t ldl, int64_t V, int64_t B, int
    p_bf16: optional bf16 shadow written after the update (GEMM operands).                    */
 int cg_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, double lr, double beta1,
              double beta2, double eps, double weight_decay, const int64_t* step_ptr, void* stream);
+/* the same update for [0, n) of one region, deferred: run by the free blocks of the next persistent
+   GEMM launch on `stream` that has >= 64 of them (a part-filling launch), else by cg_flush_deferred
+   as a cg_adamw launch -- same bits either way.  The gradient must be final in stream order (a
+   pending split-K reduce writing into g is launched first) and nothing launched before the flush may
+   read p / p_bf16 / m / v.  n % 4 == 0, p, g, m, v 16-B and p_bf16 8-B aligned. */
+int cg_adamw_defer(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, double lr,
+                   double beta1, double beta2, double eps, double weight_decay, const int64_t* step_ptr,
+                   void* stream);
+/* cg_adamw over a host list of nseg (start, length) element segments of the same flat buffers
+   (multiples of 4, at most 64): the parameters a step did not defer.  Same bits as cg_adamw. */
+int cg_adamw_segments(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, const int64_t* segs, int nseg,
+                      double lr, double beta1, double beta2, double eps, double weight_decay,
+                      const int64_t* step_ptr, void* stream);
 
 #ifdef __cplusplus
 }

@@ -84,6 +84,8 @@ _SIGS = {
                                P]),
     "cg_decode_sample": (c_int, [P, c_i64, c_i64, c_i64, c_int, P, P, P, c_i64, P]),
     "cg_adamw": (c_int, [P, P, P, P, P, c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, P, P]),
+    "cg_adamw_defer": (c_int, [P, P, P, P, P, c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, P, P]),
+    "cg_adamw_segments": (c_int, [P, P, P, P, P, P, c_int, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, P, P]),
 }
 
 _lib = None

@@ -2,7 +2,9 @@
 // the fused AdamW step over flat fp32 buffers (torch.optim.AdamW, GPT1.py:218,233).
 #include <math.h>
 
+#include "adamw.h"
 #include "common.h"
+#include "gemm_common.h"
 
 using namespace cg;
 
@@ -67,22 +69,7 @@ extern "C" int cg_ce_bwd(const float* logits, int64_t rows, int64_t V, int64_t l
 }
 
 // ---- AdamW ------------------------------------------------------------------------------
-// Same fp32 operation order as torch/optim/adam.py _single_tensor_adam (decoupled decay):
-//   p *= 1 - lr*wd ; m = m + (1-b1)*(g - m) [lerp, w<0.5] ; v = v*b2 + (1-b2)*g*g ;
-//   denom = sqrt(v)/sqrt(bc2) + eps ; p += (-lr/bc1)*m / denom
-// Explicit _rn intrinsics keep the compiler from contracting into FMAs.
-struct AdamScalars {
-    float decay, w1, b2, omb2, eps, neg_step, bc2_sqrt;
-};
-
-__device__ __forceinline__ float adam_one(float p, float g, float& m, float& v, const AdamScalars& s) {
-    p = __fmul_rn(p, s.decay);
-    m = __fadd_rn(m, __fmul_rn(s.w1, __fsub_rn(g, m)));
-    v = __fadd_rn(__fmul_rn(v, s.b2), __fmul_rn(__fmul_rn(s.omb2, g), g));
-    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), s.bc2_sqrt), s.eps);
-    return __fadd_rn(p, __fdiv_rn(__fmul_rn(s.neg_step, m), denom));
-}
-
+// element arithmetic and the per-launch scalars: adamw.h (shared with the GEMM side blocks)
 typedef float nf4 __attribute__((ext_vector_type(4)));
 typedef unsigned nu2 __attribute__((ext_vector_type(2)));
 template <bool NT>
@@ -100,21 +87,6 @@ __device__ __forceinline__ void st4(float* p, float4 x) {
     else *(float4*)p = x;
 }
 
-__device__ __forceinline__ AdamScalars adam_scalars(double lr, double beta1, double beta2, double eps, double wd,
-                                                    const int64_t* step_ptr) {
-    const double t = (double)*step_ptr;
-    AdamScalars s;
-    s.decay = (float)(1.0 - lr * wd);
-    s.w1 = (float)(1.0 - beta1);
-    s.b2 = (float)beta2;
-    s.omb2 = (float)(1.0 - beta2);
-    s.eps = (float)eps;
-    const double bc1 = 1.0 - pow(beta1, t);
-    const double bc2 = 1.0 - pow(beta2, t);
-    s.neg_step = (float)(-(lr / bc1));
-    s.bc2_sqrt = (float)sqrt(bc2);
-    return s;
-}
 
 // U float4 groups per thread per iteration (all loads issued before any arithmetic); NT: the
 // 30 B/param stream bypasses the caches (non-temporal loads and stores) -- every byte is touched once
@@ -216,6 +188,81 @@ static int adamw_launch(float* p, const float* g, float* m, float* v, uint16_t* 
     CG_LAUNCH_CHECK("cg_adamw");
     return CG_OK;
 }
+
+// AdamW over a list of flat segments (the training step's remaining parameters once its weight
+// matrices were updated early by cg_adamw_defer jobs): float4 chunk c of the concatenation ->
+// segment s by binary search over the chunk prefix counts; adam_one per element, so the bits of
+// the one-launch form
+constexpr int ADAM_MAX_SEGS = 64;
+struct AdamSegs {
+    int64_t start[ADAM_MAX_SEGS];      // element offsets (multiples of 4)
+    int64_t pre[ADAM_MAX_SEGS + 1];    // float4 chunks before segment s
+    int n;
+};
+
+__global__ __launch_bounds__(256) void k_adamw_segs(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    bf16_t* __restrict__ pb, AdamSegs sg, double lr, double beta1,
+                                                    double beta2, double eps, double wd,
+                                                    const int64_t* __restrict__ step_ptr) {
+    const AdamScalars s = adam_scalars(lr, beta1, beta2, eps, wd, step_ptr);
+    const int64_t total = sg.pre[sg.n], stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < total; c += stride) {
+        int lo = 0, hi = sg.n - 1;
+        while (lo < hi) {   // last segment with pre[seg] <= c
+            const int mid = (lo + hi + 1) >> 1;
+            if (sg.pre[mid] <= c) lo = mid;
+            else hi = mid - 1;
+        }
+        const int64_t i = sg.start[lo] + 4 * (c - sg.pre[lo]);
+        float4 pv = *(const float4*)(p + i);
+        const float4 gv = *(const float4*)(g + i);
+        float4 mv = *(const float4*)(m + i), vv = *(const float4*)(v + i);
+        pv.x = adam_one(pv.x, gv.x, mv.x, vv.x, s);
+        pv.y = adam_one(pv.y, gv.y, mv.y, vv.y, s);
+        pv.z = adam_one(pv.z, gv.z, mv.z, vv.z, s);
+        pv.w = adam_one(pv.w, gv.w, mv.w, vv.w, s);
+        *(float4*)(p + i) = pv;
+        *(float4*)(m + i) = mv;
+        *(float4*)(v + i) = vv;
+        if (pb) *(uint2*)(pb + i) = make_uint2(pack_bf2(pv.x, pv.y), pack_bf2(pv.z, pv.w));
+    }
+}
+
+extern "C" int cg_adamw_segments(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, const int64_t* segs,
+                                 int nseg, double lr, double beta1, double beta2, double eps, double weight_decay,
+                                 const int64_t* step_ptr, void* stream) {
+    CG_REQUIRE(p && g && m && v && segs && nseg >= 0 && nseg <= ADAM_MAX_SEGS,
+               "cg_adamw_segments: bad arguments (at most %d segments)", ADAM_MAX_SEGS);
+    CG_REQUIRE(((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) == 0 &&
+                   (((uintptr_t)p_bf16) & 7) == 0,
+               "cg_adamw_segments: p, g, m, v must be 16-B aligned, p_bf16 8-B aligned");
+    AdamSegs sg = {};
+    int k = 0;
+    for (int q = 0; q < nseg; ++q) {
+        const int64_t st = segs[2 * q], len = segs[2 * q + 1];
+        CG_REQUIRE(st >= 0 && len >= 0 && st % 4 == 0 && len % 4 == 0,
+                   "cg_adamw_segments: segment starts and lengths must be multiples of 4");
+        if (!len) continue;
+        sg.start[k] = st;
+        sg.pre[k + 1] = sg.pre[k] + len / 4;
+        ++k;
+    }
+    sg.n = k;
+    if (!k) return CG_OK;
+    int grid = ceil_div(sg.pre[k], 256);
+    grid = grid > 8192 ? 8192 : grid;
+    k_adamw_segs<<<grid, 256, 0, (hipStream_t)stream>>>(p, g, m, v, (bf16_t*)p_bf16, sg, lr, beta1, beta2, eps,
+                                                        weight_decay, step_ptr);
+    CG_LAUNCH_CHECK("cg_adamw_segments");
+    return CG_OK;
+}
+
+namespace cg {
+int adamw_job_launch(const AdamJob& j, hipStream_t st) {
+    return adamw_launch(j.p, j.g, j.m, j.v, (uint16_t*)j.pb, 4 * j.n4, j.lr, j.beta1, j.beta2, j.eps, j.wd, j.step, st);
+}
+}  // namespace cg
 
 extern "C" int cg_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, double lr,
                         double beta1, double beta2, double eps, double weight_decay, const int64_t* step_ptr,

@@ -393,17 +393,44 @@ static int current_device() {
 // pending jobs for a launch on stream st of the current device: only a launch on the jobs' own
 // stream and device takes them (a launch on another stream is not ordered after the slab writes).
 // Single-threaded use only, like the rest of the tuning state.
-RedJobs take_pending_reduces(hipStream_t st) {
+static AdamJob g_adam_pending[MAX_ADAM];   // cg_adamw_defer: AdamW jobs for the next launch with free blocks
+static int g_adam_n = 0;
+static hipStream_t g_adam_stream = nullptr;
+static int g_adam_device = -1;
+
+static bool adam_here(hipStream_t st) { return g_adam_n && st == g_adam_stream && current_device() == g_adam_device; }
+
+RedJobs take_pending_reduces(hipStream_t st, bool side_ok) {
     RedJobs r = {};
     if (g_red_pending.n && st == g_red_stream && current_device() == g_red_device) {
-        r = g_red_pending;
+        r.n = g_red_pending.n;
+        for (int q = 0; q < r.n; ++q) r.j[q] = g_red_pending.j[q];
         g_red_pending.n = 0;
+    }
+    if (side_ok && adam_here(st)) {
+        r.na = g_adam_n;
+        for (int q = 0; q < g_adam_n; ++q) r.a[q] = g_adam_pending[q];
+        g_adam_n = 0;
     }
     return r;
 }
 
-bool has_pending_reduces(hipStream_t st) {
-    return g_red_pending.n && st == g_red_stream && current_device() == g_red_device;
+bool has_pending_reduces(hipStream_t st, bool side_ok) {
+    return (g_red_pending.n && st == g_red_stream && current_device() == g_red_device) || (side_ok && adam_here(st));
+}
+
+int adamw_job_launch(const AdamJob& j, hipStream_t st);   // ce_adamw.hip
+
+// pending AdamW jobs as AdamW kernels on their own stream (cg_flush_deferred, a full queue, a job
+// from another stream)
+static void flush_adam() {
+    if (!g_adam_n) return;
+    const int cur = current_device();
+    if (g_adam_device >= 0 && cur != g_adam_device) (void)hipSetDevice(g_adam_device);
+    const int n = g_adam_n;
+    g_adam_n = 0;
+    for (int q = 0; q < n; ++q) (void)adamw_job_launch(g_adam_pending[q], g_adam_stream);
+    if (g_adam_device >= 0 && cur >= 0 && cur != g_adam_device) (void)hipSetDevice(cur);
 }
 
 static void launch_splitk_reduce_job(const RedJob& j, hipStream_t st);
@@ -689,9 +716,38 @@ static void launch_splitk_reduce_job(const RedJob& j, hipStream_t st) {
 }
 }  // namespace cg
 
+extern "C" int cg_adamw_defer(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, double lr,
+                              double beta1, double beta2, double eps, double weight_decay, const int64_t* step_ptr,
+                              void* stream) {
+    using namespace cg;
+    CG_REQUIRE(p && g && m && v && p_bf16 && step_ptr && n > 0 && n % 4 == 0,
+               "cg_adamw_defer: bad arguments (n must be a positive multiple of 4)");
+    CG_REQUIRE(((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) == 0 &&
+                   (((uintptr_t)p_bf16) & 7) == 0,
+               "cg_adamw_defer: p, g, m, v must be 16-B aligned, p_bf16 8-B aligned");
+    hipStream_t st = (hipStream_t)stream;
+    // the region's gradient must be final first: a pending split-K reduce writing into it goes out now
+    for (int q = 0; q < g_red_pending.n; ++q) {
+        const RedJob& J = g_red_pending.j[q];
+        if (J.out < g + n && g < J.out + 4 * J.n4) {
+            flush_pending();
+            break;
+        }
+    }
+    const int dev = current_device();
+    if (g_adam_n == MAX_ADAM || (g_adam_n && (g_adam_stream != st || g_adam_device != dev))) flush_adam();
+    g_adam_stream = st;
+    g_adam_device = dev;
+    g_adam_pending[g_adam_n++] = AdamJob{p, g, m, v, (bf16_t*)p_bf16, n / 4, lr, beta1, beta2, eps, weight_decay,
+                                         step_ptr};
+    CG_LAUNCH_CHECK("cg_adamw_defer");
+    return CG_OK;
+}
+
 extern "C" int cg_flush_deferred(void* stream) {
     (void)stream;   // pending jobs go out on the stream they were enqueued on
     cg::flush_pending();
+    cg::flush_adam();
     cg::flush_partials();
     CG_LAUNCH_CHECK("cg_flush_deferred");
     return CG_OK;

@@ -1,5 +1,6 @@
 // charpt GEMM internals shared by gemm.hip (generic path, dispatch) and gemm_bf16.hip (MFMA path).
 #pragma once
+#include "adamw.h"
 #include "common.h"
 
 namespace cg {
@@ -90,12 +91,32 @@ struct RedJob {
     int bf16;
 };
 constexpr int MAX_RED = 2;
+// An AdamW update of one weight region deferred onto the free blocks of a later part-filling
+// persistent GEMM launch (cg_adamw_defer; the training step's weight matrices once their gradient
+// is final and the backward no longer reads their bf16 shadow): adam_one per element, so the bits
+// of the AdamW kernel.  n4 float4 chunks; p, g, m, v 16-B aligned, pb 8-B aligned.
+struct AdamJob {
+    float* p;
+    const float* g;
+    float* m;
+    float* v;
+    bf16_t* pb;
+    int64_t n4;
+    double lr, beta1, beta2, eps, wd;
+    const int64_t* step;
+};
+constexpr int MAX_ADAM = 4;
 struct RedJobs {
     RedJob j[MAX_RED];
     int n;
+    AdamJob a[MAX_ADAM];
+    int na;   // AdamW jobs: only a launch with free blocks (red_tail `first` > 0) is given any
 };
-RedJobs take_pending_reduces(hipStream_t st);   // gemm.hip: pending jobs (cleared) for a launch on st
-bool has_pending_reduces(hipStream_t st);       // gemm.hip: whether a launch on st would take some
+// gemm.hip: pending jobs (cleared) for a launch on st -- the split-K reduces, and with side_ok (the
+// launch has >= SIDE_MIN free blocks) the AdamW jobs; has_pending_reduces: whether it would take any
+constexpr int SIDE_MIN = 64;
+RedJobs take_pending_reduces(hipStream_t st, bool side_ok = false);
+bool has_pending_reduces(hipStream_t st, bool side_ok = false);
 
 // out[8i .. 8i+7] = sum over slabs k = 0..S-1 (in order, fp32) of bf16 slab elements (one 16-B load
 // per slab), (+ beta out): the deferred tail and the standalone reduce of bf16 slabs (same bits)
@@ -147,6 +168,27 @@ __device__ __forceinline__ void red_tail(const RedJobs& r, int first = 0) {
             fv4* o = (fv4*)(J.out + 4 * i);
             if (J.beta != 0.f) s += J.beta * *o;
             *o = s;
+        }
+    }
+    // AdamW jobs (free blocks only: first > 0): float4 chunk per thread per step, adam_one per element
+    for (int q = 0; q < r.na; ++q) {
+        const AdamJob& J = r.a[q];
+        const AdamScalars sc = adam_scalars(J.lr, J.beta1, J.beta2, J.eps, J.wd, J.step);
+        for (int64_t i = t0; i < J.n4; i += nthr) {
+            fv4 pv = *(const fv4*)(J.p + 4 * i);
+            const fv4 gv = *(const fv4*)(J.g + 4 * i);
+            fv4 mv = *(const fv4*)(J.m + 4 * i), vv = *(const fv4*)(J.v + 4 * i);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float me = mv[e], ve = vv[e];
+                pv[e] = adam_one(pv[e], gv[e], me, ve, sc);
+                mv[e] = me;
+                vv[e] = ve;
+            }
+            *(fv4*)(J.p + 4 * i) = pv;
+            *(fv4*)(J.m + 4 * i) = mv;
+            *(fv4*)(J.v + 4 * i) = vv;
+            *(uint2*)(J.pb + 4 * i) = make_uint2(pack_bf2(pv[0], pv[1]), pack_bf2(pv[2], pv[3]));
         }
     }
 }

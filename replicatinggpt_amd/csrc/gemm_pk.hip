@@ -817,7 +817,7 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
     wait_vm<0>();  // the dummy DMAs past the last K-tile land before the workgroup's LDS is released
     // a deferred split-K reduce of an earlier launch (gemm_common.h): on the blocks beyond the items
     // when the launch has them (launch_p), else in every block's tail
-    if (red.n) red_tail(red, P > nitems ? nitems : 0);
+    if (red.n || red.na) red_tail(red, P > nitems ? nitems : 0);
 }
 
 
@@ -844,9 +844,12 @@ void launch_1(unsigned grid, int64_t M, int64_t N, int64_t K, const bf16_t* A, i
     // cg_set_tuning("gemm_group_pk", g): g row panels per group (1 = row-major); 0 = this choice.
     const int64_t tM = M / BM, tN = N / BN;
     const int gm = g_gemm_group_pk > 0 ? g_gemm_group_pk : (tN > tM ? (int)tM : 0);
+    // AdamW jobs only to a launch with >= SIDE_MIN blocks beyond its items (launch_p gives a
+    // part-filling launch its free slots when work is pending)
+    const bool side_ok = (int64_t)grid - tM * tN * split_k >= SIDE_MIN;
     k_gemm_pk<AT_, BT_, BM, BN, NBUF, EK, BK><<<grid, G::THREADS, G::LDS, st>>>(M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e,
                                                                          split_k, kchunk, ws, g_pk_flags | (gm << 8),
-                                                                         take_pending_reduces(st));
+                                                                         take_pending_reduces(st, side_ok));
 }
 
 // epilogue instantiation: slab for split-K; a fixed kind for the default 128x128 2-stage kernel's
@@ -906,7 +909,7 @@ bool launch_p(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
     if (g_gemm_max_grid > 0 && g_gemm_max_grid < slots) slots = g_gemm_max_grid;
     // a part-filling launch that will take a pending split-K reduce gets the free slots too: those
     // blocks have no items and run the reduce beside the items (red_tail's `first`)
-    const bool side = g_red_side && nitems < slots && has_pending_reduces(st);
+    const bool side = g_red_side && nitems < slots && has_pending_reduces(st, slots - nitems >= SIDE_MIN);
     const unsigned grid = (unsigned)(nitems < slots && !side ? nitems : slots);
 #define FG(AT_, BT_) launch_ek<AT_, BT_, BM, BN, NBUF, BK>(grid, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, kchunk, ws, st)
     // transposed LDS images need a multiple of 128 rows (DmaP, col_swz): other tiles serve only the

@@ -101,8 +101,13 @@ class TrainStep:
     def _fwd_bwd(self):
         _, loss = self.model(self.x, self.y)           # GPT1.py:230
         self.opt.zero_grad(set_to_none=True)           # GPT1.py:231
-        with Fn.DEFER:                                 # split-K reduces in later GEMMs' tails
-            loss.backward(self._one)                   # GPT1.py:232
+        if self.reducer is None:   # one rank: the weight matrices' AdamW beside the backward's GEMMs
+            Fn.EARLY.begin(self.opt)
+        try:
+            with Fn.DEFER:                             # split-K reduces in later GEMMs' tails
+                loss.backward(self._one)               # GPT1.py:232
+        finally:
+            Fn.EARLY.end()
         return loss
 
     def _eager(self):

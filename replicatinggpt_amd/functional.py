@@ -140,6 +140,43 @@ class DeferredReduces:
 
 
 DEFER = DeferredReduces()
+
+
+class EarlyAdam:
+    """The training step's AdamW for the weight matrices, moved into the backward (engine.TrainStep,
+    one rank): once a matrix's gradient is final and the backward reads its bf16 shadow no more --
+    right after its dgrad, whose launch also finishes its split-K reduce -- its update is queued
+    (cg_adamw_defer) for the free blocks of the next part-filling persistent GEMM launch (the N = 384
+    dgrads and the projection weight gradient have 128-224 of 512 slots free), so it runs beside
+    those GEMMs instead of in the optimizer's launch; optim.AdamW.step then updates only the rest
+    (cg_adamw_segments).  Same element arithmetic, so the same bits (tests/test_gpu_train.py).  The
+    step count is incremented when the backward starts.  Off with grad accumulation (beta 1), the
+    side stream, DP, or CHARPT_EARLY_ADAM=0."""
+
+    def __init__(self):
+        self.enabled = os.environ.get("CHARPT_EARLY_ADAM", "1") != "0"
+        self.opt = None
+
+    def begin(self, opt):
+        self.opt = None
+        if not (self.enabled and torch.cuda.is_available() and DEFER.enabled and not SIDE.enabled):
+            return False
+        if not (hasattr(opt, "early_ok") and opt.early_ok()):
+            return False
+        opt.early_begin()
+        self.opt = opt
+        return True
+
+    def region_done(self, region, g, beta):
+        """``region``'s gradient ``g`` (written with ``beta``) is final; its shadow is read no more."""
+        if self.opt is not None and g is not None and beta == 0.0 and g is region.slot:
+            self.opt.early_region(region)
+
+    def end(self):
+        self.opt = None
+
+
+EARLY = EarlyAdam()
 # LayerNorm backward column-sum reduce on the side stream (CHARPT_LN_REDUCE_SIDE=0: in line, for A/B runs)
 LN_REDUCE_SIDE = os.environ.get("CHARPT_LN_REDUCE_SIDE", "1") != "0"
 # FFN b1 gradient fused into the ReLU-backward dgrad epilogue (CHARPT_FUSE_COLPART=0: separate colsum)
@@ -662,6 +699,7 @@ class AttnSublayerFn(torch.autograd.Function):
                                   T, delta)
         else:
             linear_dgrad(dy, wp, do)
+        EARLY.region_done(proj_w, g_pw, beta_pw)   # the projection weight's last read this step
         dqkv = attention_bwd(qkv, B, T, lc.n_head, lc.head_size, o, do, lse, lc.scale, lc.p, lc.seed, lc.rng_call,
                              lc.site, ctx.mask, delta)
         g, beta, f_qkv = qkv_w.grad_target()
@@ -670,6 +708,7 @@ class AttnSublayerFn(torch.autograd.Function):
                 linear_wgrad(dqkv, a, g, beta, g is qkv_w.slot)
         da = torch.empty((B * T, C), dtype=act, device=x2.device)
         linear_dgrad(dqkv, qkv_w.operand(act), da)
+        EARLY.region_done(qkv_w, g, beta)
         dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd, dres=d32, link=ctx.in_link)
         return (dx.view(B, T, C), None, None, None, None, None, None, *f_ln, *f_qkv(), *f_pw(), *f_pb())
 
@@ -740,6 +779,7 @@ class FFNSublayerFn(torch.autograd.Function):
                                       mk, mk.stride(0), part)
         else:
             linear_dgrad(dz2, w2.operand(act), dz1, "relu_bwd", aux=h if bits is None else bits)
+        EARLY.region_done(w2, g_w2, beta_w2)   # W2's gradient is final (its reduce went with this dgrad)
         with SIDE.run(dev, dz1, a, part):
             if g_w1 is not None:
                 linear_wgrad(dz1, a, g_w1, beta_w1, g_w1 is w1.slot)
@@ -751,6 +791,7 @@ class FFNSublayerFn(torch.autograd.Function):
                     colsum_into(dz1, g_b1, beta_b1)
         da = torch.empty((B * T, C), dtype=act, device=x2.device)
         linear_dgrad(dz1, w1.operand(act), da)
+        EARLY.region_done(w1, g_w1, beta_w1)
         dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd, dres=d32, link=ctx.in_link)
         return (dx.view(B, T, C), None, None, None, None, None, None, None, *f_ln, *f_w1(), *f_b1(), *f_w2(),
                 *f_b2())

@@ -6,7 +6,7 @@ current stream (so whole training steps are capturable into a hipGraph).  Ops ar
 the "cuda" (= HIP on ROCm) device only: calling them on CPU tensors raises -- the product has no
 CPU fallback.
 """
-from typing import Optional
+from typing import List, Optional
 
 import torch
 from torch import Tensor
@@ -355,6 +355,24 @@ def adamw(p: Tensor, g: Tensor, m: Tensor, v: Tensor, p_bf16: Optional[Tensor], 
           eps: float, weight_decay: float, step: Tensor) -> None:
     L.check(L.load().cg_adamw(L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), L.ptr(p_bf16), p.numel(), lr, beta1, beta2, eps,
                               weight_decay, L.ptr(step), _s(p)), "adamw")
+
+
+@_op("adamw_defer", ("p", "m", "v", "p_bf16"))
+def adamw_defer(p: Tensor, g: Tensor, m: Tensor, v: Tensor, p_bf16: Tensor, lr: float, beta1: float, beta2: float,
+                eps: float, weight_decay: float, step: Tensor) -> None:
+    """adamw over one region, queued: run by the free blocks of the next part-filling persistent GEMM
+    launch on this stream, or by cg_flush_deferred (csrc gemm.hip cg_adamw_defer); same bits."""
+    L.check(L.load().cg_adamw_defer(L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), L.ptr(p_bf16), p.numel(), lr, beta1,
+                                    beta2, eps, weight_decay, L.ptr(step), _s(p)), "adamw_defer")
+
+
+@_op("adamw_segments", ("p", "m", "v", "p_bf16"))
+def adamw_segments(p: Tensor, g: Tensor, m: Tensor, v: Tensor, p_bf16: Optional[Tensor], segs: List[int],
+                   lr: float, beta1: float, beta2: float, eps: float, weight_decay: float, step: Tensor) -> None:
+    """adamw over [start, start + length) segments of the flat buffers (segs = [s0, n0, s1, n1, ...])."""
+    arr = (L.ctypes.c_int64 * len(segs))(*segs)
+    L.check(L.load().cg_adamw_segments(L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), L.ptr(p_bf16), arr, len(segs) // 2, lr,
+                                       beta1, beta2, eps, weight_decay, L.ptr(step), _s(p)), "adamw_segments")
 
 
 # ---------------------------------------------------------------------------------------

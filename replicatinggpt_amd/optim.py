@@ -19,6 +19,7 @@ class AdamW(torch.optim.Optimizer):
         self._m = self._v = None
         self._step_t = None
         self._psteps = None   # per-parameter step counts, once a step skipped some parameter
+        self._early = None    # flat (offset, n) ranges updated early this step (functional.EARLY)
 
     # the model whose flat store holds these parameters is found from the parameters, so
     # ``AdamW(m.parameters(), lr=5e-1)`` works exactly as GPT1.py:218 writes it
@@ -57,6 +58,44 @@ class AdamW(torch.optim.Optimizer):
             if self._psteps is not None:
                 self._psteps = self._psteps.to(st.master.device)
 
+    # -- early updates (functional.EarlyAdam, engine.TrainStep) -----------------------------------
+    def _args(self):
+        grp = self.param_groups[0]
+        b1, b2 = grp["betas"]
+        return (float(grp["lr"]), float(b1), float(b2), float(grp["eps"]), float(grp["weight_decay"]))
+
+    def early_ok(self):
+        """One step count for every parameter, all of them trained, flat buffers on the GPU."""
+        self._ensure()
+        return (self._psteps is None and self._store.master.is_cuda and
+                all(p.requires_grad for g in self.param_groups for p in g["params"]))
+
+    def early_begin(self):
+        """The step count for this step, on the device, before any early update reads it."""
+        ops.counter_add(self._step_t, 1)
+        self._early = []
+
+    def early_region(self, region):
+        """Queue the update of one packed region whose gradient is final (cg_adamw_defer)."""
+        st = self._store
+        off = (region.slot.data_ptr() - st.grad.data_ptr()) // st.grad.element_size()
+        n = region.slot.numel()
+        if off < 0 or off + n > st.numel or n % 4 or off % 4:
+            return
+        ops.adamw_defer(st.master[off:off + n], st.grad[off:off + n], self._m[off:off + n], self._v[off:off + n],
+                        st.shadow[off:off + n], *self._args(), self._step_t)
+        self._early.append((off, n))
+
+    def _rest_segments_of(self, early):
+        segs, pos = [], 0
+        for off, n in sorted(early):
+            if off > pos:
+                segs += [pos, off - pos]
+            pos = max(pos, off + n)
+        if pos < self._store.numel:
+            segs += [pos, self._store.numel - pos]
+        return segs
+
     def zero_grad(self, set_to_none=True):
         for g in self.param_groups:
             for p in g["params"]:
@@ -87,7 +126,21 @@ class AdamW(torch.optim.Optimizer):
                 if p.grad.data_ptr() != slot.data_ptr():
                     slot.copy_(p.grad)
         args = (float(grp["lr"]), float(b1), float(b2), float(grp["eps"]), float(grp["weight_decay"]))
-        if not missing and self._psteps is None:
+        if self._early is not None:
+            # the step count was advanced when the backward began and the weight matrices were
+            # updated beside the backward's GEMMs (functional.EarlyAdam): the rest, same arithmetic
+            early, self._early = self._early, None
+            if missing:
+                raise RuntimeError("charpt AdamW: a parameter had no gradient in a step with early updates")
+            segs = self._rest_segments_of(early)
+            if len(segs) // 2 <= 64:
+                ops.adamw_segments(st.master, st.grad, self._m, self._v, st.shadow, segs, *args, self._step_t)
+            else:
+                for i in range(0, len(segs), 2):
+                    a, n = segs[i], segs[i + 1]
+                    ops.adamw(st.master[a:a + n], st.grad[a:a + n], self._m[a:a + n], self._v[a:a + n],
+                              st.shadow[a:a + n], *args, self._step_t)
+        elif not missing and self._psteps is None:
             # the training path: every parameter has a gradient, one launch over the flat buffers
             ops.counter_add(self._step_t, 1)
             ops.adamw(st.master, st.grad, self._m, self._v, st.shadow, *args, self._step_t)

@@ -84,6 +84,38 @@ def test_deferred_splitk_reduces_bit_identical():
         assert torch.equal(r[1], runs[0][1]) and torch.equal(r[2], runs[0][2])
 
 
+def test_early_adamw_bit_identical():
+    """functional.EarlyAdam: the weight matrices' AdamW queued right after their last backward use
+    and run on the free blocks of later part-filling GEMM launches (cg_adamw_defer), the rest by
+    cg_adamw_segments -- losses, weights, moments and step count bit for bit the one-launch AdamW
+    (C2-width model: split-K weight gradients, 128-block dgrads), graph replay and eager; the
+    optimizer's own step with the early path off matches too (GPT1.py:232-233)."""
+    from replicatinggpt_amd import functional as Fn
+    from replicatinggpt_amd.engine import TrainStep
+    cfg = _cfg(block_size=256, n_embd=384, n_head=6, n_layers=2, batch_size=64)
+    runs = []
+    saved = Fn.EARLY.enabled
+    try:
+        for early, graph in ((False, True), (True, True), (True, False)):
+            Fn.EARLY.enabled = early
+            m, opt, s = _setup(cfg)
+            st = TrainStep(m, opt, s, use_graph=graph)
+            st.capture(restore=True)
+            losses = [float(st.step().detach()) for _ in range(3)]
+            torch.cuda.synchronize()
+            runs.append((losses, m.flat.master.detach().cpu().clone(), opt._m.cpu().clone(), opt._v.cpu().clone(),
+                         int(opt._step_t.item()), m.flat.shadow.view(torch.int16).cpu().clone()))
+    finally:
+        Fn.EARLY.enabled = saved
+    for r in runs[1:]:
+        assert r[0] == runs[0][0]
+        for a, b in zip(r[1:], runs[0][1:]):
+            if isinstance(a, torch.Tensor):
+                assert torch.equal(a, b)
+            else:
+                assert a == b
+
+
 def test_side_stream_modes_bit_identical():
     """The side stream (weight gradients, column sums and keep bits forked off the dgrad chain) only
     changes scheduling: graph-replayed steps with it on, keep-bits-only and off give the same losses
