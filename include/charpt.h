@@ -280,8 +280,9 @@ int cg_decode_sample(const float* logits, int64_t ldl, int64_t V, int64_t B, int
 int cg_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, double lr, double beta1,
              double beta2, double eps, double weight_decay, const int64_t* step_ptr, void* stream);
 /* the same update for [0, n) of one region, deferred: run by the free blocks of the next persistent
-   GEMM launch on `stream` that has >= 64 of them (a part-filling launch), else by cg_flush_deferred
-   as a cg_adamw launch -- same bits either way.  The gradient must be final in stream order (a
+   GEMM launch on `stream` that has >= 64 of them (a part-filling launch; at most 4 jobs per launch,
+   oldest first), else by cg_flush_deferred -- the jobs left, when they are slices of one set of
+   buffers, as one segmented launch -- same bits either way.  The gradient must be final in stream order (a
    pending split-K reduce writing into g is launched first) and nothing launched before the flush may
    read p / p_bf16 / m / v.  n % 4 == 0, p, g, m, v 16-B and p_bf16 8-B aligned. */
 int cg_adamw_defer(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, double lr,

@@ -229,9 +229,22 @@ __global__ __launch_bounds__(256) void k_adamw_segs(float* __restrict__ p, const
     }
 }
 
+namespace cg {
+int adamw_segments_launch(float* p, const float* g, float* m, float* v, bf16_t* pb, const int64_t* segs, int nseg,
+                          double lr, double beta1, double beta2, double eps, double wd, const int64_t* step,
+                          hipStream_t st);
+}
+
 extern "C" int cg_adamw_segments(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, const int64_t* segs,
                                  int nseg, double lr, double beta1, double beta2, double eps, double weight_decay,
                                  const int64_t* step_ptr, void* stream) {
+    return cg::adamw_segments_launch(p, g, m, v, (bf16_t*)p_bf16, segs, nseg, lr, beta1, beta2, eps, weight_decay,
+                                     step_ptr, (hipStream_t)stream);
+}
+
+int cg::adamw_segments_launch(float* p, const float* g, float* m, float* v, bf16_t* p_bf16, const int64_t* segs,
+                              int nseg, double lr, double beta1, double beta2, double eps, double weight_decay,
+                              const int64_t* step_ptr, hipStream_t stream) {
     CG_REQUIRE(p && g && m && v && segs && nseg >= 0 && nseg <= ADAM_MAX_SEGS,
                "cg_adamw_segments: bad arguments (at most %d segments)", ADAM_MAX_SEGS);
     CG_REQUIRE(((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) == 0 &&

@@ -393,7 +393,10 @@ static int current_device() {
 // pending jobs for a launch on stream st of the current device: only a launch on the jobs' own
 // stream and device takes them (a launch on another stream is not ordered after the slab writes).
 // Single-threaded use only, like the rest of the tuning state.
-static AdamJob g_adam_pending[MAX_ADAM];   // cg_adamw_defer: AdamW jobs for the next launch with free blocks
+// cg_adamw_defer: AdamW jobs for the next launches with free blocks (MAX_ADAM per launch, oldest
+// first); what no such launch took goes out at the flush as one segmented AdamW launch
+constexpr int MAX_ADAM_PENDING = 64;
+static AdamJob g_adam_pending[MAX_ADAM_PENDING];
 static int g_adam_n = 0;
 static hipStream_t g_adam_stream = nullptr;
 static int g_adam_device = -1;
@@ -408,9 +411,10 @@ RedJobs take_pending_reduces(hipStream_t st, bool side_ok) {
         g_red_pending.n = 0;
     }
     if (side_ok && adam_here(st)) {
-        r.na = g_adam_n;
-        for (int q = 0; q < g_adam_n; ++q) r.a[q] = g_adam_pending[q];
-        g_adam_n = 0;
+        r.na = g_adam_n < MAX_ADAM ? g_adam_n : MAX_ADAM;
+        for (int q = 0; q < r.na; ++q) r.a[q] = g_adam_pending[q];
+        for (int q = r.na; q < g_adam_n; ++q) g_adam_pending[q - r.na] = g_adam_pending[q];
+        g_adam_n -= r.na;
     }
     return r;
 }
@@ -420,16 +424,38 @@ bool has_pending_reduces(hipStream_t st, bool side_ok) {
 }
 
 int adamw_job_launch(const AdamJob& j, hipStream_t st);   // ce_adamw.hip
+int adamw_segments_launch(float* p, const float* g, float* m, float* v, bf16_t* pb, const int64_t* segs, int nseg,
+                          double lr, double beta1, double beta2, double eps, double wd, const int64_t* step,
+                          hipStream_t st);   // ce_adamw.hip
 
-// pending AdamW jobs as AdamW kernels on their own stream (cg_flush_deferred, a full queue, a job
-// from another stream)
+// pending AdamW jobs on their own stream (cg_flush_deferred, a full queue, a job from another
+// stream): slices of one set of flat buffers with one set of hyperparameters (the training step's
+// weight matrices) as ONE segmented launch, anything else job by job
 static void flush_adam() {
     if (!g_adam_n) return;
     const int cur = current_device();
     if (g_adam_device >= 0 && cur != g_adam_device) (void)hipSetDevice(g_adam_device);
     const int n = g_adam_n;
     g_adam_n = 0;
-    for (int q = 0; q < n; ++q) (void)adamw_job_launch(g_adam_pending[q], g_adam_stream);
+    const AdamJob* J = g_adam_pending;
+    int b = 0;   // the job with the lowest address is the segments' base
+    for (int q = 1; q < n; ++q)
+        if (J[q].p < J[b].p) b = q;
+    bool one = n > 1 && n <= 64;
+    int64_t segs[2 * MAX_ADAM_PENDING];
+    for (int q = 0; q < n && one; ++q) {
+        const int64_t d = J[q].p - J[b].p;
+        one = J[q].g - J[b].g == d && J[q].m - J[b].m == d && J[q].v - J[b].v == d && J[q].pb - J[b].pb == d &&
+              J[q].lr == J[b].lr && J[q].beta1 == J[b].beta1 && J[q].beta2 == J[b].beta2 && J[q].eps == J[b].eps &&
+              J[q].wd == J[b].wd && J[q].step == J[b].step;
+        segs[2 * q] = d;
+        segs[2 * q + 1] = 4 * J[q].n4;
+    }
+    if (one)
+        (void)adamw_segments_launch(J[b].p, J[b].g, J[b].m, J[b].v, J[b].pb, segs, n, J[b].lr, J[b].beta1, J[b].beta2,
+                                    J[b].eps, J[b].wd, J[b].step, g_adam_stream);
+    else
+        for (int q = 0; q < n; ++q) (void)adamw_job_launch(J[q], g_adam_stream);
     if (g_adam_device >= 0 && cur >= 0 && cur != g_adam_device) (void)hipSetDevice(cur);
 }
 
@@ -735,7 +761,7 @@ extern "C" int cg_adamw_defer(float* p, const float* g, float* m, float* v, uint
         }
     }
     const int dev = current_device();
-    if (g_adam_n == MAX_ADAM || (g_adam_n && (g_adam_stream != st || g_adam_device != dev))) flush_adam();
+    if (g_adam_n == MAX_ADAM_PENDING || (g_adam_n && (g_adam_stream != st || g_adam_device != dev))) flush_adam();
     g_adam_stream = st;
     g_adam_device = dev;
     g_adam_pending[g_adam_n++] = AdamJob{p, g, m, v, (bf16_t*)p_bf16, n / 4, lr, beta1, beta2, eps, weight_decay,
