@@ -106,6 +106,10 @@ class TrainStep:
         try:
             with Fn.DEFER:                             # split-K reduces in later GEMMs' tails
                 loss.backward(self._one)               # GPT1.py:232
+        except BaseException:
+            if hasattr(self.opt, "_early"):
+                self.opt._early = None                 # a failed backward leaves no half-done step behind
+            raise
         finally:
             Fn.EARLY.end()
         return loss
