@@ -290,8 +290,9 @@ def kernel_census(cfg, Bsz, T, dev):
         start of the forward, overlapped with the embedding / LN / QKV kernels, and is reported on its
         own as attention_dropmask, VALU-bound decisions/s) / bwd: causal algorithmic FLOPs
         fwd 4*B*H*(T(T+1)/2)*D, bwd 2x fwd (S recompute not counted) vs the bf16 MFMA peak, and their
-        algorithmic HBM bytes (fwd: q,k,v read + o written + lse + FWD keep words; bwd: q,k,v,o,dO
-        read + dq,dk,dv written + lse, delta + both keep-word halves) vs the HBM peak -- at T = 256
+        algorithmic HBM bytes (fwd: q,k,v read + o written + lse + FWD keep words; bwd: q,k,v,dO
+        (+ o unless delta comes precomputed, as in the C2 step) read + dq,dk,dv written + lse, delta +
+        both keep-word halves) vs the HBM peak -- at T = 256
         the attention kernels are memory/latency-bound (DESIGN §4);
       LayerNorm fwd: M*C*(4 read + 2 write) B; LayerNorm bwd (dy bf16, x, residual grad, dx, the
         consumer's dropout-applied bf16 copy): M*C*(2+4+4+4+2) B; AdamW: 30 B/param (p, g, m, v
@@ -317,12 +318,16 @@ def kernel_census(cfg, Bsz, T, dev):
         ops.attn_dropmask(Bsz, H, T, p, 1, call, 0, mask)
     t_f = _time_ms(lambda: ops.attn_fwd(qkv, Bsz, T, H, D, 0, C, 2 * C, qkv.stride(0), o, C, lse, scale, p, 1, call,
                                         0, mask if p > 0 else None, p > 0))
+    # the step's form: delta = rowsum(dO * O) from the projection dgrad's epilogue where it applies
+    # (functional.rowdot_ok: T <= 256, head 64), so the backward reads delta instead of O
+    din = Fn.ROWDOT and D == 64 and T <= 256 and T % 64 == 0
+    delta = ((do.float() * o.float()).view(Bsz, T, H, D).sum(-1).permute(0, 2, 1).contiguous() if din else None)
     t_b = _time_ms(lambda: Fn.attention_bwd(qkv, Bsz, T, H, D, o, do, lse, scale, p, 1, call, 0,
-                                            mask if p > 0 else None))
+                                            mask if p > 0 else None, delta))
     fl = 4.0 * Bsz * H * (T * (T + 1) / 2) * D
     stat = Bsz * H * T * 4
     fbytes = 4 * M * C * 2 + stat + mbytes // 2
-    bbytes = 8 * M * C * 2 + 2 * stat + mbytes
+    bbytes = (7 if din else 8) * M * C * 2 + 2 * stat + mbytes
     for name, t, f, byts in (("attention_fwd", t_f, fl, fbytes), ("attention_bwd", t_b, 2 * fl, bbytes)):
         tf = f / (t * 1e-3) / 1e12
         gbs = byts / (t * 1e-3) / 1e9
