@@ -380,6 +380,7 @@ int g_gemm_group_pk = 0;
 int g_gemm_n96 = 1;       // cg_set_tuning("gemm_n96"): 128x96 tiles for the part-filling fp32 residual forwards (gemm_pk.hip launch_n96)
 int g_defer_splitk = 0;   // cg_set_tuning("defer_splitk"): split-K reduces of fp32 STORE outputs deferred
 int g_slab_bf16 = 0;      // cg_set_tuning("slab_bf16"): split-K partial sums of fp32 STORE outputs as bf16 slabs
+int g_adam_per_launch = 0;   // cg_set_tuning("adam_per_launch"): AdamW jobs one launch's free blocks take (0 = MAX_ADAM)
 int g_red_side = 1;       // cg_set_tuning("red_side"): a part-filling persistent launch takes a pending reduce on extra blocks
 RedJobs g_red_pending = {};
 hipStream_t g_red_stream = nullptr;   // the stream the pending jobs were enqueued on
@@ -411,7 +412,8 @@ RedJobs take_pending_reduces(hipStream_t st, bool side_ok) {
         g_red_pending.n = 0;
     }
     if (side_ok && adam_here(st)) {
-        r.na = g_adam_n < MAX_ADAM ? g_adam_n : MAX_ADAM;
+        const int cap = g_adam_per_launch > 0 && g_adam_per_launch < MAX_ADAM ? g_adam_per_launch : MAX_ADAM;
+        r.na = g_adam_n < cap ? g_adam_n : cap;
         for (int q = 0; q < r.na; ++q) r.a[q] = g_adam_pending[q];
         for (int q = r.na; q < g_adam_n; ++q) g_adam_pending[q - r.na] = g_adam_pending[q];
         g_adam_n -= r.na;
@@ -531,6 +533,10 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     }
     if (!strcmp(key, "defer_splitk")) {   // off: pending reduces are flushed on the caller's next cg_flush_deferred
         g_defer_splitk = value;
+        return CG_OK;
+    }
+    if (!strcmp(key, "adam_per_launch")) {
+        g_adam_per_launch = value;
         return CG_OK;
     }
     if (!strcmp(key, "red_side")) {
