@@ -144,15 +144,9 @@ def census_op(name, M, N, K, at, bt, kind, dev, p=0.2, cold=False):
         ctr[0] += 1
         A, B, out = st["A"], st["B"], st["out"]
         if kind == "wgrad":   # the step's slot weight gradients: bf16 split-K slabs (functional.linear_wgrad)
-            slab16 = Fn.SLAB_BF16 and split > 1
-            if slab16:
-                L.check(lib.cg_set_tuning(b"slab_bf16", 1), "slab_bf16")
-            try:
-                ops.gemm(A, B, out, True, bool(at), bool(bt), M, N, K, lda, ldb, N, 0, None, None, 0, None, 0,
-                         0.0, 0, None, 0, 0.0, split, st.get("ws"))
-            finally:
-                if slab16:
-                    L.check(lib.cg_set_tuning(b"slab_bf16", 0), "slab_bf16")
+            flags = L.GEMM_SLAB_BF16 if Fn.SLAB_BF16 and split > 1 else 0
+            ops.gemm(A, B, out, True, bool(at), bool(bt), M, N, K, lda, ldb, N, 0, None, None, 0, None, 0,
+                     0.0, 0, None, 0, 0.0, split, st.get("ws"), flags)
         elif kind == "store_rowdot" and rowdot:
             ops.gemm_store_rowdot(A, B, out, M, N, K, lda, ldb, N, st["o"], N, rowdot_T, st["delta"])
         elif kind in ("store", "store_rowdot"):   # store_rowdot unsupported: the step's plain dgrad
@@ -474,6 +468,75 @@ def _log(msg):
     print(f"[bench {time.perf_counter() - _T_START:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """``bench.py --gpus N`` started without a launcher: run N ranks of this same command under
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) as a CHILD process -- this
+    process has touched no GPU and execs nothing -- and return the worst rank's exit code."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    _log(f"launching {n} ranks: {' '.join(cmd[1:])}")
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
+def dry_run(args, world, rank, local):
+    """The N-rank launch path without a GPU (gloo on CPU): every rank builds the data-parallel
+    sampler and the bucketed gradient reducer exactly as the GPU run does, times ``--steps`` steps of
+    (get_batch offsets draw, fake gradient, all-reduce AVG) between barriers, takes the max over ranks
+    and rank 0 prints the one JSON line -- so the launcher, the rank/rendezvous plumbing, the sampler
+    slicing and the single-line output contract are testable on the build container."""
+    from replicatinggpt_amd import PRESETS
+    from replicatinggpt_amd.data import BatchSampler, TokenStream
+    from replicatinggpt_amd.engine import GradReducer
+    if world > 1:
+        dist.init_process_group("gloo")
+    cfg = PRESETS[args.config]
+    Bsz, T = args.batch or cfg.batch_size, cfg.block_size
+    sampler = BatchSampler(TokenStream.synthetic(n_tokens=1 << 16), T, Bsz, world_size=world, rank=rank,
+                           generator=torch.Generator().manual_seed(cfg.seed))
+    grad = torch.zeros(1 << 12)
+    red = GradReducer(grad, bucket_bytes=4096)
+    first = []
+    for i in range(args.warmup + args.steps):
+        if i == args.warmup:
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+        ix = sampler.draw_ix("train")
+        if not first:
+            first = ix[:4].tolist()
+        grad.fill_(float(rank + 1))
+        red.all_reduce()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed])
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    print(f"[rank {rank} local {local} world {world}] first offsets {first} grad {float(grad[0])}",
+          file=sys.stderr, flush=True)
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (no GPU): launcher + sampler + gradient all-reduce", "value": None,
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed / max(1, args.steps) * 1e3, 4), "dry_run": True,
+                          "config": {"workload": args.config, "global_batch": Bsz * world, "seq_len": T,
+                                     "parallelism": f"dp{world}", "world_size": world,
+                                     "backend": "gloo" if world > 1 else None}}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -490,11 +553,20 @@ def main():
     ap.add_argument("--seg-layers", type=int, default=1,
                     help="DP: blocks per backward graph segment (gradient all-reduce overlaps the next segment; "
                          "1 = the smallest exposed last segment, block 0 + embeddings: DESIGN.md section 6)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: exercise the N-rank launch, sampler slicing and reducer on gloo")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # started as `python bench.py --gpus N`: become the launcher of N ranks (before any GPU call)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
+    if args.dry_run:
+        return dry_run(args, world, rank, local)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -568,6 +640,10 @@ def main():
             "config": {"workload": f"{args.config}: char-GPT {cfg.n_layers}L/{cfg.n_head}H/{cfg.n_embd}d, "
                                    f"block {T}, batch {Bsz}/GPU, dropout {cfg.dropout}, AdamW, full train step",
                        "global_batch": Bsz * world, "seq_len": T, "parallelism": f"dp{world}",
+                       "world_size": dist.get_world_size() if dist.is_initialized() else 1,
+                       "backend": f"{dist.get_backend()} (RCCL)" if dist.is_initialized() else None,
+                       "step_path": ("segmented backward graphs + bucketed all-reduce (DP)" if step.overlap
+                                     else "single graph (fwd + bwd + AdamW)"),
                        "graph": step.g_fb is not None or bool(step.g_seg),
                        "grad_allreduce": (f"RCCL AVG overlapped: {len(step.ranges)} backward segments"
                                           if step.overlap else ("RCCL AVG after backward" if world > 1 else None))},

@@ -13,14 +13,19 @@
  *     owns every buffer; the library never allocates, frees or synchronises the host.
  *   - every function is stream-ordered on `stream` (a hipStream_t, passed as void*), so it is
  *     capturable into a hipGraph.
- *   - state: the library keeps no per-call state, with two process-wide exceptions -- the
- *     cg_set_tuning knobs and the deferred-work queues they enable ("defer_splitk": a split-K
- *     weight-gradient reduce left for the next persistent GEMM on the same stream or
- *     cg_flush_deferred; "defer_partials": column-sum reduces queued for one launch at
- *     cg_flush_deferred; cg_adamw_defer: AdamW region updates queued for the free blocks of a
- *     later part-filling GEMM launch or cg_flush_deferred).  Those are not thread-safe: set knobs, enable deferral and make the
- *     calls it affects from one host thread.  Every other entry point is
- *     reentrant; cg_last_error_string() is per thread.
+ *   - state: the library keeps no per-call state except the DEFERRED WORK below and the
+ *     cg_set_tuning knobs, which only select kernels / schedules for A/B and test runs (never the
+ *     numerics of a call: precision and deferral are per-call flags).
+ *   - deferred work (per stream): a call asks for it explicitly -- cg_epilogue_t.flags
+ *     CG_GEMM_DEFER_REDUCE (a split-K weight-gradient reduce left pending), cg_adamw_defer, and the
+ *     CG_DEFER flag of cg_reduce_rows_ex / cg_layernorm_bwd_reduce_ex / cg_head_bwd_ex (column-sum
+ *     reduces queued for one multi-job launch).  The queue is that of the call's (device, stream):
+ *     only a later persistent GEMM launch on the SAME stream takes its jobs (in its tail / free
+ *     blocks), and cg_flush_deferred(stream) launches the rest on that stream.  A mutex guards the
+ *     queue registry, so host threads that each drive their own stream are safe; two threads
+ *     sharing one stream must order their calls themselves, as with any stream.  Until the flush,
+ *     the caller keeps every queued job's workspace alive and reads none of its outputs.
+ *   - cg_last_error_string() is per thread.
  *   - return CG_OK (0) or an error code; cg_last_error_string() gives the message.
  *   - dtype codes: CG_F32 = 0 (float), CG_BF16 = 1 (bfloat16 bits, RNE rounding).
  *   - dropout: Philox4x32-10 counter RNG, spec in oracle/philox.py and DESIGN.md; the stream id
@@ -76,12 +81,28 @@ typedef struct {
                                  column sums of each 64-row block of the output (of its bf16-
                                  rounded values, as cg_colsum would see them), [M/64][N] -- the consumer's bias-gradient partials,
                                  folded by cg_reduce_rows.  NULL: none.                     */
+    int flags;                /* CG_GEMM_* below; 0 = plain (fp32 slabs, reduce in this call) */
 } cg_epilogue_t;
+
+/* cg_epilogue_t.flags -- split-K (split_k > 1) fp32 CG_EPI_STORE outputs (the weight gradients):
+   CG_GEMM_SLAB_BF16     each split's partial sum is stored as a bf16 slab (rounded once, 2^-9
+                         relative) and the slabs are summed in split order in fp32: half the slab
+                         bytes.  Applies where the 128x128 persistent kernel runs the product (bf16
+                         operands, vectorisable output); elsewhere the call uses fp32 slabs.
+   CG_GEMM_DEFER_REDUCE  the slab reduce may stay pending on the stream's deferral queue (above):
+                         the next persistent bf16 GEMM on the stream sums it in its tail, or
+                         cg_flush_deferred(stream).  Keep the workspace alive until then.  Calls the
+                         deferral does not apply to (slab sets > 40 MB) reduce now.                */
+enum { CG_GEMM_SLAB_BF16 = 1, CG_GEMM_DEFER_REDUCE = 2 };
+/* flags of the _ex column-sum reduces: queue on the stream's deferral queue instead of launching */
+enum { CG_DEFER = 1 };
 
 const char* cg_last_error_string(void);
 int cg_version(void);
-/* process-wide tuning knobs (benchmarking / autotuning): "gemm_variant" 0 = automatic,
-   1 = 128x128 tile, 2 = 128x128 two K-tiles in flight, 3 = 256x128, 4 = 256x128 two in flight. */
+/* process-wide A/B and test knobs (kernel / schedule selection, never a call's numerics): e.g.
+   "gemm_variant" 0 = automatic, 2 = register-staged, 9 = persistent 128x128, 24 = 8-wave 256x256,
+   99 = generic; "red_side", "adam_per_launch", "gemm_n96", "ln_nt", ... (gemm.hip cg_set_tuning).
+   Set them before the calls they affect, from one thread.                                       */
 int cg_set_tuning(const char* key, int value);
 int cg_device_info(int* n_cu, int* arch_major, int* arch_minor);
 
@@ -144,6 +165,10 @@ int cg_layernorm_bwd_rows(const void* dy, int dy_dtype, const float* x, const fl
                           void* workspace, int64_t rows, int64_t C, void* stream);
 int cg_layernorm_bwd_reduce(const void* workspace, int64_t rows, int64_t C, int lp_colsum_partials, float* dw,
                             float* db, float* lp_colsum, int accumulate, int colsum_accumulate, void* stream);
+/* the same with flags: CG_DEFER queues the reduce on the stream's deferral queue                */
+int cg_layernorm_bwd_reduce_ex(const void* workspace, int64_t rows, int64_t C, int lp_colsum_partials, float* dw,
+                               float* db, float* lp_colsum, int accumulate, int colsum_accumulate, int flags,
+                               void* stream);
 
 /* ---- GEMM (nn.Linear fwd/dgrad/wgrad: GPT1.py:111-112,121,136,143,145,184) -------------
    C[m,n] = epilogue( sum_k A(m,k) * B(n,k) )
@@ -166,14 +191,19 @@ int cg_gemm_relu_bits_supported(int a_trans, int b_trans, int64_t M, int64_t N, 
    problem under the current dispatch, else 0 -- the attention backward then computes delta itself. */
 int cg_gemm_rowdot_supported(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                              int64_t ldc);
-/* cg_set_tuning("defer_splitk", 1): a split-K cg_gemm with an fp32 CG_EPI_STORE output (the weight
-   gradients) leaves its slab reduce pending -- its workspace must stay allocated -- and the next
-   persistent bf16 GEMM launch on the stream performs it in its tail (same summation order, same
-   bits); only a launch on the stream the reduce was enqueued on takes it.  cg_flush_deferred
-   launches whatever is still pending (on that stream); call it before reading the outputs. */
+/* launch everything still pending on `stream`'s deferral queue (split-K reduces, AdamW jobs, the
+   queued column-sum reduces as one launch) on that stream; call it before reading the outputs.
+   Same summation order as the in-call forms, so the same bits.                                  */
 int cg_flush_deferred(void* stream);
+/* drop everything pending on `stream`'s queue without launching it (a failed backward: its
+   gradients are abandoned).  *adam_jobs_taken (may be NULL) = the AdamW jobs GEMM launches
+   already took from this queue since its last flush / discard -- updates that have run or will
+   run; 0 means no parameter has been touched.                                                   */
+int cg_discard_deferred(void* stream, int* adam_jobs_taken);
 /* out[n] (=|+=) sum_r part[r*N + n] over rows r in order (fixed order: deterministic)          */
 int cg_reduce_rows(const float* part, int64_t rows, int64_t N, float* out, int accumulate, void* stream);
+int cg_reduce_rows_ex(const float* part, int64_t rows, int64_t N, float* out, int accumulate, int flags,
+                      void* stream);
 int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
             const void* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const cg_epilogue_t* epi, int split_k,
             void* workspace, void* stream);
@@ -250,6 +280,10 @@ int cg_head_fwd(const void* a, const void* wpad, int64_t wpad_rows, const float*
 int cg_head_bwd(const float* logits, const float* lse, const int64_t* targets, const float* g_loss, float g_mult,
                 const float* g_logits, void* dl, int64_t ld_dl, float* db, int db_accumulate, void* workspace,
                 int64_t M, int64_t V, void* stream);
+/* the same with flags: CG_DEFER queues the db column-sum reduce on the stream's deferral queue  */
+int cg_head_bwd_ex(const float* logits, const float* lse, const int64_t* targets, const float* g_loss, float g_mult,
+                   const float* g_logits, void* dl, int64_t ld_dl, float* db, int db_accumulate, void* workspace,
+                   int64_t M, int64_t V, int flags, void* stream);
 
 /* ---- batched decode for generate() (GPT1.py:196-212; replicatinggpt_amd/decode.py) ----------
    len_dev: device int64 = current sequence length (tokens in idx rows, row stride ld).          */
@@ -279,8 +313,8 @@ int cg_decode_sample(const float* logits, int64_t ldl, int64_t V, int64_t B, int
    p_bf16: optional bf16 shadow written after the update (GEMM operands).                    */
 int cg_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, double lr, double beta1,
              double beta2, double eps, double weight_decay, const int64_t* step_ptr, void* stream);
-/* the same update for [0, n) of one region, deferred: run by the free blocks of the next persistent
-   GEMM launch on `stream` that has >= 64 of them (a part-filling launch; at most 4 jobs per launch,
+/* the same update for [0, n) of one region, deferred on `stream`'s queue: run by the free blocks of
+   the next persistent GEMM launch on `stream` that has >= 64 of them (a part-filling launch; at most 4 jobs per launch,
    oldest first), else by cg_flush_deferred -- the jobs left, when they are slices of one set of
    buffers, as one segmented launch -- same bits either way.  The gradient must be final in stream order (a
    pending split-K reduce writing into g is launched first) and nothing launched before the flush may

@@ -16,6 +16,8 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "charpt.h")
 CG_F32, CG_BF16, CG_BITS = 0, 1, 2
 EPI_STORE, EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_RESID, EPI_BIAS_DROP_RESID, EPI_RELU_BWD = range(6)
 EPI_STORE_ROWDOT = 7
+GEMM_SLAB_BF16, GEMM_DEFER_REDUCE = 1, 2   # cg_epilogue_t.flags (per call: precision / deferral)
+DEFER = 1                                  # flags of the _ex column-sum reduces
 
 c_i64, c_int, c_dbl, c_flt, c_u64, P = ctypes.c_int64, ctypes.c_int, ctypes.c_double, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p
 
@@ -23,7 +25,7 @@ c_i64, c_int, c_dbl, c_flt, c_u64, P = ctypes.c_int64, ctypes.c_int, ctypes.c_do
 class Epilogue(ctypes.Structure):
     _fields_ = [("kind", c_int), ("bias", P), ("resid", P), ("ld_resid", c_i64), ("aux", P), ("aux_dtype", c_int),
                 ("ld_aux", c_i64), ("dropout_p", c_dbl), ("seed", c_u64), ("rng_call", P), ("site", c_int),
-                ("beta", c_flt), ("colpart", P)]
+                ("beta", c_flt), ("colpart", P), ("flags", c_int)]
 
 
 _SIGS = {
@@ -49,12 +51,15 @@ _SIGS = {
     "cg_layernorm_bwd_rows": (c_int, [P, c_int, P, P, P, P, P, P, P, c_dbl, c_u64, P, c_int, c_int, P, c_i64, c_i64,
                                       P]),
     "cg_layernorm_bwd_reduce": (c_int, [P, c_i64, c_i64, c_int, P, P, P, c_int, c_int, P]),
+    "cg_layernorm_bwd_reduce_ex": (c_int, [P, c_i64, c_i64, c_int, P, P, P, c_int, c_int, c_int, P]),
     "cg_gemm_workspace": (c_i64, [c_i64, c_i64, c_int]),
     "cg_gemm_colpart_supported": (c_int, [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64]),
     "cg_gemm_relu_bits_supported": (c_int, [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64]),
     "cg_gemm_rowdot_supported": (c_int, [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64]),
     "cg_flush_deferred": (c_int, [P]),
+    "cg_discard_deferred": (c_int, [P, P]),
     "cg_reduce_rows": (c_int, [P, c_i64, c_i64, P, c_int, P]),
+    "cg_reduce_rows_ex": (c_int, [P, c_i64, c_i64, P, c_int, c_int, P]),
     "cg_gemm": (c_int, [c_int, c_int, c_int, c_i64, c_i64, c_i64, P, c_i64, P, c_i64, P, c_int, c_i64,
                         ctypes.POINTER(Epilogue), c_int, P, P]),
     "cg_colsum_workspace": (c_i64, [c_i64, c_i64]),
@@ -77,6 +82,7 @@ _SIGS = {
     "cg_head_workspace": (c_i64, [c_i64, c_i64]),
     "cg_head_fwd": (c_int, [P, P, c_i64, P, P, P, P, P, P, c_i64, c_i64, c_i64, P]),
     "cg_head_bwd": (c_int, [P, P, P, P, c_flt, P, P, c_i64, P, c_int, P, c_i64, c_i64, P]),
+    "cg_head_bwd_ex": (c_int, [P, P, P, P, c_flt, P, P, c_i64, P, c_int, P, c_i64, c_i64, c_int, P]),
     "cg_decode_window": (c_int, [P, c_i64, c_i64, c_i64, P, P, P]),
     "cg_decode_embed": (c_int, [P, c_i64, P, P, c_i64, P, P, c_i64, P]),
     "cg_decode_kv_append": (c_int, [P, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, P, P, P, P]),
@@ -112,15 +118,13 @@ def load():
         fn.restype = res
         fn.argtypes = args
     _lib = lib
-    # CHARPT_TUNING="key=value,key=value": kernel-selection knobs for measurement runs (cg_set_tuning)
-    # defer_splitk / defer_partials / slab_bf16 are owned by functional.DEFER (it keeps the slab / partial
-    # workspaces alive while a reduce is pending), so they cannot be set from here; skip_splitk_reduce (wrong gradients, timing only)
-    # additionally needs CHARPT_WHATIF to name it.
+    # CHARPT_TUNING="key=value,key=value": kernel-selection knobs for measurement runs (cg_set_tuning;
+    # precision and deferral are per-call flags, not knobs); skip_splitk_reduce (wrong gradients,
+    # timing only) additionally needs CHARPT_WHATIF to name it.
     for kv in filter(None, os.environ.get("CHARPT_TUNING", "").split(",")):
         key, _, val = kv.partition("=")
         key = key.strip()
-        if key in ("defer_splitk", "defer_partials", "slab_bf16") or (key == "skip_splitk_reduce" and
-                                     "skip_splitk_reduce" not in os.environ.get("CHARPT_WHATIF", "")):
+        if key == "skip_splitk_reduce" and "skip_splitk_reduce" not in os.environ.get("CHARPT_WHATIF", ""):
             raise RuntimeError(f"charpt: CHARPT_TUNING may not set {key}")
         check(lib.cg_set_tuning(key.encode(), int(val)), f"cg_set_tuning({key})")
     return lib

@@ -20,12 +20,10 @@ void launch_reduce_partials(const float* part, int64_t K, int64_t N, float* out_
 // three segments of S columns: out_a, out_b (accumulate), out_c (accumulate_c)
 void launch_reduce_partials3(const float* part, int64_t K, int64_t N, float* out_a, float* out_b, float* out_c,
                              int64_t S, int accumulate, int accumulate_c, hipStream_t st);
-// the same, queued instead while cg_set_tuning("defer_partials") is set (one multi-job launch at
-// cg_flush_deferred); an immediate reduce into a queued job's outputs flushes the queue first
+// the same, queued on stream st's deferral queue when defer (CG_DEFER; one multi-job launch at
+// cg_flush_deferred(st), defer.h); an immediate reduce into a queued job's outputs flushes them first
 void reduce_partials_deferrable(const float* part, int64_t K, int64_t N, float* out_a, float* out_b, float* out_c,
-                                int64_t S, int accumulate, int accumulate_c, hipStream_t st);
-void flush_partials();
-extern int g_defer_partials;
+                                int64_t S, int accumulate, int accumulate_c, int defer, hipStream_t st);
 }  // namespace cg
 
 namespace cg {

@@ -14,6 +14,9 @@
 //   * k_gemm_generic -- exact-f32 MFMA (16x16x4 f32) on 64x64x16 tiles with bounds checks:
 //     any shape/stride/dtype; the fp32 parity path and odd shapes (n_embd=126, V=65).
 // Both support deterministic split-K through fp32 slabs reduced in a fixed order.
+#include <map>
+
+#include "defer.h"
 #include "gemm_common.h"
 
 using namespace cg;
@@ -378,51 +381,57 @@ int g_gemm_max_grid = 0;
 int g_gemm_group_p8 = 0;   // persistent-kernel tile order (gemm_tile.h tile_rc), cg_set_tuning knobs
 int g_gemm_group_pk = 0;
 int g_gemm_n96 = 1;       // cg_set_tuning("gemm_n96"): 128x96 tiles for the part-filling fp32 residual forwards (gemm_pk.hip launch_n96)
-int g_defer_splitk = 0;   // cg_set_tuning("defer_splitk"): split-K reduces of fp32 STORE outputs deferred
-int g_slab_bf16 = 0;      // cg_set_tuning("slab_bf16"): split-K partial sums of fp32 STORE outputs as bf16 slabs
 int g_adam_per_launch = 0;   // cg_set_tuning("adam_per_launch"): AdamW jobs one launch's free blocks take (0 = MAX_ADAM)
 int g_red_side = 1;       // cg_set_tuning("red_side"): a part-filling persistent launch takes a pending reduce on extra blocks
-RedJobs g_red_pending = {};
-hipStream_t g_red_stream = nullptr;   // the stream the pending jobs were enqueued on
-int g_red_device = -1;                // ... and that stream's device (stream handles repeat across devices)
 
 static int current_device() {
     int d = -1;
     return hipGetDevice(&d) == hipSuccess ? d : -1;
 }
 
-// pending jobs for a launch on stream st of the current device: only a launch on the jobs' own
-// stream and device takes them (a launch on another stream is not ordered after the slab writes).
-// Single-threaded use only, like the rest of the tuning state.
-// cg_adamw_defer: AdamW jobs for the next launches with free blocks (MAX_ADAM per launch, oldest
-// first); what no such launch took goes out at the flush as one segmented AdamW launch
-constexpr int MAX_ADAM_PENDING = 64;
-static AdamJob g_adam_pending[MAX_ADAM_PENDING];
-static int g_adam_n = 0;
-static hipStream_t g_adam_stream = nullptr;
-static int g_adam_device = -1;
+// the deferral registry (defer.h): one queue per (device, stream)
+std::mutex& defer_mutex() {
+    static std::mutex m;
+    return m;
+}
 
-static bool adam_here(hipStream_t st) { return g_adam_n && st == g_adam_stream && current_device() == g_adam_device; }
+DeferQueue* defer_queue(hipStream_t st, bool create) {
+    static std::map<std::pair<int, hipStream_t>, DeferQueue> reg;
+    const auto key = std::make_pair(current_device(), st);
+    auto it = reg.find(key);
+    if (it != reg.end()) return &it->second;
+    if (!create) return nullptr;
+    DeferQueue& q = reg[key];
+    q.stream = st;
+    q.device = key.first;
+    return &q;
+}
 
+// pending jobs for a launch on stream st of the current device: the stream's split-K reduces, and
+// with side_ok (the launch has >= SIDE_MIN free blocks) up to MAX_ADAM of its AdamW jobs, oldest first
 RedJobs take_pending_reduces(hipStream_t st, bool side_ok) {
     RedJobs r = {};
-    if (g_red_pending.n && st == g_red_stream && current_device() == g_red_device) {
-        r.n = g_red_pending.n;
-        for (int q = 0; q < r.n; ++q) r.j[q] = g_red_pending.j[q];
-        g_red_pending.n = 0;
-    }
-    if (side_ok && adam_here(st)) {
+    std::lock_guard<std::mutex> lk(defer_mutex());
+    DeferQueue* q = defer_queue(st, false);
+    if (!q) return r;
+    r.n = q->nred;
+    for (int i = 0; i < r.n; ++i) r.j[i] = q->red[i];
+    q->nred = 0;
+    if (side_ok && q->nadam) {
         const int cap = g_adam_per_launch > 0 && g_adam_per_launch < MAX_ADAM ? g_adam_per_launch : MAX_ADAM;
-        r.na = g_adam_n < cap ? g_adam_n : cap;
-        for (int q = 0; q < r.na; ++q) r.a[q] = g_adam_pending[q];
-        for (int q = r.na; q < g_adam_n; ++q) g_adam_pending[q - r.na] = g_adam_pending[q];
-        g_adam_n -= r.na;
+        r.na = q->nadam < cap ? q->nadam : cap;
+        for (int i = 0; i < r.na; ++i) r.a[i] = q->adam[i];
+        for (int i = r.na; i < q->nadam; ++i) q->adam[i - r.na] = q->adam[i];
+        q->nadam -= r.na;
+        q->adam_taken += r.na;
     }
     return r;
 }
 
 bool has_pending_reduces(hipStream_t st, bool side_ok) {
-    return (g_red_pending.n && st == g_red_stream && current_device() == g_red_device) || (side_ok && adam_here(st));
+    std::lock_guard<std::mutex> lk(defer_mutex());
+    const DeferQueue* q = defer_queue(st, false);
+    return q && (q->nred || (side_ok && q->nadam));
 }
 
 int adamw_job_launch(const AdamJob& j, hipStream_t st);   // ce_adamw.hip
@@ -430,49 +439,42 @@ int adamw_segments_launch(float* p, const float* g, float* m, float* v, bf16_t* 
                           double lr, double beta1, double beta2, double eps, double wd, const int64_t* step,
                           hipStream_t st);   // ce_adamw.hip
 
-// pending AdamW jobs on their own stream (cg_flush_deferred, a full queue, a job from another
-// stream): slices of one set of flat buffers with one set of hyperparameters (the training step's
-// weight matrices) as ONE segmented launch, anything else job by job
-static void flush_adam() {
-    if (!g_adam_n) return;
-    const int cur = current_device();
-    if (g_adam_device >= 0 && cur != g_adam_device) (void)hipSetDevice(g_adam_device);
-    const int n = g_adam_n;
-    g_adam_n = 0;
-    const AdamJob* J = g_adam_pending;
+// the stream's pending AdamW jobs: slices of one set of flat buffers with one set of hyperparameters
+// (the training step's weight matrices) as ONE segmented launch, anything else job by job
+void flush_adam_locked(DeferQueue& q) {
+    if (!q.nadam) return;
+    const int n = q.nadam;
+    q.nadam = 0;
+    q.adam_taken += n;   // launched: cg_discard_deferred reports them (cg_flush_deferred resets the count)
+    const AdamJob* J = q.adam;
     int b = 0;   // the job with the lowest address is the segments' base
-    for (int q = 1; q < n; ++q)
-        if (J[q].p < J[b].p) b = q;
+    for (int i = 1; i < n; ++i)
+        if (J[i].p < J[b].p) b = i;
     bool one = n > 1 && n <= 64;
     int64_t segs[2 * MAX_ADAM_PENDING];
-    for (int q = 0; q < n && one; ++q) {
-        const int64_t d = J[q].p - J[b].p;
-        one = J[q].g - J[b].g == d && J[q].m - J[b].m == d && J[q].v - J[b].v == d && J[q].pb - J[b].pb == d &&
-              J[q].lr == J[b].lr && J[q].beta1 == J[b].beta1 && J[q].beta2 == J[b].beta2 && J[q].eps == J[b].eps &&
-              J[q].wd == J[b].wd && J[q].step == J[b].step;
-        segs[2 * q] = d;
-        segs[2 * q + 1] = 4 * J[q].n4;
+    for (int i = 0; i < n && one; ++i) {
+        const int64_t d = J[i].p - J[b].p;
+        one = J[i].g - J[b].g == d && J[i].m - J[b].m == d && J[i].v - J[b].v == d && J[i].pb - J[b].pb == d &&
+              J[i].lr == J[b].lr && J[i].beta1 == J[b].beta1 && J[i].beta2 == J[b].beta2 && J[i].eps == J[b].eps &&
+              J[i].wd == J[b].wd && J[i].step == J[b].step;
+        segs[2 * i] = d;
+        segs[2 * i + 1] = 4 * J[i].n4;
     }
     if (one)
         (void)adamw_segments_launch(J[b].p, J[b].g, J[b].m, J[b].v, J[b].pb, segs, n, J[b].lr, J[b].beta1, J[b].beta2,
-                                    J[b].eps, J[b].wd, J[b].step, g_adam_stream);
+                                    J[b].eps, J[b].wd, J[b].step, q.stream);
     else
-        for (int q = 0; q < n; ++q) (void)adamw_job_launch(J[q], g_adam_stream);
-    if (g_adam_device >= 0 && cur >= 0 && cur != g_adam_device) (void)hipSetDevice(cur);
+        for (int i = 0; i < n; ++i) (void)adamw_job_launch(J[i], q.stream);
 }
 
 static void launch_splitk_reduce_job(const RedJob& j, hipStream_t st);
 
-// the pending jobs as standalone reduce kernels on their own stream and device (cg_flush_deferred,
-// a full queue, or a job arriving from another stream / device)
-static void flush_pending() {
-    if (!g_red_pending.n) return;
-    const int cur = current_device();
-    if (g_red_device >= 0 && cur != g_red_device) (void)hipSetDevice(g_red_device);
-    const RedJobs r = g_red_pending;
-    g_red_pending.n = 0;
-    for (int q = 0; q < r.n; ++q) launch_splitk_reduce_job(r.j[q], g_red_stream);
-    if (g_red_device >= 0 && cur >= 0 && cur != g_red_device) (void)hipSetDevice(cur);
+// the stream's pending split-K reduces as standalone reduce kernels (cg_flush_deferred, a full queue,
+// or an AdamW job whose gradient one of them writes)
+void flush_red_locked(DeferQueue& q) {
+    const int n = q.nred;
+    q.nred = 0;
+    for (int i = 0; i < n; ++i) launch_splitk_reduce_job(q.red[i], q.stream);
 }
 
 int g_skip_splitk_reduce = 0;  // measurement knob (WRONG results): time a step without the split-K reduce
@@ -531,10 +533,6 @@ extern "C" int cg_set_tuning(const char* key, int value) {
         g_skip_splitk_reduce = value;
         return CG_OK;
     }
-    if (!strcmp(key, "defer_splitk")) {   // off: pending reduces are flushed on the caller's next cg_flush_deferred
-        g_defer_splitk = value;
-        return CG_OK;
-    }
     if (!strcmp(key, "adam_per_launch")) {
         g_adam_per_launch = value;
         return CG_OK;
@@ -543,13 +541,10 @@ extern "C" int cg_set_tuning(const char* key, int value) {
         g_red_side = value;
         return CG_OK;
     }
-    if (!strcmp(key, "slab_bf16")) {   // split-K fp32 STORE products on the 128x128 persistent kernel
-        g_slab_bf16 = value;
-        return CG_OK;
-    }
-    if (!strcmp(key, "defer_partials")) {   // queue cg_layernorm_bwd_reduce / cg_reduce_rows until cg_flush_deferred
-        g_defer_partials = value;
-        return CG_OK;
+    if (!strcmp(key, "defer_splitk") || !strcmp(key, "slab_bf16") || !strcmp(key, "defer_partials")) {
+        set_error("cg_set_tuning: %s is a per-call flag since round 5 (cg_epilogue_t.flags CG_GEMM_DEFER_REDUCE / "
+                  "CG_GEMM_SLAB_BF16, the CG_DEFER flag of the _ex reduces)", key);
+        return CG_EINVAL;
     }
     if (!strcmp(key, "ln_waves")) {   // takes effect for workspaces sized after the call
         g_ln_waves = value;
@@ -612,9 +607,11 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
                         (uintptr_t)(e.resid ? e.resid : (const float*)C)) & 15) == 0 &&
                       (!e.resid || e.ld_resid % 4 == 0);
     bool fast = false;
-    // bf16 slabs: only the 128x128 persistent kernel writes them (fast_gemm_launch declines otherwise,
-    // nothing launched) and only the vectorised reduces read them
-    e.slab_bf16 = g_slab_bf16 && split_k > 1 && op_dtype == CG_BF16 && e.kind == CG_EPI_STORE &&
+    const int flags = epi ? epi->flags : 0;
+    CG_REQUIRE((flags & ~(CG_GEMM_SLAB_BF16 | CG_GEMM_DEFER_REDUCE)) == 0, "cg_gemm: unknown epilogue flags %#x", flags);
+    // bf16 slabs (CG_GEMM_SLAB_BF16): only the 128x128 persistent kernel writes them (fast_gemm_launch
+    // declines otherwise, nothing launched) and only the vectorised reduces read them
+    e.slab_bf16 = (flags & CG_GEMM_SLAB_BF16) && split_k > 1 && op_dtype == CG_BF16 && e.kind == CG_EPI_STORE &&
                   c_dtype == CG_F32 && vec4 && ldc == N && (M * N) % 8 == 0 && !g_skip_splitk_reduce;
     if (e.slab_bf16) {
         fast = fast_gemm_launch(a_trans, b_trans, M, N, K, (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, c_dtype,
@@ -649,16 +646,16 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
     }
     // (slab sets above 40 MB -- the C4 FFN / QKV weight gradients -- keep their own reduce kernel: in
     // the next 256x256 GEMM's tail they measured no gain, C4 58.2 vs 57.9 ms/step)
-    if (split_k > 1 && vec4 && !g_skip_splitk_reduce && g_defer_splitk && fast && e.kind == CG_EPI_STORE &&
-        c_dtype == CG_F32 && ldc == N && st != nullptr && (int64_t)split_k * M * N * 4 <= ((int64_t)40 << 20)) {
-        // deferred: summed in the tail of the next persistent GEMM launch (or cg_flush_deferred); never
-        // on the null stream, whose handle names a different queue on every device
-        const int dev = current_device();
-        if (g_red_pending.n == MAX_RED || (g_red_pending.n && (g_red_stream != st || g_red_device != dev)))
-            flush_pending();
-        g_red_stream = st;
-        g_red_device = dev;
-        g_red_pending.j[g_red_pending.n++] = RedJob{(const float*)workspace, (float*)C, M * N / 4, split_k, e.beta, e.slab_bf16};
+    if (split_k > 1 && vec4 && !g_skip_splitk_reduce && (flags & CG_GEMM_DEFER_REDUCE) && fast &&
+        e.kind == CG_EPI_STORE && c_dtype == CG_F32 && ldc == N &&
+        (int64_t)split_k * M * N * 4 <= ((int64_t)40 << 20)) {
+        // deferred: summed in the tail of the next persistent GEMM launch on this stream of this
+        // device (or cg_flush_deferred(st) there) -- the queue key holds the device, so the null
+        // stream, whose handle names a different queue on every device, is fine too
+        std::lock_guard<std::mutex> lk(defer_mutex());
+        DeferQueue& q = *defer_queue(st, true);
+        if (q.nred == MAX_RED) flush_red_locked(q);
+        q.red[q.nred++] = RedJob{(const float*)workspace, (float*)C, M * N / 4, split_k, e.beta, e.slab_bf16};
     } else if (split_k > 1 && e.slab_bf16) {
         const int64_t n8 = M * N / 8;
         k_slab16_reduce8<<<ceil_div(n8, 256), 256, 0, st>>>(workspace, split_k, n8, (float*)C, e.beta);
@@ -698,11 +695,18 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
     return CG_OK;
 }
 
-extern "C" int cg_reduce_rows(const float* part, int64_t rows, int64_t N, float* out, int accumulate, void* stream) {
+extern "C" int cg_reduce_rows_ex(const float* part, int64_t rows, int64_t N, float* out, int accumulate, int flags,
+                                 void* stream) {
     CG_REQUIRE(part && out && rows > 0 && N > 0, "cg_reduce_rows: bad arguments");
-    reduce_partials_deferrable(part, rows, N, out, nullptr, nullptr, N, accumulate, 0, (hipStream_t)stream);
+    CG_REQUIRE((flags & ~CG_DEFER) == 0, "cg_reduce_rows_ex: unknown flags %#x", flags);
+    reduce_partials_deferrable(part, rows, N, out, nullptr, nullptr, N, accumulate, 0, flags & CG_DEFER,
+                               (hipStream_t)stream);
     CG_LAUNCH_CHECK("cg_reduce_rows");
     return CG_OK;
+}
+
+extern "C" int cg_reduce_rows(const float* part, int64_t rows, int64_t N, float* out, int accumulate, void* stream) {
+    return cg_reduce_rows_ex(part, rows, N, out, accumulate, 0, stream);
 }
 
 extern "C" int64_t cg_colsum_workspace(int64_t rows, int64_t N) {
@@ -758,29 +762,49 @@ extern "C" int cg_adamw_defer(float* p, const float* g, float* m, float* v, uint
                    (((uintptr_t)p_bf16) & 7) == 0,
                "cg_adamw_defer: p, g, m, v must be 16-B aligned, p_bf16 8-B aligned");
     hipStream_t st = (hipStream_t)stream;
-    // the region's gradient must be final first: a pending split-K reduce writing into it goes out now
-    for (int q = 0; q < g_red_pending.n; ++q) {
-        const RedJob& J = g_red_pending.j[q];
-        if (J.out < g + n && g < J.out + 4 * J.n4) {
-            flush_pending();
-            break;
-        }
+    {
+        std::lock_guard<std::mutex> lk(defer_mutex());
+        DeferQueue& q = *defer_queue(st, true);
+        // the region's gradient must be final first: a pending split-K reduce writing into it goes out now
+        for (int i = 0; i < q.nred; ++i)
+            if (q.red[i].out < g + n && g < q.red[i].out + 4 * q.red[i].n4) {
+                flush_red_locked(q);
+                break;
+            }
+        if (q.nadam == MAX_ADAM_PENDING) flush_adam_locked(q);
+        q.adam[q.nadam++] = AdamJob{p, g, m, v, (bf16_t*)p_bf16, n / 4, lr, beta1, beta2, eps, weight_decay, step_ptr};
     }
-    const int dev = current_device();
-    if (g_adam_n == MAX_ADAM_PENDING || (g_adam_n && (g_adam_stream != st || g_adam_device != dev))) flush_adam();
-    g_adam_stream = st;
-    g_adam_device = dev;
-    g_adam_pending[g_adam_n++] = AdamJob{p, g, m, v, (bf16_t*)p_bf16, n / 4, lr, beta1, beta2, eps, weight_decay,
-                                         step_ptr};
     CG_LAUNCH_CHECK("cg_adamw_defer");
     return CG_OK;
 }
 
 extern "C" int cg_flush_deferred(void* stream) {
-    (void)stream;   // pending jobs go out on the stream they were enqueued on
-    cg::flush_pending();
-    cg::flush_adam();
-    cg::flush_partials();
+    using namespace cg;
+    {
+        std::lock_guard<std::mutex> lk(defer_mutex());
+        DeferQueue* q = defer_queue((hipStream_t)stream, false);
+        if (q) {
+            flush_red_locked(*q);
+            flush_adam_locked(*q);
+            flush_parts_locked(*q);
+            q->adam_taken = 0;
+        }
+    }
     CG_LAUNCH_CHECK("cg_flush_deferred");
+    return CG_OK;
+}
+
+extern "C" int cg_discard_deferred(void* stream, int* adam_jobs_taken) {
+    using namespace cg;
+    int taken = 0;
+    {
+        std::lock_guard<std::mutex> lk(defer_mutex());
+        DeferQueue* q = defer_queue((hipStream_t)stream, false);
+        if (q) {
+            taken = q->adam_taken;
+            q->nred = q->nadam = q->parts.n = q->adam_taken = 0;
+        }
+    }
+    if (adam_jobs_taken) *adam_jobs_taken = taken;
     return CG_OK;
 }

@@ -20,7 +20,7 @@ struct EpiArgs {
     int site;
     float beta;
     float* colpart;  // RELU_BWD: per-64-row-block column sums; STORE_ROWDOT: per-head row dots (k_gemm_pk only)
-    int slab_bf16;   // split-K: the per-split partial sums stored as bf16 slabs (cg_set_tuning "slab_bf16")
+    int slab_bf16;   // split-K: the per-split partial sums stored as bf16 slabs (cg_epilogue_t.flags CG_GEMM_SLAB_BF16)
 };
 
 // four consecutive slab elements as fp32 (bf16 slabs: one 8-B load, exact widening)
@@ -77,8 +77,8 @@ __device__ __forceinline__ void store_out(TC* C, int64_t off, float v, float bet
 }
 
 
-// A split-K reduce deferred out of its own cg_gemm call (cg_set_tuning("defer_splitk", 1), the
-// training backward): out[i] = sum_{s < S} ws[s n + i] (+ beta out[i]) over n = 4 n4 fp32 elements,
+// A split-K reduce deferred out of its own cg_gemm call (CG_GEMM_DEFER_REDUCE, the training
+// backward; queued per stream, defer.h): out[i] = sum_{s < S} ws[s n + i] (+ beta out[i]) over n = 4 n4 fp32 elements,
 // run in the tail of the next persistent GEMM launch on the stream (each thread takes float4
 // chunks once its block's own items are done) or by cg_flush_deferred.  Slab 0 first, then 1, ...:
 // k_splitk_reduce4's order, so the same bits.
@@ -200,7 +200,6 @@ extern int g_gemm_max_grid;
 extern int g_gemm_group_p8;
 extern int g_gemm_group_pk;
 extern int g_gemm_n96;
-extern int g_slab_bf16;
 extern int g_red_side;
 // test knob (cg_set_tuning("pk_flags", f)) for the persistent kernel's epilogue (gemm_pk.hip)
 extern int g_pk_flags;

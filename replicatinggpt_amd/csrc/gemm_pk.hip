@@ -907,9 +907,11 @@ bool launch_p(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
     const int64_t nitems = (M / BM) * (N / BN) * split_k;
     int64_t slots = (int64_t)cu_count() * G::OCC;
     if (g_gemm_max_grid > 0 && g_gemm_max_grid < slots) slots = g_gemm_max_grid;
-    // a part-filling launch that will take a pending split-K reduce gets the free slots too: those
-    // blocks have no items and run the reduce beside the items (red_tail's `first`)
-    const bool side = g_red_side && nitems < slots && has_pending_reduces(st, slots - nitems >= SIDE_MIN);
+    // a part-filling launch with >= SIDE_MIN free slots that will take pending work gets the free
+    // slots too: those blocks have no items and run the reduce / AdamW jobs beside the items
+    // (red_tail's `first`).  With fewer free slots the launch keeps grid = items and every block
+    // takes its share of a reduce after its item (a few free blocks must not carry a whole reduce).
+    const bool side = g_red_side && slots - nitems >= SIDE_MIN && has_pending_reduces(st, true);
     const unsigned grid = (unsigned)(nitems < slots && !side ? nitems : slots);
 #define FG(AT_, BT_) launch_ek<AT_, BT_, BM, BN, NBUF, BK>(grid, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, kchunk, ws, st)
     // transposed LDS images need a multiple of 128 rows (DmaP, col_swz): other tiles serve only the

@@ -233,18 +233,27 @@ extern "C" int cg_head_fwd(const void* a, const void* wpad, int64_t wpad_rows, c
     return CG_OK;
 }
 
-extern "C" int cg_head_bwd(const float* logits, const float* lse, const int64_t* targets, const float* g_loss,
-                           float g_mult, const float* g_logits, void* dl, int64_t ld_dl, float* db, int db_accumulate,
-                           void* workspace, int64_t M, int64_t V, void* stream) {
+extern "C" int cg_head_bwd_ex(const float* logits, const float* lse, const int64_t* targets, const float* g_loss,
+                              float g_mult, const float* g_logits, void* dl, int64_t ld_dl, float* db,
+                              int db_accumulate, void* workspace, int64_t M, int64_t V, int flags, void* stream) {
     CG_REQUIRE(M > 0 && V > 0 && V <= 128, "cg_head_bwd: bad sizes");
+    CG_REQUIRE((flags & ~CG_DEFER) == 0, "cg_head_bwd_ex: unknown flags %#x", flags);
     CG_REQUIRE(ld_dl % 8 == 0 && ld_dl >= V && ld_dl <= 128, "cg_head_bwd: ld_dl must be a multiple of 8 in [V, 128]");
     CG_REQUIRE(!targets || g_loss, "cg_head_bwd: targets need g_loss");
     hipStream_t st = (hipStream_t)stream;
     const int nb = ceil_div(M, HEAD_ROWS);
     k_head_bwd<<<nb, 256, 0, st>>>(logits, lse, targets, g_loss, g_mult, g_logits, (int)V, M, (bf16_t*)dl, (int)ld_dl,
                                    (float*)workspace);
-    if (db)   // queued while defer_partials is set (functional.DEFER, db a flat gradient slot)
-        reduce_partials_deferrable((const float*)workspace, nb, V, db, nullptr, nullptr, V, db_accumulate, 0, st);
+    if (db)   // CG_DEFER: queued on the stream's deferral queue (functional.DEFER, db a flat gradient slot)
+        reduce_partials_deferrable((const float*)workspace, nb, V, db, nullptr, nullptr, V, db_accumulate, 0,
+                                   flags & CG_DEFER, st);
     CG_LAUNCH_CHECK("cg_head_bwd");
     return CG_OK;
+}
+
+extern "C" int cg_head_bwd(const float* logits, const float* lse, const int64_t* targets, const float* g_loss,
+                           float g_mult, const float* g_logits, void* dl, int64_t ld_dl, float* db, int db_accumulate,
+                           void* workspace, int64_t M, int64_t V, void* stream) {
+    return cg_head_bwd_ex(logits, lse, targets, g_loss, g_mult, g_logits, dl, ld_dl, db, db_accumulate, workspace, M,
+                          V, 0, stream);
 }

@@ -439,18 +439,26 @@ extern "C" int cg_layernorm_bwd_rows(const void* dy, int dy_dtype, const float* 
                               lp_site, nullptr, nullptr, marker, 0, 0, workspace, rows, C, 1, stream);
 }
 
-extern "C" int cg_layernorm_bwd_reduce(const void* workspace, int64_t rows, int64_t C, int lp_colsum_partials,
-                                       float* dw, float* db, float* lp_colsum, int accumulate, int colsum_accumulate,
-                                       void* stream) {
+extern "C" int cg_layernorm_bwd_reduce_ex(const void* workspace, int64_t rows, int64_t C, int lp_colsum_partials,
+                                          float* dw, float* db, float* lp_colsum, int accumulate,
+                                          int colsum_accumulate, int flags, void* stream) {
     CG_REQUIRE(rows > 0 && C > 0 && C <= 1024, "cg_layernorm_bwd_reduce: need 0 < C <= 1024");
+    CG_REQUIRE((flags & ~CG_DEFER) == 0, "cg_layernorm_bwd_reduce_ex: unknown flags %#x", flags);
     CG_REQUIRE(!lp_colsum || lp_colsum_partials, "cg_layernorm_bwd_reduce: lp_colsum needs the colsum partials");
     if (!dw && !db && !lp_colsum) return CG_OK;
     const int64_t nblk = ln_bwd_blocks(rows, C);
     const int NP = lp_colsum_partials ? 3 : 2;
     reduce_partials_deferrable((const float*)workspace, nblk, NP * C, dw, db, lp_colsum, C, accumulate,
-                               colsum_accumulate, (hipStream_t)stream);
+                               colsum_accumulate, flags & CG_DEFER, (hipStream_t)stream);
     CG_LAUNCH_CHECK("cg_layernorm_bwd_reduce");
     return CG_OK;
+}
+
+extern "C" int cg_layernorm_bwd_reduce(const void* workspace, int64_t rows, int64_t C, int lp_colsum_partials,
+                                       float* dw, float* db, float* lp_colsum, int accumulate, int colsum_accumulate,
+                                       void* stream) {
+    return cg_layernorm_bwd_reduce_ex(workspace, rows, C, lp_colsum_partials, dw, db, lp_colsum, accumulate,
+                                      colsum_accumulate, 0, stream);
 }
 
 extern "C" int cg_layernorm_bwd(const void* dy, int dy_dtype, const float* x, const float* w, const float* mean,

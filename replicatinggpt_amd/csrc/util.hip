@@ -2,6 +2,7 @@
 #include <stdarg.h>
 
 #include "common.h"
+#include "defer.h"
 
 namespace cg {
 static thread_local char g_err[1024] = "";
@@ -186,25 +187,6 @@ __global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict
     reduce_partials_block(part, K, N, out_a, out_b, out_c, S, accumulate, accumulate_c, blockIdx.x, red);
 }
 
-namespace cg {
-// Deferred partial reduces (cg_set_tuning "defer_partials", owned by functional.DEFER: the caller
-// keeps every queued job's partials allocated and reads no output before cg_flush_deferred).  The
-// training backward queues its ~20 LayerNorm / bias-gradient reduces here and cg_flush_deferred
-// launches them as ONE kernel: on one hardware queue each was a ~5 us launch for ~1 us of work.
-struct PartJob {
-    const float* part;
-    int64_t K, N, S;
-    float *a, *b, *c;
-    int acc, acc_c;
-};
-constexpr int MAX_PART_JOBS = 24;
-struct PartJobs {
-    int n;
-    int start[MAX_PART_JOBS + 1];   // first block of job q; start[n] = the grid
-    PartJob j[MAX_PART_JOBS];
-};
-}  // namespace cg
-
 __global__ __launch_bounds__(256) void k_reduce_partials_multi(cg::PartJobs jobs) {
     __shared__ float red[64][17];
     const int b = blockIdx.x;
@@ -215,24 +197,16 @@ __global__ __launch_bounds__(256) void k_reduce_partials_multi(cg::PartJobs jobs
 }
 
 namespace cg {
-int g_defer_partials = 0;
-static PartJobs g_part_pending = {};
-static hipStream_t g_part_stream = nullptr;
-static int g_part_device = -1;
-
-static int part_device() {
-    int d = -1;
-    return hipGetDevice(&d) == hipSuccess ? d : -1;
-}
-
-void flush_partials() {
-    if (!g_part_pending.n) return;
-    const int cur = part_device();
-    if (g_part_device >= 0 && cur != g_part_device) (void)hipSetDevice(g_part_device);
-    const PartJobs jobs = g_part_pending;
-    g_part_pending.n = 0;
-    k_reduce_partials_multi<<<jobs.start[jobs.n], 256, 0, g_part_stream>>>(jobs);
-    if (g_part_device >= 0 && cur >= 0 && cur != g_part_device) (void)hipSetDevice(cur);
+// Deferred column-sum reduces (the CG_DEFER calls: cg_layernorm_bwd_reduce_ex, cg_reduce_rows_ex,
+// cg_head_bwd_ex; the caller keeps every queued job's partials allocated and reads no output before
+// cg_flush_deferred on that stream).  The training backward queues its ~20 LayerNorm / bias-gradient
+// reduces and the flush launches them as ONE kernel: on one hardware queue each was a ~5 us launch
+// for ~1 us of work.  The queue is the stream's DeferQueue (defer.h).
+void flush_parts_locked(DeferQueue& q) {
+    if (!q.parts.n) return;
+    const PartJobs jobs = q.parts;
+    q.parts.n = 0;
+    k_reduce_partials_multi<<<jobs.start[jobs.n], 256, 0, q.stream>>>(jobs);
 }
 
 // [p, p + n) of job j's outputs
@@ -242,53 +216,63 @@ static bool overlaps(const float* p, int64_t n, const float* q, int64_t m) {
 static bool job_outputs_overlap(const PartJob& x, const float* p, int64_t n) {
     return overlaps(x.a, x.S, p, n) || overlaps(x.b, x.S, p, n) || overlaps(x.c, x.N - 2 * x.S, p, n);
 }
-// an immediate reduce / write into [p, p + n): the queued jobs that target it go first
-void flush_partials_touching(const float* p, int64_t n) {
-    for (int q = 0; q < g_part_pending.n; ++q)
-        if (job_outputs_overlap(g_part_pending.j[q], p, n)) {
-            flush_partials();
+// an immediate reduce / write into [p, p + n) on stream st: that stream's queued jobs that target it
+// go first (caller holds the registry lock)
+static void flush_parts_touching_locked(DeferQueue* q, const float* p, int64_t n) {
+    if (!q) return;
+    for (int i = 0; i < q->parts.n; ++i)
+        if (job_outputs_overlap(q->parts.j[i], p, n)) {
+            flush_parts_locked(*q);
             return;
         }
 }
 
-static bool enqueue_partials(const PartJob& j, hipStream_t st) {
-    if (!g_defer_partials) return false;
-    const int dev = part_device();
-    bool clash = g_part_pending.n == MAX_PART_JOBS ||
-                 (g_part_pending.n && (g_part_stream != st || g_part_device != dev));
-    for (int q = 0; q < g_part_pending.n && !clash; ++q) {
-        const PartJob& x = g_part_pending.j[q];
+static void enqueue_partials(const PartJob& j, hipStream_t st) {
+    std::lock_guard<std::mutex> lk(defer_mutex());
+    DeferQueue& q = *defer_queue(st, true);
+    PartJobs& P = q.parts;
+    bool clash = P.n == MAX_PART_JOBS;
+    for (int i = 0; i < P.n && !clash; ++i) {
+        const PartJob& x = P.j[i];
         clash = job_outputs_overlap(x, j.a, j.S) || job_outputs_overlap(x, j.b, j.S) ||
                 job_outputs_overlap(x, j.c, j.N - 2 * j.S);
     }
-    if (clash) flush_partials();
-    g_part_stream = st;
-    g_part_device = dev;
-    PartJobs& P = g_part_pending;
+    if (clash) flush_parts_locked(q);
     if (!P.n) P.start[0] = 0;
     P.j[P.n] = j;
     P.start[P.n + 1] = P.start[P.n] + (int)ceil_div(j.N, 16);
     ++P.n;
-    return true;
 }
 
 void launch_reduce_partials(const float* part, int64_t K, int64_t N, float* out_a, float* out_b, int64_t S,
                             int accumulate, hipStream_t st) {
-    flush_partials_touching(out_a, S);
-    flush_partials_touching(out_b, N - S);
+    {
+        std::lock_guard<std::mutex> lk(defer_mutex());
+        DeferQueue* q = defer_queue(st, false);
+        flush_parts_touching_locked(q, out_a, S);
+        flush_parts_touching_locked(q, out_b, N - S);
+    }
     k_reduce_partials<<<ceil_div(N, 16), 256, 0, st>>>(part, K, N, out_a, out_b, nullptr, S, accumulate, 0);
 }
 void launch_reduce_partials3(const float* part, int64_t K, int64_t N, float* out_a, float* out_b, float* out_c,
                              int64_t S, int accumulate, int accumulate_c, hipStream_t st) {
-    flush_partials_touching(out_a, S);
-    flush_partials_touching(out_b, S);
-    flush_partials_touching(out_c, N - 2 * S);
+    {
+        std::lock_guard<std::mutex> lk(defer_mutex());
+        DeferQueue* q = defer_queue(st, false);
+        flush_parts_touching_locked(q, out_a, S);
+        flush_parts_touching_locked(q, out_b, S);
+        flush_parts_touching_locked(q, out_c, N - 2 * S);
+    }
     k_reduce_partials<<<ceil_div(N, 16), 256, 0, st>>>(part, K, N, out_a, out_b, out_c, S, accumulate, accumulate_c);
 }
-// the deferrable forms (cg_layernorm_bwd_reduce, cg_reduce_rows): queued while defer_partials is set
+// the deferrable forms (cg_layernorm_bwd_reduce_ex, cg_reduce_rows_ex, cg_head_bwd_ex): queued on the
+// stream's DeferQueue with CG_DEFER, else launched now
 void reduce_partials_deferrable(const float* part, int64_t K, int64_t N, float* out_a, float* out_b, float* out_c,
-                                int64_t S, int accumulate, int accumulate_c, hipStream_t st) {
-    if (enqueue_partials(PartJob{part, K, N, S, out_a, out_b, out_c, accumulate, accumulate_c}, st)) return;
+                                int64_t S, int accumulate, int accumulate_c, int defer, hipStream_t st) {
+    if (defer) {
+        enqueue_partials(PartJob{part, K, N, S, out_a, out_b, out_c, accumulate, accumulate_c}, st);
+        return;
+    }
     launch_reduce_partials3(part, K, N, out_a, out_b, out_c, S, accumulate, accumulate_c, st);
 }
 }  // namespace cg

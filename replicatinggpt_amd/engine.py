@@ -101,14 +101,16 @@ class TrainStep:
     def _fwd_bwd(self):
         _, loss = self.model(self.x, self.y)           # GPT1.py:230
         self.opt.zero_grad(set_to_none=True)           # GPT1.py:231
-        if self.reducer is None:   # one rank: the weight matrices' AdamW beside the backward's GEMMs
-            Fn.EARLY.begin(self.opt)
+        # one rank: the weight matrices' AdamW beside the backward's GEMMs
+        early = self.reducer is None and Fn.EARLY.begin(self.opt)
         try:
             with Fn.DEFER:                             # split-K reduces in later GEMMs' tails
                 loss.backward(self._one)               # GPT1.py:232
         except BaseException:
-            if hasattr(self.opt, "_early"):
-                self.opt._early = None                 # a failed backward leaves no half-done step behind
+            # DEFER discarded the queued work; the optimizer takes its step count back, or -- when
+            # some early updates had already run -- refuses further steps (optim.AdamW.early_abort)
+            if early:
+                self.opt.early_abort(Fn.DEFER.aborted_adam)
             raise
         finally:
             Fn.EARLY.end()

@@ -82,60 +82,81 @@ SIDE = SideStream()
 
 
 class DeferredReduces:
-    """The training backward's split-K weight-gradient reduces, deferred into the tail of the next
-    persistent GEMM launch on the stream (cg_set_tuning "defer_splitk"; csrc/gemm_common.h RedJob:
-    same summation order, same bits) instead of a separate kernel each.  Inside ``with DEFER:``
-    linear_wgrad keeps its slab workspaces alive; the exit launches whatever is still pending
-    (before anything reads the gradients: the optimizer or the DP all-reduce) and releases them.
-    CHARPT_DEFER_SPLITK=0 turns it off (A/B)."""
+    """The training backward's deferred work, asked for call by call (include/charpt.h "deferred
+    work"): the weight gradients into flat gradient slots leave their split-K slab reduce pending
+    (cg_epilogue_t.flags CG_GEMM_DEFER_REDUCE) for the tail of the next persistent GEMM launch on the
+    same stream (csrc/gemm_common.h RedJob: same summation order, same bits), and the LayerNorm /
+    bias-gradient column-sum reduces into slots are queued (CG_DEFER) for one multi-job launch.  The
+    queues are per stream in the library; this object only records which streams it queued work on
+    and keeps the workspaces alive.  Leaving ``with DEFER:`` flushes those streams (before anything
+    reads the gradients: the optimizer or the DP all-reduce); leaving it by an exception DISCARDS
+    their queues instead (cg_discard_deferred) and records in ``aborted_adam`` how many deferred
+    AdamW updates had already been taken by GEMM launches.  CHARPT_DEFER_SPLITK=0 turns it off (A/B)."""
 
     def __init__(self):
         self.enabled = os.environ.get("CHARPT_DEFER_SPLITK", "1") != "0"
-        # the LayerNorm / bias-gradient column-sum reduces likewise (cg_set_tuning "defer_partials"):
-        # queued and launched as ONE multi-job kernel at the flush -- on one hardware queue each was a
-        # ~5 us launch for ~1 us of work (CHARPT_DEFER_PARTIALS=0: one launch each, for A/B)
+        # the LayerNorm / bias-gradient column-sum reduces likewise: queued and launched as ONE
+        # multi-job kernel at the flush -- on one hardware queue each was a ~5 us launch for ~1 us
+        # of work (CHARPT_DEFER_PARTIALS=0: one launch each, for A/B)
         self.partials_on = os.environ.get("CHARPT_DEFER_PARTIALS", "1") != "0"
         self.active = False
         self.keep = []
+        self.streams = {}        # cuda_stream handle -> stream, every stream work was queued on
+        self.aborted_adam = 0
 
     def __enter__(self):
         if self.enabled and torch.cuda.is_available():
-            lib = L.load()
-            L.check(lib.cg_set_tuning(b"defer_splitk", 1), "defer_splitk")
             self.active = True
+            self.aborted_adam = 0
         return self
+
+    def note_stream(self):
+        """The current stream will hold deferred work (flushed / discarded at exit)."""
+        st = torch.cuda.current_stream()
+        self.streams[st.cuda_stream] = st
 
     @contextlib.contextmanager
     def partials(self, *keep):
-        """Queue the cg_layernorm_bwd_reduce / cg_reduce_rows calls made inside (their outputs must be
-        flat gradient slots, which nothing reads before DEFER closes; ``keep``: their partials,
-        held until the flush)."""
+        """Yields whether the column-sum reduce calls made inside may be queued (their ``defer``
+        argument): their outputs must be flat gradient slots, which nothing reads before DEFER
+        closes; ``keep``: their partials, held until the flush."""
         if not (self.active and self.partials_on):
-            yield
+            yield False
             return
-        lib = L.load()
-        L.check(lib.cg_set_tuning(b"defer_partials", 1), "defer_partials")
-        try:
-            yield
-        finally:
-            L.check(lib.cg_set_tuning(b"defer_partials", 0), "defer_partials")
+        self.note_stream()
+        yield True
         self.keep.extend(t for t in keep if t is not None)
 
     def flush(self):
-        """Launch every pending reduce now, on the current stream (their outputs complete in stream order)."""
-        L.check(L.load().cg_flush_deferred(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
-                "flush_deferred")
+        """Launch everything pending on the streams this scope queued work on (each on its own stream)."""
+        lib = L.load()
+        for h in list(self.streams):
+            L.check(lib.cg_flush_deferred(ctypes.c_void_p(h)), "flush_deferred")
 
-    def __exit__(self, *exc):
+    def discard(self):
+        """Drop what is pending (a failed backward); returns the AdamW jobs launches had already taken."""
+        lib = L.load()
+        taken = 0
+        for h in list(self.streams):
+            n = ctypes.c_int(0)
+            L.check(lib.cg_discard_deferred(ctypes.c_void_p(h), ctypes.byref(n)), "discard_deferred")
+            taken += n.value
+        return taken
+
+    def __exit__(self, exc_type, *exc):
         if self.active:
-            lib = L.load()
-            self.flush()
-            L.check(lib.cg_set_tuning(b"defer_splitk", 0), "defer_splitk")
-            if SIDE.enabled:   # the flush runs on the stream its reduces were enqueued on: join it
-                dev = torch.device("cuda", torch.cuda.current_device())
-                torch.cuda.current_stream(dev).wait_stream(SIDE.stream(dev))
-            self.active = False
-            self.keep.clear()
+            try:
+                if exc_type is None:
+                    self.flush()
+                else:
+                    self.aborted_adam = self.discard()
+                if SIDE.enabled:   # the flush runs on the stream its reduces were enqueued on: join it
+                    dev = torch.device("cuda", torch.cuda.current_device())
+                    torch.cuda.current_stream(dev).wait_stream(SIDE.stream(dev))
+            finally:
+                self.active = False
+                self.keep.clear()
+                self.streams.clear()
         return False
 
 
@@ -342,7 +363,7 @@ def _wgrad_split(M, N, K, fast):
 
 
 # The training path's weight gradients (flat gradient slots) take their split-K partial sums through
-# bf16 slabs (cg_set_tuning "slab_bf16": half the slab bytes written and read back; each per-split
+# bf16 slabs (per call: cg_epilogue_t.flags CG_GEMM_SLAB_BF16 -- half the slab bytes written and read back; each per-split
 # partial rounded once to bf16, the sum over splits in fp32 -- torch's bf16 path rounds the whole
 # gradient to bf16).  Temporaries (charpt::linear's backward) keep fp32 slabs.  CHARPT_SLAB_BF16=0: A/B.
 SLAB_BF16 = os.environ.get("CHARPT_SLAB_BF16", "1") != "0"
@@ -362,23 +383,16 @@ def linear_wgrad(dy2, x2, out, beta, into_slot=False):
     fast = _is_bf16(dy2.dtype) and N % 128 == 0 and K % 128 == 0 and M % 64 == 0
     split = _wgrad_split(N, K, M, fast)
     ws = None
-    defer = DEFER.active and into_slot
+    defer = DEFER.active and into_slot and split > 1
     if split > 1:
         ws = torch.empty(ops.gemm_workspace(N, K, split) // 4, dtype=torch.float32, device=dy2.device)
         if defer:
             # its reduce may run after this call returns
             DEFER.keep.extend((ws, dy2, x2))
-    slab16 = SLAB_BF16 and into_slot and split > 1 and dy2.is_cuda
-    if slab16:
-        L.check(L.load().cg_set_tuning(b"slab_bf16", 1), "slab_bf16")
-    try:
-        ops.gemm(dy2, x2, out, _is_bf16(dy2.dtype), True, True, N, K, M, N, K, out.stride(0), L.EPI_STORE, None,
-                 None, 0, None, 0, 0.0, 0, None, 0, float(beta), split, ws)
-    finally:
-        if slab16:
-            L.check(L.load().cg_set_tuning(b"slab_bf16", 0), "slab_bf16")
-    if DEFER.active and not defer and split > 1:
-        DEFER.flush()
+            DEFER.note_stream()
+    flags = (L.GEMM_SLAB_BF16 if SLAB_BF16 and into_slot and split > 1 else 0) | (L.GEMM_DEFER_REDUCE if defer else 0)
+    ops.gemm(dy2, x2, out, _is_bf16(dy2.dtype), True, True, N, K, M, N, K, out.stride(0), L.EPI_STORE, None,
+             None, 0, None, 0, 0.0, 0, None, 0, float(beta), split, ws, flags)
     return out
 
 
@@ -504,8 +518,8 @@ def layernorm_bwd(dy2, x2, w_reg, b_reg, mean, rstd, dres=None, want_lp=False, l
         # the reduce joins the backward's one multi-job launch at the DEFER flush
         ops.layernorm_bwd_rows(dy2, x2, w_reg.master, mean, rstd, dres, dx, lp, ws, gcs is not None, p, seed, rng,
                                site)
-        with DEFER.partials(ws):
-            ops.layernorm_bwd_reduce(ws, rows, C, gcs is not None, gw, gb, gcs, bool(bw or bb), bool(bcs))
+        with DEFER.partials(ws) as queued:
+            ops.layernorm_bwd_reduce(ws, rows, C, gcs is not None, gw, gb, gcs, bool(bw or bb), bool(bcs), queued)
     else:
         ops.layernorm_bwd(dy2, x2, w_reg.master, mean, rstd, dres, dx, lp, gw, gb, bool(bw or bb), ws, gcs, bool(bcs),
                           p, seed, rng, site)
@@ -785,8 +799,8 @@ class FFNSublayerFn(torch.autograd.Function):
                 linear_wgrad(dz1, a, g_w1, beta_w1, g_w1 is w1.slot)
             if g_b1 is not None:
                 if part is not None:
-                    with DEFER.partials(part) if g_b1 is b1.slot else contextlib.nullcontext():
-                        ops.reduce_rows(part, part.shape[0], part.shape[1], g_b1, bool(beta_b1))
+                    with DEFER.partials(part) if g_b1 is b1.slot else contextlib.nullcontext(False) as queued:
+                        ops.reduce_rows(part, part.shape[0], part.shape[1], g_b1, bool(beta_b1), queued)
                 else:
                     colsum_into(dz1, g_b1, beta_b1)
         da = torch.empty((B * T, C), dtype=act, device=x2.device)
@@ -903,9 +917,9 @@ class HeadLossFn(torch.autograd.Function):
         if g_loss is None:
             t1 = None
         # the lm_head bias gradient's column-sum reduce joins DEFER's multi-job flush when it targets the slot
-        with DEFER.partials(ws) if (gb is not None and gb is lm_b.slot) else contextlib.nullcontext():
+        with DEFER.partials(ws) if (gb is not None and gb is lm_b.slot) else contextlib.nullcontext(False) as queued:
             ops.head_bwd(logits, lse, t1, None if g_loss is None else g_loss.reshape(1).float().contiguous(), 1.0 / M,
-                         gl, dl, gb, bool(beta_b), ws)
+                         gl, dl, gb, bool(beta_b), ws, queued)
         g, beta, f_lw = lm_w.grad_target()
         if g is not None:
             if g.data_ptr() == lm_w.slot.data_ptr():

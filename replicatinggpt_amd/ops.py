@@ -143,10 +143,11 @@ def layernorm_bwd_rows(dy: Tensor, x: Tensor, w: Tensor, mean: Tensor, rstd: Ten
 @_op("layernorm_bwd_reduce", ("dw", "db", "lp_colsum"))
 def layernorm_bwd_reduce(ws: Tensor, rows: int, C: int, colsum_partials: bool, dw: Optional[Tensor],
                          db: Optional[Tensor], lp_colsum: Optional[Tensor], accumulate: bool,
-                         colsum_accumulate: bool) -> None:
-    L.check(L.load().cg_layernorm_bwd_reduce(L.ptr(ws), rows, C, int(colsum_partials), L.ptr(dw), L.ptr(db),
-                                             L.ptr(lp_colsum), int(accumulate), int(colsum_accumulate), _s(ws)),
-            "layernorm_bwd_reduce")
+                         colsum_accumulate: bool, defer: bool = False) -> None:
+    """defer: queued on the stream's deferral queue (CG_DEFER) until cg_flush_deferred."""
+    L.check(L.load().cg_layernorm_bwd_reduce_ex(L.ptr(ws), rows, C, int(colsum_partials), L.ptr(dw), L.ptr(db),
+                                                L.ptr(lp_colsum), int(accumulate), int(colsum_accumulate),
+                                                L.DEFER if defer else 0, _s(ws)), "layernorm_bwd_reduce")
 
 
 def layernorm_bwd_workspace(rows, C):
@@ -154,14 +155,32 @@ def layernorm_bwd_workspace(rows, C):
 
 
 # ---------------------------------------------------------------------------------------
+def _gemm_extents(a, b, out, a_trans, b_trans, M, N, K, lda, ldb, ldc, what="gemm"):
+    """Host check that every element cg_gemm will address lies inside its tensor (the C ABI sees
+    only pointers): A(m,k) = A[k lda + m] (a_trans) or A[m lda + k]; B(n,k) likewise; C[m ldc + n]."""
+    need_a = (K - 1) * lda + M if a_trans else (M - 1) * lda + K
+    need_b = (K - 1) * ldb + N if b_trans else (N - 1) * ldb + K
+    need_c = (M - 1) * ldc + N
+    for name, t, need in (("A", a, need_a), ("B", b, need_b), ("C", out, need_c)):
+        if t is None or t.device.type == "meta":
+            continue
+        # views (a column block of qkv, ...) address their storage past their own numel
+        avail = t.untyped_storage().nbytes() // t.element_size() - t.storage_offset()
+        if need > avail:
+            raise ValueError(f"charpt {what}: operand {name} needs {need} elements for M={M} N={N} K={K} "
+                             f"(trans {int(a_trans)}{int(b_trans)}, ld {lda}/{ldb}/{ldc}), its storage has {avail}")
+
+
 @_op("gemm", ("out", "ws"))
 def gemm(a: Tensor, b: Tensor, out: Tensor, op_bf16: bool, a_trans: bool, b_trans: bool, M: int, N: int, K: int,
          lda: int, ldb: int, ldc: int, epi: int, bias: Optional[Tensor], resid: Optional[Tensor], ld_resid: int,
          aux: Optional[Tensor], ld_aux: int, dropout_p: float, seed: int, rng_call: Optional[Tensor], site: int,
-         beta: float, split_k: int, ws: Optional[Tensor]) -> None:
+         beta: float, split_k: int, ws: Optional[Tensor], flags: int = 0) -> None:
+    """flags: cg_epilogue_t.flags (L.GEMM_SLAB_BF16 | L.GEMM_DEFER_REDUCE) of a split-K weight gradient."""
+    _gemm_extents(a, b, out, a_trans, b_trans, M, N, K, lda, ldb, ldc)
     e = L.Epilogue(epi, L.ptr(bias), L.ptr(resid), ld_resid, L.ptr(aux),
                    L.dtype_code(aux.dtype) if aux is not None else 0, ld_aux, dropout_p, seed, L.ptr(rng_call), site,
-                   beta)
+                   beta, None, flags)
     L.check(L.load().cg_gemm(L.CG_BF16 if op_bf16 else L.CG_F32, int(a_trans), int(b_trans), M, N, K, L.ptr(a), lda,
                              L.ptr(b), ldb, L.ptr(out), L.dtype_code(out.dtype), ldc, e, split_k, L.ptr(ws), _s(out)),
             "gemm")
@@ -173,6 +192,7 @@ def gemm_bias_relu_bits(a: Tensor, b: Tensor, out: Tensor, M: int, N: int, K: in
     """out = bf16 relu(a[M,K] @ b[N,K]^T + bias) and its ReLU keep bits (CG_BITS: int32 words
     [M, ld_bits], bit n % 32 of word n / 32 = out[m, n] != 0) for the ReLU-backward dgrad.  Fails
     (CG_EINVAL) unless cg_gemm_relu_bits_supported."""
+    _gemm_extents(a, b, out, False, False, M, N, K, lda, ldb, ldc, "gemm_bias_relu_bits")
     e = L.Epilogue(L.EPI_BIAS_RELU, L.ptr(bias), None, 0, L.ptr(bits), L.CG_BITS, ld_bits, 0.0, 0, None, 0, 0.0)
     L.check(L.load().cg_gemm(L.CG_BF16, 0, 0, M, N, K, L.ptr(a), lda, L.ptr(b), ldb, L.ptr(out),
                              L.dtype_code(out.dtype), ldc, e, 1, None, _s(out)), "gemm_bias_relu_bits")
@@ -184,6 +204,7 @@ def gemm_relu_bwd_colpart(a: Tensor, b: Tensor, out: Tensor, M: int, N: int, K: 
     """out = relu_bwd(a[M,K] @ b[N,K]^T, aux) in bf16 with the column sums of every 64-row block of
     the output into colpart [M/64, N] (the consumer's bias-gradient partials; cg_reduce_rows folds
     them).  Fails (CG_EINVAL) unless the dispatch takes the 128x128 persistent kernel."""
+    _gemm_extents(a, b, out, False, True, M, N, K, lda, ldb, ldc, "gemm_relu_bwd_colpart")
     e = L.Epilogue(L.EPI_RELU_BWD, None, None, 0, L.ptr(aux), L.dtype_code(aux.dtype), ld_aux, 0.0, 0, None, 0, 0.0,
                    L.ptr(colpart))
     L.check(L.load().cg_gemm(L.CG_BF16, 0, 1, M, N, K, L.ptr(a), lda, L.ptr(b), ldb, L.ptr(out),
@@ -196,6 +217,7 @@ def gemm_store_rowdot(a: Tensor, b: Tensor, out: Tensor, M: int, N: int, K: int,
     """out = bf16(a[M,K] @ b[N,K]^T) (the attention-output gradient dO) and the attention backward's
     delta[b, h, t] = sum_e out[b*T + t, 64h + e] * o[b*T + t, 64h + e] (fp32 [M/T, N/64, T]) from
     the rounded values.  Fails (CG_EINVAL) unless cg_gemm_rowdot_supported."""
+    _gemm_extents(a, b, out, False, True, M, N, K, lda, ldb, ldc, "gemm_store_rowdot")
     e = L.Epilogue(L.EPI_STORE_ROWDOT, None, None, T, L.ptr(o), L.dtype_code(o.dtype), ld_o, 0.0, 0, None, 0, 0.0,
                    L.ptr(delta))
     L.check(L.load().cg_gemm(L.CG_BF16, 0, 1, M, N, K, L.ptr(a), lda, L.ptr(b), ldb, L.ptr(out),
@@ -207,8 +229,10 @@ def gemm_rowdot_supported(M, N, K, lda, ldb, ldc):
 
 
 @_op("reduce_rows", ("out",))
-def reduce_rows(part: Tensor, rows: int, N: int, out: Tensor, accumulate: bool) -> None:
-    L.check(L.load().cg_reduce_rows(L.ptr(part), rows, N, L.ptr(out), int(accumulate), _s(out)), "reduce_rows")
+def reduce_rows(part: Tensor, rows: int, N: int, out: Tensor, accumulate: bool, defer: bool = False) -> None:
+    """defer: queued on the stream's deferral queue (CG_DEFER) until cg_flush_deferred."""
+    L.check(L.load().cg_reduce_rows_ex(L.ptr(part), rows, N, L.ptr(out), int(accumulate), L.DEFER if defer else 0,
+                                       _s(out)), "reduce_rows")
 
 
 def gemm_workspace(M, N, split_k):
@@ -303,11 +327,13 @@ def head_fwd(a: Tensor, wpad: Tensor, bias: Tensor, targets: Optional[Tensor], l
 
 @_op("head_bwd", ("dl", "db", "ws"))
 def head_bwd(logits: Tensor, lse: Tensor, targets: Optional[Tensor], g_loss: Optional[Tensor], g_mult: float,
-             g_logits: Optional[Tensor], dl: Tensor, db: Optional[Tensor], db_accumulate: bool, ws: Tensor) -> None:
+             g_logits: Optional[Tensor], dl: Tensor, db: Optional[Tensor], db_accumulate: bool, ws: Tensor,
+             defer: bool = False) -> None:
+    """defer: the db column-sum reduce is queued on the stream's deferral queue (CG_DEFER)."""
     M, V = logits.shape
-    L.check(L.load().cg_head_bwd(L.ptr(logits), L.ptr(lse), L.ptr(targets), L.ptr(g_loss), g_mult, L.ptr(g_logits),
-                                 L.ptr(dl), dl.stride(0), L.ptr(db), int(db_accumulate), L.ptr(ws), M, V, _s(logits)),
-            "head_bwd")
+    L.check(L.load().cg_head_bwd_ex(L.ptr(logits), L.ptr(lse), L.ptr(targets), L.ptr(g_loss), g_mult,
+                                    L.ptr(g_logits), L.ptr(dl), dl.stride(0), L.ptr(db), int(db_accumulate), L.ptr(ws),
+                                    M, V, L.DEFER if defer else 0, _s(logits)), "head_bwd")
 
 
 # ---------------------------------------------------------------------------------------

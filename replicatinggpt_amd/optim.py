@@ -20,6 +20,7 @@ class AdamW(torch.optim.Optimizer):
         self._step_t = None
         self._psteps = None   # per-parameter step counts, once a step skipped some parameter
         self._early = None    # flat (offset, n) ranges updated early this step (functional.EARLY)
+        self._poisoned = None  # why the state is half a step ahead (a failed backward after early updates ran)
 
     # the model whose flat store holds these parameters is found from the parameters, so
     # ``AdamW(m.parameters(), lr=5e-1)`` works exactly as GPT1.py:218 writes it
@@ -70,10 +71,29 @@ class AdamW(torch.optim.Optimizer):
         return (self._psteps is None and self._store.master.is_cuda and
                 all(p.requires_grad for g in self.param_groups for p in g["params"]))
 
+    def _check_poisoned(self):
+        if self._poisoned is not None:
+            raise RuntimeError(f"charpt AdamW: {self._poisoned}; load a checkpoint (load_state_dict) to continue")
+
     def early_begin(self):
         """The step count for this step, on the device, before any early update reads it."""
+        self._check_poisoned()
         ops.counter_add(self._step_t, 1)
         self._early = []
+
+    def early_abort(self, updates_taken):
+        """The backward of a step with early updates failed and its deferred work was discarded
+        (functional.DEFER).  No update ran (``updates_taken`` == 0): the step count goes back and the
+        state is exactly as before the step.  Otherwise some weight matrices already took this step's
+        update and the rest did not: the optimizer refuses further steps until its state is reloaded."""
+        if self._early is None:
+            return
+        self._early = None
+        if updates_taken == 0:
+            ops.counter_add(self._step_t, -1)
+        else:
+            self._poisoned = (f"a failed backward left a half-applied step ({updates_taken} weight-matrix updates "
+                              "ran beside it, the rest did not)")
 
     def early_region(self, region):
         """Queue the update of one packed region whose gradient is final (cg_adamw_defer)."""
@@ -82,6 +102,7 @@ class AdamW(torch.optim.Optimizer):
         n = region.slot.numel()
         if off < 0 or off + n > st.numel or n % 4 or off % 4:
             return
+        Fn.DEFER.note_stream()   # the job sits on this stream's deferral queue until a GEMM takes it / the flush
         ops.adamw_defer(st.master[off:off + n], st.grad[off:off + n], self._m[off:off + n], self._v[off:off + n],
                         st.shadow[off:off + n], *self._args(), self._step_t)
         self._early.append((off, n))
@@ -111,6 +132,7 @@ class AdamW(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         self._ensure()
+        self._check_poisoned()
         Fn.SIDE.join()   # weight gradients computed on the side stream must be final
         st = self._store
         grp = self.param_groups[0]
@@ -131,7 +153,9 @@ class AdamW(torch.optim.Optimizer):
             # updated beside the backward's GEMMs (functional.EarlyAdam): the rest, same arithmetic
             early, self._early = self._early, None
             if missing:
-                raise RuntimeError("charpt AdamW: a parameter had no gradient in a step with early updates")
+                self._early_step_with_missing(early, missing, args)
+                st._shadow_version = st.version()
+                return loss
             segs = self._rest_segments_of(early)
             if len(segs) // 2 <= 64:
                 ops.adamw_segments(st.master, st.grad, self._m, self._v, st.shadow, segs, *args, self._step_t)
@@ -159,6 +183,24 @@ class AdamW(torch.optim.Optimizer):
                           st.shadow[off:off + n], *args, step)
         st._shadow_version = st.version()
         return loss
+
+    def _early_step_with_missing(self, early, missing, args):
+        """A step with early updates in which some parameters had no gradient (torch.optim.AdamW
+        skips those: no decay, no moment update, no step count).  The early updates ran with the
+        shared count, already advanced; switch to per-parameter counts, take the advance back for
+        the skipped parameters and update the remaining ones one by one with their own counts."""
+        st = self._store
+        self._split_steps()   # every count already includes this step's advance
+        skip = {id(p) for p in missing}
+        for i, p, off in self._param_slices():
+            if id(p) in skip:
+                ops.counter_add(self._psteps[i:i + 1], -1)
+                continue
+            if any(a <= off < a + n for a, n in early):
+                continue   # updated beside the backward
+            n = p.numel()
+            ops.adamw(st.master[off:off + n], st.grad[off:off + n], self._m[off:off + n], self._v[off:off + n],
+                      st.shadow[off:off + n], *args, self._psteps[i:i + 1])
 
     def _split_steps(self):
         """Switch to per-parameter step counts (first step on which some parameter had no grad)."""
@@ -220,6 +262,7 @@ class AdamW(torch.optim.Optimizer):
                 self._m[off:off + n].copy_(s["exp_avg"].reshape(-1))
                 self._v[off:off + n].copy_(s["exp_avg_sq"].reshape(-1))
                 steps.append(int(float(s["step"])))
+        self._poisoned = None
         if len(set(steps)) <= 1:
             self._psteps = None
             self._step_t.fill_(steps[0] if steps else 0)

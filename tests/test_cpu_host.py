@@ -171,3 +171,18 @@ def test_checkpoint_roundtrip_cpu(tmp_path):
     assert len(sd) == len(b.state_dict()) and sum(k.endswith("tril") for k in sd) == 2 * 4
     with pytest.raises(ValueError):
         ck.load_checkpoint(mp, b)
+
+
+def test_gemm_operand_extent_guard():
+    """ops.gemm checks on the host that every element cg_gemm will address lies in its operand's
+    storage (the C ABI sees only pointers): a transposed-B layout given an [N, K] tensor is refused
+    before any launch; a column-block view addressed through its parent's row stride passes."""
+    from replicatinggpt_amd.ops import _gemm_extents
+    parent = torch.empty(100, 30)
+    _gemm_extents(parent[:, 10:20], torch.empty(5, 10), torch.empty(100, 5), False, False, 100, 5, 10, 30, 10, 5)
+    with pytest.raises(ValueError, match="operand B"):
+        _gemm_extents(torch.empty(256, 64), torch.empty(32, 64), torch.empty(256, 32), False, True, 256, 32, 64, 64,
+                      64, 32)
+    with pytest.raises(ValueError, match="operand C"):
+        _gemm_extents(torch.empty(256, 64), torch.empty(32, 64), torch.empty(255, 32), False, False, 256, 32, 64, 64,
+                      64, 32)

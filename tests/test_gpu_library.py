@@ -168,3 +168,112 @@ def test_wgrad_into_temporary_inside_defer_is_complete():
         snap = tmp.clone()
     torch.cuda.synchronize()
     assert torch.equal(snap, ref)
+
+
+def _deferred_workload(seed):
+    """One stream's share of a training backward's deferred work (include/charpt.h "deferred work"):
+    a split-K weight gradient with bf16 slabs and a deferred reduce, a queued column-sum reduce, an
+    AdamW update of that gradient queued for a GEMM's free blocks, a part-filling persistent GEMM
+    (out[16384, 384] = a b^T: 384 128x128 items on 512 slots, like the N = 384 dgrads) that takes the
+    pending jobs, and the stream's flush.  Operand extents: a [16384, 1152], b [384, 1152] (NT)."""
+    from replicatinggpt_amd import _lib as L
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    M, N, K = 384, 1536, 16384
+    t = {"dy": torch.randn(K, M, device=DEV, generator=g).to(torch.bfloat16),
+         "x": torch.randn(K, N, device=DEV, generator=g).to(torch.bfloat16),
+         "part": torch.randn(256, 1152, device=DEV, generator=g),
+         "a": torch.randn(16384, 1152, device=DEV, generator=g).to(torch.bfloat16),
+         "b": torch.randn(384, 1152, device=DEV, generator=g).to(torch.bfloat16),
+         "p": torch.randn(M * N, device=DEV, generator=g) * 0.02}
+    t["ws"] = torch.empty(_ops().gemm_workspace(M, N, 14) // 4, device=DEV)
+    t["gw"] = torch.empty(M, N, device=DEV)
+    t["gb"] = torch.zeros(1152, device=DEV)
+    t["m"], t["v"] = torch.zeros_like(t["p"]), torch.zeros_like(t["p"])
+    t["pb"] = torch.empty(M * N, dtype=torch.bfloat16, device=DEV)
+    t["out"] = torch.empty(16384, 384, dtype=torch.bfloat16, device=DEV)
+    t["step"] = torch.ones(1, dtype=torch.int64, device=DEV)
+    flags = L.GEMM_SLAB_BF16 | L.GEMM_DEFER_REDUCE
+    return t, flags
+
+
+def _run_deferred(t, flags, sync=None):
+    import ctypes
+    from replicatinggpt_amd import _lib as L
+    O = _ops()
+    step = sync or (lambda: None)
+    M, N, K = 384, 1536, 16384
+    step()
+    O.gemm(t["dy"], t["x"], t["gw"], True, True, True, M, N, K, M, N, N, 0, None, None, 0, None, 0, 0.0, 0, None, 0,
+           0.0, 14, t["ws"], flags)
+    step()
+    O.reduce_rows(t["part"], 256, 1152, t["gb"], False, True)
+    step()
+    O.adamw_defer(t["p"], t["gw"].view(-1), t["m"], t["v"], t["pb"], 1e-3, 0.9, 0.999, 1e-8, 0.01, t["step"])
+    step()
+    O.gemm(t["a"], t["b"], t["out"], True, False, False, 16384, 384, 1152, 1152, 1152, 384, 0, None, None, 0, None,
+           0, 0.0, 0, None, 0, 0.0, 1, None)
+    step()
+    L.check(L.load().cg_flush_deferred(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+
+
+def test_deferred_work_two_threads_two_streams_match_single_thread():
+    """deferral is per call and its queues per stream, so two host threads, each
+    driving its own stream with deferred split-K reduces, queued column sums and deferred AdamW
+    jobs -- their library calls interleaved step by step through a barrier -- produce exactly the
+    bits of the same two workloads run one after the other on one thread."""
+    import threading
+    ref = []
+    for seed in (11, 12):
+        t, flags = _deferred_workload(seed)
+        _run_deferred(t, flags)
+        torch.cuda.synchronize()
+        ref.append({k: v.clone() for k, v in t.items()})
+    work = [_deferred_workload(seed) for seed in (11, 12)]
+    streams = [torch.cuda.Stream() for _ in work]
+    torch.cuda.synchronize()
+    bar = threading.Barrier(2)
+    errs = []
+
+    def body(i):
+        try:
+            torch.cuda.set_device(0)
+            with torch.cuda.stream(streams[i]):
+                _run_deferred(*work[i], sync=lambda: bar.wait(timeout=60))
+        except BaseException as e:   # noqa: BLE001 -- reported below
+            errs.append(e)
+            bar.abort()
+
+    th = [threading.Thread(target=body, args=(i,)) for i in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    torch.cuda.synchronize()
+    assert not errs, errs
+    for (t, _), r in zip(work, ref):
+        for k in ("gw", "gb", "p", "m", "v", "pb", "out"):
+            assert torch.equal(t[k], r[k]), k
+
+
+def test_discard_deferred_reports_taken_adam_jobs():
+    """cg_discard_deferred drops a stream's queue without launching it and reports how many
+    deferred AdamW jobs launches had already taken (a failed backward: 0 = no parameter touched)."""
+    import ctypes
+    from replicatinggpt_amd import _lib as L
+    O = _ops()
+    t, flags = _deferred_workload(5)
+    t["gw"].fill_(0.125)
+    p0 = t["p"].clone()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    n = ctypes.c_int(-1)
+    O.adamw_defer(t["p"], t["gw"].view(-1), t["m"], t["v"], t["pb"], 1e-3, 0.9, 0.999, 1e-8, 0.01, t["step"])
+    L.check(L.load().cg_discard_deferred(st, ctypes.byref(n)))
+    L.check(L.load().cg_flush_deferred(st))
+    torch.cuda.synchronize()
+    assert n.value == 0 and torch.equal(t["p"], p0)
+    O.adamw_defer(t["p"], t["gw"].view(-1), t["m"], t["v"], t["pb"], 1e-3, 0.9, 0.999, 1e-8, 0.01, t["step"])
+    O.gemm(t["a"], t["b"], t["out"], True, False, False, 16384, 384, 1152, 1152, 1152, 384, 0, None, None, 0, None,
+           0, 0.0, 0, None, 0, 0.0, 1, None)   # 384 items on 512 slots: its free blocks take the job
+    L.check(L.load().cg_discard_deferred(st, ctypes.byref(n)))
+    torch.cuda.synchronize()
+    assert n.value == 1 and not torch.equal(t["p"], p0)

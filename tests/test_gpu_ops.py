@@ -430,7 +430,7 @@ def test_gemm_tile_order_is_bitwise_invariant(M, N, K, split):
                                          (256, 2048, 4096, 4)])
 @pytest.mark.parametrize("defer", [False, True])
 def test_gemm_bf16_slabs(M, N, K, split, defer):
-    """cg_set_tuning("slab_bf16") (the training backward's weight gradients, GPT1.py:232 backward):
+    """cg_epilogue_t.flags CG_GEMM_SLAB_BF16 (the training backward's weight gradients, GPT1.py:232 backward):
     the split-K partial sums go through bf16 slabs.  The output is exactly the fp32 sum, in split
     order, of each split's fp32 partial (a split-1 GEMM over that K chunk: same MFMA order) rounded
     to bf16 -- bit for bit, with the reduce in line or deferred into the next GEMM's tail / the
@@ -442,20 +442,15 @@ def test_gemm_bf16_slabs(M, N, K, split, defer):
     B = (torch.randn(K, N, device=DEV) * 0.5).to(torch.bfloat16)
     ws = torch.empty(ops().gemm_workspace(M, N, split) // 4, dtype=torch.float32, device=DEV)
     out = torch.full((M, N), float("nan"), device=DEV)
-    try:
-        L.check(lib.cg_set_tuning(b"slab_bf16", 1))
-        L.check(lib.cg_set_tuning(b"defer_splitk", int(defer)))
-        ops().gemm(A, B, out, True, True, True, M, N, K, M, N, N, 0, None, None, 0, None, 0, 0.0, 0, None, 0, 0.0,
-                   split, ws)
-        if defer:   # a later persistent launch on the stream takes the pending reduce in its tail
-            x = torch.randn(256, 128, device=DEV).to(torch.bfloat16)
-            y = torch.empty(256, 128, dtype=torch.bfloat16, device=DEV)
-            ops().gemm(x, x[:128], y, True, False, False, 256, 128, 128, 128, 128, 128, 0, None, None, 0, None, 0,
-                       0.0, 0, None, 0, 0.0, 1, None)
-            L.check(lib.cg_flush_deferred(L.ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
-    finally:
-        L.check(lib.cg_set_tuning(b"slab_bf16", 0))
-        L.check(lib.cg_set_tuning(b"defer_splitk", 0))
+    flags = L.GEMM_SLAB_BF16 | (L.GEMM_DEFER_REDUCE if defer else 0)
+    ops().gemm(A, B, out, True, True, True, M, N, K, M, N, N, 0, None, None, 0, None, 0, 0.0, 0, None, 0, 0.0,
+               split, ws, flags)
+    if defer:   # a later persistent launch on the stream takes the pending reduce in its tail
+        x = torch.randn(256, 128, device=DEV).to(torch.bfloat16)
+        y = torch.empty(256, 128, dtype=torch.bfloat16, device=DEV)
+        ops().gemm(x, x[:128], y, True, False, False, 256, 128, 128, 128, 128, 128, 0, None, None, 0, None, 0,
+                   0.0, 0, None, 0, 0.0, 1, None)
+        L.check(lib.cg_flush_deferred(L.ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
     kc = -(-(K // 64) // split) * 64
     want = None
     for sp in range(split):
@@ -1024,7 +1019,7 @@ def test_bf16_rounding_matches_torch():
 
 
 def test_deferred_partial_reduces_match_immediate():
-    """cg_set_tuning("defer_partials"): cg_reduce_rows / cg_layernorm_bwd_reduce calls are queued and
+    """CG_DEFER (cg_reduce_rows_ex / cg_layernorm_bwd_reduce_ex): the reduce calls are queued and
     cg_flush_deferred runs them as one multi-job kernel -- the same per-job bits as the immediate
     launches, including a second job accumulating into the first job's output (queued jobs whose
     outputs it overlaps are flushed first) and an immediate reduce into a queued output."""
@@ -1039,18 +1034,12 @@ def test_deferred_partial_reduces_match_immediate():
 
     def run(defer):
         outs = [torch.full((n,), 0.5, device=DEV) for _, n in shapes]
-        if defer:
-            L.check(lib.cg_set_tuning(b"defer_partials", 1))
-        try:
-            for p, o in zip(parts, outs):
-                O.reduce_rows(p, p.shape[0], p.shape[1], o, False)
-            O.reduce_rows(extra, 128, 1536, outs[1], True)         # accumulates onto a queued output
-            ws = torch.empty(O.colsum_workspace(64, 384) // 4 + 1, device=DEV)
-            O.colsum(extra[:64, :384].contiguous(), outs[3], True, ws)   # immediate reduce, queued target
-            O.reduce_rows(parts[0], 256, 1152, outs[0], True)
-        finally:
-            if defer:
-                L.check(lib.cg_set_tuning(b"defer_partials", 0))
+        for p, o in zip(parts, outs):
+            O.reduce_rows(p, p.shape[0], p.shape[1], o, False, defer)
+        O.reduce_rows(extra, 128, 1536, outs[1], True, defer)         # accumulates onto a queued output
+        ws = torch.empty(O.colsum_workspace(64, 384) // 4 + 1, device=DEV)
+        O.colsum(extra[:64, :384].contiguous(), outs[3], True, ws)   # immediate reduce, queued target
+        O.reduce_rows(parts[0], 256, 1152, outs[0], True, defer)
         L.check(lib.cg_flush_deferred(ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
         torch.cuda.synchronize()
         return [o.cpu() for o in outs]

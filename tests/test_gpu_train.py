@@ -202,3 +202,93 @@ def test_gpt1_driver_loss_curve_matches_reference(tmp_path, capsys, dtype, tol0)
     assert sum(len(s) for s in sample) + len(sample) - 1 == 41    # decode of 1 + 40 tokens
     sd = torch.load(out, weights_only=True)
     assert len(sd) == 210 and sum(k.endswith("tril") for k in sd) == 36
+
+
+@pytest.mark.parametrize("fail_at", [1, 9])
+def test_failed_backward_with_early_adamw(fail_at):
+    """a backward that raises inside a step with early AdamW updates.  DEFER
+    discards its queued work (cg_discard_deferred) instead of flushing it.  Raised before any
+    weight-matrix update ran (the 1st weight gradient, C2-width model), the optimizer takes its
+    step count back: master, m, v, shadow and step count equal the state before the step, and the
+    next step is the step an uninterrupted loop would take.  Raised after some updates ran (the 9th:
+    the last layer's matrices were already updated beside its dgrads), the optimizer refuses
+    further steps until its state is reloaded."""
+    from replicatinggpt_amd import functional as Fn
+    from replicatinggpt_amd.engine import TrainStep
+    cfg = _cfg(block_size=256, n_embd=384, n_head=6, n_layers=2, batch_size=16)
+    m, opt, s = _setup(cfg)
+    st = TrainStep(m, opt, s, use_graph=False)
+    st.sampler.get_batch("train", out=(st.x, st.y))
+    st._eager()
+    torch.cuda.synchronize()
+    assert Fn.EARLY.enabled and opt.early_ok()
+
+    def snap():
+        torch.cuda.synchronize()
+        return [t.detach().clone() for t in (m.flat.master, opt._m, opt._v, opt._step_t, m.flat.shadow)]
+
+    before = snap()
+    real, calls = Fn.linear_wgrad, [0]
+
+    def failing(*a, **k):
+        calls[0] += 1
+        if calls[0] == fail_at:
+            raise RuntimeError("injected")
+        return real(*a, **k)
+
+    Fn.linear_wgrad = failing
+    try:
+        with pytest.raises(RuntimeError, match="injected"):
+            st._eager()
+    finally:
+        Fn.linear_wgrad = real
+    after = snap()
+    same = all(torch.equal(a, b) for a, b in zip(before, after))
+    if fail_at == 1:
+        assert same and opt._poisoned is None
+        st._eager()   # continues as if the failed step had not happened
+        torch.cuda.synchronize()
+        assert int(opt._step_t.item()) == int(before[3].item()) + 1
+    else:
+        assert not same and opt._poisoned is not None
+        with pytest.raises(RuntimeError, match="half-applied"):
+            st._eager()
+        sd = opt.state_dict()
+        opt.load_state_dict(sd)   # reloading the state clears the refusal
+        st._eager()
+        torch.cuda.synchronize()
+
+
+def test_missing_grad_in_early_step_skips_like_torch():
+    """with early updates on, a parameter without .grad is skipped as
+    torch.optim.AdamW skips it (no decay, no moments, its step count stays) while every other
+    parameter takes the step -- the same result as the same step with the early path off."""
+    from replicatinggpt_amd import functional as Fn
+    cfg = _cfg(block_size=256, n_embd=384, n_head=6, n_layers=2, batch_size=16)
+    res = []
+    saved = Fn.EARLY.enabled
+    try:
+        for early in (False, True):
+            Fn.EARLY.enabled = early
+            m, opt, s = _setup(cfg)
+            x, y = s.get_batch("train")
+            for it in range(2):
+                _, loss = m(x, y)
+                opt.zero_grad(set_to_none=True)
+                began = Fn.EARLY.begin(opt) if early else False
+                try:
+                    with Fn.DEFER:
+                        loss.backward()
+                finally:
+                    Fn.EARLY.end()
+                if it == 1:
+                    m.ln_f.weight.grad = None   # this parameter skips step 2
+                opt.step()
+            assert began == early
+            torch.cuda.synchronize()
+            sd = opt.state_dict()
+            res.append((m.flat.master.detach().cpu().clone(), [float(v["step"]) for v in sd["state"].values()]))
+    finally:
+        Fn.EARLY.enabled = saved
+    assert torch.equal(res[0][0], res[1][0])
+    assert res[0][1] == res[1][1] and 1.0 in res[0][1] and 2.0 in res[0][1]

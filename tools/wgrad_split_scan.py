@@ -1,4 +1,4 @@
-"""Split-K scan of the weight-gradient GEMMs with bf16 slabs (cg_set_tuning "slab_bf16", the training
+"""Split-K scan of the weight-gradient GEMMs with bf16 slabs (cg_epilogue_t.flags CG_GEMM_SLAB_BF16, the training
 step's form): GEMM + standalone slab reduce per call, hipGraph of 20 calls (bench._time_ms), against
 the split functional._wgrad_split picks.  GPU only.
 usage: python tools/wgrad_split_scan.py [c2|c4] [splits]"""
@@ -18,7 +18,6 @@ def main():
     splits = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "8,12,14,16,18,24,28,32,40,48,56,64").split(",")]
     d, M = (384, 16384) if cfg == "c2" else (768, 65536)
     lib = L.load()
-    L.check(lib.cg_set_tuning(b"slab_bf16", 1))
     for name, m, n in (("proj_wgrad", d, d), ("qkv_wgrad", 3 * d, d), ("ffn2_wgrad", d, 4 * d),
                        ("ffn1_wgrad", 4 * d, d)):
         A = (torch.randn(M, m, device="cuda") * 0.5).to(torch.bfloat16)
@@ -35,11 +34,10 @@ def main():
 
             def run(sp=sp, ws=ws):
                 ops.gemm(A, B, out, True, True, True, m, n, M, m, n, n, 0, None, None, 0, None, 0, 0.0, 0, None, 0,
-                         0.0, sp, ws)
+                         0.0, sp, ws, L.GEMM_SLAB_BF16)
             t = bench._time_ms(run) * 1e3
             line += f" s{sp} {t:5.1f}"
         print(line, flush=True)
-    L.check(lib.cg_set_tuning(b"slab_bf16", 0))
 
 
 if __name__ == "__main__":
