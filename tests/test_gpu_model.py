@@ -441,3 +441,30 @@ def test_fused_b1_gradient_training_parity():
     for a, b in zip(runs[0][0], runs[1][0]):
         assert abs(a - b) < 1e-4 * abs(b)
     assert relerr(runs[1][1], runs[0][1]) < 1e-3
+
+
+def test_decode_engine_c5_batch_matches_reference_loop():
+    """C5 at the benchmarked batch (bench.bench_generate: 256 sequences x 500 new tokens, greedy,
+    the reference-trained C1 weights = the model.pth of GPT1.py:239-241): the decode engine's 256-row
+    batch through both phases (K/V cache up to block_size, then the sliding window) equals the
+    reference's literal loop (GPT1.py:196-212, full forward per token) row by row on a slice of rows
+    with distinct prompts, and from the bench's zeros prompt every row is the reference's own greedy
+    stream (tests/golden/trained_c1.pt)."""
+    from safetensors.torch import load_file
+    from replicatinggpt_amd import BigramLanguageModel, GPTConfig
+    sd = load_file(golden_path("model_c1_trained.safetensors"))
+    gold = torch.load(golden_path("trained_c1.pt"), weights_only=True)
+    m = BigramLanguageModel(GPTConfig(dtype="fp32"))
+    m.load_state_dict(sd, strict=False)
+    m = m.to(DEV).eval()
+    g = torch.Generator().manual_seed(21)
+    idx = torch.randint(0, 65, (256, 1), generator=g).to(DEV)
+    rows = torch.tensor([0, 1, 77, 128, 200, 255], device=DEV)
+    with torch.no_grad():
+        got = m.generate(idx, 500, greedy=True)
+        want = m.generate(idx[rows], 500, greedy=True, engine=False)
+        zeros = m.generate(torch.zeros((256, 1), dtype=torch.long, device=DEV), 500, greedy=True)
+    assert got.shape == (256, 501)
+    assert torch.equal(got[rows], want)
+    ref = gold["streams"]["zeros"]["tokens"][0].to(DEV)
+    assert torch.equal(zeros, ref.expand(256, -1))
