@@ -383,6 +383,7 @@ int g_gemm_group_pk = 0;
 int g_gemm_n96 = 1;       // cg_set_tuning("gemm_n96"): 128x96 tiles for the part-filling fp32 residual forwards (gemm_pk.hip launch_n96)
 int g_adam_per_launch = 0;   // cg_set_tuning("adam_per_launch"): AdamW jobs one launch's free blocks take (0 = MAX_ADAM)
 int g_red_side = 1;       // cg_set_tuning("red_side"): a part-filling persistent launch takes a pending reduce on extra blocks
+int g_adam_batch = 1;     // cg_set_tuning("adam_batch"), A/B build only: the side blocks' AdamW chunks in flight per thread
 
 static int current_device() {
     int d = -1;
@@ -425,6 +426,9 @@ RedJobs take_pending_reduces(hipStream_t st, bool side_ok) {
         q->nadam -= r.na;
         q->adam_taken += r.na;
     }
+#ifdef CG_AB_VARIANTS
+    r.adam_batch = g_adam_batch;
+#endif
     return r;
 }
 
@@ -535,6 +539,13 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     }
     if (!strcmp(key, "adam_per_launch")) {
         g_adam_per_launch = value;
+        return CG_OK;
+    }
+    if (!strcmp(key, "adam_batch")) {
+#ifndef CG_AB_VARIANTS
+        CG_REQUIRE(value == 1, "cg_set_tuning: adam_batch %d is an A/B variant, not in this build (make ab)", value);
+#endif
+        g_adam_batch = value;
         return CG_OK;
     }
     if (!strcmp(key, "red_side")) {

@@ -111,6 +111,7 @@ struct RedJobs {
     int n;
     AdamJob a[MAX_ADAM];
     int na;   // AdamW jobs: only a launch with free blocks (red_tail `first` > 0) is given any
+    int adam_batch;   // A/B build only (cg_set_tuning "adam_batch"): chunks in flight per thread (1 = product loop)
 };
 // gemm.hip: pending jobs (cleared) for a launch on st -- the split-K reduces, and with side_ok (the
 // launch has >= SIDE_MIN free blocks) the AdamW jobs; has_pending_reduces: whether it would take any
@@ -170,7 +171,54 @@ __device__ __forceinline__ void red_tail(const RedJobs& r, int first = 0) {
             *o = s;
         }
     }
-    // AdamW jobs (free blocks only: first > 0): float4 chunk per thread per step, adam_one per element
+#ifdef CG_AB_VARIANTS
+    // A/B: four float4 chunks in flight per thread, all loads first.  Batch b of
+    // thread t holds chunks t + (4 b + s) nthr, s = 0..3 -- disjoint batches (stride 4 nthr), so every
+    // chunk is updated exactly once, as in the product loop below.
+    // adam_batch 5: the same loop with batches stepping by nthr (overlapping: chunk t + k nthr is
+    // re-processed by up to four batches of thread t) -- the candidate cause of round 4's failure
+    if (r.adam_batch == 4 || r.adam_batch == 5) {
+        const int64_t stride = r.adam_batch == 4 ? 4 * nthr : nthr;
+        for (int q = 0; q < r.na; ++q) {
+            const AdamJob& J = r.a[q];
+            const AdamScalars sc = adam_scalars(J.lr, J.beta1, J.beta2, J.eps, J.wd, J.step);
+            for (int64_t i0 = t0; i0 < J.n4; i0 += stride) {
+                fv4 pv[4], gv[4], mv[4], vv[4];
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const int64_t i = i0 + s * nthr;
+                    if (i < J.n4) {
+                        pv[s] = *(const fv4*)(J.p + 4 * i);
+                        gv[s] = *(const fv4*)(J.g + 4 * i);
+                        mv[s] = *(const fv4*)(J.m + 4 * i);
+                        vv[s] = *(const fv4*)(J.v + 4 * i);
+                    }
+                }
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const int64_t i = i0 + s * nthr;
+                    if (i < J.n4) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            float me = mv[s][e], ve = vv[s][e];
+                            pv[s][e] = adam_one(pv[s][e], gv[s][e], me, ve, sc);
+                            mv[s][e] = me;
+                            vv[s][e] = ve;
+                        }
+                        *(fv4*)(J.p + 4 * i) = pv[s];
+                        *(fv4*)(J.m + 4 * i) = mv[s];
+                        *(fv4*)(J.v + 4 * i) = vv[s];
+                        *(uint2*)(J.pb + 4 * i) = make_uint2(pack_bf2(pv[s][0], pv[s][1]), pack_bf2(pv[s][2], pv[s][3]));
+                    }
+                }
+            }
+        }
+        return;
+    }
+#endif
+    // AdamW jobs (free blocks only: first > 0): float4 chunk per thread per step, adam_one per element.
+    // Thread t of the nthr side threads owns chunks t, t + nthr, t + 2 nthr, ...: each chunk exactly
+    // once (a bijection chunk -> (thread, step)), so no chunk's update can read another's store.
     for (int q = 0; q < r.na; ++q) {
         const AdamJob& J = r.a[q];
         const AdamScalars sc = adam_scalars(J.lr, J.beta1, J.beta2, J.eps, J.wd, J.step);

@@ -1,6 +1,8 @@
 """Which elements a GEMM-hosted deferred AdamW job (cg_adamw_defer taken by a part-filling
 persistent GEMM's free blocks) gets wrong against cg_adamw -- for A/B builds through CHARPT_LIB.
-GPU only.  usage: python tools/early_probe2.py"""
+GPU only.  usage: python tools/early_probe2.py [batch,batch,...]  (the A/B build's cg_set_tuning
+"adam_batch": 1 = product loop, 4 = four disjoint chunks in flight per thread, 5 = four chunks in flight
+with batches stepping by nthr -- overlapping, round 4's candidate bug)."""
 import os
 import sys
 
@@ -11,6 +13,13 @@ from replicatinggpt_amd import _lib as L, ops  # noqa: E402
 
 
 def main():
+    for batch in [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "1").split(",")]:
+        L.check(L.load().cg_set_tuning(b"adam_batch", batch))
+        for rep in range(3):
+            probe(batch, rep)
+
+
+def probe(batch, rep):
     torch.manual_seed(0)
     dev = "cuda"
     n = 1 << 20
@@ -36,7 +45,7 @@ def main():
     bad = (P != ref[0])[a:a + b].view(-1, 4).any(1).nonzero().view(-1)
     same = (P == p)[a:a + b].view(-1, 4).all(1).nonzero().view(-1)
     nthr = 128 * 256
-    print("lib", os.path.basename(L.LIB_PATH), "wrong chunks", bad.numel(), "of", b // 4, "never updated", same.numel(),
+    print("lib", os.path.basename(L.LIB_PATH), "adam_batch", batch, "rep", rep, "wrong chunks", bad.numel(), "of", b // 4, "never updated", same.numel(),
           "first wrong", bad[:6].tolist(), "mod nthr", (bad[:6] % nthr).tolist(), "div nthr", (bad[:6] // nthr).tolist(),
           flush=True)
 
