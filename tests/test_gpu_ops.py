@@ -587,8 +587,10 @@ def test_gemm_store_rowdot(M, C, T):
     assert err <= 1e-5 * max(1.0, exp.abs().max().item()), err
     # outside the persistent kernel's shapes the call fails instead of silently skipping delta
     assert not O.gemm_rowdot_supported(1000, C, C, C, C, C)
-    with pytest.raises(RuntimeError):
-        O.gemm_store_rowdot(dy[:1000], w, do[:1000], 1000, C, C, C, C, C, o[:1000], C, 200, delta)
+    dy1, o1 = torch.zeros(1000, C, device=DEV, dtype=torch.bfloat16), torch.zeros(1000, C, device=DEV, dtype=torch.bfloat16)
+    do1 = torch.empty(1000, C, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="ROWDOT"):
+        O.gemm_store_rowdot(dy1, w, do1, 1000, C, C, C, C, C, o1, C, 200, delta)
 
 
 @pytest.mark.parametrize("T", [256, 192, 64])

@@ -292,3 +292,28 @@ def test_missing_grad_in_early_step_skips_like_torch():
         Fn.EARLY.enabled = saved
     assert torch.equal(res[0][0], res[1][0])
     assert res[0][1] == res[1][1] and 1.0 in res[0][1] and 2.0 in res[0][1]
+
+
+def test_c2_width_bf16_loss_curve_tracks_fp32(tmp_path, capsys):
+    """the bf16 path's numerics choices (bf16 split-K slabs for the weight
+    gradients, the early AdamW, bf16 operands / activations) do not shift training at C2 width:
+    GPT1.py's loop (python -m replicatinggpt_amd.gpt1 --preset c2: 6L/6H/384d, block 256; batch 16
+    for time) on input.txt for 200 steps at lr 2e-4, once on the bf16 path and once on the exact fp32
+    HIP path -- same seeded init, same batch offsets, same Philox dropout masks.  The eval losses
+    (estimate_loss every 50 steps over 20 batches) must agree within 0.03 nats at every point, and the
+    training must make progress (the curve falls by > 0.5 nats)."""
+    from replicatinggpt_amd import gpt1
+    curves = {}
+    for dtype in ("fp32", "bf16"):
+        gpt1.main(["--preset", "c2", "--batch-size", "16", "--lr", "2e-4", "--max-iters", "201",
+                   "--eval-interval", "50", "--eval-iters", "20", "--max-new-tokens", "1", "--out", "",
+                   "--dtype", dtype])
+        lines = capsys.readouterr().out.splitlines()
+        pat = re.compile(r"^step (\d+) : train loss (\d+\.\d{4}), val loss = (\d+\.\d{4})$")
+        curves[dtype] = [tuple(float(v) for v in mt.groups()) for mt in map(pat.match, lines) if mt]
+    a, b = curves["fp32"], curves["bf16"]
+    print("fp32", a, "\nbf16", b)
+    assert [c[0] for c in a] == [c[0] for c in b] == [0, 50, 100, 150, 200]
+    for (it, tr, va), (_, tr16, va16) in zip(a, b):
+        assert abs(tr - tr16) <= 0.03 and abs(va - va16) <= 0.03, (it, tr, va, tr16, va16)
+    assert a[0][2] - a[-1][2] > 0.5
