@@ -93,7 +93,7 @@ def cpu_baseline(cfg, seconds=12.0, batch=16):
 COLD_BYTES = 1 << 29   # census operand sets cycle through >= 512 MB: twice the 256 MB Infinity Cache
 
 
-def census_op(name, M, N, K, at, bt, kind, dev, p=0.2, cold=False):
+def census_op(name, M, N, K, at, bt, kind, dev, p=0.2, cold=False, capture=None):
     """Operands and a launch closure for one census GEMM with the epilogue the training step uses
     (functional.py AttnSublayerFn / FFNSublayerFn): "store" (bf16 output), "bias_resid" (fp32
     output = x + o W^T + b: the attention projection), "bias_relu_bits" (bf16 relu(a W1^T + b1) and
@@ -133,6 +133,8 @@ def census_op(name, M, N, K, at, bt, kind, dev, p=0.2, cold=False):
         return st
 
     first = make_set()
+    if capture is not None:   # the caller reads the first operand set's outputs (A/B tools)
+        capture.update(first)
     nbytes = sum(t.numel() * t.element_size() for t in first.values())
     sets = [first] + [make_set() for _ in range(max(1, -(-COLD_BYTES // max(1, nbytes))) - 1)] if cold else [first]
     bias = torch.randn(N, device=dev) * 0.1
