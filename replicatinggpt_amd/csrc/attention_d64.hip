@@ -25,6 +25,7 @@
 
 namespace cg {
 int g_attn_variant = 0;
+int g_attn_bwd_lpt = 1;   // merged resident backward: dK/dV workgroups first per XCD (0: interleaved, A/B)
 
 #ifdef CG_ATTN_STAMPS
 // Diagnostic build only (make attnstamps; tools/attn_stamps.py): per workgroup of the resident
@@ -1425,11 +1426,21 @@ __global__ __launch_bounds__(256, 2) void k_attn_bwd_d64r(int H, const bf16_t* _
                                                           bf16_t* __restrict__ dq, int64_t lddq, bf16_t* __restrict__ dk,
                                                           bf16_t* __restrict__ dv, int64_t lddkv, float scale,
                                                           const uint32_t* __restrict__ mask_fwd,
-                                                          const uint32_t* __restrict__ mask_bwd, float dscale) {
+                                                          const uint32_t* __restrict__ mask_bwd, float dscale,
+                                                          int lpt) {
     __shared__ __attribute__((aligned(16))) char smem[NT * 2 * TILE + 2 * 64 * NT * 4];
     ATTN_STAMP(0, attn_now());
     int x, id;
-    block_coords<false>(x, id);
+    const int n = (int)gridDim.y, w = (int)blockIdx.y;
+    if (lpt && (n & 15) == 0) {
+        // longest first within each XCD: the dispatcher deals workgroup w to XCD w & 7, in order of
+        // w >> 3 there; each XCD owns n/16 consecutive (b, h) and runs all their dK/dV workgroups (22 us
+        // at C2) before their dQ workgroups (16 us), so the 1.5-round grid's second round is dQ only
+        const int half = n >> 4, xcd = w & 7, j = w >> 3, bh0 = xcd * half;
+        id = j < half ? 2 * (bh0 + j) + 1 : 2 * (bh0 + j - half);
+    } else {
+        block_coords<false>(x, id);
+    }
     if (id & 1)
         dkdv_res<DROP, NT, !DIN>(id >> 1, smem, H, q, k, v, ld, dout, ldd, lse, delta, o, ldo, dk, dv, lddkv, scale,
                                  mask_bwd, dscale);
@@ -1786,10 +1797,10 @@ void launch_bwd_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* 
 #define BWDR(DIN_)                                                                                                 \
     RES_SWITCH(T, if (d.mask) k_attn_bwd_d64r<true, NT_, DIN_><<<grid, 256, 0, st>>>(                            \
                           H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, dk, dv, lddkv, scale, d.mask,    \
-                          d.mask_bwd, d.dscale);                                                                    \
+                          d.mask_bwd, d.dscale, g_attn_bwd_lpt);                                                    \
                else k_attn_bwd_d64r<false, NT_, DIN_><<<grid, 256, 0, st>>>(                                     \
                           H, q, k, v, ld, o, ldo, dout, ldd, lse, delta, dq, lddq, dk, dv, lddkv, scale, nullptr,   \
-                          nullptr, 1.f))
+                          nullptr, 1.f, g_attn_bwd_lpt))
         if (delta_ready) {
             BWDR(true);
         } else {

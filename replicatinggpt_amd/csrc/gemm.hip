@@ -483,6 +483,7 @@ void flush_red_locked(DeferQueue& q) {
 
 int g_skip_splitk_reduce = 0;  // measurement knob (WRONG results): time a step without the split-K reduce
 extern int g_attn_variant;  // attention_d64.hip
+extern int g_attn_bwd_lpt;  // attention_d64.hip
 extern int g_ln_rpb;  // layernorm.hip
 extern int g_adamw_mode;  // ce_adamw.hip
 extern int g_ln_waves;  // layernorm.hip
@@ -494,7 +495,8 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     CG_REQUIRE(key, "cg_set_tuning: null key");
     if (!strcmp(key, "gemm_variant")) {
         // default build: automatic (0), the register-staged fallback (2), the persistent 128x128 (9)
-        // and 256x256 (24) tiles, the generic kernels (99); the measured-slower A/B tiles only in
+        // and 256x256 (24) tiles, the generic kernels (99); the measured-slower A/B tiles (among
+        // them 26, the 256x256 tile on the staggered 8-phase schedule) only in
         // libcharpt_hip_ab.so (`make ab`, CG_AB_VARIANTS)
 #ifndef CG_AB_VARIANTS
         CG_REQUIRE(value == 0 || value == 2 || value == 9 || value == 24 || value == 99,
@@ -523,6 +525,11 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     }
     if (!strcmp(key, "pk_flags")) {
         g_pk_flags = value;
+        return CG_OK;
+    }
+    if (!strcmp(key, "attn_bwd_lpt")) {   // A/B: merged resident backward workgroup order (1 = dK/dV first)
+        CG_REQUIRE(value == 0 || value == 1, "cg_set_tuning: attn_bwd_lpt must be 0 or 1");
+        g_attn_bwd_lpt = value;
         return CG_OK;
     }
     if (!strcmp(key, "attn_variant")) {

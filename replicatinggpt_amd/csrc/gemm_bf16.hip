@@ -205,7 +205,7 @@ static bool pk128(int v) { return v == 9; }
 // column partials come from the 128x128 persistent kernel's per-item ReLU-backward epilogue (not its
 // pk_flags bit-1 per-fragment form) and from the 8-wave 256x256 persistent kernel
 static bool colpart_ok(int v, int at, int split_k) {
-    return (v == 24 || (pk128(v) && !(g_pk_flags & 2))) && split_k == 1 && !at;
+    return (v == 24 || v == 26 || (pk128(v) && !(g_pk_flags & 2))) && split_k == 1 && !at;
 }
 
 bool gemm_colpart_supported(int at, int bt, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc) {

@@ -378,37 +378,6 @@ __device__ __forceinline__ void epi_item(fv4 (&acc)[4][4], int64_t mr, int64_t n
     store_item<WIDE>(acc, mr, nc, Cv, c_dtype, ldc);
 }
 
-// Dropout keep nibbles of a wave's 64 x 16NJ item fragment for any NJ: as drop_nibbles, lanes l and
-// l ^ 16 hold the two 4-column halves of one 8-column Philox group, but the pair splits the work by
-// rows -- lane half odd = (lane >> 4) & 1 evaluates rows i = 2 odd, 2 odd + 1 for every j -- and
-// trades one word per j.  Same bits.
-template <int NJ>
-__device__ __forceinline__ void drop_nibbles_rows(const EpiArgs& epi, uint64_t stream, int64_t mr, int64_t nc, int64_t N,
-                                                  uint32_t (&nib)[4][NJ]) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t odd = (lane >> 4) & 1;
-    const int64_t c8 = nc & ~(int64_t)7;
-    uint32_t mine[NJ], other[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-        mine[j] = 0u;
-#pragma unroll
-        for (int ii = 0; ii < 2; ++ii) {
-            const uint64_t idx = (uint64_t)(mr + 16 * (2 * odd + ii)) * (uint64_t)N + (uint64_t)(c8 + 16 * j);
-            mine[j] |= keep8_bits(philox_group(epi.seed, stream, idx >> 3), epi.thr) << (8 * ii);
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) other[j] = (uint32_t)__shfl_xor((int)mine[j], 16, 64);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const uint32_t w = ((uint32_t)(i >> 1) == odd) ? mine[j] : other[j];
-            nib[i][j] = (w >> (8 * (i & 1) + 4 * odd)) & 0xfu;
-        }
-}
-
 // The fp32 residual epilogues (CG_EPI_BIAS_RESID, CG_EPI_BIAS_DROP_RESID) of a 64 x 16NJ wave tile:
 // epi_item's arithmetic and order (bias, dropout, residual), operands loaded before the first store.
 template <int EK, int NJ>

@@ -561,6 +561,46 @@ def test_gemm_n96_matches_128x128_bitwise(M, K, kind):
     if kind == "bias_resid":
         assert relerr(outs[0], ref + resid.double()) < 1e-5
 
+
+@pytest.mark.parametrize("kind", ["bias_resid", "bias_drop_resid"])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_gemm_p8_residual_epilogue_matches_128x128_bitwise(kind, inplace):
+    """The 256x256 kernel's fp32 residual epilogue (gemm_p8.hip P8_RESID: the C4 projection and FFN2
+    forwards, GPT1.py:136,145-147; residual loaded per 32-row half band before its stores, dropout
+    bits from drop_nibbles_rows) against the 128x128 persistent kernel on the same operands: the
+    same K order per output element and the same bias -> dropout -> residual order, so equal bit for
+    bit -- also when the output overwrites the residual in place (x += ...)."""
+    from replicatinggpt_amd import _lib as L
+    Fn, lib = F(), L.load()
+    M, N, K = 1024, 768, 640
+    torch.manual_seed(13)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV)
+    resid = torch.randn(M, N, device=DEV)
+    outs = []
+    try:
+        for v in (24, 9):
+            L.check(lib.cg_set_tuning(b"gemm_variant", v))
+            call = torch.tensor([4], dtype=torch.int64, device=DEV)
+            o = resid.clone() if inplace else torch.full((M, N), float("nan"), device=DEV)
+            r = o if inplace else resid
+            kw = dict(dropout_p=0.2, seed=5, rng_call=call, site=3) if kind == "bias_drop_resid" else {}
+            Fn.linear_fwd(x, w, o, kind, bias=bias, resid=r, **kw)
+            outs.append(o)
+    finally:
+        L.check(lib.cg_set_tuning(b"gemm_variant", 0))
+    torch.cuda.synchronize()
+    assert not torch.isnan(outs[0]).any()
+    assert torch.equal(outs[0], outs[1])
+    ref = x.double() @ w.double().t() + bias.double()
+    if kind == "bias_resid":
+        assert relerr(outs[0], ref + resid.double()) < 1e-5
+    else:
+        keep = philox.keep_mask(5, (4 << 8) | 3, np.arange(M * N), 0.2).reshape(M, N)
+        want = resid.double() + torch.from_numpy(keep).to(DEV).double() * ref * float(np.float32(1 / 0.8))
+        assert relerr(outs[0], want) < 1e-5
+
 @pytest.mark.parametrize("M,C,T", [(16384, 384, 256), (2048, 768, 128), (1024, 384, 64), (512, 128, 256)])
 def test_gemm_store_rowdot(M, C, T):
     """CG_EPI_STORE_ROWDOT (the projection dgrad dO = dy W, GPT1.py:136, with the attention backward's

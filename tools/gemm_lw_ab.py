@@ -1,7 +1,11 @@
 """Loader-wave persistent GEMM (cg_set_tuning "gemm_lw") against the default one, same process:
 every C2 / C4 census op (bench.census_op: the step's fused epilogue) -- outputs compared bit for bit
 between the two variants, then the per-launch time of each (HIP events over a hipGraph replay of 30
-launches, bench.time_gemm), rounds interleaved.  usage: python tools/gemm_lw_ab.py [c2|c4] [rounds]"""
+launches, bench.time_gemm), rounds interleaved.  usage: python tools/gemm_lw_ab.py [c2|c4] [rounds]
+
+Historical: the "gemm_lw" knob and its kernel variant were removed after this A/B (round 5,
+profiles/r5_gemm_loader_wave_ab.txt: +23 % on the C2 family); cg_set_tuning now rejects the key,
+so the script only runs against a tree that still carries the variant."""
 import os
 import statistics
 import sys
