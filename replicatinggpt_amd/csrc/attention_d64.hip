@@ -20,6 +20,7 @@
 //    tile, loaded a tile ahead with the K/V (or Q/dO) staging loads and applied as v_bfe_i32 +
 //    v_and_b32 per element; the 1/(1-p) is applied once at the end.
 #include <float.h>
+#include <type_traits>
 
 #include "attention_common.h"
 
@@ -1703,6 +1704,215 @@ __global__ __launch_bounds__(256, 2) void k_attn_fwd_d64d(int64_t T_, int H, con
     }
 }
 
+#ifdef CG_AB_VARIANTS   // A/B only (attn_variant 4): measured slower than the ring kernel, profiles/r5_attn_fwd_pingpong_ab.txt
+// =====================================================================================
+// Forward at T % 256 == 0, T >= 512: two waves per SIMD in ping-pong (MI355X_MICROARCH.md "Two
+// waves per SIMD"; cdna guide "Fused attention prefill").  One 512-thread workgroup per CU; wave w
+// owns query group g = 2 (w & 3) + (w >> 2) of the 256-query block (team w >> 2: the even / odd
+// groups, so both teams have the same diagonal tail).  A group's key tile t is two items, each one
+// barrier-delimited segment:
+//   M(t) = O^T += V^T P^T of tile t - 1, then S^T = K Q^T of tile t   (16 MFMAs, LDS reads)
+//   V(t) = causal mask, row max, lazy rescale, exp2 / pack / row sums, keep bits   (VALU)
+// and team 1 runs one segment behind team 0, so on every SIMD one wave's MFMA segment sits beside
+// the other's softmax.  Per group the arithmetic and its order are fwd_group_tile's (S, mask,
+// rescale, P, then P V before the next rescale): the same bits as the ring kernel.
+// K/V tiles: 4-slot LDS ring (16 KB each), tile u + 2 requested by LDS-DMA at segment 2u (its slot's
+// previous tile u - 2 was last read, by team 1's P V, in segment 2u - 1), every wave's DMAs of tile
+// u retired by the counted wait + barrier opening segment 2u.  Keep words: the group's FWD tiles
+// 0..ng-1 are contiguous in the mask image, copied once per block into a per-wave LDS region.
+// =====================================================================================
+constexpr int PP_SLOTS = 4, PP_KW_TILES = 16;   // T <= 1024: a group spans <= 16 key tiles
+constexpr int PP_LDS = PP_SLOTS * 2 * TILE + 8 * PP_KW_TILES * 256;   // 64 KB ring + 32 KB keep words
+
+template <bool DROP>
+__device__ __forceinline__ void fwd_pp_block(int qblk, int bh, char* smem, int64_t T_, int H,
+                                             const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+                                             const bf16_t* __restrict__ v, int64_t ld, bf16_t* __restrict__ o,
+                                             int64_t ldo, float* __restrict__ lse, float scale_log2,
+                                             const uint32_t* __restrict__ mask, float dscale) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), team = wave >> 2, wq = wave & 3;
+    const int g = 2 * wq + team;
+    const int b = bh / H, hh = bh % H;
+    const int Q0 = qblk * 256, q0 = Q0 + 32 * g;
+    const int64_t boff = (int64_t)b * T_, ntile = mask_tiles(T_);
+    const bf16_t* kb_ = k + boff * ld + hh * 64;
+    const bf16_t* vb_ = v + boff * ld + hh * 64;
+    const bf16_t* qb_ = q + boff * ld + hh * 64;
+    const int ng = (q0 + 31) / 64 + 1;          // this group's key tiles
+    const int nmax = (Q0 + 255) / 64 + 1;       // the block's (group 7)
+    const uint32_t lds0 = lds_base(smem);
+    const uint32_t kw_lds = lds0 + (uint32_t)(PP_SLOTS * 2 * TILE + wave * PP_KW_TILES * 256);
+    const char* kw = smem + PP_SLOTS * 2 * TILE + wave * PP_KW_TILES * 256;
+    uint32_t doff[2];
+    dma_lane_offs(ld, wq, lane, doff);
+    // tile t: K by team 0's waves, V by team 1's, 2 DMA instructions per wave
+    auto issue_tile = [&](int t) {
+        dma_tile_s(team ? vb_ : kb_, ld, (int64_t)t * 64, doff,
+                   lds0 + (uint32_t)((t & 3) * 2 * TILE + (team ? TILE : 0)), wq);
+    };
+    sv8 qf[4];
+    {
+        const int64_t qa = q0 + (lane & 31);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) gload16(qf[ks], qb_ + qa * ld + 16 * ks + 8 * (lane >> 5));
+    }
+    if constexpr (DROP) {   // keep words of tiles 0..ng-1: 4 tiles (1 KB) per wave-instruction
+        const uint32_t* mrow = mask + ((int64_t)bh * ntile + mask_fwd_tile(q0 >> 5, 0)) * 64;
+        const int nw = ng * 64;
+        for (int i = 0; i < (ng + 3) / 4; ++i) {
+            const int w = i * 256 + lane * 4;
+            dma16sl(mrow, (uint32_t)((w + 4 <= nw ? w : nw - 4) * 4), kw_lds + 1024u * i);   // past ng: unused
+        }
+    }
+    issue_tile(0);
+    if (nmax > 1) issue_tile(1);
+    // Q, keep words and tile 0 landed for every wave (tile 1 may stay in flight)
+    if (nmax > 1) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) asm volatile("" : "+v"(qf[ks]));
+    fv16 oacc[2] = {fv16{}, fv16{}}, s[2] = {fv16{}, fv16{}};
+    sv8 pf[2][2] = {};
+    float m_run = -FLT_MAX;
+    fv4 l_run = fv4{};
+    const sv8 ones = rowsum_ones(lane);
+    // M(t): P V of tile t - 1 (PV), then S of tile t (S); every LDS fragment is read before the first
+    // MFMA.  Both subtiles always: on a diagonal tile whose second subtile lies wholly above the
+    // diagonal, V(t) sets it to -inf, so its P is 0 and it adds exact zeros to l and O (the bits of
+    // fwd_group_tile<.., 1, 0>).
+    auto m_item = [&](int t, auto PV, auto S) {
+        const char* Vi = smem + ((t - 1) & 3) * 2 * TILE + TILE;
+        const char* Ki = smem + (t & 3) * 2 * TILE;
+        sv8 vf[2][2][2], kf[2][4];
+        if constexpr (decltype(PV)::value) {
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int sk = 0; sk < 2; ++sk)
+#pragma unroll
+                    for (int dt = 0; dt < 2; ++dt) vf[kt][sk][dt] = frag_tr(Vi, 32 * kt, sk, 32 * dt, lane);
+        }
+        if constexpr (decltype(S)::value) {
+#pragma unroll
+            for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) kf[sb][ks] = frag_row(Ki, 32 * sb, ks, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (decltype(PV)::value) {
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int sk = 0; sk < 2; ++sk) {
+                    oacc[0] = mfma32(vf[kt][sk][0], pf[kt][sk], oacc[0]);
+                    oacc[1] = mfma32(vf[kt][sk][1], pf[kt][sk], oacc[1]);
+                }
+        }
+        if constexpr (decltype(S)::value) {
+            s[0] = fv16{};
+            s[1] = fv16{};
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+                s[0] = mfma32(kf[0][ks], qf[ks], s[0]);
+                s[1] = mfma32(kf[1][ks], qf[ks], s[1]);
+            }
+        }
+    };
+    // V(t): causal mask, row max, lazy rescale, P (fwd_group_tile's order)
+    auto v_item = [&](int t) {
+        const int rel = q0 - 64 * t;   // this group's first query against the tile's first key
+        uint32_t mw = 0u;
+        if constexpr (DROP) mw = *(const uint32_t*)(kw + t * 256 + lane * 4);
+        if (rel == 32) {
+            mask_upper(s[1], lane & 31, 0, lane, -INFINITY);
+        } else if (rel == 0) {
+            mask_upper(s[0], lane & 31, 0, lane, -INFINITY);
+            s[1] = fv16{} - INFINITY;
+        }
+        rescale_if(tile_max<2>(s) * scale_log2, m_run, l_run, oacc);
+        softmax_pack<DROP, 2>(s, scale_log2, m_run, l_run, mw, pf, ones);
+    };
+    // segment k opens with a barrier; at k = 2u every wave's DMAs of tile u have landed first (tile
+    // u + 1 may stay in flight) and tile u + 2 is requested after it
+    const int nseg = 2 * nmax + 2;
+    auto seg = [&](int kseg) {
+        if (kseg > 0) {
+            if (kseg & 1) {
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            } else if ((kseg >> 1) + 1 < nmax) {
+                asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            }
+        }
+        if (!(kseg & 1) && (kseg >> 1) + 2 < nmax) issue_tile((kseg >> 1) + 2);
+    };
+    using Y = std::true_type;
+    using N_ = std::false_type;
+    // team 0 runs item i in segment i, team 1 in segment i + 1 (items: M(0) V(0) M(1) V(1) .. M(ng));
+    // straight-line bodies per team, so the loop-carried registers need no copies between paths
+    if (team == 0) {
+        seg(0);
+        m_item(0, N_{}, Y{});
+        seg(1);
+        v_item(0);
+#pragma unroll 1
+        for (int t = 1; t < ng; ++t) {
+            seg(2 * t);
+            m_item(t, Y{}, Y{});
+            seg(2 * t + 1);
+            v_item(t);
+        }
+        seg(2 * ng);
+        m_item(ng, Y{}, N_{});
+#pragma unroll 1
+        for (int kseg = 2 * ng + 1; kseg < nseg; ++kseg) seg(kseg);
+    } else {
+        seg(0);
+        seg(1);
+        m_item(0, N_{}, Y{});
+        seg(2);
+        v_item(0);
+#pragma unroll 1
+        for (int t = 1; t < ng; ++t) {
+            seg(2 * t + 1);
+            m_item(t, Y{}, Y{});
+            seg(2 * t + 2);
+            v_item(t);
+        }
+        seg(2 * ng + 1);
+        m_item(ng, Y{}, N_{});
+#pragma unroll 1
+        for (int kseg = 2 * ng + 2; kseg < nseg; ++kseg) seg(kseg);
+    }
+    const float lt = l_run[0];   // every accumulator register holds query lane & 31's sum
+    const int64_t qa = q0 + (lane & 31);
+    store_rows_wide(o + (boff + qa) * ldo + hh * 64, oacc, dscale / lt, lane);
+    if (lane < 32) lse[(int64_t)bh * T_ + qa] = (m_run + __log2f(lt)) * LN2;
+}
+
+template <bool DROP>
+__global__ __launch_bounds__(512, 1) void k_attn_fwd_pp(int64_t T_, int H, const bf16_t* __restrict__ q,
+                                                        const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                                                        int64_t ld, bf16_t* __restrict__ o, int64_t ldo,
+                                                        float* __restrict__ lse, float scale_log2,
+                                                        const uint32_t* __restrict__ mask, float dscale) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int x, bh;
+    block_coords<false>(x, bh);
+    const int nq = (int)(T_ / 256), first = nq - 1 - x;
+    const int npass = x == first ? 1 : 2;
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);   // the younger team
+#pragma unroll 1
+    for (int pass = 0; pass < npass; ++pass) {
+        if (pass) __syncthreads();
+        fwd_pp_block<DROP>(pass ? x : first, bh, smem, T_, H, q, k, v, ld, o, ldo, lse, scale_log2, mask, dscale);
+    }
+}
+
+#endif
+
 }  // namespace
 
 namespace attn {
@@ -1743,6 +1953,18 @@ void launch_fwd_d64(int64_t B, int64_t T, int H, const bf16_t* q, const bf16_t* 
         else
             k_attn_fwd_d64d<false, false><<<grid, 256, 0, st>>>(T, H, q, k, v, ld, o, ldo, lse, scale * LOG2E,
                                                                 nullptr, 1.f);
+        return;
+    }
+#endif
+#ifdef CG_AB_VARIANTS
+    if (T % 256 == 0 && T >= 512 && T <= 64 * PP_KW_TILES && g_attn_variant == 4) {
+        // A/B: the 8-wave ping-pong forward
+        if (d.mask)
+            k_attn_fwd_pp<true><<<grid, 512, PP_LDS, st>>>(T, H, q, k, v, ld, o, ldo, lse, scale * LOG2E, d.mask,
+                                                          d.dscale);
+        else
+            k_attn_fwd_pp<false><<<grid, 512, PP_LDS, st>>>(T, H, q, k, v, ld, o, ldo, lse, scale * LOG2E, nullptr,
+                                                           1.f);
         return;
     }
 #endif
