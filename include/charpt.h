@@ -207,6 +207,18 @@ int cg_reduce_rows_ex(const float* part, int64_t rows, int64_t N, float* out, in
 int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
             const void* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const cg_epilogue_t* epi, int split_k,
             void* workspace, void* stream);
+/* A residual-stream GEMM with the LayerNorm that reads its output, in one launch (the attention
+   projection + ln2, the FFN's second Linear + the next block's ln1 / ln_f: GPT1.py:136,145-147,
+   159-160,163-164,173): out = resid + [dropout](A W^T + bias) (fp32; epi kind CG_EPI_BIAS_RESID or
+   CG_EPI_BIAS_DROP_RESID with bias and resid, beta 0, flags 0), and y = LN(out; ln_w, ln_b) (bf16,
+   row stride N), mean, rstd -- bit for bit cg_gemm followed by cg_layernorm_fwd.  A [M][K] and
+   W [N][K] bf16 (lda, ldw), 16-B aligned operands.  Only where
+   cg_gemm_resid_layernorm_supported(M, N, K) says 1 (N == 384, M % 64 == 0, K % 64 == 0);
+   otherwise CG_EINVAL.                                                                         */
+int cg_gemm_resid_layernorm_supported(int64_t M, int64_t N, int64_t K);
+int cg_gemm_resid_layernorm(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* W, int64_t ldw,
+                            float* out, int64_t ldc, const cg_epilogue_t* epi, const float* ln_w, const float* ln_b,
+                            void* y, float* mean, float* rstd, float eps, void* stream);
 /* column sums of a [rows, N] matrix (bias gradients): out[n] (=|+=) sum_m X[m,n]            */
 int64_t cg_colsum_workspace(int64_t rows, int64_t N);
 int cg_colsum(const void* X, int x_dtype, int64_t rows, int64_t N, int64_t ldx, float* out, int accumulate,

@@ -56,6 +56,9 @@ _SIGS = {
     "cg_gemm_colpart_supported": (c_int, [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64]),
     "cg_gemm_relu_bits_supported": (c_int, [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64]),
     "cg_gemm_rowdot_supported": (c_int, [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64]),
+    "cg_gemm_resid_layernorm_supported": (c_int, [c_i64, c_i64, c_i64]),
+    "cg_gemm_resid_layernorm": (c_int, [c_i64, c_i64, c_i64, P, c_i64, P, c_i64, P, c_i64, ctypes.POINTER(Epilogue), P, P,
+                                        P, P, P, c_flt, P]),
     "cg_flush_deferred": (c_int, [P]),
     "cg_discard_deferred": (c_int, [P, P]),
     "cg_reduce_rows": (c_int, [P, c_i64, c_i64, P, c_int, P]),

@@ -610,6 +610,34 @@ extern "C" int64_t cg_gemm_workspace(int64_t M, int64_t N, int split_k) {
     return split_k > 1 ? (int64_t)split_k * M * N * (int64_t)sizeof(float) : 0;
 }
 
+extern "C" int cg_gemm_resid_layernorm_supported(int64_t M, int64_t N, int64_t K) {
+    return gemm_resid_ln_supported(M, N, K) ? 1 : 0;
+}
+
+extern "C" int cg_gemm_resid_layernorm(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* W,
+                                       int64_t ldw, float* out, int64_t ldc, const cg_epilogue_t* epi,
+                                       const float* ln_w, const float* ln_b, void* y, float* mean, float* rstd,
+                                       float eps, void* stream) {
+    CG_REQUIRE(gemm_resid_ln_supported(M, N, K),
+               "cg_gemm_resid_layernorm: unsupported shape M=%lld N=%lld K=%lld (N == 384, M %% 64 == 0, K %% 64 == 0)",
+               (long long)M, (long long)N, (long long)K);
+    CG_REQUIRE(epi && (epi->kind == CG_EPI_BIAS_RESID || epi->kind == CG_EPI_BIAS_DROP_RESID) && epi->bias &&
+                   epi->resid && epi->beta == 0.f && epi->flags == 0 && !epi->colpart,
+               "cg_gemm_resid_layernorm: needs a BIAS_RESID / BIAS_DROP_RESID epilogue with bias and residual, beta 0");
+    CG_REQUIRE(A && W && out && ln_w && ln_b && y && mean && rstd, "cg_gemm_resid_layernorm: null pointer");
+    CG_REQUIRE(lda >= K && ldw >= K && lda % 8 == 0 && ldw % 8 == 0 && ldc >= N && ldc % 4 == 0 &&
+                   epi->ld_resid >= N && epi->ld_resid % 4 == 0,
+               "cg_gemm_resid_layernorm: bad leading dimensions");
+    CG_REQUIRE((((uintptr_t)A | (uintptr_t)W | (uintptr_t)out | (uintptr_t)epi->resid | (uintptr_t)epi->bias |
+                 (uintptr_t)ln_w | (uintptr_t)ln_b | (uintptr_t)y) & 15) == 0,
+               "cg_gemm_resid_layernorm: operands must be 16-B aligned");
+    const EpiArgs e = make_epi(epi);
+    gemm_resid_ln_launch(M, K, (const bf16_t*)A, lda, (const bf16_t*)W, ldw, out, ldc, e, ln_w, ln_b, (bf16_t*)y, mean,
+                         rstd, eps, (hipStream_t)stream);
+    CG_LAUNCH_CHECK("cg_gemm_resid_layernorm");
+    return CG_OK;
+}
+
 extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, const void* A,
                        int64_t lda, const void* B, int64_t ldb, void* C, int c_dtype, int64_t ldc,
                        const cg_epilogue_t* epi, int split_k, void* workspace, void* stream) {

@@ -272,6 +272,11 @@ bool pk_gemm_launch(int variant, int at, int bt, int64_t M, int64_t N, int64_t K
                     float* ws, hipStream_t st);
 
 // persistent 8-wave LDS-DMA kernels (gemm_p8.hip), variant >= 20 (20 = automatic tile choice)
+// gemm_ln.hip: the residual GEMM + next LayerNorm kernel (N = 384 row panels)
+bool gemm_resid_ln_supported(int64_t M, int64_t N, int64_t K);
+void gemm_resid_ln_launch(int64_t M, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, float* X,
+                          int64_t ldx, const EpiArgs& e, const float* lnw, const float* lnb, bf16_t* Y, float* mean,
+                          float* rstd, float eps, hipStream_t st);
 bool p8_gemm_launch(int variant, int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda,
                     const bf16_t* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k,
                     float* ws, hipStream_t st);

@@ -42,6 +42,47 @@ struct VecIO<4> {
     }
 };
 
+// One row in the lane layout below (lane l holds elements (j*64 + l)*VEC + q): mean, variance (two
+// passes over the registers, wave_sum_dpp), rstd and the affine output.  Shared by ln_fwd_rows and
+// the residual GEMM + LayerNorm epilogue (gemm_ln.hip), so both give the same bits.
+template <int VEC, int NJ, typename TY, bool FULL>
+__device__ __forceinline__ void ln_fwd_row(const float (&v)[NJ][VEC], const float (&wv)[NJ][VEC],
+                                           const float (&bv)[NJ][VEC], int C, float invC, float eps, int lane,
+                                           TY* __restrict__ yr, float& mu_out, float& rs_out) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) s += v[j][q];
+    const float mu = wave_sum_dpp(s) * invC;
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int e = (j * 64 + lane) * VEC;
+        if (FULL || e < C) {
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) {
+                const float d = v[j][q] - mu;
+                ss += d * d;
+            }
+        }
+    }
+    const float var = wave_sum_dpp(ss) * invC;
+    const float rs = 1.0f / sqrtf(var + eps);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int e = (j * 64 + lane) * VEC;
+        if (FULL || e < C) {
+            float o[VEC];
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) o[q] = (v[j][q] - mu) * rs * wv[j][q] + bv[j][q];
+            VecIO<VEC>::st(yr + e, o);
+        }
+    }
+    mu_out = mu;
+    rs_out = rs;
+}
+
 // One wave per row, RPW rows per wave: every load of the wave's rows is issued before the first
 // reduction, and gamma/beta are held in registers for all of them (they were re-read after each
 // row's reductions, on the critical path).
@@ -84,37 +125,8 @@ __device__ __forceinline__ void ln_fwd_rows(const float* __restrict__ x, const f
         for (int i = 0; i < RPW; ++i) {
             const int64_t r = r0 + i * stride;
             if (r >= rows) break;
-            float s = 0.f;
-#pragma unroll
-            for (int j = 0; j < NJ; ++j)
-#pragma unroll
-                for (int q = 0; q < VEC; ++q) s += v[i][j][q];
-            const float mu = wave_sum_dpp(s) * invC;
-            float ss = 0.f;
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int e = (j * 64 + lane) * VEC;
-                if (FULL || e < C) {
-#pragma unroll
-                    for (int q = 0; q < VEC; ++q) {
-                        const float d = v[i][j][q] - mu;
-                        ss += d * d;
-                    }
-                }
-            }
-            const float var = wave_sum_dpp(ss) * invC;
-            const float rs = 1.0f / sqrtf(var + eps);
-            TY* yr = y + r * C;
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int e = (j * 64 + lane) * VEC;
-                if (FULL || e < C) {
-                    float o[VEC];
-#pragma unroll
-                    for (int q = 0; q < VEC; ++q) o[q] = (v[i][j][q] - mu) * rs * wv[j][q] + bv[j][q];
-                    VecIO<VEC>::st(yr + e, o);
-                }
-            }
+            float mu, rs;
+            ln_fwd_row<VEC, NJ, TY, FULL>(v[i], wv, bv, C, invC, eps, lane, y + r * C, mu, rs);
             if (lane == 0) {
                 mean_out[r] = mu;
                 rstd_out[r] = rs;

@@ -315,6 +315,45 @@ def linear_fwd(x2, w, out, epi="store", bias=None, resid=None, aux=None, dropout
     return out
 
 
+# CHARPT_GEMM_LN=1: the residual GEMMs with the next LayerNorm in their epilogue (cg_gemm_resid_
+# layernorm).  Off by default: bitwise equal, the kernel alone is 3 us faster than GEMM + LayerNorm
+# at the C2 projection and 0.6 us at FFN2, but the C2 step measured 2.8446 vs 2.8410 ms with ln2 and
+# ln_f fused (and 2.870 vs 2.811 with every ln1 too, which loses the LayerNorm + keep-bit launch):
+# profiles/r5_gemm_ln_ab.txt
+GEMM_LN = os.environ.get("CHARPT_GEMM_LN", "0") == "1"
+
+
+def linear_fwd_resid_ln(x2, w, out, bias, resid, next_ln, act, dropout_p=0.0, seed=0, rng_call=None, site=0):
+    """out[M,N] = resid + dropout(x2 @ w^T + bias) (fp32) and, when the kernel takes this shape
+    (cg_gemm_resid_layernorm: N = 384, bf16), the LayerNorm that reads out next (next_ln = (weight
+    Region, bias Region, eps): the same block's ln2 after the projection, the next block's ln1 or ln_f
+    after the FFN) in the same launch.  Returns the handoff (key, y, mean, rstd) that pre_ln() gives
+    the consumer, or None after the plain GEMM."""
+    M, K = x2.shape
+    N = w.shape[0]
+    if next_ln is None or not GEMM_LN or act != torch.bfloat16 or not ops.gemm_resid_layernorm_supported(M, N, K):
+        linear_fwd(x2, w, out, "bias_drop_resid" if dropout_p > 0 else "bias_resid", bias=bias, resid=resid,
+                   dropout_p=dropout_p, seed=seed, rng_call=rng_call, site=site)
+        return None
+    lw, lb, eps = next_ln
+    y = torch.empty((M, N), dtype=act, device=x2.device)
+    mean = torch.empty(M, dtype=torch.float32, device=x2.device)
+    rstd = torch.empty(M, dtype=torch.float32, device=x2.device)
+    ops.gemm_resid_layernorm(x2, w, out, M, N, K, x2.stride(0), w.stride(0), out.stride(0), bias, resid,
+                             resid.stride(0), float(dropout_p), int(seed), rng_call, int(site), lw.master, lb.master,
+                             y, mean, rstd, float(eps))
+    return ((lw.master.data_ptr(), lb.master.data_ptr(), act, float(eps)), y, mean, rstd)
+
+
+def pre_ln(x, ln_w, ln_b, act, eps=1e-5):
+    """(y, mean, rstd) of LayerNorm(x; ln_w, ln_b) when the GEMM that wrote x computed them
+    (linear_fwd_resid_ln's handoff on the tensor) for exactly this LayerNorm, else None."""
+    h = getattr(x, "_charpt_ln", None)
+    if h is None or h[0] != (ln_w.master.data_ptr(), ln_b.master.data_ptr(), act, float(eps)):
+        return None
+    return h[1], h[2], h[3]
+
+
 def linear_dgrad(dy2, w, out, epi="store", aux=None):
     """out[M,K] = epi(dy2[M,N] @ w[N,K])"""
     M, N = dy2.shape
@@ -607,12 +646,13 @@ def _regions_params(regs):
 
 class LayerCtx:
     """Per-call context for a sublayer: geometry, dropout and dtype."""
-    __slots__ = ("n_head", "head_size", "scale", "p", "seed", "rng_call", "site", "act", "premask")
+    __slots__ = ("n_head", "head_size", "scale", "p", "seed", "rng_call", "site", "act", "premask", "next_ln")
 
-    def __init__(self, n_head, head_size, scale, p, seed, rng_call, site, act, premask=None):
+    def __init__(self, n_head, head_size, scale, p, seed, rng_call, site, act, premask=None, next_ln=None):
         self.n_head, self.head_size, self.scale, self.p = n_head, head_size, scale, p
         self.seed, self.rng_call, self.site, self.act = seed, rng_call, site, act
         self.premask = premask   # (mask tensor, event) from BigramLanguageModel._launch_premasks
+        self.next_ln = next_ln   # (weight Region, bias Region, eps) of the LayerNorm that reads the output
 
 
 # ---------------------------------------------------------------------------------------
@@ -661,7 +701,10 @@ class AttnSublayerFn(torch.autograd.Function):
         x2 = x.reshape(B * T, C)
         act = lc.act
         pm = lc.premask
-        if pm is None and lc.p > 0 and LN_MASK and premask_ok(act, T, lc.head_size):
+        pre = pre_ln(x, ln_w, ln_b, act)
+        if pre is not None:   # ln1 came with x from the previous FFN's GEMM (the keep bits: attention_fwd)
+            a, mean, rstd = pre
+        elif pm is None and lc.p > 0 and LN_MASK and premask_ok(act, T, lc.head_size):
             a, mean, rstd, mask = layernorm_attn_mask(x2, ln_w.master, ln_b.master, act, B, lc.n_head, T, lc.p,
                                                       lc.seed, lc.rng_call, lc.site)
             pm = (mask, None)
@@ -673,13 +716,15 @@ class AttnSublayerFn(torch.autograd.Function):
         lse, ctx.mask = attention_fwd(qkv, B, T, lc.n_head, lc.head_size, o, lc.scale, lc.p, lc.seed, lc.rng_call,
                                       lc.site, pm)
         out = torch.empty((B * T, C), dtype=torch.float32, device=x.device)
-        linear_fwd(o, proj_w.operand(act), out, "bias_resid", bias=proj_b.master, resid=x2)
+        ln_next = linear_fwd_resid_ln(o, proj_w.operand(act), out, proj_b.master, x2, lc.next_ln, act)
         ctx.save_for_backward(x2, a, mean, rstd, qkv, o, lse)
         ctx.lc, ctx.regs, ctx.shape = lc, (ln_w, ln_b, qkv_w, proj_w, proj_b), (B, T, C)
         ctx.in_link = _link_of(x)
         ctx.link = GradLink(0.0, 0, None, 0, proj_b, act)
         out_v = out.view(B, T, C)
         out_v._charpt_link = ctx.link
+        if ln_next is not None:
+            out_v._charpt_ln = ln_next
         return out_v
 
     @staticmethod
@@ -735,7 +780,8 @@ class FFNSublayerFn(torch.autograd.Function):
         B, T, C = x.shape
         x2 = x.reshape(B * T, C)
         act = lc.act
-        a, mean, rstd = layernorm(x2, ln_w.master, ln_b.master, act)
+        pre = pre_ln(x, ln_w, ln_b, act)   # ln2 from the projection GEMM's epilogue
+        a, mean, rstd = pre if pre is not None else layernorm(x2, ln_w.master, ln_b.master, act)
         F4 = w1.master.shape[0]
         h = torch.empty((B * T, F4), dtype=act, device=x.device)
         bits = None
@@ -748,14 +794,16 @@ class FFNSublayerFn(torch.autograd.Function):
         else:
             linear_fwd(a, w1.operand(act), h, "bias_relu", bias=b1.master)
         out = torch.empty((B * T, C), dtype=torch.float32, device=x.device)
-        linear_fwd(h, w2.operand(act), out, "bias_drop_resid", bias=b2.master, resid=x2, dropout_p=lc.p,
-                   seed=lc.seed, rng_call=lc.rng_call, site=lc.site)
+        ln_next = linear_fwd_resid_ln(h, w2.operand(act), out, b2.master, x2, lc.next_ln, act, dropout_p=lc.p,
+                                      seed=lc.seed, rng_call=lc.rng_call, site=lc.site)
         ctx.save_for_backward(x2, a, mean, rstd, h, bits)
         ctx.lc, ctx.regs, ctx.shape = lc, (ln_w, ln_b, w1, b1, w2, b2), (B, T, C)
         ctx.in_link = _link_of(x)
         ctx.link = GradLink(lc.p, lc.seed, lc.rng_call, lc.site, b2, act)
         out_v = out.view(B, T, C)
         out_v._charpt_link = ctx.link
+        if ln_next is not None:
+            out_v._charpt_ln = ln_next
         return out_v
 
     @staticmethod
@@ -819,7 +867,8 @@ class HeadLossFn(torch.autograd.Function):
         B, T, C = x.shape
         M = B * T
         x2 = x.reshape(M, C)
-        a, mean, rstd = layernorm(x2, ln_w.master, ln_b.master, act)
+        pre = pre_ln(x, ln_w, ln_b, act)   # ln_f from the last FFN GEMM's epilogue
+        a, mean, rstd = pre if pre is not None else layernorm(x2, ln_w.master, ln_b.master, act)
         V = lm_w.master.shape[0]
         ctx.fused = _head_fused_ok(act, lm_w, M, C, V)
         ctx.in_link = _link_of(x)

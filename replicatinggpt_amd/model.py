@@ -196,10 +196,17 @@ class Block(nn.Module):
         ln1w, ln1b = self.ln1._regions()
         qkv = self.sa_heads.qkv_region()
         pw, pb = self.sa_heads.proj_regions()
+        ln2w, ln2b = self.ln2._regions()
+        lc.next_ln = (ln2w, ln2b, self.ln2.eps)   # the projection GEMM also computes ln2 (functional.pre_ln)
         x = Fn.AttnSublayerFn.apply(x, lc, ln1w, ln1b, qkv, pw, pb, *ln1w.params, *ln1b.params, *qkv.params,
                                     *pw.params, *pb.params)
         lc2 = self.ffwd.layer_ctx(x)
-        ln2w, ln2b = self.ln2._regions()
+        # the next block's ln1 or the model's ln_f, from the FFN GEMM's epilogue -- not ln1 when that
+        # block's attention drops out: its LayerNorm launch also makes the keep bits (functional.
+        # layernorm_attn_mask), cheaper than a keep-bit launch of their own (profiles/r5_gemm_ln_ab.txt)
+        nxt, att = getattr(self, "_charpt_next_ln", (None, None))
+        if nxt is not None and (att is None or not (self.training and att.heads[0].dropout.p > 0)):
+            lc2.next_ln = (*nxt._regions(), nxt.eps)
         w1, b1, w2, b2 = self.ffwd.regions()
         return Fn.FFNSublayerFn.apply(x, lc2, ln2w, ln2b, w1, b1, w2, b2, *ln2w.params, *ln2b.params, *w1.params,
                                       *b1.params, *w2.params, *b2.params)
@@ -351,6 +358,9 @@ class BigramLanguageModel(nn.Module):
         self.lm_head = Linear(d, cfg.vocab_size)                                 # GPT1.py:174
         for l, blk in enumerate(self.blocks):
             blk.set_layer_index(l)
+            # the LayerNorm that reads this block's output (functional.linear_fwd_resid_ln)
+            nxt = (self.blocks[l + 1].ln1, self.blocks[l + 1].sa_heads) if l + 1 < len(self.blocks) else (self.ln_f, None)
+            object.__setattr__(blk, "_charpt_next_ln", nxt)
         self._fwd_rng = None
         self._premasks = None
         self.register_buffer("_rng_counter", torch.zeros(1, dtype=torch.int64), persistent=False)

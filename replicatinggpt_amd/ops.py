@@ -224,6 +224,27 @@ def gemm_store_rowdot(a: Tensor, b: Tensor, out: Tensor, M: int, N: int, K: int,
                              L.dtype_code(out.dtype), ldc, e, 1, None, _s(out)), "gemm_store_rowdot")
 
 
+@_op("gemm_resid_layernorm", ("out", "y", "mean", "rstd"))
+def gemm_resid_layernorm(a: Tensor, w: Tensor, out: Tensor, M: int, N: int, K: int, lda: int, ldw: int, ldc: int,
+                         bias: Tensor, resid: Tensor, ld_resid: int, dropout_p: float, seed: int,
+                         rng_call: Optional[Tensor], site: int, ln_w: Tensor, ln_b: Tensor, y: Tensor, mean: Tensor,
+                         rstd: Tensor, eps: float) -> None:
+    """out = resid + dropout(a[M,K] @ w[N,K]^T + bias) (fp32; dropout_p 0: none) and y = LayerNorm(out;
+    ln_w, ln_b) (bf16, row stride N), mean, rstd in one launch -- the bits of gemm(...,
+    "bias_[drop_]resid") followed by layernorm_fwd.  Fails (CG_EINVAL) unless
+    gemm_resid_layernorm_supported(M, N, K)."""
+    _gemm_extents(a, w, out, False, False, M, N, K, lda, ldw, ldc, "gemm_resid_layernorm")
+    kind = L.EPI_BIAS_DROP_RESID if dropout_p > 0 else L.EPI_BIAS_RESID
+    e = L.Epilogue(kind, L.ptr(bias), L.ptr(resid), ld_resid, None, 0, 0, dropout_p, seed, L.ptr(rng_call), site, 0.0)
+    L.check(L.load().cg_gemm_resid_layernorm(M, N, K, L.ptr(a), lda, L.ptr(w), ldw, L.ptr(out), ldc, e, L.ptr(ln_w),
+                                             L.ptr(ln_b), L.ptr(y), L.ptr(mean), L.ptr(rstd), eps, _s(out)),
+            "gemm_resid_layernorm")
+
+
+def gemm_resid_layernorm_supported(M, N, K):
+    return bool(L.load().cg_gemm_resid_layernorm_supported(M, N, K))
+
+
 def gemm_rowdot_supported(M, N, K, lda, ldb, ldc):
     return bool(L.load().cg_gemm_rowdot_supported(0, 1, M, N, K, lda, ldb, ldc))
 

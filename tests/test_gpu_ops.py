@@ -122,6 +122,76 @@ def test_layernorm_fwd_attn_dropmask_matches_separate_launches(C, B, H, T, p):
     assert not torch.isnan(outs[0][1]).any()
 
 
+@pytest.mark.parametrize("M,K", [(16384, 384), (16384, 1536), (64, 64), (192, 640)])
+@pytest.mark.parametrize("p", [0.0, 0.2])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_gemm_resid_layernorm_matches_two_launches(M, K, p, inplace):
+    """cg_gemm_resid_layernorm (the C2 projection / FFN2 forward with the next LayerNorm in its
+    epilogue, GPT1.py:136,145-147 + 159-160,173) == cg_gemm (bias + [dropout +] residual, fp32) then
+    cg_layernorm_fwd, bit for bit at the step's shapes: x, y, mean and rstd -- also with x written
+    over the residual (the in-place residual stream); x against fp64 and the oracle's dropout mask."""
+    O = ops()
+    N = 384
+    torch.manual_seed(17)
+    a = (torch.randn(M, K, device=DEV) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV) * 0.1
+    resid = torch.randn(M, N, device=DEV)
+    lw = torch.randn(N, device=DEV) * 0.1 + 1
+    lb = torch.randn(N, device=DEV) * 0.1
+    assert O.gemm_resid_layernorm_supported(M, N, K)
+    outs = []
+    for fused in (True, False):
+        call = torch.tensor([6], dtype=torch.int64, device=DEV)
+        x = resid.clone() if inplace else torch.full((M, N), float("nan"), device=DEV)
+        r = x if inplace else resid
+        y = torch.full((M, N), float("nan"), device=DEV).to(torch.bfloat16)
+        mean, rstd = torch.full((M,), float("nan"), device=DEV), torch.full((M,), float("nan"), device=DEV)
+        if fused:
+            O.gemm_resid_layernorm(a, w, x, M, N, K, K, K, N, bias, r, N, p, 41, call, 2, lw, lb, y, mean, rstd, 1e-5)
+        else:
+            kind = 4 if p > 0 else 3
+            O.gemm(a, w, x, True, False, False, M, N, K, K, K, N, kind, bias, r, N, None, 0, p, 41, call, 2, 0.0, 1,
+                   None)
+            O.layernorm_fwd(x, lw, lb, y, mean, rstd, 1e-5)
+        torch.cuda.synchronize()
+        outs.append((x, y.view(torch.int16), mean, rstd))
+    # x: the same K order as cg_gemm's persistent kernels (M % 128 == 0); the generic kernel that
+    # cg_gemm falls back to below that sums in another order
+    if M % 128 == 0:
+        assert torch.equal(outs[0][0], outs[1][0])
+    else:
+        assert relerr(outs[0][0], outs[1][0]) < 1e-6
+    # y, mean, rstd: k_ln_fwd's bits on the fused kernel's own x
+    y2 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    m2, r2 = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    O.layernorm_fwd(outs[0][0], lw, lb, y2, m2, r2, 1e-5)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][1], y2.view(torch.int16))
+    assert torch.equal(outs[0][2], m2) and torch.equal(outs[0][3], r2)
+    assert not torch.isnan(outs[0][0]).any() and not torch.isnan(outs[0][2]).any()
+    acc = a.double() @ w.double().t() + bias.double()
+    if p > 0:
+        keep = philox.keep_mask(41, (6 << 8) | 2, np.arange(M * N), p).reshape(M, N)
+        acc = torch.from_numpy(keep).to(DEV).double() * acc * float(np.float32(1 / (1 - p)))
+    assert relerr(outs[0][0], resid.double() + acc) < 1e-5
+
+
+def test_gemm_resid_layernorm_rejects_unsupported():
+    O = ops()
+    assert not O.gemm_resid_layernorm_supported(128, 768, 384)
+    assert not O.gemm_resid_layernorm_supported(100, 384, 384)
+    a = torch.zeros(128, 384, device=DEV, dtype=torch.bfloat16)
+    w = torch.zeros(768, 384, device=DEV, dtype=torch.bfloat16)
+    x = torch.zeros(128, 768, device=DEV)
+    y = torch.zeros(128, 768, device=DEV, dtype=torch.bfloat16)
+    v = torch.zeros(768, device=DEV)
+    st = torch.zeros(128, device=DEV)
+    with pytest.raises(RuntimeError, match="unsupported shape"):
+        O.gemm_resid_layernorm(a, w, x, 128, 768, 384, 384, 384, 768, v, x, 768, 0.0, 0, None, 0, v, v, y, st, st,
+                               1e-5)
+
+
 @pytest.mark.parametrize("C", [384, 768, 126])
 @pytest.mark.parametrize("with_link", [False, True])
 def test_layernorm_bwd_rows_then_reduce_is_bitwise_ex(C, with_link):

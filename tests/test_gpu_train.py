@@ -141,6 +141,40 @@ def test_side_stream_modes_bit_identical():
         assert torch.equal(r[1], runs[0][1])
 
 
+@pytest.mark.parametrize("p", [0.2, 0.0])
+def test_gemm_layernorm_fusion_bit_identical(p):
+    """The residual GEMMs with the next LayerNorm in their epilogue (functional.GEMM_LN: ln2 after the
+    projection, ln_f after the last FFN, ln1 too when the next attention has no dropout) give the
+    separate-launch step's losses and weights bit for bit (n_embd 384: the fused kernel's width)."""
+    from replicatinggpt_amd import functional as Fn
+    from replicatinggpt_amd.engine import TrainStep
+    cfg = _cfg(n_embd=384, n_head=6, n_layers=3, dropout=p)
+    runs = []
+    saved = Fn.GEMM_LN
+    calls = {"n": 0}
+    real = Fn.ops.gemm_resid_layernorm
+
+    def counting(*a, **k):
+        calls["n"] += 1
+        return real(*a, **k)
+    try:
+        Fn.ops.gemm_resid_layernorm = counting
+        for fused in (False, True):
+            Fn.GEMM_LN = fused
+            m, opt, s = _setup(cfg)
+            st = TrainStep(m, opt, s, use_graph=True)
+            st.capture(restore=True)
+            losses = [float(st.step().detach()) for _ in range(3)]
+            torch.cuda.synchronize()
+            runs.append((losses, m.flat.master.detach().cpu().clone()))
+    finally:
+        Fn.GEMM_LN = saved
+        Fn.ops.gemm_resid_layernorm = real
+    assert calls["n"] > 0
+    assert runs[1][0] == runs[0][0]
+    assert torch.equal(runs[1][1], runs[0][1])
+
+
 def test_checkpoint_resume_is_bit_identical(tmp_path):
     """save_checkpoint after 3 steps, load into a fresh model/optimizer with a scrambled CPU
     generator: the next 3 steps (batch offsets, Philox dropout masks, AdamW) equal the

@@ -6,6 +6,9 @@ box drift cancels out of the comparison.
 variants: single          one graph: fwd + bwd (+ early AdamW) + AdamW (the 1-GPU bench path)
           seg<k>          the DP path at W = 1: backward graph segments of k blocks, reducer, AdamW graph
           red             reducer without overlap: fwd+bwd graph, (no-op) all-reduce, AdamW graph
+          <v>:<knob>=<int>  variant v captured with cg_set_tuning(knob, int) (reset to 0 after its
+                           capture; the kernel choice / arguments it sets are baked into the graphs);
+                           <v>:Fn.<NAME>=<int>  the same with a functional.py module switch (e.g. GEMM_LN)
 usage: python tools/step_ab.py [c2|c4] single,seg1,seg2 [rounds] [steps]"""
 import json
 import os
@@ -22,6 +25,18 @@ from replicatinggpt_amd.engine import GradReducer, TrainStep  # noqa: E402
 
 
 def make(variant, cfgname, dev):
+    knob = None
+    if ":" in variant:
+        variant, kv = variant.split(":", 1)
+        k, v = kv.split("=")
+        knob = (k.encode(), int(v))
+        if k.startswith("Fn."):
+            from replicatinggpt_amd import functional as Fn
+            knob = (k, getattr(Fn, k[3:]))
+            setattr(Fn, k[3:], type(knob[1])(int(v)))
+        else:
+            from replicatinggpt_amd import _lib as L
+            L.check(L.load().cg_set_tuning(knob[0], knob[1]), "tuning")
     cfg = PRESETS[cfgname].with_(dtype="bf16")
     torch.manual_seed(cfg.seed)
     model = BigramLanguageModel(cfg).to(dev)
@@ -38,6 +53,12 @@ def make(variant, cfgname, dev):
     else:
         raise ValueError(variant)
     step.capture()
+    if knob is not None and isinstance(knob[0], str):
+        from replicatinggpt_amd import functional as Fn
+        setattr(Fn, knob[0][3:], knob[1])   # restore the module switch
+    elif knob is not None:
+        from replicatinggpt_amd import _lib as L
+        L.check(L.load().cg_set_tuning(knob[0], 1 if knob[0] == b"attn_bwd_lpt" else 0), "tuning")
     return step
 
 
