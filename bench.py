@@ -404,6 +404,25 @@ def pmc_traffic(config, dom):
     return None
 
 
+def step_kernel(config, dom):
+    """The dominant op's in-step launch time from the committed rocprofv3 kernel trace of a bench run
+    (tools/gpu_prof_bench.sh -> tools/step_kernels.py -> profiles/r<N>_step_kernels_<config>.json, the
+    latest round first): in the step a launch may host deferred reduces / AdamW jobs on free slots
+    and finds its operands colder than the census's back-to-back replays.  None when no file has it."""
+    for rnd in ("r5",):
+        path = os.path.join(ROOT, "profiles", f"{rnd}_step_kernels_{config}.json")
+        try:
+            op = json.load(open(path))["ops"][dom["name"]]
+        except (OSError, KeyError, ValueError):
+            continue
+        if op.get("in_step_avg_us") is None:
+            return None
+        return {"in_step_avg_launch_ms": round(op["in_step_avg_us"] / 1e3, 5), "in_step_kernel": op["kernel"],
+                "in_step_census_ms_same_trace": round(op["census_us"] / 1e3, 5), "in_step_shared_with": op["shared_with"],
+                "in_step_source": os.path.relpath(path, ROOT)}
+    return None
+
+
 PEAK_FP32_TFLOPS = 157.3     # MI355X f32 MFMA / vector peak (MI355X_MICROARCH.md)
 
 
@@ -634,6 +653,9 @@ def main():
             pt = pmc_traffic(args.config, dom)
             if pt is not None:
                 roofline["traffic"], roofline["traffic_source"] = pt["bytes"], pt["source"]
+            sk = step_kernel(args.config, dom)
+            if sk is not None:   # beside the census figure: the same op inside the training step
+                roofline.update(sk)
         result = {
             "metric": "train tokens/sec at 1/2/4/8 MI355X + MFMA util, char-GPT block 256",
             "value": round(value, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
