@@ -320,6 +320,9 @@ void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
                     }
                 }
             }
+#ifdef CG_P8_WHATIF
+            if (ldc < 0)   // what-if build: the item's stores skipped (a host-never-true test keeps the math)
+#endif
             store_bf16_wide<FM>(acc, (bf16_t*)Cv, ldc, mr, nc);
 #pragma unroll
             for (int i = 0; i < FM; ++i)
