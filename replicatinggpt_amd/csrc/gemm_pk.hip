@@ -477,9 +477,10 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
 #ifdef CG_PK_WHATIF
     // diagnostic build only (make whatif; tools/gemm_whatif.py): pk_flags bit 4 skips the in-loop
     // DMAs, bit 5 the MFMAs, bit 6 the item epilogues -- wrong results, timing only
-    const bool WI_NODMA = flags & 16, WI_NOMFMA = flags & 32, WI_NOEPI = flags & 64;
+    // bit 3: only each block's LAST item stores (what the stores at the earlier item ends cost)
+    const bool WI_NODMA = flags & 16, WI_NOMFMA = flags & 32, WI_NOEPI = flags & 64, WI_LASTONLY = flags & 8;
 #else
-    constexpr bool WI_NODMA = false, WI_NOMFMA = false, WI_NOEPI = false;
+    constexpr bool WI_NODMA = false, WI_NOMFMA = false, WI_NOEPI = false, WI_LASTONLY = false;
 #endif
     da.init(lda, wave, lane);
     db.init(ldb, wave, lane);
@@ -734,7 +735,7 @@ void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
             if (m0 < 0 || m0 + BM > M || n0 < 0 || n0 + BN > N || sp < 0 || sp >= split_k)
                 atomicAdd(&g_pk_bounds[2], 1ull);
 #endif
-            if (WI_NOEPI) {
+            if (WI_NOEPI || (WI_LASTONLY && cj + 1 < my_items)) {
             } else if constexpr (EK == EK_SLAB16) {   // bf16 slab: 16-B row segments, as a bf16 output
                 store_item<true>(acc, mr, nc, (bf16_t*)ws + (int64_t)sp * M * N, CG_BF16, N);
             } else if (EK == EK_SLAB || split_k > 1) {

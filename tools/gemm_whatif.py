@@ -1,7 +1,7 @@
 """Where the persistent 128x128 GEMM's time goes, by subtraction: loads the what-if build
 (make -C replicatinggpt_amd/csrc whatif; gemm_pk.hip CG_PK_WHATIF) and times each C2 shape with the
 in-loop LDS-DMAs, the MFMAs and/or the item epilogues skipped (pk_flags bits 4 / 5 / 6 -- wrong
-results, timing only).  GPU only.  usage: python tools/gemm_whatif.py [c2|c4]"""
+results, timing only; WHATIF_MODES=stores: bit 3, only each block's last item stores).  GPU only.  usage: python tools/gemm_whatif.py [c2|c4]"""
 import os
 import sys
 
@@ -15,6 +15,8 @@ from replicatinggpt_amd import _lib as L  # noqa: E402
 
 MODES = [("all", 0), ("no DMA", 16), ("no MFMA", 32), ("no epilogue", 64), ("no DMA+epi", 80),
          ("no MFMA+epi", 96), ("no DMA+MFMA", 48), ("none (loop skeleton)", 112)]
+if os.environ.get("WHATIF_MODES") == "stores":   # the item-end stores: all / the block's last item only / none
+    MODES = [("all", 0), ("last item only", 8), ("no epilogue", 64)]
 
 
 def main():
