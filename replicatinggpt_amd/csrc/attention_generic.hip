@@ -308,6 +308,115 @@ __global__ __launch_bounds__(256) void k_attn_fwd_f32mfma(int64_t T_, int H, int
     if (g == 0) lse[(int64_t)bh * T_ + qa] = m_run + logf(l_run);
 }
 
+// Sequence-resident form of k_attn_fwd_f32mfma for T <= 256 (the generate() window and the fp32
+// model's eval forward): one 8-wave block per (b, h) stages every K / V row of the sequence in LDS
+// once (the 64-query blocks above re-load the causal prefix: 10 tile loads per (b, h) at T = 256
+// instead of 4, each behind its own barrier), then wave w runs 16-query groups w and 15 - w (equal
+// causal work per wave) with the per-group arithmetic of k_attn_fwd_f32mfma unchanged -- the same
+// MFMAs in the same order, the same online softmax over the same 64-key tiles -- so the outputs
+// are bitwise those of the 64-query-block kernel.
+template <int DP4>
+__global__ __launch_bounds__(512) void k_attn_fwd_f32res(int64_t T_, int H, int D, const float* __restrict__ q,
+                                                         const float* __restrict__ k, const float* __restrict__ v,
+                                                         int64_t ld, float* __restrict__ o, int64_t ldo,
+                                                         float* __restrict__ lse, float scale) {
+    constexpr int KS = DP4 / 4;
+    constexpr int KLD = DP4 + 1, VLD = 33;
+    __shared__ float Ks[256 * KLD];
+    __shared__ float Vs[256 * VLD];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, li = lane & 15;
+    const int bh = blockIdx.x, b = bh / H, h = bh % H;
+    const float* qb = q + (int64_t)b * T_ * ld + h * D;
+    const float* kb = k + (int64_t)b * T_ * ld + h * D;
+    const float* vb = v + (int64_t)b * T_ * ld + h * D;
+    for (int i = tid; i < 256 * 32; i += 512) {
+        const int r = i >> 5, e = i & 31;
+        const bool ok = r < T_ && e < D;
+        if (e < DP4) Ks[r * KLD + e] = ok ? kb[(int64_t)r * ld + e] : 0.f;
+        Vs[r * VLD + e] = ok ? vb[(int64_t)r * ld + e] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int gi = 0; gi < 2; ++gi) {
+        const int64_t qw0 = 16 * (gi == 0 ? wave : 15 - wave);
+        if (qw0 >= T_) continue;
+        const int64_t qa = qw0 + li;
+        float qf[KS];
+#pragma unroll
+        for (int t = 0; t < KS; ++t) {
+            const int e = 4 * t + g;
+            qf[t] = (qa < T_ && e < D) ? qb[qa * ld + e] : 0.f;
+        }
+        fv4 oacc[2] = {fv4{0.f, 0.f, 0.f, 0.f}, fv4{0.f, 0.f, 0.f, 0.f}};
+        float m_run = -INFINITY, l_run = 0.f;
+        const int nkv = (int)((qw0 + 15) / 64) + 1;   // the 64-key tiles with k0 <= qw0 + 15, in order
+        for (int kv = 0; kv < nkv; ++kv) {
+            const int64_t k0 = (int64_t)kv * 64;
+            const float* Kt = Ks + k0 * KLD;
+            const float* Vt = Vs + k0 * VLD;
+            fv4 st[4];
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt) {
+                fv4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int t = 0; t < KS; ++t) c = mfma_f32x4(Kt[(16 * kt + li) * KLD + 4 * t + g], qf[t], c);
+                st[kt] = c;
+            }
+            float mx = -INFINITY;
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t key = k0 + 16 * kt + 4 * g + r;
+                    float x = st[kt][r] * scale;
+                    if (key > qa || key >= T_) x = -INFINITY;
+                    st[kt][r] = x;
+                    mx = fmaxf(mx, x);
+                }
+            mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            const float m_new = fmaxf(m_run, mx);
+            const float alpha = m_new == -INFINITY ? 1.f : expf(m_run - m_new);
+            float ps = 0.f;
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float p = st[kt][r] == -INFINITY ? 0.f : expf(st[kt][r] - m_new);
+                    st[kt][r] = p;
+                    ps += p;
+                }
+            ps += __shfl_xor(ps, 16, 64);
+            ps += __shfl_xor(ps, 32, 64);
+            l_run = l_run * alpha + ps;
+            m_run = m_new;
+            oacc[0] *= alpha;
+            oacc[1] *= alpha;
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const int key = 16 * kt + 4 * g + s;
+#pragma unroll
+                    for (int et = 0; et < 2; ++et)
+                        oacc[et] = mfma_f32x4(Vt[key * VLD + 16 * et + li], st[kt][s], oacc[et]);
+                }
+        }
+        if (qa >= T_) continue;
+        const float inv = 1.f / l_run;
+        float* orow = o + ((int64_t)b * T_ + qa) * ldo + h * D;
+#pragma unroll
+        for (int et = 0; et < 2; ++et)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int e = 16 * et + 4 * g + r;
+                if (e < D) orow[e] = oacc[et][r] * inv;
+            }
+        if (g == 0) lse[(int64_t)bh * T_ + qa] = m_run + logf(l_run);
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_attn_fwd_generic(int64_t T_, int H, int D, const T* __restrict__ q,
                                                           const T* __restrict__ k, const T* __restrict__ v, int64_t ld,
@@ -725,7 +834,18 @@ int attn_fwd_impl(int dtype, int64_t B, int64_t T, int64_t H, int64_t D, const v
     } else {
         dim3 grid(ceil_div(T, GB), (unsigned)(B * H));
         const size_t lds = generic_lds<float>((int)D, 3, 1);
-        if (dtype == CG_F32 && !d.thr && D <= 32) {
+        if (dtype == CG_F32 && !d.thr && D <= 32 && T <= 256 && g_attn_variant != 1) {
+            // attn_variant 1 (A/B, tests): the 64-query-block kernel below
+#define AR(dp) k_attn_fwd_f32res<dp><<<(unsigned)(B * H), 512, 0, st>>>(T, (int)H, (int)D, (const float*)q, \
+                                                                     (const float*)k, (const float*)v, ld_qkv, \
+                                                                     (float*)o, ld_o, lse, scale)
+            const int dp4 = (int)((D + 3) / 4) * 4;
+            if (dp4 <= 8) AR(8);
+            else if (dp4 <= 16) AR(16);
+            else if (dp4 <= 24) AR(24);
+            else AR(32);
+#undef AR
+        } else if (dtype == CG_F32 && !d.thr && D <= 32) {
             dim3 g2(ceil_div(T, 64), (unsigned)(B * H));
 #define AF(dp)                                                                                                  \
     k_attn_fwd_f32mfma<dp><<<g2, 256, 0, st>>>(T, (int)H, (int)D, (const float*)q, (const float*)k, (const float*)v, \

@@ -806,6 +806,38 @@ def test_attention_fwd_bwd(B, T, H, D, p, dt):
             assert ok, (name, st)
 
 
+@pytest.mark.parametrize("B,T,H,D", [(256, 256, 6, 21), (2, 37, 3, 21), (3, 200, 2, 8), (2, 256, 2, 32),
+                                     (1, 130, 4, 16), (2, 16, 1, 21)])
+def test_attention_fp32_resident_matches_query_blocks(B, T, H, D):
+    """The sequence-resident fp32 MFMA forward (k_attn_fwd_f32res, T <= 256: the generate() window at
+    C5, 256 x 256 x 6 heads of 21) gives the 64-query-block kernel's bits (attn_variant 1) for O and
+    lse, and fp64 within 1e-5."""
+    from replicatinggpt_amd import _lib as L
+    lib = L.load()
+    Fn = F()
+    torch.manual_seed(8)
+    d = H * D
+    qkv = (torch.randn(B * T, 3 * d) * 0.7).to(DEV)
+    scale = (3.0 * D) ** -0.5
+    outs = []
+    for v in (1, 0):
+        L.check(lib.cg_set_tuning(b"attn_variant", v))
+        try:
+            o = torch.full((B * T, d), float("nan"), device=DEV)
+            lse, _ = Fn.attention_fwd(qkv, B, T, H, D, o, scale, 0.0, 0, None, 0)
+            torch.cuda.synchronize()
+        finally:
+            L.check(lib.cg_set_tuning(b"attn_variant", 0))
+        outs.append((o, lse.clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    if B * T <= 4096:
+        qd = qkv.double().cpu()
+        q, k, v = (qd[:, i * d:(i + 1) * d].view(B, T, H, D) for i in range(3))
+        ref = _attn_ref(q, k, v, scale, 0.0, 0, 0)
+        assert relerr(outs[1][0], ref.reshape(B * T, d)) < 1e-5
+
+
 def test_attention_fast_matches_generic_bf16():
     """The MFMA head_size-64 kernels against the generic kernels on identical bf16 inputs."""
     Fn = F()

@@ -3,7 +3,8 @@
 hipGraph replay of 20 launches (HIP events), rounds interleaved; then, with `gen`, one C5 generate
 (256 x 500 greedy, fp32, C1 golden weights) timed under the variant named second.
 usage: python tools/f32_fwd_ab.py [rounds]            (kernel A/B)
-       python tools/f32_fwd_ab.py gen <98|0>          (generate under one variant, fresh process)"""
+       python tools/f32_fwd_ab.py gen <98|0> [knob]   (generate with cg_set_tuning(knob, value), knob
+                                                      gemm_variant by default; fresh process)"""
 import os
 import statistics
 import sys
@@ -66,10 +67,10 @@ def kernels(rounds):
               f"k_gemm_f32n {b:7.1f} us ({tf / b * 1e6:6.1f} TF/s)  {b / a - 1:+.1%}", flush=True)
 
 
-def gen(variant):
+def gen(variant, knob="gemm_variant"):
     from safetensors.torch import load_file
     from replicatinggpt_amd import BigramLanguageModel, GPTConfig
-    L.check(L.load().cg_set_tuning(b"gemm_variant", variant))
+    L.check(L.load().cg_set_tuning(knob.encode(), variant))
     sd = load_file(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests", "golden",
                                 "model_c1_trained.safetensors"))
     m = BigramLanguageModel(GPTConfig(dtype="fp32"))
@@ -83,12 +84,12 @@ def gen(variant):
         out = m.generate(idx, 500, greedy=True, generator=torch.Generator().manual_seed(1337))
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    print(f"gemm_variant {variant}: generate 256x500 {dt * 1e3:.1f} ms = {256 * 500 / dt:.0f} tok/s, "
+    print(f"{knob} {variant}: generate 256x500 {dt * 1e3:.1f} ms = {256 * 500 / dt:.0f} tok/s, "
           f"checksum {int(out.sum())}", flush=True)
 
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "gen":
-        gen(int(sys.argv[2]))
+        gen(int(sys.argv[2]), *(sys.argv[3:4]))
     else:
         kernels(int(sys.argv[1]) if len(sys.argv) > 1 else 5)
