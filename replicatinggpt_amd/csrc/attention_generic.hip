@@ -321,7 +321,9 @@ __global__ __launch_bounds__(512) void k_attn_fwd_f32res(int64_t T_, int H, int 
                                                          int64_t ld, float* __restrict__ o, int64_t ldo,
                                                          float* __restrict__ lse, float scale) {
     constexpr int KS = DP4 / 4;
-    constexpr int KLD = DP4 + 1, VLD = 33;
+    // V rows hold only the DP4 padded dimensions (the O^T MFMAs' dims DP4..31 read zeros): 51 KB of
+    // LDS at DP4 = 24, three blocks per CU
+    constexpr int KLD = DP4 + 1, VLD = DP4 + 1;
     __shared__ float Ks[256 * KLD];
     __shared__ float Vs[256 * VLD];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -333,8 +335,10 @@ __global__ __launch_bounds__(512) void k_attn_fwd_f32res(int64_t T_, int H, int 
     for (int i = tid; i < 256 * 32; i += 512) {
         const int r = i >> 5, e = i & 31;
         const bool ok = r < T_ && e < D;
-        if (e < DP4) Ks[r * KLD + e] = ok ? kb[(int64_t)r * ld + e] : 0.f;
-        Vs[r * VLD + e] = ok ? vb[(int64_t)r * ld + e] : 0.f;
+        if (e < DP4) {
+            Ks[r * KLD + e] = ok ? kb[(int64_t)r * ld + e] : 0.f;
+            Vs[r * VLD + e] = ok ? vb[(int64_t)r * ld + e] : 0.f;
+        }
     }
     __syncthreads();
 #pragma unroll 1
@@ -399,8 +403,10 @@ __global__ __launch_bounds__(512) void k_attn_fwd_f32res(int64_t T_, int H, int 
                 for (int s = 0; s < 4; ++s) {
                     const int key = 16 * kt + 4 * g + s;
 #pragma unroll
-                    for (int et = 0; et < 2; ++et)
-                        oacc[et] = mfma_f32x4(Vt[key * VLD + 16 * et + li], st[kt][s], oacc[et]);
+                    for (int et = 0; et < 2; ++et) {
+                        const int e = 16 * et + li;
+                        oacc[et] = mfma_f32x4(e < DP4 ? Vt[key * VLD + e] : 0.f, st[kt][s], oacc[et]);
+                    }
                 }
         }
         if (qa >= T_) continue;
