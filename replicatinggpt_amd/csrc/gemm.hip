@@ -534,7 +534,8 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     }
     if (!strcmp(key, "attn_variant")) {
 #ifndef CG_AB_VARIANTS
-        // 0 automatic, 1 ring kernels at T <= 256, 2 separate resident dQ / dK-dV launches (A/B build
+        // 0 automatic, 1 ring kernels at T <= 256 (and the 64-query-block fp32 forward instead of the
+        // sequence-resident one), 2 separate resident dQ / dK-dV launches (A/B build
         // also 4: the 8-wave ping-pong forward at T % 256 == 0, 512..1024)
         CG_REQUIRE(value >= 0 && value <= 2, "cg_set_tuning: attn_variant %d is an A/B variant, not in this build (make ab)",
                    value);
