@@ -195,6 +195,46 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32(int64_t M, int64_t N, int64
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
         }
     }
+    const int kind = epi.kind;
+    if (split_k == 1 && epi.beta == 0.f &&
+        (kind == CG_EPI_STORE || kind == CG_EPI_BIAS || kind == CG_EPI_BIAS_RELU || kind == CG_EPI_BIAS_RESID)) {
+        // every operand of the tile's epilogue (bias, residual) loaded before its first store: loaded
+        // per element (epi_scalar + store_out), each load waited for every earlier store too (vmcnt
+        // counts both), one HBM round trip per output element of the lane.  Same arithmetic and
+        // order as epi_scalar: bias added only when present, ReLU, then resid + v.
+        const bool hb = kind != CG_EPI_STORE && epi.bias, hr = kind == CG_EPI_BIAS_RESID && epi.resid;
+        float bv[2] = {0.f, 0.f}, rv[4][2][4];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int64_t n = n0 + wn * 32 + 16 * j + li;
+            if (hb && n < N) bv[j] = epi.bias[n];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t m = m0 + wm * 64 + 16 * i + 4 * g + r;
+                    const int64_t n = n0 + wn * 32 + 16 * j + li;
+                    rv[i][j][r] = (hr && m < M && n < N) ? epi.resid[m * epi.ld_resid + n] : 0.f;
+                }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t m = m0 + wm * 64 + 16 * i + 4 * g + r;
+                    const int64_t n = n0 + wn * 32 + 16 * j + li;
+                    float v = acc[i][j][r];
+                    if (hb) v += bv[j];
+                    if (kind == CG_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
+                    if (hr) v = rv[i][j][r] + v;
+                    if (m < M && n < N) C[m * ldc + n] = v;
+                }
+        return;
+    }
     const uint64_t stream = (epi.kind == CG_EPI_BIAS_DROP_RESID && epi.thr) ? dropout_stream(epi.rng_call, epi.site) : 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
