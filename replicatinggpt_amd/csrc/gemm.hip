@@ -528,6 +528,7 @@ extern int g_ln_rpb;  // layernorm.hip
 extern int g_adamw_mode;  // ce_adamw.hip
 extern int g_ln_waves;  // layernorm.hip
 extern int g_ln_pf;     // layernorm.hip
+extern int g_ln_rl;     // layernorm.hip
 extern int g_ln_nt;     // layernorm.hip
 }
 
@@ -565,6 +566,11 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     }
     if (!strcmp(key, "pk_flags")) {
         g_pk_flags = value;
+        return CG_OK;
+    }
+    if (!strcmp(key, "ln_rl")) {   // A/B: the LayerNorm backward rows' next loads before the current stores
+        CG_REQUIRE(value == 0 || value == 1, "cg_set_tuning: ln_rl must be 0 or 1");
+        g_ln_rl = value;
         return CG_OK;
     }
     if (!strcmp(key, "attn_bwd_lpt")) {   // A/B: merged resident backward workgroup order (1 = dK/dV first)

@@ -59,6 +59,11 @@ namespace cg {
 int g_ln_rpb = 0;     // cg_set_tuning("ln_rpb"): rows per backward block (0 = automatic)
 int g_ln_waves = 0;   // cg_set_tuning("ln_waves"): waves per backward block, 4 or 8 (0 = automatic)
 int g_ln_pf = 0;      // cg_set_tuning("ln_pf"): 1 = next row's loads before the current row (FULL shapes)
+// cg_set_tuning("ln_rl"): 1 (default) = the NT backward rows at C = 384 issue the next row's loads after
+// computing the current row's outputs and before storing them (0: load, compute, store per row -- each
+// row's loads then wait for the previous row's stores, vmcnt counting both).  Not at C = 768: there the
+// held outputs cost the 4-wave blocks a wave per SIMD (158 -> 184 VGPRs)
+int g_ln_rl = 1;
 // cg_set_tuning("ln_nt"): the backward's non-temporal streams (k_ln_bwd NTM) for the FULL C = 384 / 768
 // rows; -1 (default) = 3: the residual gradient and x read and dx written non-temporally.  dx is read
 // again only by the next LayerNorm backward, after the sublayer's GEMMs and attention, so caching it
@@ -113,7 +118,7 @@ struct LnRow {
 // the next row's loads before reducing the current one (double-buffered rows) gained nothing at
 // C4 and lost 15-25 % at C2 (occupancy); ~4.8 TB/s at C4, 5.2 TB/s at C2 without dropout.
 // NTM (VEC 2 / 4): 1 the residual gradient read non-temporally, 2 also x, 3 also the dx store
-template <int VEC, int NJ, typename TDY, int WAVES, bool FULL = false, bool PF = false, int NTM = 0>
+template <int VEC, int NJ, typename TDY, int WAVES, bool FULL = false, bool PF = false, int NTM = 0, bool RL = false>
 __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ dy, const float* __restrict__ x,
                                                            const float* __restrict__ w, const float* __restrict__ mean,
                                                            const float* __restrict__ rstd,
@@ -161,8 +166,11 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
     // element e = (64 j + lane) VEC is (j VEC) >> 3 for every lane (no carry: 8 VEC <= 64).
     constexpr int NCALL = (NJ * VEC + 7) / 8;
     const bool row_groups = (C & 7) == 0;
-    auto process = [&](int64_t r, const LnRow<VEC, NJ>& b, auto hr) {
+    // ST: store the row's outputs here; else leave them in oo / zz for store_row (RL)
+    auto process = [&](int64_t r, const LnRow<VEC, NJ>& b, auto hr, auto stc, float (&oo)[NJ][VEC],
+                       float (&zz)[NJ][VEC]) {
         constexpr bool HR = decltype(hr)::value;
+        constexpr bool ST = decltype(stc)::value;
         uint32_t kbyte[NJ];   // keep bits of the 8-group holding this lane's element e, per j
         if (lp.out && lp.thr && row_groups) {
             uint32_t kb[NCALL];
@@ -205,8 +213,13 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
                     o[q] = b.rs * (g[j][q] - c1 - xh[j][q] * c2);
                     if (HR) o[q] += b.rv[j][q];
                 }
-                if constexpr (NTM >= 3 && VEC >= 2) st_nt<VEC>(dx + r * C + e, o);
-                else VecIO<VEC>::st(dx + r * C + e, o);
+                if constexpr (ST) {
+                    if constexpr (NTM >= 3 && VEC >= 2) st_nt<VEC>(dx + r * C + e, o);
+                    else VecIO<VEC>::st(dx + r * C + e, o);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < VEC; ++q) oo[j][q] = o[q];
+                }
                 if (lp.out) {
                     float z[VEC];
                     if (lp.thr && row_groups) {
@@ -225,10 +238,26 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
 #pragma unroll
                         for (int q = 0; q < VEC; ++q) z[q] = o[q];
                     }
-                    VecIO<VEC>::st(lp.out + r * C + e, z);
+                    if constexpr (ST) {
+                        VecIO<VEC>::st(lp.out + r * C + e, z);
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < VEC; ++q) zz[j][q] = z[q];
+                    }
 #pragma unroll
                     for (int q = 0; q < VEC; ++q) acs[j][q] += z[q];
                 }
+            }
+        }
+    };
+    auto store_row = [&](int64_t r, const float (&oo)[NJ][VEC], const float (&zz)[NJ][VEC]) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int e = (j * 64 + lane) * VEC;
+            if (FULL || e < C) {
+                if constexpr (NTM >= 3 && VEC >= 2) st_nt<VEC>(dx + r * C + e, oo[j]);
+                else VecIO<VEC>::st(dx + r * C + e, oo[j]);
+                if (lp.out) VecIO<VEC>::st(lp.out + r * C + e, zz[j]);
             }
         }
     };
@@ -238,6 +267,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
     // 64 VEC NJ, no lane guards) a row's loads are then one basic block, issued back to back
     // PF: the next row's loads are issued before the current row is processed (two rows in flight per
     // wave; more VGPRs -- cg_set_tuning("ln_pf"))
+    // RL: the next row's loads are issued after the current row's outputs are computed and before
+    // they are stored, so they do not wait for those stores (one row of loads in flight, as before)
+    float oo[NJ][VEC], zz[NJ][VEC];
     auto row_loop = [&](auto hr) {
         if constexpr (PF) {
             if (n > 0) {
@@ -247,8 +279,20 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
                 for (int i = 0; i < n; ++i) {
                     LnRow<VEC, NJ> Bn;
                     if (i + 1 < n) load(r0 + i + 1, Bn, hr);
-                    process(r0 + i, A, hr);
+                    process(r0 + i, A, hr, std::true_type{}, oo, zz);
                     A = Bn;
+                }
+            }
+        } else if constexpr (RL) {
+            if (n > 0) {
+                LnRow<VEC, NJ> A;
+                load(r0, A, hr);
+#pragma unroll 1
+                for (int i = 0; i < n; ++i) {
+                    process(r0 + i, A, hr, std::false_type{}, oo, zz);
+                    if (i + 1 < n) load(r0 + i + 1, A, hr);
+                    __builtin_amdgcn_sched_barrier(0);
+                    store_row(r0 + i, oo, zz);
                 }
             }
         } else {
@@ -256,7 +300,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_ln_bwd(const TDY* __restrict__ d
             for (int i = 0; i < n; ++i) {
                 LnRow<VEC, NJ> A;
                 load(r0 + i, A, hr);
-                process(r0 + i, A, hr);
+                process(r0 + i, A, hr, std::true_type{}, oo, zz);
             }
         }
     };
@@ -340,14 +384,19 @@ int launch_ln_bwd(const TDY* dy, const float* x, const float* w, const float* me
             k_ln_bwd<V, N, TDY, 8, F, P><<<(unsigned)nblk, 512, lds, st>>>(dy, x, w, mean, rstd, dres, dx, lp, part,    \
                                                                            rows, C, rpb);                      \
     } while (0)
-#define LNB_NT(V, N, M_)                                                                                       \
+#define LNB_NT_(V, N, M_, RL_)                                                                                 \
     do {                                                                                                       \
         if (waves == 4)                                                                                        \
-            k_ln_bwd<V, N, TDY, 4, true, false, M_><<<(unsigned)nblk, 256, lds, st>>>(dy, x, w, mean, rstd, dres, dx, \
-                                                                                      lp, part, rows, C, rpb); \
+            k_ln_bwd<V, N, TDY, 4, true, false, M_, RL_><<<(unsigned)nblk, 256, lds, st>>>(                      \
+                dy, x, w, mean, rstd, dres, dx, lp, part, rows, C, rpb);                                         \
         else                                                                                                   \
-            k_ln_bwd<V, N, TDY, 8, true, false, M_><<<(unsigned)nblk, 512, lds, st>>>(dy, x, w, mean, rstd, dres, dx, \
-                                                                                      lp, part, rows, C, rpb); \
+            k_ln_bwd<V, N, TDY, 8, true, false, M_, RL_><<<(unsigned)nblk, 512, lds, st>>>(                      \
+                dy, x, w, mean, rstd, dres, dx, lp, part, rows, C, rpb);                                         \
+    } while (0)
+#define LNB_NT(V, N, M_)                  \
+    do {                                  \
+        if (g_ln_rl && V == 2) LNB_NT_(V, N, M_, true); \
+        else LNB_NT_(V, N, M_, false);    \
     } while (0)
 #define LNB(V, N, F)                        \
     do {                                    \
@@ -371,6 +420,7 @@ int launch_ln_bwd(const TDY* dy, const float* x, const float* w, const float* me
 #undef LNB
 #undef LNB_
 #undef LNB_NT
+#undef LNB_NT_
     if (!defer && (dw || db || dbias))
         launch_reduce_partials3(part, nblk, NP * C, dw, db, dbias, C, accumulate, dbias_accumulate, st);
     return CG_OK;

@@ -231,6 +231,45 @@ def test_layernorm_bwd_rows_then_reduce_is_bitwise_ex(C, with_link):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("rows", [16384, 1000, 7])
+@pytest.mark.parametrize("with_link", [False, True])
+def test_layernorm_bwd_row_loop_order_is_bitwise(rows, with_link):
+    """The C = 384 backward rows with the next row's loads issued before the current row's stores
+    (ln_rl 1, the default) == the load / compute / store order (ln_rl 0) bit for bit: dx, the
+    consumer's dropout-applied bf16 copy, dgamma / dbeta and the copy's column sums; C2's 16384 rows
+    (4 rows per wave), a ragged count and fewer rows than waves."""
+    from replicatinggpt_amd import _lib as L
+    lib = L.load()
+    torch.manual_seed(5)
+    O = ops()
+    C = 384
+    x = (torch.randn(rows, C) * 2 + 0.5).to(DEV)
+    w = (torch.randn(C) * 0.1 + 1).to(DEV)
+    mean, rstd = x.mean(1), x.var(1, unbiased=False).add(1e-5).rsqrt()
+    dy = torch.randn(rows, C, device=DEV).to(torch.bfloat16)
+    dres = torch.randn(rows, C, device=DEV)
+    call = torch.tensor([9], dtype=torch.int64, device=DEV)
+    p = 0.2 if with_link else 0.0
+    outs = []
+    try:
+        for rl in (0, 1):
+            L.check(lib.cg_set_tuning(b"ln_rl", rl))
+            dx = torch.full((rows, C), float("nan"), device=DEV)
+            lp = torch.empty(rows, C, dtype=torch.bfloat16, device=DEV) if with_link else None
+            dw, db = torch.ones(C, device=DEV), torch.ones(C, device=DEV)
+            cs = torch.ones(C, device=DEV) if with_link else None
+            ws = torch.full((O.layernorm_bwd_workspace(rows, C) // 4 + 1,), float("nan"), device=DEV)
+            O.layernorm_bwd(dy, x, w, mean, rstd, dres, dx, lp, dw, db, True, ws, cs, True, p, 11,
+                            call if p else None, 4)
+            torch.cuda.synchronize()
+            outs.append([t.cpu() for t in (dx, lp, dw, db, cs) if t is not None])
+    finally:
+        L.check(lib.cg_set_tuning(b"ln_rl", 1))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert not torch.isnan(outs[1][0]).any()
+
+
 @pytest.mark.parametrize("M,Fh,C", [(2048, 1536, 384), (16384, 3072, 768)])
 def test_relu_keep_bits_roundtrip(M, Fh, C):
     """FeedForward's ReLU keep bits (CG_BITS): the W1 forward with bits gives the same bf16 h as the
