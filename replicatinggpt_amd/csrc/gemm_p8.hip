@@ -344,36 +344,48 @@ void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
                 }
             }
             const bool drop = epi.kind == CG_EPI_BIAS_DROP_RESID && epi.thr;
+            // 32-row half bands t = (band t / 2, half t % 2), each half's residual loaded before the
+            // previous half's stores: vmcnt counts loads and stores together, so a load issued after
+            // them would wait for every earlier store of the item first (different rows, so an
+            // in-place residual is read before any store can reach it)
+            float4 r[2][FN];
+            uint32_t nib[4][FN];
+            auto load_half = [&](int t) {
+                const int64_t mh = mr + 64 * (t >> 1) + 32 * (t & 1);
 #pragma unroll
-            for (int hb = 0; hb < FM / 4; ++hb) {
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+                        r[i][j] = *(const float4*)(epi.resid + (mh + 16 * i) * epi.ld_resid + nc + 16 * j);
+            };
+            load_half(0);
+#pragma unroll
+            for (int t = 0; t < 2 * (FM / 4); ++t) {
+                const int hb = t >> 1, hh = t & 1;
                 const int64_t mb = mr + 64 * hb;
-                // two 32-row halves of residual (32 registers each); the band's keep bits are computed
-                // while the first half's loads are in flight
-                float4 r[2][FN];
-                uint32_t nib[4][FN];
+                if (hh == 0 && drop) drop_nibbles_rows<FN>(epi, stream, mb, nc, N, nib);
 #pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
+                for (int i = 0; i < 2; ++i)
 #pragma unroll
-                    for (int i = 0; i < 2; ++i)
+                    for (int j = 0; j < FN; ++j) {
+                        const int ii = 2 * hh + i;
+                        fv4& v = acc[4 * hb + ii][j];
+                        if (drop) {
 #pragma unroll
-                        for (int j = 0; j < FN; ++j)
-                            r[i][j] = *(const float4*)(epi.resid + (mb + 16 * (2 * hh + i)) * epi.ld_resid + nc + 16 * j);
-                    if (hh == 0 && drop) drop_nibbles_rows<FN>(epi, stream, mb, nc, N, nib);
-#pragma unroll
-                    for (int i = 0; i < 2; ++i)
-#pragma unroll
-                        for (int j = 0; j < FN; ++j) {
-                            const int ii = 2 * hh + i;
-                            fv4& v = acc[4 * hb + ii][j];
-                            if (drop) {
-#pragma unroll
-                                for (int q = 0; q < 4; ++q) v[q] = ((nib[ii][j] >> q) & 1u) ? v[q] * epi.dscale : 0.f;
-                            }
-                            v[0] = r[i][j].x + v[0]; v[1] = r[i][j].y + v[1]; v[2] = r[i][j].z + v[2]; v[3] = r[i][j].w + v[3];
-                            *(float4*)((float*)Cv + (mb + 16 * ii) * ldc + nc + 16 * j) = make_float4(v[0], v[1], v[2], v[3]);
-                            v = fv4{0.f, 0.f, 0.f, 0.f};
+                            for (int q = 0; q < 4; ++q) v[q] = ((nib[ii][j] >> q) & 1u) ? v[q] * epi.dscale : 0.f;
                         }
-                }
+                        v[0] = r[i][j].x + v[0]; v[1] = r[i][j].y + v[1]; v[2] = r[i][j].z + v[2]; v[3] = r[i][j].w + v[3];
+                    }
+                if (t + 1 < 2 * (FM / 4)) load_half(t + 1);
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) {
+                        const int ii = 2 * hh + i;
+                        fv4& v = acc[4 * hb + ii][j];
+                        *(float4*)((float*)Cv + (mb + 16 * ii) * ldc + nc + 16 * j) = make_float4(v[0], v[1], v[2], v[3]);
+                        v = fv4{0.f, 0.f, 0.f, 0.f};
+                    }
             }
         } else {
 #pragma unroll
