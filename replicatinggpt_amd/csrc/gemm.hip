@@ -569,7 +569,7 @@ extern "C" int cg_set_tuning(const char* key, int value) {
         return CG_OK;
     }
     if (!strcmp(key, "ln_rl")) {   // A/B: the LayerNorm backward rows' next loads before the current stores
-        CG_REQUIRE(value == 0 || value == 1, "cg_set_tuning: ln_rl must be 0 or 1");
+        CG_REQUIRE(value >= 0 && value <= 2, "cg_set_tuning: ln_rl must be 0, 1 or 2 (2: also at C = 768)");
         g_ln_rl = value;
         return CG_OK;
     }

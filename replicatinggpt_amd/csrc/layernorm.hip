@@ -62,7 +62,8 @@ int g_ln_pf = 0;      // cg_set_tuning("ln_pf"): 1 = next row's loads before the
 // cg_set_tuning("ln_rl"): 1 (default) = the NT backward rows at C = 384 issue the next row's loads after
 // computing the current row's outputs and before storing them (0: load, compute, store per row -- each
 // row's loads then wait for the previous row's stores, vmcnt counting both).  Not at C = 768: there the
-// held outputs cost the 4-wave blocks a wave per SIMD (158 -> 184 VGPRs)
+// held outputs cost the 4-wave blocks a wave per SIMD (158 -> 184 VGPRs; 2 = there too, A/B: C4 step
+// 50.85 -> 51.05 ms, profiles/r5_ln_bwd_row_order_ab.txt)
 int g_ln_rl = 1;
 // cg_set_tuning("ln_nt"): the backward's non-temporal streams (k_ln_bwd NTM) for the FULL C = 384 / 768
 // rows; -1 (default) = 3: the residual gradient and x read and dx written non-temporally.  dx is read
@@ -395,7 +396,7 @@ int launch_ln_bwd(const TDY* dy, const float* x, const float* w, const float* me
     } while (0)
 #define LNB_NT(V, N, M_)                  \
     do {                                  \
-        if (g_ln_rl && V == 2) LNB_NT_(V, N, M_, true); \
+        if (g_ln_rl == 2 || (g_ln_rl && V == 2)) LNB_NT_(V, N, M_, true); \
         else LNB_NT_(V, N, M_, false);    \
     } while (0)
 #define LNB(V, N, F)                        \
