@@ -2,7 +2,8 @@
 (default) at the C5 generate() window shapes (256 x 256 rows, C1 width 126), per-launch time from a
 hipGraph replay of 20 launches (HIP events), rounds interleaved; then, with `gen`, one C5 generate
 (256 x 500 greedy, fp32, C1 golden weights) timed under the variant named second.
-usage: python tools/f32_fwd_ab.py [rounds]            (kernel A/B)
+usage: python tools/f32_fwd_ab.py [rounds]            (kernel A/B; needs the trial kernel, not in the tree)
+       python tools/f32_fwd_ab.py now [rounds]        (the current library's fp32 products at those shapes)
        python tools/f32_fwd_ab.py gen <98|0> [knob]   (generate with cg_set_tuning(knob, value), knob
                                                       gemm_variant by default; fresh process)"""
 import os
@@ -88,8 +89,23 @@ def gen(variant, knob="gemm_variant"):
           f"checksum {int(out.sum())}", flush=True)
 
 
+def now(rounds):
+    L.load()
+    dev = torch.device("cuda")
+    t = {n: [] for n, *_ in SHAPES}
+    for _ in range(rounds):
+        for name, M, N, K, kind in SHAPES:
+            t[name].append(graph_us(launch_fn(M, N, K, kind, dev)))
+            torch.cuda.empty_cache()
+    for name, M, N, K, kind in SHAPES:
+        a = statistics.median(t[name])
+        print(f"{name:5s} M={M} N={N} K={K} epi {kind}: {a:7.1f} us ({2 * M * N * K / a / 1e6:6.1f} TF/s)", flush=True)
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "gen":
+    if len(sys.argv) > 1 and sys.argv[1] == "now":
+        now(int(sys.argv[2]) if len(sys.argv) > 2 else 5)
+    elif len(sys.argv) > 1 and sys.argv[1] == "gen":
         gen(int(sys.argv[2]), *(sys.argv[3:4]))
     else:
         kernels(int(sys.argv[1]) if len(sys.argv) > 1 else 5)
