@@ -253,9 +253,99 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32(int64_t M, int64_t N, int64
             }
 }
 
+// ---------------------------------------------------------------------------------------
+// fp32 forward (NT) products with few rows (M <= 2048: generate()'s per-token steps, 256 rows) --
+// k_gemm_f32's 128 x 64 tiles leave most CUs idle there and pay a global-load round trip per 16-deep
+// K-step.  One wave per 32 x 32 tile: each 128-deep K chunk's operands (a lane's A / B values for 32
+// k4-steps) are loaded straight to registers, all in flight together, then its MFMAs.  The same
+// v_mfma_f32_16x16x4_f32 lane / k assignment, k order and zero-padded K (to a multiple of 16) as
+// k_gemm_f32, and its epilogue arithmetic with the operands loaded before the stores: bitwise its
+// result.
+template <int EK>
+__global__ __launch_bounds__(64) void k_gemm_f32s(int64_t M, int64_t N, int64_t K, const float* __restrict__ A,
+                                                  int64_t lda, const float* __restrict__ B, int64_t ldb,
+                                                  float* __restrict__ C, int64_t ldc, EpiArgs epi) {
+    const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+    const int64_t m0 = (int64_t)blockIdx.x * 32, n0 = (int64_t)blockIdx.y * 32;
+    const int64_t kpad = (K + 15) / 16 * 16;   // k_gemm_f32's padded depth
+    fv4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = fv4{0.f, 0.f, 0.f, 0.f};
+    const int64_t ra0 = m0 + li, ra1 = m0 + 16 + li, rb0 = n0 + li, rb1 = n0 + 16 + li;
+    for (int64_t kc = 0; kc < kpad; kc += 128) {
+        float a[2][32], b[2][32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) {
+            const int64_t k = kc + 4 * t + g;
+            const bool kin = k < K;
+            a[0][t] = (kin && ra0 < M) ? A[ra0 * lda + k] : 0.f;
+            a[1][t] = (kin && ra1 < M) ? A[ra1 * lda + k] : 0.f;
+            b[0][t] = (kin && rb0 < N) ? B[rb0 * ldb + k] : 0.f;
+            b[1][t] = (kin && rb1 < N) ? B[rb1 * ldb + k] : 0.f;
+        }
+#pragma unroll
+        for (int t = 0; t < 32; ++t) {
+            if (kc + 4 * t < kpad) {   // wave-uniform: k_gemm_f32's k4-steps only
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][t], b[j][t], acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+    constexpr bool BIAS = EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_BIAS_RESID;
+    const bool hb = BIAS && epi.bias, hr = EK == CG_EPI_BIAS_RESID && epi.resid;
+    float bv[2] = {0.f, 0.f}, rv[2][2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int64_t n = n0 + 16 * j + li;
+        if (hb && n < N) bv[j] = epi.bias[n];
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t m = m0 + 16 * i + 4 * g + r, n = n0 + 16 * j + li;
+                rv[i][j][r] = (hr && m < M && n < N) ? epi.resid[m * epi.ld_resid + n] : 0.f;
+            }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t m = m0 + 16 * i + 4 * g + r, n = n0 + 16 * j + li;
+                float v = acc[i][j][r];
+                if (hb) v += bv[j];
+                if (EK == CG_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
+                if (hr) v = rv[i][j][r] + v;
+                if (m < M && n < N) C[m * ldc + n] = v;
+            }
+}
+
+// the small-M kernel's conditions (else k_gemm_f32); gemm_variant 98 forces k_gemm_f32 (A/B, tests)
+bool launch_f32s(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
+                 int64_t ldc, const EpiArgs& e, hipStream_t st) {
+    if (g_gemm_variant == 98 || e.beta != 0.f || M > 2048) return false;
+    const dim3 grid((unsigned)((M + 31) / 32), (unsigned)((N + 31) / 32));
+#define KS(EK_) k_gemm_f32s<EK_><<<grid, 64, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e)
+    switch (e.kind) {
+        case CG_EPI_STORE: KS(CG_EPI_STORE); return true;
+        case CG_EPI_BIAS: KS(CG_EPI_BIAS); return true;
+        case CG_EPI_BIAS_RELU: KS(CG_EPI_BIAS_RELU); return true;
+        case CG_EPI_BIAS_RESID: KS(CG_EPI_BIAS_RESID); return true;
+        default: return false;
+    }
+#undef KS
+}
+
 void launch_f32(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                 const float* B, int64_t ldb, float* C, int64_t ldc, const EpiArgs& e, int split_k, float* ws,
                 hipStream_t st) {
+    if (!a_trans && !b_trans && split_k == 1 && launch_f32s(M, N, K, A, lda, B, ldb, C, ldc, e, st)) return;
     int64_t kchunk = (K + split_k - 1) / split_k;
     kchunk = (kchunk + FBKK - 1) / FBKK * FBKK;
     dim3 grid((unsigned)(((M + FBM - 1) / FBM) * ((N + FBN - 1) / FBN)), (unsigned)split_k);
@@ -536,11 +626,12 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     CG_REQUIRE(key, "cg_set_tuning: null key");
     if (!strcmp(key, "gemm_variant")) {
         // default build: automatic (0), the register-staged fallback (2), the persistent 128x128 (9)
-        // and 256x256 (24) tiles, the generic kernels (99); the measured-slower A/B tiles (among
+        // and 256x256 (24) tiles, k_gemm_f32 for every fp32 product (98: not the small-M
+        // kernel), the generic kernels (99); the measured-slower A/B tiles (among
         // them 26, the 256x256 tile on the staggered 8-phase schedule) only in
         // libcharpt_hip_ab.so (`make ab`, CG_AB_VARIANTS)
 #ifndef CG_AB_VARIANTS
-        CG_REQUIRE(value == 0 || value == 2 || value == 9 || value == 24 || value == 99,
+        CG_REQUIRE(value == 0 || value == 2 || value == 9 || value == 24 || value == 98 || value == 99,
                    "cg_set_tuning: gemm_variant %d is an A/B variant, not in this build (make ab)", value);
 #endif
         g_gemm_variant = value;

@@ -1158,6 +1158,41 @@ def test_gemm_f32_mfma_matches_generic(at, bt, M, N, K, split):
         assert relerr(out, ref) < 1e-5
 
 
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+@pytest.mark.parametrize("M,N,K", [(256, 378, 126), (256, 126, 504), (256, 65, 126), (1, 504, 126), (33, 70, 5),
+                                   (2048, 126, 200), (100, 33, 257)])
+def test_gemm_f32_small_m_matches_128x64_bitwise(kind, M, N, K):
+    """The small-M fp32 forward kernel (k_gemm_f32s, M <= 2048) against k_gemm_f32 (gemm_variant 98):
+    same MFMA lane / k order and padded depth, same epilogue arithmetic -> bitwise equal."""
+    from replicatinggpt_amd import _lib as L
+    lib = L.load()
+    torch.manual_seed(31)
+    A = torch.randn(M, K, device=DEV)
+    B = torch.randn(N, K, device=DEV)
+    bias = torch.randn(N, device=DEV)
+    resid = torch.randn(M, N, device=DEV)
+    outs = []
+    for v in (98, 0):
+        L.check(lib.cg_set_tuning(b"gemm_variant", v))
+        try:
+            out = torch.full((M, N), float("nan"), device=DEV)
+            ops().gemm(A, B, out, False, False, False, M, N, K, K, K, N, kind, bias if kind else None,
+                       resid if kind == 3 else None, N if kind == 3 else 0, None, 0, 0.0, 0, None, 0, 0.0, 1, None)
+            torch.cuda.synchronize()
+        finally:
+            L.check(lib.cg_set_tuning(b"gemm_variant", 0))
+        outs.append(out)
+    ref = A.double().cpu() @ B.double().cpu().T
+    if kind:
+        ref = ref + bias.double().cpu()
+    if kind == 2:
+        ref = torch.relu(ref)
+    if kind == 3:
+        ref = ref + resid.double().cpu()
+    assert relerr(outs[1], ref) < 1e-5
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+
+
 def test_adamw_matches_torch():
     n = 1000
     torch.manual_seed(8)
