@@ -12,6 +12,9 @@
 // phase is captured once as a hipGraph and replayed per token.
 #include "common.h"
 
+namespace cg {
+int g_decode_attn_rows = 1;   // cg_set_tuning("decode_attn_rows"): 0 = k_decode_attn for every layout (A/B, tests)
+}
 namespace {
 using namespace cg;
 
@@ -116,6 +119,107 @@ __global__ __launch_bounds__(256) void k_decode_attn(const float* __restrict__ q
     if (lane < D) o[b * ldo + h * D + lane] = out;
 }
 
+// k_decode_attn for the phase-1 cache ([B, H, Tmax, D], key rows contiguous, 16-B aligned chunks): one
+// 64-thread block per (b, h).  A lane-per-key load reads one float of each of 64 rows per instruction --
+// D instructions per chunk and operand, each touching ~D/1.5 cache lines -- and the rows of 6 waves a CU
+// holds do not stay in its L1 between those instructions: the kernel ran at 1.4 TB/s of K / V at 256 keys
+// and its time grew with the line count per instruction (row stride 32 floats: 0.75 TB/s;
+// tools/decode_attn_probe.py).  Here a chunk's 64 K and V rows (64 D contiguous floats each) are read as
+// float4s, lane l taking float4 l + 64 r, the next chunk's loads issued before the current chunk's
+// arithmetic, and staged through LDS so that each lane then reads its key's row (stride D: conflict-free
+// for odd D).  Per lane the arithmetic is k_decode_attn's, value for value (a lane past the last key
+// reads zero rows instead of key 0's: its p is 0 either way), so the output is bitwise the same.
+template <int DP>
+__global__ __launch_bounds__(64) void k_decode_attn_rows(const float* __restrict__ q, int64_t ldq,
+                                                         const float* __restrict__ kc, const float* __restrict__ vc,
+                                                         int64_t sb, int64_t sh, int64_t B, int64_t H, int64_t D,
+                                                         const int64_t* __restrict__ len_dev, int64_t nfix, float scale,
+                                                         float* __restrict__ o, int64_t ldo) {
+    constexpr int R4 = DP;   // float4s per lane per operand: 64 rows x DP floats / 4 / 64 lanes
+    __shared__ float4 ks4[16 * DP], vs4[16 * DP];
+    const float* ks = (const float*)ks4;
+    const float* vs = (const float*)vs4;
+    const int lane = threadIdx.x;
+    const int64_t bh = blockIdx.x;
+    const int64_t b = bh / H, h = bh % H;
+    const int64_t n = len_dev ? *len_dev : nfix;  // keys 0..n-1
+    const float4* K4 = (const float4*)(kc + b * sb + h * sh);
+    const float4* V4 = (const float4*)(vc + b * sb + h * sh);
+    const int64_t f4 = 16 * D;   // float4s per 64-row chunk
+    float qv[DP], acc[DP];
+#pragma unroll
+    for (int e = 0; e < DP; ++e) {
+        qv[e] = e < D ? q[b * ldq + h * D + e] : 0.f;
+        acc[e] = 0.f;
+    }
+    float4 kr[R4 / 4], vr[R4 / 4];
+    auto load = [&](int64_t c0) {
+        const int64_t lim = ((n - c0 < 64 ? n - c0 : 64) * D + 3) / 4;   // float4s holding the chunk's keys
+#pragma unroll
+        for (int r = 0; r < R4 / 4; ++r) {
+            const int64_t i = lane + 64 * r;
+            const bool in = i < f4 && i < lim;
+            kr[r] = in ? K4[c0 / 4 * D + i] : float4{0.f, 0.f, 0.f, 0.f};
+            vr[r] = in ? V4[c0 / 4 * D + i] : float4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    float m = -INFINITY, l = 0.f;
+    load(0);
+    for (int64_t c0 = 0; c0 < n; c0 += 64) {
+        const int64_t cnt = (n - c0 < 64 ? n - c0 : 64) * D;   // floats of the chunk's keys
+        __syncthreads();   // the previous chunk's rows are read (one wave: no wait for other waves)
+#pragma unroll
+        for (int r = 0; r < R4 / 4; ++r) {
+            const int64_t i = lane + 64 * r;
+            if (i < f4) {
+                float4 kx = kr[r], vx = vr[r];
+                // a float4 straddling the last key: floats past it zero (key 0's floats in k_decode_attn
+                // never reach a valid lane's row either way)
+                const int64_t f = 4 * i;
+                if (f + 4 > cnt) {
+                    if (f + 0 >= cnt) kx.x = vx.x = 0.f;
+                    if (f + 1 >= cnt) kx.y = vx.y = 0.f;
+                    if (f + 2 >= cnt) kx.z = vx.z = 0.f;
+                    if (f + 3 >= cnt) kx.w = vx.w = 0.f;
+                }
+                ks4[i] = kx;
+                vs4[i] = vx;
+            }
+        }
+        __syncthreads();
+        if (c0 + 64 < n) load(c0 + 64);
+        const int64_t j = c0 + lane;
+        const bool ok = j < n;
+        float kv[DP], vv[DP];
+#pragma unroll
+        for (int e = 0; e < DP; ++e) {
+            kv[e] = e < D ? ks[lane * D + e] : 0.f;
+            vv[e] = e < D ? vs[lane * D + e] : 0.f;
+        }
+        float s = 0.f;
+#pragma unroll
+        for (int e = 0; e < DP; ++e) s = fmaf(qv[e], kv[e], s);
+        s = ok ? s * scale : -INFINITY;
+        const float m_new = fmaxf(m, wave_max(s));
+        const float alpha = __expf(m - m_new);
+        const float p = ok ? __expf(s - m_new) : 0.f;
+        l = l * alpha + wave_sum(p);
+        m = m_new;
+#pragma unroll
+        for (int e = 0; e < DP; ++e) acc[e] = fmaf(p, vv[e], acc[e] * alpha);
+    }
+    const float inv = 1.f / l;
+    float out = 0.f;
+#pragma unroll
+    for (int e = 0; e < DP; ++e) {
+        if (e < D) {   // wave-uniform
+            const float t = wave_sum_dpp(acc[e]);
+            out = lane == e ? t * inv : out;
+        }
+    }
+    if (lane < D) o[b * ldo + h * D + lane] = out;
+}
+
 // next token per row from logits [B, V]: greedy = first argmax (torch.argmax tie rule); else
 // inverse-CDF sampling of softmax(logits) with u = Philox(seed, stream = step)[b] / 2^32.
 // Writes idx[b, len] (len = *len_dev) -- the caller then advances *len_dev.
@@ -193,7 +297,13 @@ extern "C" int cg_decode_attn(const float* q, int64_t ldq, const float* k, const
                               float scale, float* o, int64_t ldo, void* stream) {
     CG_REQUIRE(B > 0 && H > 0 && D > 0 && D <= 64, "cg_decode_attn: needs D <= 64");
     CG_REQUIRE(len_dev || nkeys > 0, "cg_decode_attn: needs at least one key");
-    if (D <= 24)
+    // contiguous, 16-B aligned key rows (the phase-1 cache): the coalesced-chunk kernel
+    const bool rows = g_decode_attn_rows && D <= 24 && sj == D && sh % 4 == 0 && sb % 4 == 0 &&
+                      ((uintptr_t)k & 15) == 0 && ((uintptr_t)v & 15) == 0;
+    if (rows)
+        k_decode_attn_rows<24><<<(unsigned)(B * H), 64, 0, (hipStream_t)stream>>>(q, ldq, k, v, sb, sh, B, H, D,
+                                                                                  len_dev, nkeys, scale, o, ldo);
+    else if (D <= 24)
         k_decode_attn<24><<<ceil_div(B * H, 4), 256, 0, (hipStream_t)stream>>>(q, ldq, k, v, sb, sh, sj, B, H, D,
                                                                                len_dev, nkeys, scale, o, ldo);
     else

@@ -614,6 +614,7 @@ void flush_red_locked(DeferQueue& q) {
 int g_skip_splitk_reduce = 0;  // measurement knob (WRONG results): time a step without the split-K reduce
 extern int g_attn_variant;  // attention_d64.hip
 extern int g_attn_bwd_lpt;  // attention_d64.hip
+extern int g_decode_attn_rows;  // decode.hip
 extern int g_ln_rpb;  // layernorm.hip
 extern int g_adamw_mode;  // ce_adamw.hip
 extern int g_ln_waves;  // layernorm.hip
@@ -662,6 +663,11 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     if (!strcmp(key, "ln_rl")) {   // A/B: the LayerNorm backward rows' next loads before the current stores
         CG_REQUIRE(value >= 0 && value <= 2, "cg_set_tuning: ln_rl must be 0, 1 or 2 (2: also at C = 768)");
         g_ln_rl = value;
+        return CG_OK;
+    }
+    if (!strcmp(key, "decode_attn_rows")) {   // A/B: the coalesced-chunk phase-1 decode attention (decode.hip)
+        CG_REQUIRE(value == 0 || value == 1, "cg_set_tuning: decode_attn_rows must be 0 or 1");
+        g_decode_attn_rows = value;
         return CG_OK;
     }
     if (!strcmp(key, "attn_bwd_lpt")) {   // A/B: merged resident backward workgroup order (1 = dK/dV first)

@@ -410,6 +410,39 @@ def test_decode_attn_any_key_count(n):
     assert relerr(o, ref) < 1e-5
 
 
+@pytest.mark.parametrize("D,Tmax", [(21, 256), (16, 256), (24, 128), (7, 64)])
+@pytest.mark.parametrize("n", [1, 3, 63, 64, 65, 100, 127, 200, 256])
+def test_decode_attn_rows_matches_lane_per_key_bitwise(D, Tmax, n):
+    """The coalesced-chunk phase-1 decode attention (k_decode_attn_rows: contiguous, 16-B aligned cache
+    rows) against the lane-per-key kernel (decode_attn_rows 0): the same per-lane arithmetic -> bitwise
+    equal, at key counts inside, at and across 64-key chunks, up to the cache's last row."""
+    from replicatinggpt_amd import _lib as L, ops
+    if n > Tmax:
+        pytest.skip("more keys than cache rows")
+    lib = L.load()
+    B, H = 5, 6
+    torch.manual_seed(1000 * D + n)
+    kc = torch.randn(B, H, Tmax, D, device=DEV)
+    vc = torch.randn(B, H, Tmax, D, device=DEV)
+    q = torch.randn(B, 3 * H * D, device=DEV)   # the qkv rows' q part, row stride 3 H D
+    ln = torch.tensor([n], dtype=torch.int64, device=DEV)
+    outs = []
+    for v in (0, 1):
+        L.check(lib.cg_set_tuning(b"decode_attn_rows", v))
+        try:
+            o = torch.full((B, H * D), float("nan"), device=DEV)
+            ops.decode_attn(q, q.stride(0), kc, 0, vc, 0, H * Tmax * D, Tmax * D, D, B, H, D, ln, 0, D ** -0.5, o)
+            torch.cuda.synchronize()
+        finally:
+            L.check(lib.cg_set_tuning(b"decode_attn_rows", 1))
+        outs.append(o)
+    qq = q[:, :H * D].double().view(B, H, 1, D)
+    s = (qq @ kc[:, :, :n].double().transpose(-1, -2)) * D ** -0.5
+    ref = (torch.softmax(s, -1) @ vc[:, :, :n].double()).view(B, H * D)
+    assert relerr(outs[1], ref) < 1e-5
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+
+
 def test_fused_b1_gradient_training_parity():
     """CHARPT_FUSE_COLPART (FFN b1 gradient fused into the ReLU-backward dgrad epilogue) on vs off:
     both sum the same bf16-rounded dz1, so a few bf16 training steps agree to summation-order
