@@ -129,10 +129,14 @@ __global__ __launch_bounds__(256) void k_decode_attn(const float* __restrict__ q
 // arithmetic, and staged through LDS so that each lane then reads its key's row (stride D: conflict-free
 // for odd D).  Per lane the arithmetic is k_decode_attn's, value for value (a lane past the last key
 // reads zero rows instead of key 0's: its p is 0 either way), so the output is bitwise the same.
-template <int DP>
+// SJ: key rows sj floats apart (phase 2's last layer: the window's qkv rows, sj = 3 C) -- the chunk's
+// floats read as dwords, lane l taking float l + 64 r of the chunk's 64 D (row (l + 64 r) / D), so an
+// instruction spans ~64 / D rows instead of 64.
+template <int DP, bool SJ = false>
 __global__ __launch_bounds__(64) void k_decode_attn_rows(const float* __restrict__ q, int64_t ldq,
                                                          const float* __restrict__ kc, const float* __restrict__ vc,
-                                                         int64_t sb, int64_t sh, int64_t B, int64_t H, int64_t D,
+                                                         int64_t sb, int64_t sh, int64_t sj, int64_t B, int64_t H,
+                                                         int64_t D,
                                                          const int64_t* __restrict__ len_dev, int64_t nfix, float scale,
                                                          float* __restrict__ o, int64_t ldo) {
     constexpr int R4 = DP;   // float4s per lane per operand: 64 rows x DP floats / 4 / 64 lanes
@@ -153,7 +157,35 @@ __global__ __launch_bounds__(64) void k_decode_attn_rows(const float* __restrict
         acc[e] = 0.f;
     }
     float4 kr[R4 / 4], vr[R4 / 4];
+    float kr1[SJ ? DP : 1], vr1[SJ ? DP : 1];
+    const float* Kb = kc + b * sb + h * sh;
+    const float* Vb = vc + b * sb + h * sh;
+    int off[SJ ? DP : 1];   // SJ: float l + 64 r of a chunk at row * sj + e (INT_MAX: past the chunk)
+    if constexpr (SJ) {
+        int row = lane / (int)D, e = lane - row * (int)D;
+        const int drow = 64 / (int)D, de = 64 - drow * (int)D;
+#pragma unroll
+        for (int r = 0; r < DP; ++r) {
+            off[r] = lane + 64 * r < 64 * D ? row * (int)sj + e : INT_MAX;
+            row += drow;
+            e += de;
+            if (e >= D) e -= (int)D, ++row;
+        }
+    }
     auto load = [&](int64_t c0) {
+        if constexpr (SJ) {
+            const int64_t rows = n - c0 < 64 ? n - c0 : 64;
+            const int lim = (int)(rows * sj);   // offsets of the chunk's keys (e < D <= sj)
+            const float* kb = Kb + c0 * sj;
+            const float* vb = Vb + c0 * sj;
+#pragma unroll
+            for (int r = 0; r < DP; ++r) {
+                const bool in = off[r] < lim;
+                kr1[r] = in ? kb[off[r]] : 0.f;
+                vr1[r] = in ? vb[off[r]] : 0.f;
+            }
+            return;
+        }
         const int64_t lim = ((n - c0 < 64 ? n - c0 : 64) * D + 3) / 4;   // float4s holding the chunk's keys
 #pragma unroll
         for (int r = 0; r < R4 / 4; ++r) {
@@ -168,8 +200,18 @@ __global__ __launch_bounds__(64) void k_decode_attn_rows(const float* __restrict
     for (int64_t c0 = 0; c0 < n; c0 += 64) {
         const int64_t cnt = (n - c0 < 64 ? n - c0 : 64) * D;   // floats of the chunk's keys
         __syncthreads();   // the previous chunk's rows are read (one wave: no wait for other waves)
+        if constexpr (SJ) {
 #pragma unroll
-        for (int r = 0; r < R4 / 4; ++r) {
+            for (int r = 0; r < DP; ++r) {
+                const int64_t i = lane + 64 * r;
+                if (i < 64 * D) {
+                    ((float*)ks4)[i] = kr1[r];
+                    ((float*)vs4)[i] = vr1[r];
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < (SJ ? 0 : R4 / 4); ++r) {
             const int64_t i = lane + 64 * r;
             if (i < f4) {
                 float4 kx = kr[r], vx = vr[r];
@@ -301,8 +343,11 @@ extern "C" int cg_decode_attn(const float* q, int64_t ldq, const float* k, const
     const bool rows = g_decode_attn_rows && D <= 24 && sj == D && sh % 4 == 0 && sb % 4 == 0 &&
                       ((uintptr_t)k & 15) == 0 && ((uintptr_t)v & 15) == 0;
     if (rows)
-        k_decode_attn_rows<24><<<(unsigned)(B * H), 64, 0, (hipStream_t)stream>>>(q, ldq, k, v, sb, sh, B, H, D,
+        k_decode_attn_rows<24><<<(unsigned)(B * H), 64, 0, (hipStream_t)stream>>>(q, ldq, k, v, sb, sh, sj, B, H, D,
                                                                                   len_dev, nkeys, scale, o, ldo);
+    else if (g_decode_attn_rows && D <= 24 && sj >= D && sj < (1 << 24))   // key rows sj floats apart (a window's qkv rows)
+        k_decode_attn_rows<24, true><<<(unsigned)(B * H), 64, 0, (hipStream_t)stream>>>(
+            q, ldq, k, v, sb, sh, sj, B, H, D, len_dev, nkeys, scale, o, ldo);
     else if (D <= 24)
         k_decode_attn<24><<<ceil_div(B * H, 4), 256, 0, (hipStream_t)stream>>>(q, ldq, k, v, sb, sh, sj, B, H, D,
                                                                                len_dev, nkeys, scale, o, ldo);

@@ -443,6 +443,40 @@ def test_decode_attn_rows_matches_lane_per_key_bitwise(D, Tmax, n):
     assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
 
 
+@pytest.mark.parametrize("D,T", [(21, 256), (16, 200), (24, 64)])
+@pytest.mark.parametrize("n", [1, 64, 65, 131, 256])
+def test_decode_attn_rows_strided_matches_lane_per_key_bitwise(D, T, n):
+    """The same comparison on phase 2's layout: keys and values in a window's qkv rows (row stride
+    3 H D, K at column H D, V at 2 H D; not 16-B aligned) -- the strided-chunk kernel against the
+    lane-per-key one, bitwise."""
+    from replicatinggpt_amd import _lib as L, ops
+    if n > T:
+        pytest.skip("more keys than window rows")
+    lib = L.load()
+    B, H = 5, 6
+    C = H * D
+    torch.manual_seed(2000 * D + n)
+    qkv = torch.randn(B, T, 3 * C, device=DEV)
+    q = torch.randn(B, 3 * C, device=DEV)
+    ln = torch.tensor([n], dtype=torch.int64, device=DEV)
+    outs = []
+    for v in (0, 1):
+        L.check(lib.cg_set_tuning(b"decode_attn_rows", v))
+        try:
+            o = torch.full((B, C), float("nan"), device=DEV)
+            ops.decode_attn(q, q.stride(0), qkv, C, qkv, 2 * C, T * 3 * C, D, 3 * C, B, H, D, ln, 0, D ** -0.5, o)
+            torch.cuda.synchronize()
+        finally:
+            L.check(lib.cg_set_tuning(b"decode_attn_rows", 1))
+        outs.append(o)
+    kk = qkv[:, :n, C:2 * C].double().view(B, n, H, D).transpose(1, 2)
+    vv = qkv[:, :n, 2 * C:].double().view(B, n, H, D).transpose(1, 2)
+    s = (q[:, :C].double().view(B, H, 1, D) @ kk.transpose(-1, -2)) * D ** -0.5
+    ref = (torch.softmax(s, -1) @ vv).reshape(B, C)
+    assert relerr(outs[1], ref) < 1e-5
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+
+
 def test_fused_b1_gradient_training_parity():
     """CHARPT_FUSE_COLPART (FFN b1 gradient fused into the ReLU-backward dgrad epilogue) on vs off:
     both sum the same bf16-rounded dz1, so a few bf16 training steps agree to summation-order

@@ -54,6 +54,19 @@ def case(B, H, D, n, sj, T=256):
           f"{mb / t:5.2f} TB/s); copy of those rows {tc:7.2f} us", flush=True)
 
 
+def window(B, H, D, T):
+    """phase 2's call: the last query against a window's qkv rows (row stride 3 C)"""
+    C = H * D
+    qkv = torch.randn(B, T, 3 * C, device="cuda")
+    q = torch.randn(B, 3 * C, device="cuda")
+    o = torch.empty(B, C, device="cuda")
+
+    def run():
+        ops.decode_attn(q, 3 * C, qkv, C, qkv, 2 * C, T * 3 * C, D, 3 * C, B, H, D, None, T, D ** -0.5, o)
+    t = graph_us(run)
+    print(f"B={B:4d} H={H} D={D} n={T:3d} window qkv rows: {t:7.2f} us", flush=True)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "ab":   # lane-per-key (0) vs coalesced-chunk (1) kernel
         from replicatinggpt_amd import _lib as L
@@ -62,6 +75,7 @@ if __name__ == "__main__":
             print(f"decode_attn_rows {v}", flush=True)
             for n in (1, 64, 128, 256):
                 case(256, 6, 21, n, 21)
+            window(256, 6, 21, 256)
         sys.exit(0)
     for n in (64, 128, 256):
         case(256, 6, 21, n, 21)
