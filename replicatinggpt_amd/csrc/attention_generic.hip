@@ -332,13 +332,22 @@ __global__ __launch_bounds__(512) void k_attn_fwd_f32res(int64_t T_, int H, int 
     const float* qb = q + (int64_t)b * T_ * ld + h * D;
     const float* kb = k + (int64_t)b * T_ * ld + h * D;
     const float* vb = v + (int64_t)b * T_ * ld + h * D;
-    for (int i = tid; i < 256 * 32; i += 512) {
-        const int r = i >> 5, e = i & 31;
+    // every K / V element of the thread loaded before the first LDS write (a load-write loop waits
+    // for each load in turn: 32 dependent round trips per thread before any MFMA)
+    constexpr int NL = 256 * DP4 / 512;
+    float kx[NL], vx[NL];
+#pragma unroll
+    for (int u = 0; u < NL; ++u) {
+        const int i = tid + 512 * u, r = i / DP4, e = i - r * DP4;
         const bool ok = r < T_ && e < D;
-        if (e < DP4) {
-            Ks[r * KLD + e] = ok ? kb[(int64_t)r * ld + e] : 0.f;
-            Vs[r * VLD + e] = ok ? vb[(int64_t)r * ld + e] : 0.f;
-        }
+        kx[u] = ok ? kb[(int64_t)r * ld + e] : 0.f;
+        vx[u] = ok ? vb[(int64_t)r * ld + e] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < NL; ++u) {
+        const int i = tid + 512 * u, r = i / DP4, e = i - r * DP4;
+        Ks[r * KLD + e] = kx[u];
+        Vs[r * VLD + e] = vx[u];
     }
     __syncthreads();
 #pragma unroll 1
