@@ -203,36 +203,55 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32(int64_t M, int64_t N, int64
         // counts both), one HBM round trip per output element of the lane.  Same arithmetic and
         // order as epi_scalar: bias added only when present, ReLU, then resid + v.
         const bool hb = kind != CG_EPI_STORE && epi.bias, hr = kind == CG_EPI_BIAS_RESID && epi.resid;
-        float bv[2] = {0.f, 0.f}, rv[4][2][4];
+        float bv[2] = {0.f, 0.f}, rv[2][2][4];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int64_t n = n0 + wn * 32 + 16 * j + li;
             if (hb && n < N) bv[j] = epi.bias[n];
         }
+        // row fragments in two halves (i = 0-1, 2-3): each half's residuals loaded before the previous
+        // half's stores, one half's registers live at a time
+        auto load_half = [&](int hf) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+            for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+                for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int64_t m = m0 + wm * 64 + 16 * i + 4 * g + r;
-                    const int64_t n = n0 + wn * 32 + 16 * j + li;
-                    rv[i][j][r] = (hr && m < M && n < N) ? epi.resid[m * epi.ld_resid + n] : 0.f;
-                }
+                    for (int r = 0; r < 4; ++r) {
+                        const int64_t m = m0 + wm * 64 + 16 * (2 * hf + ii) + 4 * g + r;
+                        const int64_t n = n0 + wn * 32 + 16 * j + li;
+                        rv[ii][j][r] = (hr && m < M && n < N) ? epi.resid[m * epi.ld_resid + n] : 0.f;
+                    }
+        };
+        load_half(0);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int hf = 0; hf < 2; ++hf) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+            for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int64_t m = m0 + wm * 64 + 16 * i + 4 * g + r;
-                    const int64_t n = n0 + wn * 32 + 16 * j + li;
-                    float v = acc[i][j][r];
-                    if (hb) v += bv[j];
-                    if (kind == CG_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
-                    if (hr) v = rv[i][j][r] + v;
-                    if (m < M && n < N) C[m * ldc + n] = v;
-                }
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = 2 * hf + ii;
+                        float v = acc[i][j][r];
+                        if (hb) v += bv[j];
+                        if (kind == CG_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
+                        if (hr) v = rv[ii][j][r] + v;
+                        acc[i][j][r] = v;
+                    }
+            if (hf == 0) load_half(1);
+#pragma unroll
+            for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = 2 * hf + ii;
+                        const int64_t m = m0 + wm * 64 + 16 * i + 4 * g + r;
+                        const int64_t n = n0 + wn * 32 + 16 * j + li;
+                        if (m < M && n < N) C[m * ldc + n] = acc[i][j][r];
+                    }
+        }
         return;
     }
     const uint64_t stream = (epi.kind == CG_EPI_BIAS_DROP_RESID && epi.thr) ? dropout_stream(epi.rng_call, epi.site) : 0;

@@ -346,6 +346,10 @@ int launch_ln_fwd(const float* x, const float* w, const float* b, TY* y, float* 
         // narrow rows (C1 / C5: C = 126, 504 B): one 8-B chunk per lane and 8 rows per wave in flight --
         // the generic (1, 32) form issued 4-B loads through 32 bounds-checked chunks, 2 rows per wave
         // (28 us for the [65536, 126] decode window: 2.4 TB/s)
+        if (rows < 8192) {   // generate()'s 256-row steps: one row per wave, every CU's share in flight at once
+            k_ln_fwd<2, 1, TY, 1><<<ceil_div(rows, 4), 256, 0, st>>>(x, w, b, y, mean, rstd, rows, C, eps);
+            return CG_OK;
+        }
         constexpr int RPW8 = 8;
         int grid8 = ceil_div(rows, 4 * RPW8);
         grid8 = grid8 > 4096 ? 4096 : grid8;

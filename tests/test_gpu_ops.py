@@ -1315,3 +1315,28 @@ def test_adamw_rounding_is_explicit():
     torch.cuda.synchronize()
     assert np.array_equal(md.cpu().numpy(), M) and np.array_equal(vd.cpu().numpy(), V)
     assert np.array_equal(pd.cpu().numpy(), P)
+
+
+@pytest.mark.parametrize("C", [126, 64])
+def test_layernorm_fwd_narrow_row_paths_bitwise(C):
+    """Narrow-row LayerNorm forward: the one-row-per-wave launch (< 8192 rows, generate()'s 256-row
+    steps) and the 8-rows-per-wave launch (the decode window's 65536 rows) share ln_fwd_row -> the
+    same bits for the same rows."""
+    torch.manual_seed(C)
+    x = torch.randn(65536, C, device=DEV) * 3 + 1
+    w = torch.randn(C, device=DEV)
+    b = torch.randn(C, device=DEV)
+    outs = []
+    for rows in (65536, 256, 8191, 1):
+        y = torch.empty(rows, C, device=DEV)
+        mean = torch.empty(rows, device=DEV)
+        rstd = torch.empty(rows, device=DEV)
+        ops().layernorm_fwd(x[:rows], w, b, y, mean, rstd, 1e-5)
+        torch.cuda.synchronize()
+        outs.append((y, mean, rstd))
+    ref = torch.nn.functional.layer_norm(x[:256].double().cpu(), (C,), w.double().cpu(), b.double().cpu(), 1e-5)
+    assert relerr(outs[1][0], ref) < 1e-5
+    for y, mean, rstd in outs[1:]:
+        n = y.shape[0]
+        assert torch.equal(y, outs[0][0][:n]) and torch.equal(mean, outs[0][1][:n])
+        assert torch.equal(rstd, outs[0][2][:n])
