@@ -368,12 +368,18 @@ __global__ __launch_bounds__(512) void k_attn_fwd_f32res(int64_t T_, int H, int 
             const int64_t k0 = (int64_t)kv * 64;
             const float* Kt = Ks + k0 * KLD;
             const float* Vt = Vs + k0 * VLD;
+            // 16-key sub-tiles past the group's last query (k0 + 16 kt > qw0 + 15) are fully masked: their
+            // scores are -inf, their p exact zeros, so their S and O MFMAs and softmax terms change
+            // nothing (max with -inf, + 0, MFMA products all 0) -- skipped, the result bitwise the same
+            const int nkt = (int)((qw0 + 15 - k0) / 16 + 1 < 4 ? (qw0 + 15 - k0) / 16 + 1 : 4);   // wave-uniform
             fv4 st[4];
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt) {
                 fv4 c = {0.f, 0.f, 0.f, 0.f};
+                if (kt < nkt) {
 #pragma unroll
-                for (int t = 0; t < KS; ++t) c = mfma_f32x4(Kt[(16 * kt + li) * KLD + 4 * t + g], qf[t], c);
+                    for (int t = 0; t < KS; ++t) c = mfma_f32x4(Kt[(16 * kt + li) * KLD + 4 * t + g], qf[t], c);
+                }
                 st[kt] = c;
             }
             float mx = -INFINITY;
@@ -385,7 +391,7 @@ __global__ __launch_bounds__(512) void k_attn_fwd_f32res(int64_t T_, int H, int 
                     float x = st[kt][r] * scale;
                     if (key > qa || key >= T_) x = -INFINITY;
                     st[kt][r] = x;
-                    mx = fmaxf(mx, x);
+                    if (kt < nkt) mx = fmaxf(mx, x);
                 }
             mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
             mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
@@ -396,9 +402,11 @@ __global__ __launch_bounds__(512) void k_attn_fwd_f32res(int64_t T_, int H, int 
             for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float p = st[kt][r] == -INFINITY ? 0.f : expf(st[kt][r] - m_new);
-                    st[kt][r] = p;
-                    ps += p;
+                    if (kt < nkt) {
+                        const float p = st[kt][r] == -INFINITY ? 0.f : expf(st[kt][r] - m_new);
+                        st[kt][r] = p;
+                        ps += p;
+                    }
                 }
             ps += __shfl_xor(ps, 16, 64);
             ps += __shfl_xor(ps, 32, 64);
@@ -407,7 +415,8 @@ __global__ __launch_bounds__(512) void k_attn_fwd_f32res(int64_t T_, int H, int 
             oacc[0] *= alpha;
             oacc[1] *= alpha;
 #pragma unroll
-            for (int kt = 0; kt < 4; ++kt)
+            for (int kt = 0; kt < 4; ++kt) {
+                if (kt >= nkt) break;
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
                     const int key = 16 * kt + 4 * g + s;
@@ -417,6 +426,7 @@ __global__ __launch_bounds__(512) void k_attn_fwd_f32res(int64_t T_, int H, int 
                         oacc[et] = mfma_f32x4(e < DP4 ? Vt[key * VLD + e] : 0.f, st[kt][s], oacc[et]);
                     }
                 }
+            }
         }
         if (qa >= T_) continue;
         const float inv = 1.f / l_run;
