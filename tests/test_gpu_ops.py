@@ -1040,7 +1040,7 @@ def test_attention_bwd_regenerates_mask():
     assert torch.equal(g1, g2)
 
 
-@pytest.mark.parametrize("V,T,C,B", [(65, 40, 126, 3), (65, 256, 384, 64), (65, 100, 200, 5), (200, 64, 128, 4),
+@pytest.mark.parametrize("V,T,C,B", [(65, 40, 126, 3), (65, 256, 126, 7), (65, 9, 21, 2), (65, 256, 384, 64), (65, 100, 200, 5), (200, 64, 128, 4),
                                      (600, 64, 96, 3), (65, 64, 384, 16), (65, 32, 192, 128), (65, 1024, 768, 64)])
 def test_embedding_fwd_bwd(V, T, C, B):
     """Token + position embeddings and their deterministic backward (the token gradient's 4-wave
@@ -1055,7 +1055,7 @@ def test_embedding_fwd_bwd(V, T, C, B):
     x = torch.empty(B, T, C, device=DEV)
     ops().embed_fwd(idx.to(DEV), wte.to(DEV), wpe.to(DEV), x)
     ref = wte[idx] + wpe[:T]
-    assert relerr(x, ref) < 1e-6
+    assert torch.equal(x.cpu(), ref)   # one fp32 add per element
     dx = torch.randn(B, T, C)
     dwte = torch.empty(V, C, device=DEV)
     dwpe = torch.empty(max(64, T), C, device=DEV)
