@@ -345,11 +345,104 @@ __global__ __launch_bounds__(64) void k_gemm_f32s(int64_t M, int64_t N, int64_t 
             }
 }
 
-// the small-M kernel's conditions (else k_gemm_f32); gemm_variant 98 forces k_gemm_f32 (A/B, tests)
+// The same products with the whole K slab resident (K <= 624, even; 8-B aligned rows): one 4-wave block per
+// 32 x 32 tile loads its 32 A rows and 32 B rows once (every float2 of the slab in flight together,
+// coalesced along K) into LDS, then each wave runs its 16 x 16 fragment's MFMA chain from LDS.  k_gemm_f32s
+// walked K in 128-deep register chunks, one load round trip each, on 32 waves for the C5 FFN2 (19 us).
+// Same lane / k order, padded depth and epilogue as k_gemm_f32: bitwise its result.
+template <int EK, int U>   // U = ceil(kpad / 128): float2 columns per thread and row
+__global__ __launch_bounds__(256, 1) void k_gemm_f32r(int64_t M, int64_t N, int64_t K, const float* __restrict__ A,
+                                                      int64_t lda, const float* __restrict__ B, int64_t ldb,
+                                                      float* __restrict__ C, int64_t ldc, EpiArgs epi) {
+    extern __shared__ __attribute__((aligned(16))) float smr[];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
+    const int64_t kpad = (K + 15) / 16 * 16;   // k_gemm_f32's padded depth
+    const int KS = (int)kpad + 4;               // LDS row stride (floats)
+    float* As = smr;
+    float* Bs = smr + 32 * KS;
+    const int64_t mb = (int64_t)blockIdx.x * 32, nb = (int64_t)blockIdx.y * 32;
+    const int rr = tid >> 6, c = tid & 63;      // rows rr + 4 s, float2 columns c + 64 u
+    float2 av[8][U], bv[8][U];
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = rr + 4 * s;
+            const int64_t k = 2 * (c + 64 * u);
+            const bool kin = k < K;   // K even: k + 1 < K as well
+            av[s][u] = (kin && mb + r < M) ? *(const float2*)(A + (mb + r) * lda + k) : make_float2(0.f, 0.f);
+            bv[s][u] = (kin && nb + r < N) ? *(const float2*)(B + (nb + r) * ldb + k) : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = rr + 4 * s, k = 2 * (c + 64 * u);
+            if (k < kpad) {
+                *(float2*)(As + r * KS + k) = av[s][u];
+                *(float2*)(Bs + r * KS + k) = bv[s][u];
+            }
+        }
+    __syncthreads();
+    const int i = w >> 1, j = w & 1;
+    const float* ar = As + (16 * i + li) * KS + g;
+    const float* br = Bs + (16 * j + li) * KS + g;
+    fv4 acc = fv4{0.f, 0.f, 0.f, 0.f};
+    const int nt = (int)(kpad / 4);
+#pragma unroll 4
+    for (int t = 0; t < nt; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[4 * t], br[4 * t], acc, 0, 0, 0);
+    constexpr bool BIAS = EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_BIAS_RESID;
+    const bool hb = BIAS && epi.bias, hr = EK == CG_EPI_BIAS_RESID && epi.resid;
+    const int64_t m0 = mb + 16 * i, n = nb + 16 * j + li;
+    const float bb = (hb && n < N) ? epi.bias[n] : 0.f;
+    float rv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + 4 * g + r;
+        rv[r] = (hr && m < M && n < N) ? epi.resid[m * epi.ld_resid + n] : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + 4 * g + r;
+        float v = acc[r];
+        if (hb) v += bb;
+        if (EK == CG_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
+        if (hr) v = rv[r] + v;
+        if (m < M && n < N) C[m * ldc + n] = v;
+    }
+}
+
+// the small-M kernel's conditions (else k_gemm_f32); gemm_variant 98 forces k_gemm_f32,
+// 97 k_gemm_f32s (A/B, tests)
 bool launch_f32s(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
                  int64_t ldc, const EpiArgs& e, hipStream_t st) {
     if (g_gemm_variant == 98 || e.beta != 0.f || M > 2048) return false;
     const dim3 grid((unsigned)((M + 31) / 32), (unsigned)((N + 31) / 32));
+    const int64_t kpad = (K + 15) / 16 * 16;
+    if (g_gemm_variant != 97 && K % 2 == 0 && kpad <= 624 && lda % 2 == 0 && ldb % 2 == 0 &&
+        (((uintptr_t)A | (uintptr_t)B) & 7) == 0 &&
+        (e.kind == CG_EPI_STORE || e.kind == CG_EPI_BIAS || e.kind == CG_EPI_BIAS_RELU || e.kind == CG_EPI_BIAS_RESID)) {
+        const int U = (int)((kpad + 127) / 128);
+        const size_t lds = (size_t)2 * 32 * (kpad + 4) * sizeof(float);
+#define KR(EK_, U_) k_gemm_f32r<EK_, U_><<<grid, 256, lds, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e)
+#define KRU(EK_)                  \
+    switch (U) {                  \
+        case 1: KR(EK_, 1); break; \
+        case 2: KR(EK_, 2); break; \
+        case 3: KR(EK_, 3); break; \
+        case 4: KR(EK_, 4); break; \
+        default: KR(EK_, 5); break; \
+    }
+        switch (e.kind) {
+            case CG_EPI_STORE: KRU(CG_EPI_STORE); break;
+            case CG_EPI_BIAS: KRU(CG_EPI_BIAS); break;
+            case CG_EPI_BIAS_RELU: KRU(CG_EPI_BIAS_RELU); break;
+            default: KRU(CG_EPI_BIAS_RESID); break;
+        }
+#undef KRU
+#undef KR
+        return true;
+    }
 #define KS(EK_) k_gemm_f32s<EK_><<<grid, 64, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e)
     switch (e.kind) {
         case CG_EPI_STORE: KS(CG_EPI_STORE); return true;
@@ -647,11 +740,12 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     if (!strcmp(key, "gemm_variant")) {
         // default build: automatic (0), the register-staged fallback (2), the persistent 128x128 (9)
         // and 256x256 (24) tiles, k_gemm_f32 for every fp32 product (98: not the small-M
-        // kernel), the generic kernels (99); the measured-slower A/B tiles (among
+        // kernels; 97: k_gemm_f32s, not the K-resident one), the generic kernels (99); the
+        // measured-slower A/B tiles (among
         // them 26, the 256x256 tile on the staggered 8-phase schedule) only in
         // libcharpt_hip_ab.so (`make ab`, CG_AB_VARIANTS)
 #ifndef CG_AB_VARIANTS
-        CG_REQUIRE(value == 0 || value == 2 || value == 9 || value == 24 || value == 98 || value == 99,
+        CG_REQUIRE(value == 0 || value == 2 || value == 9 || value == 24 || value == 97 || value == 98 || value == 99,
                    "cg_set_tuning: gemm_variant %d is an A/B variant, not in this build (make ab)", value);
 #endif
         g_gemm_variant = value;

@@ -1160,10 +1160,11 @@ def test_gemm_f32_mfma_matches_generic(at, bt, M, N, K, split):
 
 @pytest.mark.parametrize("kind", [0, 1, 2, 3])
 @pytest.mark.parametrize("M,N,K", [(256, 378, 126), (256, 126, 504), (256, 65, 126), (1, 504, 126), (33, 70, 5),
-                                   (2048, 126, 200), (100, 33, 257)])
+                                   (2048, 126, 200), (100, 33, 257), (70, 90, 624), (64, 64, 2), (31, 17, 640)])
 def test_gemm_f32_small_m_matches_128x64_bitwise(kind, M, N, K):
-    """The small-M fp32 forward kernel (k_gemm_f32s, M <= 2048) against k_gemm_f32 (gemm_variant 98):
-    same MFMA lane / k order and padded depth, same epilogue arithmetic -> bitwise equal."""
+    """The small-M fp32 forward kernels (M <= 2048: k_gemm_f32r with the K slab in LDS for even K <= 624,
+    else k_gemm_f32s; gemm_variant 97 forces k_gemm_f32s) against k_gemm_f32 (gemm_variant 98): same
+    MFMA lane / k order and padded depth, same epilogue arithmetic -> bitwise equal."""
     from replicatinggpt_amd import _lib as L
     lib = L.load()
     torch.manual_seed(31)
@@ -1172,7 +1173,7 @@ def test_gemm_f32_small_m_matches_128x64_bitwise(kind, M, N, K):
     bias = torch.randn(N, device=DEV)
     resid = torch.randn(M, N, device=DEV)
     outs = []
-    for v in (98, 0):
+    for v in (98, 97, 0):
         L.check(lib.cg_set_tuning(b"gemm_variant", v))
         try:
             out = torch.full((M, N), float("nan"), device=DEV)
@@ -1189,8 +1190,9 @@ def test_gemm_f32_small_m_matches_128x64_bitwise(kind, M, N, K):
         ref = torch.relu(ref)
     if kind == 3:
         ref = ref + resid.double().cpu()
-    assert relerr(outs[1], ref) < 1e-5
+    assert relerr(outs[2], ref) < 1e-5
     assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+    assert torch.equal(outs[0].view(torch.int32), outs[2].view(torch.int32))
 
 
 def test_adamw_matches_torch():

@@ -4,6 +4,7 @@ hipGraph replay of 20 launches (HIP events), rounds interleaved; then, with `gen
 (256 x 500 greedy, fp32, C1 golden weights) timed under the variant named second.
 usage: python tools/f32_fwd_ab.py [rounds]            (kernel A/B; needs the trial kernel, not in the tree)
        python tools/f32_fwd_ab.py now [rounds]        (the current library's fp32 products at those shapes)
+       python tools/f32_fwd_ab.py small [variant]     (the 256-row products of generate()'s steps)
        python tools/f32_fwd_ab.py gen <98|0> [knob]   (generate with cg_set_tuning(knob, value), knob
                                                       gemm_variant by default; fresh process)"""
 import os
@@ -18,6 +19,8 @@ from replicatinggpt_amd import _lib as L, ops  # noqa: E402
 
 SHAPES = [("qkv", 65536, 378, 126, 0), ("proj", 65536, 126, 126, 3), ("ffn1", 65536, 504, 126, 2),
           ("ffn2", 65536, 126, 504, 3)]
+SMALL = [("qkv", 256, 378, 126, 0), ("proj", 256, 126, 126, 3), ("ffn1", 256, 504, 126, 2),
+         ("ffn2", 256, 126, 504, 3), ("head", 256, 65, 126, 1)]
 
 
 def launch_fn(M, N, K, kind, dev):
@@ -89,7 +92,8 @@ def gen(variant, knob="gemm_variant"):
           f"checksum {int(out.sum())}", flush=True)
 
 
-def now(rounds):
+def now(rounds, shapes=None):
+    SHAPES = shapes or globals()["SHAPES"]
     L.load()
     dev = torch.device("cuda")
     t = {n: [] for n, *_ in SHAPES}
@@ -105,6 +109,9 @@ def now(rounds):
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "now":
         now(int(sys.argv[2]) if len(sys.argv) > 2 else 5)
+    elif len(sys.argv) > 1 and sys.argv[1] == "small":   # generate()'s 256-row products, knob gemm_variant
+        L.check(L.load().cg_set_tuning(b"gemm_variant", int(sys.argv[2]) if len(sys.argv) > 2 else 0))
+        now(3, SMALL)
     elif len(sys.argv) > 1 and sys.argv[1] == "gen":
         gen(int(sys.argv[2]), *(sys.argv[3:4]))
     else:
