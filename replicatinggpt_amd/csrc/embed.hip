@@ -60,8 +60,10 @@ __global__ __launch_bounds__(256) void k_embed_fwd_pairs(const int64_t* __restri
                                                          int64_t n2, int64_t T, int64_t C, int64_t V) {
     const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (j >= n2) return;
-    const int64_t c2 = C >> 1, row = j / c2, c = 2 * (j - row * c2);
-    const int64_t t = row % T;
+    // 32-bit index arithmetic (the host keeps n2 < 2^31): a 64-bit division is a long software sequence
+    const uint32_t c2 = (uint32_t)(C >> 1), rw = (uint32_t)j / c2;
+    const int64_t row = rw, c = 2 * (int64_t)((uint32_t)j - rw * c2);
+    const int64_t t = (int64_t)(rw % (uint32_t)T);
     int64_t tok = idx[row];
     tok = tok < 0 ? 0 : (tok >= V ? V - 1 : tok);  // out-of-range ids are a caller error (torch raises)
     const float2 u = *(const float2*)(wte + tok * C + c), w = *(const float2*)(wpe + t * C + c);
@@ -87,7 +89,7 @@ extern "C" int cg_embed_fwd(const int64_t* idx, const float* wte, const float* w
         return CG_OK;
     }
     const bool al8 = ((((uintptr_t)wte) | ((uintptr_t)wpe) | ((uintptr_t)x)) & 7) == 0;
-    if (C % 2 == 0 && al8) {
+    if (C % 2 == 0 && al8 && rows * (C / 2) < ((int64_t)1 << 31)) {
         const int64_t n2 = rows * (C / 2);
         k_embed_fwd_pairs<<<(unsigned)((n2 + 255) / 256), 256, 0, st>>>(idx, wte, wpe, x, n2, T, C, V);
         CG_LAUNCH_CHECK("cg_embed_fwd");
