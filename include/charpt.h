@@ -101,7 +101,8 @@ const char* cg_last_error_string(void);
 int cg_version(void);
 /* process-wide A/B and test knobs (kernel / schedule selection, never a call's numerics): e.g.
    "gemm_variant" 0 = automatic, 2 = register-staged, 9 = persistent 128x128, 24 = 8-wave 256x256,
-   99 = generic; "red_side", "adam_per_launch", "gemm_n96", "ln_nt", ... (gemm.hip cg_set_tuning).
+   97 / 98 = fp32 small-M chunked kernel / 128x64 kernel only, 99 = generic; "decode_attn_rows",
+   "red_side", "adam_per_launch", "gemm_n96", "ln_nt", ... (gemm.hip cg_set_tuning).
    Set them before the calls they affect, from one thread.                                       */
 int cg_set_tuning(const char* key, int value);
 int cg_device_info(int* n_cu, int* arch_major, int* arch_minor);
