@@ -226,7 +226,7 @@ def gemm_census(cfg, Bsz, T, dev, cold=False):
         ms = time_gemm(name, m, n, k, at, bt, kind, dev, cold=cold)
         split = Fn._wgrad_split(m, n, k, True) if kind == "wgrad" else 1
         out.append({"name": name, "M": m, "N": n, "K": k, "epilogue": kind, "ms": ms, "launches": cnt,
-                    "flops": 2.0 * m * n * k, "split": split,
+                    "flops": 2.0 * m * n * k, "split": split, "layout": (bool(at), bool(bt)),
                     "kernel": gemm_kernel_name(m, n, at, bt, split, dev, kind)})
         torch.cuda.empty_cache()
     return out
@@ -390,7 +390,7 @@ def pmc_traffic(config, dom):
     the latest round's file first); None when no file covers this exact shape, split and epilogue
     (files before round 4 timed every forward / dgrad with a plain store: they match only the
     plain-store and weight-gradient ops)."""
-    for rnd in ("r4", "r3", "r2", "r1"):
+    for rnd in ("r6", "r5", "r4", "r3", "r2", "r1"):
         path = os.path.join(ROOT, "profiles", f"{rnd}_pmc_gemm_traffic_{config}.json")
         try:
             op = json.load(open(path))["ops"][dom["name"]]
@@ -404,12 +404,75 @@ def pmc_traffic(config, dom):
     return None
 
 
+GEMM_FNS = {"relu_bwd_colpart": "gemm_relu_bwd_colpart", "bias_relu_bits": "gemm_bias_relu_bits",
+            "store_rowdot": "gemm_store_rowdot"}
+
+
+def in_step_launch_ms(model, opt, sampler, dom, replays=7):
+    """The dominant op's average launch duration INSIDE the training step, measured live: one more
+    hipGraph of the whole step (forward, backward, AdamW -- the timed region's graph, same model) is
+    captured with an external timing event recorded before and after every launch of that op (the
+    ops-module entry it goes through, matched on M, N, K and layout), replayed ``replays`` times after
+    the timed region, and the event pairs of each replay averaged (median over replays).  In the step
+    a launch also runs whatever deferred split-K reduce / AdamW work it hosts on free slots, and finds
+    its operands as the step leaves them (colder than the census's back-to-back replays).  HIP events
+    on the step's stream: the event record nodes sit between the op's kernel and its neighbours, so
+    the figure is that kernel's duration plus at most the record nodes' own latency.
+    Returns (ms, launches per step) or None when the events cannot be captured."""
+    from replicatinggpt_amd import ops
+    from replicatinggpt_amd.engine import TrainStep
+    fname = GEMM_FNS.get(dom["epilogue"], "gemm")
+    orig = getattr(ops, fname)
+    pairs = []
+
+    def probe(*a, **k):
+        if fname == "gemm":
+            key, lay = (a[6], a[7], a[8]), (bool(a[4]), bool(a[5]))
+        else:
+            key, lay = (a[3], a[4], a[5]), (False, dom["name"].endswith("dgrad"))
+        want = (dom["M"], dom["N"], dom["K"]) == key and (fname != "gemm" or lay == dom["layout"])
+        if not (want and torch.cuda.is_current_stream_capturing()):
+            return orig(*a, **k)
+        s, e = (torch.cuda.Event(enable_timing=True, external=True) for _ in range(2))
+        s.record()
+        r = orig(*a, **k)
+        e.record()
+        pairs.append((s, e))
+        return r
+    setattr(ops, fname, probe)
+    try:
+        st = TrainStep(model, opt, sampler, None, use_graph=True)
+        st.capture(warmup=1)
+    except Exception as ex:   # noqa: BLE001 -- a runtime without timed external events: no live figure
+        _log(f"in-step probe unavailable: {type(ex).__name__}: {ex}")
+        return None
+    finally:
+        setattr(ops, fname, orig)
+    if not pairs:
+        return None
+    per = []
+    try:
+        for _ in range(replays):
+            st.step()
+            torch.cuda.synchronize()
+            per.append(sum(s.elapsed_time(e) for s, e in pairs) / len(pairs))
+    except Exception as ex:   # noqa: BLE001
+        _log(f"in-step probe unavailable: {type(ex).__name__}: {ex}")
+        return None
+    finally:
+        del st
+        torch.cuda.empty_cache()
+    per.sort()
+    return per[len(per) // 2], len(pairs)
+
+
 def step_kernel(config, dom):
     """The dominant op's in-step launch time from the committed rocprofv3 kernel trace of a bench run
     (tools/gpu_prof_bench.sh -> tools/step_kernels.py -> profiles/r<N>_step_kernels_<config>.json, the
     latest round first): in the step a launch may host deferred reduces / AdamW jobs on free slots
-    and finds its operands colder than the census's back-to-back replays.  None when no file has it."""
-    for rnd in ("r5",):
+    and finds its operands colder than the census's back-to-back replays.  None when no file has it.
+    Not a measurement of this run: the bench line carries it under roofline.committed_trace."""
+    for rnd in ("r6", "r5"):
         path = os.path.join(ROOT, "profiles", f"{rnd}_step_kernels_{config}.json")
         try:
             op = json.load(open(path))["ops"][dom["name"]]
@@ -571,9 +634,10 @@ def main():
     ap.add_argument("--no-generate", action="store_true", help="skip the C5 batched-decode measurement")
     ap.add_argument("--overlap", type=int, default=None, choices=[0, 1],
                     help="force the segmented (DP-overlap) backward on/off (default: on when N > 1)")
-    ap.add_argument("--seg-layers", type=int, default=1,
+    ap.add_argument("--seg-layers", type=int, default=2,
                     help="DP: blocks per backward graph segment (gradient all-reduce overlaps the next segment; "
-                         "1 = the smallest exposed last segment, block 0 + embeddings: DESIGN.md section 6)")
+                         "the last segment, blocks 0..seg-1 + embeddings, is exposed: DESIGN.md section 6. "
+                         "2: +0.7 %% at W = 1 against +1.8 %% for 1, profiles/r5_dp_path_w1_step_ab.txt)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: exercise the N-rank launch, sampler slicing and reducer on gloo")
     args = ap.parse_args()
@@ -588,10 +652,17 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
     if args.dry_run:
         return dry_run(args, world, rank, local)
+    # test hooks (tests/test_gpu_bench_dp.py): CHARPT_DP_BACKEND=gloo and CHARPT_DP_ONE_DEVICE=1 run the
+    # N-rank path on one GPU -- every rank on cuda:0, gradients averaged over gloo (SUM + divide)
+    backend = os.environ.get("CHARPT_DP_BACKEND", "nccl")
+    local_dev = 0 if os.environ.get("CHARPT_DP_ONE_DEVICE") == "1" else local
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(local_dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_dev))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", local_dev)
 
     from replicatinggpt_amd import AdamW, BigramLanguageModel, PRESETS
     from replicatinggpt_amd.data import BatchSampler, TokenStream
@@ -638,24 +709,43 @@ def main():
 
     result = None
     _log(f"timed {args.steps} steps: {elapsed / args.steps * 1e3:.3f} ms/step")
+    step_path = ("segmented backward graphs + bucketed all-reduce (DP)" if step.overlap
+                 else "single graph (fwd + bwd + AdamW)")
+    graphed, nseg = step.g_fb is not None or bool(step.g_seg), len(step.ranges)
+    overlap = step.overlap
+    red_kind = "RCCL AVG" if backend == "nccl" else f"{backend} SUM + divide"
+    del step   # the probe below captures its own graph of the step
+    torch.cuda.empty_cache()
     if rank == 0:
         roofline, census = None, None
         if not args.no_census:
             census = gemm_census(cfg, Bsz, T, dev)
             dom = max(census, key=lambda c: c["ms"] * c["launches"])
-            achieved = dom["flops"] / (dom["ms"] * 1e-3) / 1e12
-            roofline = {"bound": "mfma", "kernel": f"cg_gemm bf16 {dom['name']} M={dom['M']} N={dom['N']} K={dom['K']}"
-                                                  f" ({dom['kernel']}, split {dom['split']}, epilogue {dom['epilogue']})",
+            c_ach = dom["flops"] / (dom["ms"] * 1e-3) / 1e12
+            kname = (f"cg_gemm bf16 {dom['name']} M={dom['M']} N={dom['N']} K={dom['K']}"
+                     f" ({dom['kernel']}, split {dom['split']}, epilogue {dom['epilogue']})")
+            # the line's figure: the op's launches inside the training step, timed live (HIP events
+            # in a graph of the step); the census (same op, 30 back-to-back launches) beside it
+            _log("in-step probe of the dominant op")
+            live = in_step_launch_ms(model, opt, sampler, dom)
+            ms_op = live[0] if live else dom["ms"]
+            achieved = dom["flops"] / (ms_op * 1e-3) / 1e12
+            roofline = {"bound": "mfma", "kernel": kname,
                         "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                        "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
-                        "traffic": None, "avg_launch_ms": round(dom["ms"], 5),
-                        "gemm_family": gemm_family(census)}
+                        "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "flops_per_launch": dom["flops"],
+                        "avg_launch_ms": round(ms_op, 5),
+                        "timing": ("in-step: HIP events around each of the op's launches in a hipGraph of the "
+                                   f"training step, {live[1]} launches per step, median of 7 replays after the "
+                                   "timed region" if live else "census (in-step probe unavailable)"),
+                        "census_avg_launch_ms": round(dom["ms"], 5), "census_achieved": round(c_ach, 1),
+                        "census_frac": round(c_ach / PEAK_BF16_TFLOPS, 4),
+                        "traffic": None, "gemm_family": gemm_family(census)}
             pt = pmc_traffic(args.config, dom)
             if pt is not None:
                 roofline["traffic"], roofline["traffic_source"] = pt["bytes"], pt["source"]
             sk = step_kernel(args.config, dom)
-            if sk is not None:   # beside the census figure: the same op inside the training step
-                roofline.update(sk)
+            if sk is not None:   # a committed rocprofv3 trace of an earlier run: not this run's measurement
+                roofline["committed_trace"] = sk
         result = {
             "metric": "train tokens/sec at 1/2/4/8 MI355X + MFMA util, char-GPT block 256",
             "value": round(value, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
@@ -665,12 +755,11 @@ def main():
                                    f"block {T}, batch {Bsz}/GPU, dropout {cfg.dropout}, AdamW, full train step",
                        "global_batch": Bsz * world, "seq_len": T, "parallelism": f"dp{world}",
                        "world_size": dist.get_world_size() if dist.is_initialized() else 1,
-                       "backend": f"{dist.get_backend()} (RCCL)" if dist.is_initialized() else None,
-                       "step_path": ("segmented backward graphs + bucketed all-reduce (DP)" if step.overlap
-                                     else "single graph (fwd + bwd + AdamW)"),
-                       "graph": step.g_fb is not None or bool(step.g_seg),
-                       "grad_allreduce": (f"RCCL AVG overlapped: {len(step.ranges)} backward segments"
-                                          if step.overlap else ("RCCL AVG after backward" if world > 1 else None))},
+                       "backend": ((f"{dist.get_backend()} (RCCL)" if dist.get_backend() == "nccl" else dist.get_backend())
+                                   if dist.is_initialized() else None),
+                       "step_path": step_path, "graph": graphed,
+                       "grad_allreduce": (f"{red_kind} overlapped: {nseg} backward segments"
+                                          if overlap else (f"{red_kind} after backward" if world > 1 else None))},
             "mfu_step": round(mfu, 4), "flops_per_token": F, "final_loss": round(final_loss, 4),
             "roofline": roofline,
         }

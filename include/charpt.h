@@ -19,9 +19,12 @@
  *   - deferred work (per stream): a call asks for it explicitly -- cg_epilogue_t.flags
  *     CG_GEMM_DEFER_REDUCE (a split-K weight-gradient reduce left pending), cg_adamw_defer, and the
  *     CG_DEFER flag of cg_reduce_rows_ex / cg_layernorm_bwd_reduce_ex / cg_head_bwd_ex (column-sum
- *     reduces queued for one multi-job launch).  The queue is that of the call's (device, stream):
- *     only a later persistent GEMM launch on the SAME stream takes its jobs (in its tail / free
- *     blocks), and cg_flush_deferred(stream) launches the rest on that stream.  A mutex guards the
+ *     reduces queued for one multi-job launch).  The queue is that of the call's stream, keyed by
+ *     (the stream's own device, stream) whatever device is current in the calling thread: only a
+ *     later persistent GEMM launch on the SAME stream takes its jobs (in its tail / free blocks),
+ *     and cg_flush_deferred(stream) launches the rest on that stream, with the stream's device made
+ *     current for the launches (the caller's restored).  A flushed or discarded queue is dropped,
+ *     so a new stream that reuses a destroyed stream's handle starts with an empty one.  A mutex guards the
  *     queue registry, so host threads that each drive their own stream are safe; two threads
  *     sharing one stream must order their calls themselves, as with any stream.  Until the flush,
  *     the caller keeps every queued job's workspace alive and reads none of its outputs.
@@ -330,7 +333,7 @@ int cg_adamw(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int
    the next persistent GEMM launch on `stream` that has >= 64 of them (a part-filling launch; at most 4 jobs per launch,
    oldest first), else by cg_flush_deferred -- the jobs left, when they are slices of one set of
    buffers, as one segmented launch -- same bits either way.  The gradient must be final in stream order (a
-   pending split-K reduce writing into g is launched first) and nothing launched before the flush may
+   pending split-K reduce or queued column-sum reduce writing into g is launched first) and nothing launched before the flush may
    read p / p_bf16 / m / v.  n % 4 == 0, p, g, m, v 16-B and p_bf16 8-B aligned. */
 int cg_adamw_defer(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, double lr,
                    double beta1, double beta2, double eps, double weight_decay, const int64_t* step_ptr,

@@ -39,8 +39,12 @@ struct DeferQueue {
 
 // the registry lock; every function below expects the caller to hold it
 std::mutex& defer_mutex();
-// the queue of stream st on the current device; nullptr when it has none and !create
+// the queue of stream st (keyed by the stream's own device); nullptr when it has none and !create
 DeferQueue* defer_queue(hipStream_t st, bool create);
+// remove an emptied queue from the registry (q is invalid afterwards)
+void defer_queue_drop(DeferQueue* q);
+// queued column-sum reduces whose outputs overlap [p, p + n) go out now (util.hip)
+void flush_parts_touching_locked(DeferQueue* q, const float* p, int64_t n);
 // launch (on the queue's stream) and clear one kind of job
 void flush_red_locked(DeferQueue& q);
 void flush_adam_locked(DeferQueue& q);

@@ -632,15 +632,32 @@ static int current_device() {
     return hipGetDevice(&d) == hipSuccess ? d : -1;
 }
 
+// the device a stream belongs to: hipStreamGetDevice for a created stream, the current device for
+// the null stream.  The queue key must not depend on the calling thread's current device: the
+// autograd device thread queues work with the tensor's device current, while the flush may come
+// from a thread whose current device is another one.
+static int stream_device(hipStream_t st) {
+    if (st) {
+        hipDevice_t d = -1;
+        if (hipStreamGetDevice(st, &d) == hipSuccess && d >= 0) return (int)d;
+    }
+    return current_device();
+}
+
 // the deferral registry (defer.h): one queue per (device, stream)
 std::mutex& defer_mutex() {
     static std::mutex m;
     return m;
 }
 
-DeferQueue* defer_queue(hipStream_t st, bool create) {
+static std::map<std::pair<int, hipStream_t>, DeferQueue>& defer_registry() {
     static std::map<std::pair<int, hipStream_t>, DeferQueue> reg;
-    const auto key = std::make_pair(current_device(), st);
+    return reg;
+}
+
+DeferQueue* defer_queue(hipStream_t st, bool create) {
+    auto& reg = defer_registry();
+    const auto key = std::make_pair(stream_device(st), st);
     auto it = reg.find(key);
     if (it != reg.end()) return &it->second;
     if (!create) return nullptr;
@@ -649,6 +666,25 @@ DeferQueue* defer_queue(hipStream_t st, bool create) {
     q.device = key.first;
     return &q;
 }
+
+// an emptied queue leaves the registry: a stream destroyed after its flush / discard leaves no queue
+// behind for a new stream that reuses its handle
+void defer_queue_drop(DeferQueue* q) {
+    if (q && !q->nred && !q->nadam && !q->parts.n) defer_registry().erase(std::make_pair(q->device, q->stream));
+}
+
+// launches of a queue's flush run with the queue's device current (a kernel goes to the stream's
+// device), the caller's device restored after
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(int dev) {
+        const int cur = current_device();
+        if (dev >= 0 && cur != dev && hipSetDevice(dev) == hipSuccess) prev = cur;
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
 
 // pending jobs for a launch on stream st of the current device: the stream's split-K reduces, and
 // with side_ok (the launch has >= SIDE_MIN free blocks) up to MAX_ADAM of its AdamW jobs, oldest first
@@ -1070,12 +1106,15 @@ extern "C" int cg_adamw_defer(float* p, const float* g, float* m, float* v, uint
     {
         std::lock_guard<std::mutex> lk(defer_mutex());
         DeferQueue& q = *defer_queue(st, true);
-        // the region's gradient must be final first: a pending split-K reduce writing into it goes out now
+        DeviceScope ds(q.device);
+        // the region's gradient must be final first: a pending split-K reduce or column-sum reduce
+        // writing into it goes out now
         for (int i = 0; i < q.nred; ++i)
             if (q.red[i].out < g + n && g < q.red[i].out + 4 * q.red[i].n4) {
                 flush_red_locked(q);
                 break;
             }
+        flush_parts_touching_locked(&q, g, n);
         if (q.nadam == MAX_ADAM_PENDING) flush_adam_locked(q);
         q.adam[q.nadam++] = AdamJob{p, g, m, v, (bf16_t*)p_bf16, n / 4, lr, beta1, beta2, eps, weight_decay, step_ptr};
     }
@@ -1089,10 +1128,12 @@ extern "C" int cg_flush_deferred(void* stream) {
         std::lock_guard<std::mutex> lk(defer_mutex());
         DeferQueue* q = defer_queue((hipStream_t)stream, false);
         if (q) {
+            DeviceScope ds(q->device);
             flush_red_locked(*q);
             flush_adam_locked(*q);
             flush_parts_locked(*q);
             q->adam_taken = 0;
+            defer_queue_drop(q);
         }
     }
     CG_LAUNCH_CHECK("cg_flush_deferred");
@@ -1108,6 +1149,7 @@ extern "C" int cg_discard_deferred(void* stream, int* adam_jobs_taken) {
         if (q) {
             taken = q->adam_taken;
             q->nred = q->nadam = q->parts.n = q->adam_taken = 0;
+            defer_queue_drop(q);
         }
     }
     if (adam_jobs_taken) *adam_jobs_taken = taken;

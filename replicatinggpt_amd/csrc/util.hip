@@ -218,7 +218,7 @@ static bool job_outputs_overlap(const PartJob& x, const float* p, int64_t n) {
 }
 // an immediate reduce / write into [p, p + n) on stream st: that stream's queued jobs that target it
 // go first (caller holds the registry lock)
-static void flush_parts_touching_locked(DeferQueue* q, const float* p, int64_t n) {
+void flush_parts_touching_locked(DeferQueue* q, const float* p, int64_t n) {
     if (!q) return;
     for (int i = 0; i < q->parts.n; ++i)
         if (job_outputs_overlap(q->parts.j[i], p, n)) {

@@ -101,7 +101,7 @@ class DeferredReduces:
         self.partials_on = os.environ.get("CHARPT_DEFER_PARTIALS", "1") != "0"
         self.active = False
         self.keep = []
-        self.streams = {}        # cuda_stream handle -> stream, every stream work was queued on
+        self.streams = {}        # (device index, cuda_stream handle) -> stream, every stream work was queued on
         self.aborted_adam = 0
 
     def __enter__(self):
@@ -113,7 +113,7 @@ class DeferredReduces:
     def note_stream(self):
         """The current stream will hold deferred work (flushed / discarded at exit)."""
         st = torch.cuda.current_stream()
-        self.streams[st.cuda_stream] = st
+        self.streams[(st.device.index, st.cuda_stream)] = st
 
     @contextlib.contextmanager
     def partials(self, *keep):
@@ -130,16 +130,18 @@ class DeferredReduces:
     def flush(self):
         """Launch everything pending on the streams this scope queued work on (each on its own stream)."""
         lib = L.load()
-        for h in list(self.streams):
-            L.check(lib.cg_flush_deferred(ctypes.c_void_p(h)), "flush_deferred")
+        for (dev, h) in list(self.streams):
+            with torch.cuda.device(dev):   # (the library keys queues by the stream's own device too)
+                L.check(lib.cg_flush_deferred(ctypes.c_void_p(h)), "flush_deferred")
 
     def discard(self):
         """Drop what is pending (a failed backward); returns the AdamW jobs launches had already taken."""
         lib = L.load()
         taken = 0
-        for h in list(self.streams):
+        for (dev, h) in list(self.streams):
             n = ctypes.c_int(0)
-            L.check(lib.cg_discard_deferred(ctypes.c_void_p(h), ctypes.byref(n)), "discard_deferred")
+            with torch.cuda.device(dev):
+                L.check(lib.cg_discard_deferred(ctypes.c_void_p(h), ctypes.byref(n)), "discard_deferred")
             taken += n.value
         return taken
 
@@ -151,8 +153,9 @@ class DeferredReduces:
                 else:
                     self.aborted_adam = self.discard()
                 if SIDE.enabled:   # the flush runs on the stream its reduces were enqueued on: join it
-                    dev = torch.device("cuda", torch.cuda.current_device())
-                    torch.cuda.current_stream(dev).wait_stream(SIDE.stream(dev))
+                    for d in {dv for dv, _ in self.streams} or {torch.cuda.current_device()}:
+                        dev = torch.device("cuda", d)
+                        torch.cuda.current_stream(dev).wait_stream(SIDE.stream(dev))
             finally:
                 self.active = False
                 self.keep.clear()

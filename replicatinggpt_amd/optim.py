@@ -188,15 +188,19 @@ class AdamW(torch.optim.Optimizer):
         """A step with early updates in which some parameters had no gradient (torch.optim.AdamW
         skips those: no decay, no moment update, no step count).  The early updates ran with the
         shared count, already advanced; switch to per-parameter counts, take the advance back for
-        the skipped parameters and update the remaining ones one by one with their own counts."""
+        the skipped parameters and update the remaining ones one by one with their own counts.  A
+        parameter whose .grad was dropped AFTER its region's early update (weights and moments already
+        advanced from the flat gradient) keeps the advance: taking the count back would leave it
+        inconsistent with its moments; it stepped as if its gradient had stayed."""
         st = self._store
         self._split_steps()   # every count already includes this step's advance
         skip = {id(p) for p in missing}
         for i, p, off in self._param_slices():
-            if id(p) in skip:
+            updated = any(a <= off < a + n for a, n in early)
+            if id(p) in skip and not updated:
                 ops.counter_add(self._psteps[i:i + 1], -1)
                 continue
-            if any(a <= off < a + n for a, n in early):
+            if updated:
                 continue   # updated beside the backward
             n = p.numel()
             ops.adamw(st.master[off:off + n], st.grad[off:off + n], self._m[off:off + n], self._v[off:off + n],

@@ -710,6 +710,51 @@ def test_gemm_p8_residual_epilogue_matches_128x128_bitwise(kind, inplace):
         want = resid.double() + torch.from_numpy(keep).to(DEV).double() * ref * float(np.float32(1 / 0.8))
         assert relerr(outs[0], want) < 1e-5
 
+# every 256x256 (8-wave) variant in the loaded library: the product's 24, and with the A/B build 20-26
+_P8_FULL = ([20, 21, 22, 23, 24, 25, 26] if "_ab" in os.environ.get("CHARPT_LIB", "") else [24])
+
+
+@pytest.mark.parametrize("variant", _P8_FULL)
+@pytest.mark.parametrize("N,K,bt,kind", [(2304, 768, 0, "store"), (768, 3072, 0, "bias_resid"),
+                                         (768, 2304, 1, "store")])
+def test_gemm_256_variants_full_size(variant, N, K, bt, kind):
+    """each 256x256 variant at the C4 row count (M = 65,536: the QKV forward,
+    FFN2 forward with its fp32 residual epilogue and the QKV dgrad, GPT1.py:111-112,121,145) -- a
+    size-dependent indexing fault (round 5's half-row-shift trial passed at M <= 8192 and faulted at
+    its first M = 65,536 launch) fails here, not on the first real launch.  Bitwise against the
+    128x128 persistent kernel (same K order per element), and against torch's fp32 GEMM on the GPU."""
+    from replicatinggpt_amd import _lib as L
+    Fn, lib = F(), L.load()
+    if lib.cg_set_tuning(b"gemm_variant", variant) != 0:
+        pytest.skip(f"gemm_variant {variant} is A/B-only (not in this library build)")
+    L.check(lib.cg_set_tuning(b"gemm_variant", 0))
+    M = 65536
+    torch.manual_seed(17)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(K, N, device=DEV) if bt else torch.randn(N, K, device=DEV)).mul_(K ** -0.5).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV) if kind == "bias_resid" else None
+    resid = torch.randn(M, N, device=DEV) if kind == "bias_resid" else None
+    outs = []
+    try:
+        for v in (variant, 9):
+            L.check(lib.cg_set_tuning(b"gemm_variant", v))
+            f32 = kind == "bias_resid"
+            o = torch.full((M, N), float("nan"), device=DEV, dtype=torch.float32 if f32 else torch.bfloat16)
+            epi = Fn.EPI["bias_resid"] if f32 else 0
+            ops().gemm(x, w, o, True, False, bool(bt), M, N, K, K, N if bt else K, N, epi, bias, resid, N if f32 else 0,
+                       None, 0, 0.0, 0, None, 0, 0.0, 1, None)
+            torch.cuda.synchronize()
+            outs.append(o)
+    finally:
+        L.check(lib.cg_set_tuning(b"gemm_variant", 0))
+    assert not torch.isnan(outs[0].float()).any()
+    assert torch.equal(outs[0], outs[1])
+    ref = x.float() @ (w.float() if bt else w.float().t())
+    if kind == "bias_resid":
+        ref = ref + bias + resid
+    assert relerr(outs[0].float(), ref) < (1e-5 if kind == "bias_resid" else 8e-3)
+
+
 @pytest.mark.parametrize("M,C,T", [(16384, 384, 256), (2048, 768, 128), (1024, 384, 64), (512, 128, 256)])
 def test_gemm_store_rowdot(M, C, T):
     """CG_EPI_STORE_ROWDOT (the projection dgrad dO = dy W, GPT1.py:136, with the attention backward's

@@ -351,3 +351,31 @@ def test_c2_width_bf16_loss_curve_tracks_fp32(tmp_path, capsys):
     for (it, tr, va), (_, tr16, va16) in zip(a, b):
         assert abs(tr - tr16) <= 0.03 and abs(va - va16) <= 0.03, (it, tr, va, tr16, va16)
     assert a[0][2] - a[-1][2] > 0.5
+
+
+def test_deferred_work_on_a_non_current_device():
+    """the deferred split-K reduces / column sums / AdamW jobs are queued by the
+    autograd device thread (the tensor's device current) and flushed from the main thread; the
+    library keys each queue by the STREAM's own device and DEFER flushes under that device, so a model
+    on cuda:1 trained while cuda:0 is current gives the bits it gives on cuda:0.  Needs two GPUs
+    (the driver's 1-GPU box skips it)."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    from replicatinggpt_amd import AdamW, BigramLanguageModel
+    from replicatinggpt_amd.data import BatchSampler, TokenStream
+    from replicatinggpt_amd.engine import TrainStep
+    cfg = _cfg(block_size=256, n_embd=384, n_head=6, n_layers=2, batch_size=16)
+    res = []
+    for dev in ("cuda:0", "cuda:1"):
+        torch.cuda.set_device(0)
+        torch.manual_seed(1337)
+        m = BigramLanguageModel(cfg).to(dev)
+        opt = AdamW(m.parameters(), lr=1e-3)
+        s = BatchSampler(TokenStream.synthetic(device=dev), cfg.block_size, cfg.batch_size,
+                         generator=torch.Generator().manual_seed(3))
+        st = TrainStep(m, opt, s, None, use_graph=False)
+        losses = [float(st.step().detach()) for _ in range(3)]
+        torch.cuda.synchronize(dev)
+        res.append((losses, m.flat.master.detach().cpu()))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1])
