@@ -408,19 +408,48 @@ GEMM_FNS = {"relu_bwd_colpart": "gemm_relu_bwd_colpart", "bias_relu_bits": "gemm
             "store_rowdot": "gemm_store_rowdot"}
 
 
+class _TimingEvent:
+    """A HIP event recorded through the library (cg_timing_event_record): inside a graph capture an
+    external event-record node, which torch's own Event may not create on ROCm."""
+
+    def __init__(self, lib):
+        import ctypes
+        from replicatinggpt_amd import _lib as L
+        self.lib, self.L, self.h = lib, L, ctypes.c_void_p()
+        L.check(lib.cg_timing_event_create(ctypes.byref(self.h)), "timing_event_create")
+
+    def record(self):
+        self.L.check(self.lib.cg_timing_event_record(self.h, self.L.stream_ptr()), "timing_event_record")
+
+    def elapsed_ms(self, end):
+        import ctypes
+        ms = ctypes.c_float()
+        self.L.check(self.lib.cg_timing_event_elapsed(self.h, end.h, ctypes.byref(ms)), "timing_event_elapsed")
+        return ms.value
+
+    def __del__(self):
+        try:
+            self.lib.cg_timing_event_destroy(self.h)
+        except Exception:   # noqa: BLE001 -- interpreter shutdown
+            pass
+
+
 def in_step_launch_ms(model, opt, sampler, dom, replays=7):
     """The dominant op's average launch duration INSIDE the training step, measured live: one more
     hipGraph of the whole step (forward, backward, AdamW -- the timed region's graph, same model) is
     captured with an external timing event recorded before and after every launch of that op (the
-    ops-module entry it goes through, matched on M, N, K and layout), replayed ``replays`` times after
-    the timed region, and the event pairs of each replay averaged (median over replays).  In the step
-    a launch also runs whatever deferred split-K reduce / AdamW work it hosts on free slots, and finds
-    its operands as the step leaves them (colder than the census's back-to-back replays).  HIP events
-    on the step's stream: the event record nodes sit between the op's kernel and its neighbours, so
-    the figure is that kernel's duration plus at most the record nodes' own latency.
-    Returns (ms, launches per step) or None when the events cannot be captured."""
-    from replicatinggpt_amd import ops
+    ops-module entry it goes through, matched on M, N, K and layout; cg_timing_event_record),
+    replayed ``replays`` times after the timed region, and the event pairs of each replay averaged
+    (median over replays).  In the step a launch also runs whatever deferred split-K reduce / AdamW
+    work it hosts on free slots, and finds its operands as the step leaves them (colder than the
+    census's back-to-back replays).  HIP events on the step's stream: the record nodes sit between
+    the op's kernel and its neighbours: an extra record node right before each start event times one
+    node-to-node hand-off, which is subtracted (the raw figure is reported beside it).  Returns (ms,
+    launches per step, the probe graph's ms per step, raw ms) or None when the events cannot be
+    captured."""
+    from replicatinggpt_amd import _lib as L, ops
     from replicatinggpt_amd.engine import TrainStep
+    lib = L.load()
     fname = GEMM_FNS.get(dom["epilogue"], "gemm")
     orig = getattr(ops, fname)
     pairs = []
@@ -429,41 +458,43 @@ def in_step_launch_ms(model, opt, sampler, dom, replays=7):
         if fname == "gemm":
             key, lay = (a[6], a[7], a[8]), (bool(a[4]), bool(a[5]))
         else:
-            key, lay = (a[3], a[4], a[5]), (False, dom["name"].endswith("dgrad"))
-        want = (dom["M"], dom["N"], dom["K"]) == key and (fname != "gemm" or lay == dom["layout"])
+            key, lay = (a[3], a[4], a[5]), dom["layout"]
+        want = (dom["M"], dom["N"], dom["K"]) == key and lay == dom["layout"]
         if not (want and torch.cuda.is_current_stream_capturing()):
             return orig(*a, **k)
-        s, e = (torch.cuda.Event(enable_timing=True, external=True) for _ in range(2))
+        z, s, e = _TimingEvent(lib), _TimingEvent(lib), _TimingEvent(lib)
+        z.record()   # z -> s: two adjacent record nodes, the cost of one node hand-off
         s.record()
         r = orig(*a, **k)
         e.record()
-        pairs.append((s, e))
+        pairs.append((z, s, e))
         return r
     setattr(ops, fname, probe)
+    st = None
     try:
         st = TrainStep(model, opt, sampler, None, use_graph=True)
         st.capture(warmup=1)
+        if not pairs:
+            return None
+        per, raw, steps = [], [], []
+        for _ in range(replays):
+            t0 = time.perf_counter()
+            st.step()
+            torch.cuda.synchronize()
+            steps.append((time.perf_counter() - t0) * 1e3)
+            r = sum(s.elapsed_ms(e) for _, s, e in pairs) / len(pairs)
+            d = sum(z.elapsed_ms(s) for z, s, _ in pairs) / len(pairs)
+            raw.append(r)
+            per.append(r - d)
     except Exception as ex:   # noqa: BLE001 -- a runtime without timed external events: no live figure
         _log(f"in-step probe unavailable: {type(ex).__name__}: {ex}")
         return None
     finally:
         setattr(ops, fname, orig)
-    if not pairs:
-        return None
-    per = []
-    try:
-        for _ in range(replays):
-            st.step()
-            torch.cuda.synchronize()
-            per.append(sum(s.elapsed_time(e) for s, e in pairs) / len(pairs))
-    except Exception as ex:   # noqa: BLE001
-        _log(f"in-step probe unavailable: {type(ex).__name__}: {ex}")
-        return None
-    finally:
         del st
         torch.cuda.empty_cache()
-    per.sort()
-    return per[len(per) // 2], len(pairs)
+    med = lambda x: sorted(x)[len(x) // 2]   # noqa: E731
+    return med(per), len(pairs), med(steps), med(raw)
 
 
 def step_kernel(config, dom):
@@ -736,7 +767,9 @@ def main():
                         "avg_launch_ms": round(ms_op, 5),
                         "timing": ("in-step: HIP events around each of the op's launches in a hipGraph of the "
                                    f"training step, {live[1]} launches per step, median of 7 replays after the "
-                                   "timed region" if live else "census (in-step probe unavailable)"),
+                                   f"timed region, less one event-node hand-off (raw {live[3] * 1e3:.2f} us; that "
+                                   f"graph's step {live[2]:.3f} ms incl. host sync)"
+                                   if live else "census (in-step probe unavailable)"),
                         "census_avg_launch_ms": round(dom["ms"], 5), "census_achieved": round(c_ach, 1),
                         "census_frac": round(c_ach / PEAK_BF16_TFLOPS, 4),
                         "traffic": None, "gemm_family": gemm_family(census)}

@@ -109,6 +109,14 @@ int cg_version(void);
    Set them before the calls they affect, from one thread.                                       */
 int cg_set_tuning(const char* key, int value);
 int cg_device_info(int* n_cu, int* arch_major, int* arch_minor);
+/* measurement (bench.py's in-step roofline): a timing event recorded on `stream` -- inside a
+   hipGraph capture as an EXTERNAL event-record node (hipEventRecordExternal), so that each replay
+   re-records it and two such events time the kernels captured between them on that stream.
+   cg_timing_event_elapsed: milliseconds between two recorded events (after they completed).     */
+int cg_timing_event_create(void** event);
+int cg_timing_event_record(void* event, void* stream);
+int cg_timing_event_elapsed(void* start, void* end, float* ms);
+int cg_timing_event_destroy(void* event);
 
 /* ---- utility ------------------------------------------------------------------------ */
 /* *counter += delta (one thread); snapshot variant: *snap = *counter, *counter += 1.       */

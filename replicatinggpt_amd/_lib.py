@@ -95,6 +95,10 @@ _SIGS = {
     "cg_adamw": (c_int, [P, P, P, P, P, c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, P, P]),
     "cg_adamw_defer": (c_int, [P, P, P, P, P, c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, P, P]),
     "cg_adamw_segments": (c_int, [P, P, P, P, P, P, c_int, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, P, P]),
+    "cg_timing_event_create": (c_int, [ctypes.POINTER(P)]),
+    "cg_timing_event_record": (c_int, [P, P]),
+    "cg_timing_event_elapsed": (c_int, [P, P, ctypes.POINTER(c_flt)]),
+    "cg_timing_event_destroy": (c_int, [P]),
 }
 
 _lib = None

@@ -771,6 +771,59 @@ extern int g_ln_rl;     // layernorm.hip
 extern int g_ln_nt;     // layernorm.hip
 }
 
+extern "C" int cg_timing_event_create(void** event) {
+    CG_REQUIRE(event, "cg_timing_event_create: null");
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) {
+        cg::set_error("cg_timing_event_create: hipEventCreate failed");
+        return CG_EHIP;
+    }
+    *event = (void*)e;
+    return CG_OK;
+}
+
+extern "C" int cg_timing_event_record(void* event, void* stream) {
+    CG_REQUIRE(event, "cg_timing_event_record: null event");
+    hipStream_t st = (hipStream_t)stream;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    hipGraph_t g = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t nd = 0;
+    hipError_t r = hipStreamGetCaptureInfo_v2(st, &cs, &id, &g, &deps, &nd);
+    if (r == hipSuccess && cs == hipStreamCaptureStatusActive) {
+        // an event-record node appended to the capture by hand (hipEventRecordWithFlags with
+        // hipEventRecordExternal is refused during capture on this runtime): it depends on the
+        // stream's current capture frontier and becomes the new frontier
+        hipGraphNode_t node = nullptr;
+        r = hipGraphAddEventRecordNode(&node, g, deps, nd, (hipEvent_t)event);
+        if (r == hipSuccess) r = hipStreamUpdateCaptureDependencies(st, &node, 1, hipStreamSetCaptureDependencies);
+    } else if (r == hipSuccess) {
+        r = hipEventRecord((hipEvent_t)event, st);
+    }
+    if (r != hipSuccess) {
+        (void)hipGetLastError();   // leave no sticky error for the caller's next launch check
+        cg::set_error("cg_timing_event_record: %s", hipGetErrorString(r));
+        return CG_EHIP;
+    }
+    return CG_OK;
+}
+
+extern "C" int cg_timing_event_elapsed(void* start, void* end, float* ms) {
+    CG_REQUIRE(start && end && ms, "cg_timing_event_elapsed: null");
+    const hipError_t r = hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end);
+    if (r != hipSuccess) {
+        cg::set_error("cg_timing_event_elapsed: %s", hipGetErrorString(r));
+        return CG_EHIP;
+    }
+    return CG_OK;
+}
+
+extern "C" int cg_timing_event_destroy(void* event) {
+    if (event) (void)hipEventDestroy((hipEvent_t)event);
+    return CG_OK;
+}
+
 extern "C" int cg_set_tuning(const char* key, int value) {
     CG_REQUIRE(key, "cg_set_tuning: null key");
     if (!strcmp(key, "gemm_variant")) {

@@ -12,8 +12,8 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpu
 trace=$(find $R/gpurun_out/prof_$tag -name 'run_kernel_trace.csv' | head -1)
 stats=$(find $R/gpurun_out/prof_$tag -name 'run_kernel_stats.csv' | head -1)
 cp "$stats" $R/gpurun_out/prof_$tag/kernel_stats.csv
-cd $R && python3 tools/step_kernels.py "$trace" $cfg gpurun_out/prof_$tag/step_kernels_$cfg.json 10 \
+cd $R && python3 tools/step_kernels.py "$trace" $cfg gpurun_out/prof_$tag/step_kernels_$cfg.json 10 8 \
   > gpurun_out/prof_$tag/step_kernels.txt 2>&1
-python3 tools/trace_timeline.py "$trace" k_embed_fwd 10 > gpurun_out/prof_$tag/timeline.txt 2>&1
+python3 tools/trace_timeline.py "$trace" k_embed_fwd 10 8 > gpurun_out/prof_$tag/timeline.txt 2>&1
 rm -f "$trace"
 echo done

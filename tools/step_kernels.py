@@ -6,7 +6,9 @@ identical launches (time_gemm; a weight gradient's burst alternates GEMM and spl
 bursts give each census op its kernel (name + grid); the window gives that kernel's average
 duration and launches per step inside the training step.  A kernel that two census ops share
 (same instantiation and grid) gets the mixed in-step average and lists the other ops.
-usage: python tools/step_kernels.py <run_kernel_trace.csv> <c2|c4> <out.json> [steps]"""
+skip: training-step replays at the end of the trace that are not the timed region's (bench.py's
+in-step probe replays 1 eager + 7 graph steps after it: pass 8).
+usage: python tools/step_kernels.py <run_kernel_trace.csv> <c2|c4> <out.json> [steps] [skip]"""
 import csv
 import json
 import os
@@ -23,6 +25,7 @@ def clean(name):
 def main():
     path, config, out = sys.argv[1], sys.argv[2], sys.argv[3]
     steps = int(sys.argv[4]) if len(sys.argv) > 4 else 10
+    skip = int(sys.argv[5]) if len(sys.argv) > 5 else 0
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
@@ -30,6 +33,8 @@ def main():
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), clean(r["Kernel_Name"]), grid))
     rows.sort()
     marks = [s for s, e, n, g in rows if "k_embed_fwd" in n]
+    if skip:
+        marks = marks[:-skip]
     if len(marks) < steps + 1:
         raise SystemExit(f"only {len(marks)} steps in the trace")
     t0, t1 = marks[-steps - 1], marks[-1]

@@ -1,7 +1,8 @@
 """Timeline statistics of a rocprofv3 kernel trace (csv) over a window of training steps:
 per queue busy time, the union of all kernels' busy time (GPU not idle), and the idle gaps.
-usage: python tools/trace_timeline.py <run_kernel_trace.csv> [marker-kernel-substring] [steps]
-The window is the last `steps` occurrences of the marker kernel (default k_embed_fwd: one per step)."""
+usage: python tools/trace_timeline.py <run_kernel_trace.csv> [marker-kernel-substring] [steps] [skip] [gaps]
+The window is the last `steps` occurrences of the marker kernel (default k_embed_fwd: one per step)
+before the last `skip` ones (bench.py's in-step probe adds 8 steps after the timed region)."""
 import csv
 import re
 import sys
@@ -18,6 +19,9 @@ def main():
                      re.sub(r"\(.*$", "", name).replace("void ", "").replace("cg::", "")[:48]))
     rows.sort()
     marks = [s for s, e, q, n in rows if marker in n]
+    skip = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+    if skip:
+        marks = marks[:-skip]
     if len(marks) < steps + 1:
         print("not enough steps"); return
     t0, t1 = marks[-steps - 1], marks[-1]
@@ -46,7 +50,7 @@ def main():
     print(f"  any kernel running: {busy / 1e3 / steps:.1f} us/step ({busy / wall:.0%}); idle "
           f"{(wall - busy) / 1e3 / steps:.1f} us/step in {len(gaps) / steps:.0f} gaps/step")
     gaps.sort(reverse=True)
-    for g, at, prev, nxt in gaps[:int(sys.argv[4]) if len(sys.argv) > 4 else 12]:
+    for g, at, prev, nxt in gaps[:int(sys.argv[5]) if len(sys.argv) > 5 else 12]:
         print(f"    gap {g / 1e3:6.1f} us: after q{prev[0]} {prev[1]:48s} -> q{nxt[0]} {nxt[1]}")
 
 
