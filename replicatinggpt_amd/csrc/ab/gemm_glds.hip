@@ -8,10 +8,10 @@
 // MFMAs.  The LDS-DMA destination is linear per wave instruction (base + 16*lane), so the XOR
 // swizzle of the images (gemm_tile.h) is applied to the per-lane GLOBAL source address instead
 // (the source permutation and the read permutation are the same involution).
-#include "gemm_tile.h"
+// A/B-only (never the product library: `make ab`, CG_AB_VARIANTS): measured slower than gemm_pk.hip.
+#include "../gemm_tile.h"
 
 namespace cg {
-#ifdef CG_AB_VARIANTS   // A/B-only kernel (measured slower than gemm_pk.hip): `make ab`
 namespace {
 using namespace gt;
 
@@ -162,13 +162,11 @@ void launch_d(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, 
 }
 
 }  // namespace
-#endif
 
 bool glds_gemm_launch(int v, int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda,
                       const bf16_t* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k,
                       float* ws, hipStream_t st) {
     switch (v) {
-#ifdef CG_AB_VARIANTS
         case 5: launch_d<128, 128, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st); return true;
         case 6: launch_d<128, 128, 3>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st); return true;
         case 7:
@@ -176,7 +174,6 @@ bool glds_gemm_launch(int v, int at, int bt, int64_t M, int64_t N, int64_t K, co
             launch_d<256, 128, 2>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
             return true;
         case 8: launch_d<128, 128, 4>(at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st); return true;
-#endif
         default: return pk_gemm_launch(v, at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st);
     }
 }

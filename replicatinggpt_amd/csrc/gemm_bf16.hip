@@ -263,8 +263,13 @@ bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf1
         return true;
     if (e.aux_dtype == CG_BITS && !pk128(v)) return false;   // only the two persistent kernels read / write keep bits
     if (v >= 20) v = 2;
+#ifdef CG_AB_VARIANTS   // the LDS-DMA variants 5-8 (ab/gemm_glds.hip), else the persistent kernels
     if (v >= 5 && glds_gemm_launch(v, at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st))
         return true;
+#else
+    if (v >= 5 && pk_gemm_launch(v, at, bt, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k, ws, st))
+        return true;
+#endif
 #ifdef CG_AB_VARIANTS
     if ((v == 3 || v == 4) && M % 256) v = 1;
     switch (v) {

@@ -28,10 +28,19 @@ def _makefile():
     return open(os.path.join(CSRC, "Makefile")).read()
 
 
+def _text_with_local_headers(src):
+    """the source and the csrc headers it includes (the kernels may live in a header: attention_d64.h)"""
+    text = open(os.path.join(CSRC, src)).read()
+    for h in re.findall(r'^#include "([^"]+)"', text, re.M):
+        if os.path.exists(os.path.join(CSRC, h)) and not h.endswith("common.h"):
+            text += open(os.path.join(CSRC, h)).read()
+    return text
+
+
 def _product_sources():
     mk = _makefile()
     srcs = re.search(r"^SRCS := (.*)$", mk, re.M).group(1).split()
-    return [s for s in srcs if re.search(r"\bgload(16|4|4s)\(", open(os.path.join(CSRC, s)).read())]
+    return [s for s in srcs if re.search(r"\bgload(16|4|4s)\(", _text_with_local_headers(s))]
 
 
 def _flags(src):
