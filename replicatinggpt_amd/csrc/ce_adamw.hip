@@ -152,63 +152,7 @@ __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const floa
     }
 }
 
-// Block-contiguous form: block b streams float4 chunks [b*per, (b+1)*per) of every buffer, U chunks per
-// thread in flight (each wave's loads of one buffer cover one contiguous 1 KB), instead of the
-// grid-stride form's 32 MB-apart windows of all 8192 blocks at once.  Same adam_one per element:
-// the same bits.
-template <bool NT, int U>
-__global__ __launch_bounds__(256) void k_adamw_blk(float* __restrict__ p, const float* __restrict__ g,
-                                                   float* __restrict__ m, float* __restrict__ v,
-                                                   bf16_t* __restrict__ pb, int64_t n4, int64_t per, double lr,
-                                                   double beta1, double beta2, double eps, double wd,
-                                                   const int64_t* __restrict__ step_ptr) {
-    const AdamScalars s = adam_scalars(lr, beta1, beta2, eps, wd, step_ptr);
-    const int64_t c0 = (int64_t)blockIdx.x * per;
-    const int64_t c1 = c0 + per < n4 ? c0 + per : n4;
-    int64_t c = c0 + threadIdx.x;
-    for (; c + (U - 1) * 256 < c1; c += U * 256) {
-        float4 pv[U], gv[U], mv[U], vv[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t j = 4 * (c + u * 256);
-            pv[u] = ld4<NT>(p + j);
-            gv[u] = ld4<NT>(g + j);
-            mv[u] = ld4<NT>(m + j);
-            vv[u] = ld4<NT>(v + j);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t j = 4 * (c + u * 256);
-            pv[u].x = adam_one(pv[u].x, gv[u].x, mv[u].x, vv[u].x, s);
-            pv[u].y = adam_one(pv[u].y, gv[u].y, mv[u].y, vv[u].y, s);
-            pv[u].z = adam_one(pv[u].z, gv[u].z, mv[u].z, vv[u].z, s);
-            pv[u].w = adam_one(pv[u].w, gv[u].w, mv[u].w, vv[u].w, s);
-            st4<NT>(p + j, pv[u]);
-            st4<NT>(m + j, mv[u]);
-            st4<NT>(v + j, vv[u]);
-            if (pb) {
-                const uint2 w = make_uint2(pack_bf2(pv[u].x, pv[u].y), pack_bf2(pv[u].z, pv[u].w));
-                if constexpr (NT) __builtin_nontemporal_store(nu2{w.x, w.y}, (nu2*)(pb + j));
-                else *(uint2*)(pb + j) = w;
-            }
-        }
-    }
-    for (; c < c1; c += 256) {
-        const int64_t j = 4 * c;
-        float4 pv = ld4<NT>(p + j), gv = ld4<NT>(g + j), mv = ld4<NT>(m + j), vv = ld4<NT>(v + j);
-        pv.x = adam_one(pv.x, gv.x, mv.x, vv.x, s);
-        pv.y = adam_one(pv.y, gv.y, mv.y, vv.y, s);
-        pv.z = adam_one(pv.z, gv.z, mv.z, vv.z, s);
-        pv.w = adam_one(pv.w, gv.w, mv.w, vv.w, s);
-        st4<NT>(p + j, pv);
-        st4<NT>(m + j, mv);
-        st4<NT>(v + j, vv);
-        if (pb) *(uint2*)(pb + j) = make_uint2(pack_bf2(pv.x, pv.y), pack_bf2(pv.z, pv.w));
-    }
-}
-
 namespace cg {
-int g_adamw_blocks = 0;   // cg_set_tuning("adamw_blocks"): grid of the block-contiguous modes (0: 4 per CU)
 // cg_set_tuning("adamw_mode"): 0 automatic -- non-temporal loads/stores with two float4 groups per
 // thread in flight once the 30 B/param stream is far past the 256 MB Infinity Cache (n >= 32 M: C4
 // 86 M params, -2.4 % same-box interleaved A/B), plain loads/stores below (C2 10.8 M: the NT form is
@@ -239,21 +183,6 @@ static int adamw_launch(float* p, const float* g, float* m, float* v, uint16_t* 
     else if (mode == 3) ADAMW(true, false, 2);
     else if (mode == 4) ADAMW(true, true, 4);    // A/B: four groups in flight per thread
     else if (mode == 5) ADAMW(true, false, 4);
-    else if (mode >= 6 && mode <= 9 && n % 4 == 0) {
-        // block-contiguous chunks (A/B): 6 NT U2, 7 plain U2, 8 NT U4, 9 plain U1
-        const int64_t n4 = n / 4;
-        const int nb = g_adamw_blocks > 0 ? g_adamw_blocks : 4 * gemm_cu_count();
-        const int64_t per = (n4 + nb - 1) / nb;
-        const unsigned gb = (unsigned)((n4 + per - 1) / per);
-#define ADAMWB(NT_, U_)                                                                                       \
-        k_adamw_blk<NT_, U_><<<gb, 256, 0, st>>>(p, g, m, v, (bf16_t*)p_bf16, n4, per, lr, beta1, beta2, eps, \
-                                                 weight_decay, step_ptr)
-        if (mode == 6) ADAMWB(true, 2);
-        else if (mode == 7) ADAMWB(false, 2);
-        else if (mode == 8) ADAMWB(true, 4);
-        else ADAMWB(false, 1);
-#undef ADAMWB
-    }
     else ADAMW(true, false, 1);
 #undef ADAMW
     CG_LAUNCH_CHECK("cg_adamw");

@@ -765,7 +765,6 @@ extern int g_attn_bwd_lpt;  // attention_d64.hip
 extern int g_decode_attn_rows;  // decode.hip
 extern int g_ln_rpb;  // layernorm.hip
 extern int g_adamw_mode;  // ce_adamw.hip
-extern int g_adamw_blocks;
 extern int g_ln_waves;  // layernorm.hip
 extern int g_ln_pf;     // layernorm.hip
 extern int g_ln_rl;     // layernorm.hip
@@ -918,13 +917,8 @@ extern "C" int cg_set_tuning(const char* key, int value) {
         return CG_OK;
     }
     if (!strcmp(key, "adamw_mode")) {
-        CG_REQUIRE(value >= 0 && value <= 9, "cg_set_tuning: adamw_mode out of range");
+        CG_REQUIRE(value >= 0 && value <= 5, "cg_set_tuning: adamw_mode out of range");
         g_adamw_mode = value;
-        return CG_OK;
-    }
-    if (!strcmp(key, "adamw_blocks")) {
-        CG_REQUIRE(value >= 0, "cg_set_tuning: adamw_blocks < 0");
-        g_adamw_blocks = value;
         return CG_OK;
     }
     if (!strcmp(key, "ln_nt")) {   // the LayerNorm backward's non-temporal streams (-1 automatic, 0..3)

@@ -4,6 +4,8 @@ the same box shows.  Interleaved rounds (same process) of the grid-stride modes 
 9 plain x1; adamw_blocks = 4/8/16 per CU), each 20 launches replayed from a hipGraph on the step's
 long-lived buffers (bench._time_ms, warm 20), every mode bitwise against mode 1; and a float4 copy of
 the same 2.58 GB (read 16 B + write 14 B per param, as AdamW) for the box's ceiling.
+The block-contiguous modes were measured slower (profiles/r6_adamw_ceiling_c4.txt) and removed from the
+library; this script needs the commit that had them (git log -S k_adamw_blk).
 usage: python tools/adamw_blk_ab.py [c4|c2]"""
 import os
 import sys
