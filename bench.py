@@ -362,8 +362,16 @@ def kernel_census(cfg, Bsz, T, dev):
     # launches ran up to 20 % slower (profiles/r4_adamw_ab.txt)
     t = _time_ms(lambda: ops.adamw(pp, g, m, v, p16, 1e-3, 0.9, 0.999, 1e-8, 0.01, step_t), warm=20)
     gbs = 30 * n / (t * 1e-3) / 1e9
+    # the box's ceiling for AdamW's near-1:1 read/write mix: a copy reading 16 B and writing 14 B per
+    # parameter (profiles/r6_adamw_ceiling_c4.txt: LayerNorm's 2:1 read-heavy stream runs faster)
+    src = torch.empty(4 * n, dtype=torch.float32, device=dev)
+    dst = torch.empty(7 * n // 2, dtype=torch.float32, device=dev)
+    tc = _time_ms(lambda: dst.copy_(src[:dst.numel()]), warm=5)
+    cgbs = 28 * n / (tc * 1e-3) / 1e9
+    del src, dst
     out["adamw"] = {"ms": round(t, 4), "params": n, "bytes": 30 * n, "achieved": round(gbs, 1), "unit": "GB/s",
-                    "peak": PEAK_HBM_GBS, "frac": round(gbs / PEAK_HBM_GBS, 4)}
+                    "peak": PEAK_HBM_GBS, "frac": round(gbs / PEAK_HBM_GBS, 4),
+                    "copy_same_mix_GB/s": round(cgbs, 1), "frac_of_copy": round(gbs / cgbs, 4)}
     return out
 
 
