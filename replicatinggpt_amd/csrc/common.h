@@ -100,6 +100,23 @@ __device__ __forceinline__ void gload4s(uint32_t& dst, const void* sbase, uint32
     asm volatile("global_load_dword %0, %1, %2" : "=v"(dst) : "v"(voff), "s"(sbase) : "memory");
 }
 typedef float fv4 __attribute__((ext_vector_type(4)));
+
+// A GEMM output's 16-B store.  CG_STORE_SC1 (A/B build, make sc1): global_store_dwordx4 ... sc1 -- the
+// line leaves the XCD's L2 (MI355X_MICROARCH.md store flavours) instead of staying there dirty, so the
+// output stream neither evicts the operand panels the LDS-DMA reads nor is written back at the kernel
+// boundary.  The s_nop: the store reads its 128-bit data after issue, and hipcc's hazard recognizer
+// does not see inside the asm (it reused the data registers as the next store's address at once).
+template <typename T>
+__device__ __forceinline__ void st_out16(T* p, const T& v) {
+    static_assert(sizeof(T) == 16, "16-B stores");
+#ifdef CG_STORE_SC1
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 d = __builtin_bit_cast(u32x4, v);
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(d) : "memory");
+#else
+    *p = v;
+#endif
+}
 typedef __bf16 bfv8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }

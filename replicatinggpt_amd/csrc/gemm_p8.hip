@@ -383,7 +383,8 @@ void k_gemm_p8(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, in
                     for (int j = 0; j < FN; ++j) {
                         const int ii = 2 * hh + i;
                         fv4& v = acc[4 * hb + ii][j];
-                        *(float4*)((float*)Cv + (mb + 16 * ii) * ldc + nc + 16 * j) = make_float4(v[0], v[1], v[2], v[3]);
+                        st_out16((float4*)((float*)Cv + (mb + 16 * ii) * ldc + nc + 16 * j),
+                                 make_float4(v[0], v[1], v[2], v[3]));
                         v = fv4{0.f, 0.f, 0.f, 0.f};
                     }
             }

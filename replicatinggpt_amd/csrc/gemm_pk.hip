@@ -115,7 +115,7 @@ __device__ __forceinline__ void store4_plain(const fv4& v, int64_t m, int64_t n,
     if (c_dtype == CG_BF16)
         *(uint2*)((bf16_t*)Cv + m * ldc + n) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
     else
-        *(float4*)((float*)Cv + m * ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+        st_out16((float4*)((float*)Cv + m * ldc + n), make_float4(v[0], v[1], v[2], v[3]));
 }
 
 // Dropout keep bits of a wave's 64x64 item fragment, 4 per (i, j) -- bit q <-> column
@@ -405,7 +405,7 @@ __device__ __forceinline__ void epi_resid_nj(fv4 (&acc)[4][NJ], int64_t mr, int6
                 for (int q = 0; q < 4; ++q) v[q] = ((nib[i][j] >> q) & 1u) ? v[q] * epi.dscale : 0.f;
             }
             v[0] = r[i][j].x + v[0]; v[1] = r[i][j].y + v[1]; v[2] = r[i][j].z + v[2]; v[3] = r[i][j].w + v[3];
-            *(float4*)(C + (mr + 16 * i) * ldc + nc + 16 * j) = make_float4(v[0], v[1], v[2], v[3]);
+            st_out16((float4*)(C + (mr + 16 * i) * ldc + nc + 16 * j), make_float4(v[0], v[1], v[2], v[3]));
         }
 }
 

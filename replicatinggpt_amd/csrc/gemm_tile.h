@@ -333,17 +333,7 @@ __device__ __forceinline__ void store_bf16_wide(const fv4 (&v)[FM][4], bf16_t* C
             const uint32_t bx = pack_bf2(v[i][jp + 1][0], v[i][jp + 1][1]), by = pack_bf2(v[i][jp + 1][2], v[i][jp + 1][3]);
             const auto sx = __builtin_amdgcn_permlane16_swap(ax, bx, false, false);
             const auto sy = __builtin_amdgcn_permlane16_swap(ay, by, false, false);
-#ifdef CG_STORE_SC1
-            // A/B build only (make sc1): the output row segments stored sc1 -- the line leaves the
-            // XCD's L2 instead of staying there (MI355X_MICROARCH.md store flavours), so the output
-            // stream does not evict the operand panels the next K-tiles' LDS-DMA reads
-            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-            const u32x4 d4 = {sx[0], sy[0], sx[1], sy[1]};
-            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(C + (mr + 16 * i) * ldc + col + 16 * jp), "v"(d4)
-                         : "memory");
-#else
-            *(uint4*)(C + (mr + 16 * i) * ldc + col + 16 * jp) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
-#endif
+            st_out16((uint4*)(C + (mr + 16 * i) * ldc + col + 16 * jp), make_uint4(sx[0], sy[0], sx[1], sy[1]));
         }
 }
 }  // namespace cg
