@@ -129,7 +129,10 @@ def load():
         raise RuntimeError(f"charpt: {LIB_PATH} is not built; run `python __graft_entry__.py` (build()) first. "
                            "There is no CPU fallback for the HIP hot path.")
     lib = ctypes.CDLL(LIB_PATH)
+    ab = bool(os.environ.get("CHARPT_LIB"))
     for name, (res, args) in _SIGS.items():
+        if ab and not hasattr(lib, name):   # an A/B build of an older tree: the entry points it has
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

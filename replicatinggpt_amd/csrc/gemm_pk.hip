@@ -1054,7 +1054,8 @@ void pk_pair_launch(int64_t dM, int64_t dN, int64_t dK, const bf16_t* dA, int64_
     int64_t slots = (int64_t)cu_count() * G::OCC;
     if (g_gemm_max_grid > 0 && g_gemm_max_grid < slots) slots = g_gemm_max_grid;
     const unsigned grid = (unsigned)(items < slots ? items : slots);
-    const RedJobs red = take_pending_reduces(st, false);
+    // pending reduces, and AdamW jobs (cg_adamw_defer): in every block's tail after its items
+    const RedJobs red = take_pending_reduces(st, true);
 #define PAIR(E1, E2) k_gemm_pk_pair<E1, E2><<<grid, G::THREADS, G::LDS, st>>>(p1, p2, red)
     const bool s16 = we.slab_bf16;
     switch (de.kind) {
