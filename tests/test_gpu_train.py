@@ -262,7 +262,9 @@ def test_failed_backward_with_early_adamw(fail_at):
         return [t.detach().clone() for t in (m.flat.master, opt._m, opt._v, opt._step_t, m.flat.shadow)]
 
     before = snap()
-    real, calls = Fn.linear_wgrad, [0]
+    # the backward's weight-gradient launches: linear_wgrad, or linear_pair (a Linear's dgrad + weight
+    # gradient as one cg_gemm_pair launch) -- the fail_at-th of them raises
+    real, real_pair, calls = Fn.linear_wgrad, Fn.linear_pair, [0]
 
     def failing(*a, **k):
         calls[0] += 1
@@ -270,12 +272,21 @@ def test_failed_backward_with_early_adamw(fail_at):
             raise RuntimeError("injected")
         return real(*a, **k)
 
-    Fn.linear_wgrad = failing
+    def failing_pair(*a, **k):
+        calls[0] += 1
+        if calls[0] == fail_at:
+            raise RuntimeError("injected")
+        if real_pair(*a, **k):
+            return True
+        calls[0] -= 1   # not paired: the linear_wgrad that follows counts
+        return False
+
+    Fn.linear_wgrad, Fn.linear_pair = failing, failing_pair
     try:
         with pytest.raises(RuntimeError, match="injected"):
             st._eager()
     finally:
-        Fn.linear_wgrad = real
+        Fn.linear_wgrad, Fn.linear_pair = real, real_pair
     after = snap()
     same = all(torch.equal(a, b) for a, b in zip(before, after))
     if fail_at == 1:
