@@ -219,30 +219,6 @@ int cg_reduce_rows_ex(const float* part, int64_t rows, int64_t N, float* out, in
 int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
             const void* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const cg_epilogue_t* epi, int split_k,
             void* workspace, void* stream);
-/* A GEMM call as a struct (cg_gemm's arguments, op dtype bf16). */
-typedef struct {
-    int a_trans, b_trans;
-    int64_t M, N, K;
-    const void* A;
-    int64_t lda;
-    const void* B;
-    int64_t ldb;
-    void* C;
-    int c_dtype;
-    int64_t ldc;
-    const cg_epilogue_t* epi;
-    int split_k;
-    void* workspace;
-} cg_gemm_desc_t;
-/* A Linear's backward pair (GPT1.py:111-112,136,143,145): its input gradient `dgrad` (a_trans 0,
-   b_trans 1, split 1; epilogue CG_EPI_STORE, CG_EPI_RELU_BWD or CG_EPI_STORE_ROWDOT, beta 0, no flags)
-   and its weight gradient `wgrad` (a_trans 1, b_trans 1, split_k >= 2 with a workspace, fp32 output,
-   CG_EPI_STORE; flags CG_GEMM_SLAB_BF16 / CG_GEMM_DEFER_REDUCE as for cg_gemm).  Where
-   cg_gemm_pair_supported(dgrad, wgrad) is 1 both run as ONE persistent launch (the blocks the dgrad's
-   tiles leave idle start on weight-gradient items; one launch / prologue / drain); otherwise as
-   cg_gemm(dgrad) then cg_gemm(wgrad).  Results are identical to those two calls either way.        */
-int cg_gemm_pair(const cg_gemm_desc_t* dgrad, const cg_gemm_desc_t* wgrad, void* stream);
-int cg_gemm_pair_supported(const cg_gemm_desc_t* dgrad, const cg_gemm_desc_t* wgrad);
 /* A residual-stream GEMM with the LayerNorm that reads its output, in one launch (the attention
    projection + ln2, the FFN's second Linear + the next block's ln1 / ln_f: GPT1.py:136,145-147,
    159-160,163-164,173): out = resid + [dropout](A W^T + bias) (fp32; epi kind CG_EPI_BIAS_RESID or

@@ -28,13 +28,6 @@ class Epilogue(ctypes.Structure):
                 ("beta", c_flt), ("colpart", P), ("flags", c_int)]
 
 
-class GemmDesc(ctypes.Structure):
-    """cg_gemm_desc_t (include/charpt.h): one cg_gemm call's arguments (bf16 operands)."""
-    _fields_ = [("a_trans", c_int), ("b_trans", c_int), ("M", c_i64), ("N", c_i64), ("K", c_i64), ("A", P),
-                ("lda", c_i64), ("B", P), ("ldb", c_i64), ("C", P), ("c_dtype", c_int), ("ldc", c_i64),
-                ("epi", ctypes.POINTER(Epilogue)), ("split_k", c_int), ("workspace", P)]
-
-
 _SIGS = {
     "cg_last_error_string": (ctypes.c_char_p, []),
     "cg_version": (c_int, []),
@@ -102,8 +95,6 @@ _SIGS = {
     "cg_adamw": (c_int, [P, P, P, P, P, c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, P, P]),
     "cg_adamw_defer": (c_int, [P, P, P, P, P, c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, P, P]),
     "cg_adamw_segments": (c_int, [P, P, P, P, P, P, c_int, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, P, P]),
-    "cg_gemm_pair": (c_int, [ctypes.POINTER(GemmDesc), ctypes.POINTER(GemmDesc), P]),
-    "cg_gemm_pair_supported": (c_int, [ctypes.POINTER(GemmDesc), ctypes.POINTER(GemmDesc)]),
     "cg_timing_event_create": (c_int, [ctypes.POINTER(P)]),
     "cg_timing_event_record": (c_int, [P, P]),
     "cg_timing_event_elapsed": (c_int, [P, P, ctypes.POINTER(c_flt)]),

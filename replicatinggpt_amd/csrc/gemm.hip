@@ -984,59 +984,6 @@ extern "C" int cg_gemm_resid_layernorm(int64_t M, int64_t N, int64_t K, const vo
     return CG_OK;
 }
 
-// the split-K reduce of a slab launch (cg_gemm, cg_gemm_pair): deferred to the next persistent launch on
-// the stream (CG_GEMM_DEFER_REDUCE, slab set <= 40 MB), or its own kernel now
-static void splitk_finish(int64_t M, int64_t N, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k,
-                          void* workspace, int flags, bool fast, bool vec4, hipStream_t st) {
-    // (slab sets above 40 MB -- the C4 FFN / QKV weight gradients -- keep their own reduce kernel: in
-    // the next 256x256 GEMM's tail they measured no gain, C4 58.2 vs 57.9 ms/step)
-    if (split_k > 1 && vec4 && !g_skip_splitk_reduce && (flags & CG_GEMM_DEFER_REDUCE) && fast &&
-        e.kind == CG_EPI_STORE && c_dtype == CG_F32 && ldc == N &&
-        (int64_t)split_k * M * N * 4 <= ((int64_t)40 << 20)) {
-        // deferred: summed in the tail of the next persistent GEMM launch on this stream of this
-        // device (or cg_flush_deferred(st) there) -- the queue key holds the device, so the null
-        // stream, whose handle names a different queue on every device, is fine too
-        std::lock_guard<std::mutex> lk(defer_mutex());
-        DeferQueue& q = *defer_queue(st, true);
-        if (q.nred == MAX_RED) flush_red_locked(q);
-        q.red[q.nred++] = RedJob{(const float*)workspace, (float*)C, M * N / 4, split_k, e.beta, e.slab_bf16};
-    } else if (split_k > 1 && e.slab_bf16) {
-        const int64_t n8 = M * N / 8;
-        k_slab16_reduce8<<<ceil_div(n8, 256), 256, 0, st>>>(workspace, split_k, n8, (float*)C, e.beta);
-    } else if (split_k > 1 && vec4 && !g_skip_splitk_reduce) {
-        const int n4 = (int)(M * N / 4);
-#define SKR(TC_, S_)                                                                                  \
-    k_splitk_reduce4<TC_, S_><<<ceil_div(n4, 256), 256, 0, st>>>((const float*)workspace, split_k, (int)M, \
-                                                                 (int)N, (TC_*)C, ldc, e)
-#define SKR_ANY(TC_)                        \
-    switch (split_k) {                      \
-        case 2: SKR(TC_, 2); break;         \
-        case 4: SKR(TC_, 4); break;         \
-        case 8: SKR(TC_, 8); break;         \
-        case 12: SKR(TC_, 12); break;       \
-        case 14: SKR(TC_, 14); break;       \
-        case 16: SKR(TC_, 16); break;       \
-        case 32: SKR(TC_, 32); break;       \
-        default: SKR(TC_, 0); break;        \
-    }
-        if (c_dtype == CG_BF16) {
-            SKR_ANY(bf16_t)
-        } else {
-            SKR_ANY(float)
-        }
-#undef SKR_ANY
-#undef SKR
-    } else if (split_k > 1) {
-        const int64_t n = M * N;
-        if (c_dtype == CG_BF16)
-            k_splitk_reduce<bf16_t><<<ceil_div(n, 256), 256, 0, st>>>((const float*)workspace, split_k, M, N,
-                                                                      (bf16_t*)C, ldc, e);
-        else
-            k_splitk_reduce<float><<<ceil_div(n, 256), 256, 0, st>>>((const float*)workspace, split_k, M, N,
-                                                                     (float*)C, ldc, e);
-    }
-}
-
 extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, const void* A,
                        int64_t lda, const void* B, int64_t ldb, void* C, int c_dtype, int64_t ldc,
                        const cg_epilogue_t* epi, int split_k, void* workspace, void* stream) {
@@ -1091,54 +1038,54 @@ extern "C" int cg_gemm(int op_dtype, int a_trans, int b_trans, int64_t M, int64_
         launch_generic<float, float>(a_trans, b_trans, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, e, split_k,
                                      workspace, st);
     }
-    splitk_finish(M, N, C, c_dtype, ldc, e, split_k, workspace, flags, fast, vec4, st);
-    CG_LAUNCH_CHECK("cg_gemm");
-    return CG_OK;
-}
-
-static int gemm_desc_call(const cg_gemm_desc_t* d, void* stream) {
-    return cg_gemm(CG_BF16, d->a_trans, d->b_trans, d->M, d->N, d->K, d->A, d->lda, d->B, d->ldb, d->C, d->c_dtype,
-                   d->ldc, d->epi, d->split_k, d->workspace, stream);
-}
-
-// the slab form cg_gemm would give the weight gradient (its e.slab_bf16 rule)
-static EpiArgs pair_wgrad_epi(const cg_gemm_desc_t* w) {
-    EpiArgs e = make_epi(w->epi);
-    const int flags = w->epi ? w->epi->flags : 0;
-    e.slab_bf16 = (flags & CG_GEMM_SLAB_BF16) && w->split_k > 1 && e.kind == CG_EPI_STORE && w->c_dtype == CG_F32 &&
-                  w->ldc == w->N && (w->M * w->N) % 8 == 0 && !g_skip_splitk_reduce;
-    return e;
-}
-
-static bool pair_ok(const cg_gemm_desc_t* d, const cg_gemm_desc_t* w, bool launch, hipStream_t st) {
-    if (!d || !w || d->a_trans || !d->b_trans || !w->a_trans || !w->b_trans || d->split_k != 1 || w->c_dtype != CG_F32)
-        return false;
-    if (d->M <= 0 || d->N <= 0 || d->K <= 0 || w->M <= 0 || w->N <= 0 || w->K <= 0 || w->split_k > 64) return false;
-    const int wflags = w->epi ? w->epi->flags : 0, dflags = d->epi ? d->epi->flags : 0;
-    if (dflags || (wflags & ~(CG_GEMM_SLAB_BF16 | CG_GEMM_DEFER_REDUCE)) || g_skip_splitk_reduce) return false;
-    const EpiArgs de = make_epi(d->epi), we = pair_wgrad_epi(w);
-    return pair_gemm_launch(d->M, d->N, d->K, (const bf16_t*)d->A, d->lda, (const bf16_t*)d->B, d->ldb, d->C, d->c_dtype,
-                            d->ldc, de, w->M, w->N, w->K, (const bf16_t*)w->A, w->lda, (const bf16_t*)w->B, w->ldb,
-                            w->C, w->ldc, we, w->split_k, (float*)w->workspace, st, launch);
-}
-
-extern "C" int cg_gemm_pair_supported(const cg_gemm_desc_t* dgrad, const cg_gemm_desc_t* wgrad) {
-    return pair_ok(dgrad, wgrad, false, nullptr) ? 1 : 0;
-}
-
-extern "C" int cg_gemm_pair(const cg_gemm_desc_t* dgrad, const cg_gemm_desc_t* wgrad, void* stream) {
-    CG_REQUIRE(dgrad && wgrad, "cg_gemm_pair: null descriptor");
-    hipStream_t st = (hipStream_t)stream;
-    if (!pair_ok(dgrad, wgrad, true, st)) {   // not one launch: the two calls, same results
-        const int r = gemm_desc_call(dgrad, stream);
-        return r != CG_OK ? r : gemm_desc_call(wgrad, stream);
+    // (slab sets above 40 MB -- the C4 FFN / QKV weight gradients -- keep their own reduce kernel: in
+    // the next 256x256 GEMM's tail they measured no gain, C4 58.2 vs 57.9 ms/step)
+    if (split_k > 1 && vec4 && !g_skip_splitk_reduce && (flags & CG_GEMM_DEFER_REDUCE) && fast &&
+        e.kind == CG_EPI_STORE && c_dtype == CG_F32 && ldc == N &&
+        (int64_t)split_k * M * N * 4 <= ((int64_t)40 << 20)) {
+        // deferred: summed in the tail of the next persistent GEMM launch on this stream of this
+        // device (or cg_flush_deferred(st) there) -- the queue key holds the device, so the null
+        // stream, whose handle names a different queue on every device, is fine too
+        std::lock_guard<std::mutex> lk(defer_mutex());
+        DeferQueue& q = *defer_queue(st, true);
+        if (q.nred == MAX_RED) flush_red_locked(q);
+        q.red[q.nred++] = RedJob{(const float*)workspace, (float*)C, M * N / 4, split_k, e.beta, e.slab_bf16};
+    } else if (split_k > 1 && e.slab_bf16) {
+        const int64_t n8 = M * N / 8;
+        k_slab16_reduce8<<<ceil_div(n8, 256), 256, 0, st>>>(workspace, split_k, n8, (float*)C, e.beta);
+    } else if (split_k > 1 && vec4 && !g_skip_splitk_reduce) {
+        const int n4 = (int)(M * N / 4);
+#define SKR(TC_, S_)                                                                                  \
+    k_splitk_reduce4<TC_, S_><<<ceil_div(n4, 256), 256, 0, st>>>((const float*)workspace, split_k, (int)M, \
+                                                                 (int)N, (TC_*)C, ldc, e)
+#define SKR_ANY(TC_)                        \
+    switch (split_k) {                      \
+        case 2: SKR(TC_, 2); break;         \
+        case 4: SKR(TC_, 4); break;         \
+        case 8: SKR(TC_, 8); break;         \
+        case 12: SKR(TC_, 12); break;       \
+        case 14: SKR(TC_, 14); break;       \
+        case 16: SKR(TC_, 16); break;       \
+        case 32: SKR(TC_, 32); break;       \
+        default: SKR(TC_, 0); break;        \
     }
-    const cg_gemm_desc_t* w = wgrad;
-    const EpiArgs we = pair_wgrad_epi(w);
-    const bool vec4 = w->N % 4 == 0 && w->ldc % 4 == 0 && w->M * w->N < (int64_t)1 << 31;
-    splitk_finish(w->M, w->N, w->C, CG_F32, w->ldc, we, w->split_k, w->workspace, w->epi ? w->epi->flags : 0, true,
-                  vec4, st);
-    CG_LAUNCH_CHECK("cg_gemm_pair");
+        if (c_dtype == CG_BF16) {
+            SKR_ANY(bf16_t)
+        } else {
+            SKR_ANY(float)
+        }
+#undef SKR_ANY
+#undef SKR
+    } else if (split_k > 1) {
+        const int64_t n = M * N;
+        if (c_dtype == CG_BF16)
+            k_splitk_reduce<bf16_t><<<ceil_div(n, 256), 256, 0, st>>>((const float*)workspace, split_k, M, N,
+                                                                      (bf16_t*)C, ldc, e);
+        else
+            k_splitk_reduce<float><<<ceil_div(n, 256), 256, 0, st>>>((const float*)workspace, split_k, M, N,
+                                                                     (float*)C, ldc, e);
+    }
+    CG_LAUNCH_CHECK("cg_gemm");
     return CG_OK;
 }
 

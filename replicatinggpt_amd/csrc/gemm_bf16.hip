@@ -232,49 +232,6 @@ bool gemm_rowdot_supported(int at, int bt, int64_t M, int64_t N, int64_t K, int6
     return fast_shape_ok(M, N, K, lda, ldb, ldc, 1) && rowdot_ok(pick_variant(at, bt, M, N, 1), at, 1, N);
 }
 
-// cg_gemm_pair's conditions: both products on the 128x128 persistent kernel exactly as two cg_gemm calls
-// would run them (the dgrad's fixed epilogue kinds, the weight gradient's slab items), the dgrad's
-// item count a multiple of 8; launch = false only checks.
-bool pair_gemm_launch(int64_t dM, int64_t dN, int64_t dK, const bf16_t* dA, int64_t dlda, const bf16_t* dB,
-                      int64_t dldb, void* dC, int dc_dtype, int64_t dldc, const EpiArgs& de, int64_t wM, int64_t wN,
-                      int64_t wK, const bf16_t* wA, int64_t wlda, const bf16_t* wB, int64_t wldb, void* wC,
-                      int64_t wldc, const EpiArgs& we, int split_k, float* ws, hipStream_t st, bool launch) {
-    if (!fast_shape_ok(dM, dN, dK, dlda, dldb, dldc, 1) || !fast_shape_ok(wM, wN, wK, wlda, wldb, wldc, split_k))
-        return false;
-    if (pick_variant(0, 1, dM, dN, 1) != 9 || pick_variant(1, 1, wM, wN, split_k) != 9 || (g_pk_flags & 2)) return false;
-    if (((dM / 128) * (dN / 128)) % 8 || split_k < 2 || !ws || wldc != wN) return false;
-    if ((((uintptr_t)dA) | ((uintptr_t)dB) | ((uintptr_t)dC) | ((uintptr_t)wA) | ((uintptr_t)wB) | ((uintptr_t)wC) |
-         ((uintptr_t)ws)) & 15)
-        return false;
-    {   // uneven split-K: every split non-empty
-        const int64_t nkt = wK / FBK, nkc = (nkt + split_k - 1) / split_k;
-        if ((split_k - 1) * nkc >= nkt) return false;
-    }
-    if (we.kind != CG_EPI_STORE || we.bias || we.resid || we.aux || we.colpart) return false;
-    if (de.beta != 0.f || de.bias || de.resid) return false;
-    if (de.aux && ((((uintptr_t)de.aux) & 15) || de.ld_aux % 8)) return false;
-    switch (de.kind) {
-        case CG_EPI_STORE:
-            if (de.aux || de.colpart) return false;
-            break;
-        case CG_EPI_RELU_BWD:
-            if (dc_dtype != CG_BF16 || !de.aux || (de.aux_dtype != CG_BF16 && de.aux_dtype != CG_BITS)) return false;
-            if (de.aux_dtype == CG_BITS && !relu_bits_ok(9, 0, 1, dN)) return false;
-            if (de.colpart && !colpart_ok(9, 0, 1)) return false;
-            break;
-        case CG_EPI_STORE_ROWDOT:
-            if (!rowdot_ok(9, 0, 1, dN) || !de.aux || de.aux_dtype != CG_BF16 || !de.colpart || de.ld_resid <= 0 ||
-                dM % de.ld_resid || dc_dtype != CG_BF16 || (((uintptr_t)de.colpart) & 3))
-                return false;
-            break;
-        default: return false;
-    }
-    if (launch)
-        pk_pair_launch(dM, dN, dK, dA, dlda, dB, dldb, dC, dc_dtype, dldc, de, wM, wN, wK, wA, wlda, wB, wldb, wC, wldc,
-                       we, split_k, ws, st);
-    return true;
-}
-
 bool fast_gemm_launch(int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda, const bf16_t* B,
                       int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k, float* ws,
                       hipStream_t st) {

@@ -270,16 +270,6 @@ bool glds_gemm_launch(int variant, int at, int bt, int64_t M, int64_t N, int64_t
 bool pk_gemm_launch(int variant, int at, int bt, int64_t M, int64_t N, int64_t K, const bf16_t* A, int64_t lda,
                     const bf16_t* B, int64_t ldb, void* C, int c_dtype, int64_t ldc, const EpiArgs& e, int split_k,
                     float* ws, hipStream_t st);
-// cg_gemm_pair: a dgrad (NT, split 1, STORE / RELU_BWD / STORE_ROWDOT) and a split-K weight gradient (TT,
-// slabs) in one k_gemm_pk_pair launch (gemm_pk.hip); pair_gemm_launch (gemm_bf16.hip) validates first
-void pk_pair_launch(int64_t dM, int64_t dN, int64_t dK, const bf16_t* dA, int64_t dlda, const bf16_t* dB, int64_t dldb,
-                    void* dC, int dc_dtype, int64_t dldc, const EpiArgs& de, int64_t wM, int64_t wN, int64_t wK,
-                    const bf16_t* wA, int64_t wlda, const bf16_t* wB, int64_t wldb, void* wC, int64_t wldc,
-                    const EpiArgs& we, int split_k, float* ws, hipStream_t st);
-bool pair_gemm_launch(int64_t dM, int64_t dN, int64_t dK, const bf16_t* dA, int64_t dlda, const bf16_t* dB,
-                      int64_t dldb, void* dC, int dc_dtype, int64_t dldc, const EpiArgs& de, int64_t wM, int64_t wN,
-                      int64_t wK, const bf16_t* wA, int64_t wlda, const bf16_t* wB, int64_t wldb, void* wC,
-                      int64_t wldc, const EpiArgs& we, int split_k, float* ws, hipStream_t st, bool launch);
 
 // persistent 8-wave LDS-DMA kernels (gemm_p8.hip), variant >= 20 (20 = automatic tile choice)
 // gemm_ln.hip: the residual GEMM + next LayerNorm kernel (N = 384 row panels)

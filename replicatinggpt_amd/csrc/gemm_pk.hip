@@ -441,15 +441,12 @@ constexpr int EK_ANY = -1, EK_SLAB = 6, EK_SLAB16 = 8;   // 7: CG_EPI_STORE_ROWD
 // amdgpu_waves_per_eu: LDS caps residency at OCC blocks, so tell the scheduler the real occupancy;
 // left at its default it schedules for 8+ waves/SIMD, keeps ONE A fragment register and waits
 // lgkmcnt(0) before every 4 MFMAs (LDS latency exposed 8x per K-tile)
-// The kernel body for one product, as a device function: k_gemm_pk runs one, k_gemm_pk_pair two in
-// sequence.  bb = this block's first item of the product (its items are bb, bb + P, bb + 2P, ... of the
-// product's nitems; k_gemm_pk: bb = blockIdx.x).
 template <bool AT, bool BT, int BM, int BN, int NBUF, int EK, int BK>
-__device__ __forceinline__ void pk_body(char* smem, int bb, int P, int64_t M, int64_t N, int64_t K,
-                                        const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
-                                        int64_t ldb, void* __restrict__ Cv, int c_dtype, int64_t ldc,
-                                        EpiArgs epi, int split_k, int64_t kchunk, float* __restrict__ ws,
-                                        int flags) {
+__global__ __launch_bounds__((GeoP<BM, BN, NBUF, BK>::THREADS), (GeoP<BM, BN, NBUF, BK>::OCC))
+__attribute__((amdgpu_waves_per_eu(1, GeoP<BM, BN, NBUF, BK>::WPE)))
+void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
+               const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype, int64_t ldc,
+               EpiArgs epi, int split_k, int64_t kchunk, float* __restrict__ ws, int flags, RedJobs red) {
     static_assert(BK == 64 || BK == 32, "BK");
     constexpr int NS = BK / 32;   // 32-deep MFMA slices per K-tile
     using G = GeoP<BM, BN, NBUF, BK>;
@@ -459,6 +456,7 @@ __device__ __forceinline__ void pk_body(char* smem, int bb, int P, int64_t M, in
     using DA = DmaP<AT, BM, G::WAVES, BK>;
     using DB = DmaP<BT, BN, G::WAVES, BK>;
     constexpr int LPT = DA::PER_WAVE + DB::PER_WAVE;  // DMA instructions per thread per K-tile
+    extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / G::WN, wn = wave % G::WN;
     const int tilesN = (int)(N / BN);
@@ -467,7 +465,7 @@ __device__ __forceinline__ void pk_body(char* smem, int bb, int P, int64_t M, in
     // split s covers K-tiles [s*nkc, min((s+1)*nkc, nkt)): the last split may be shorter (uneven
     // split-K: any split count, not only divisors of the K-tile count)
     const int nkt = (int)(K / BK), nkc = (int)(kchunk / BK);
-    const int b = bb;
+    const int P = gridDim.x, b = blockIdx.x;
     const int my_items = b < nitems ? (nitems - 1 - b) / P + 1 : 0;
     auto split_nk = [&](int sp) { return nkt - sp * nkc < nkc ? nkt - sp * nkc : nkc; };
     const uint64_t stream =
@@ -787,67 +785,11 @@ __device__ __forceinline__ void pk_body(char* smem, int bb, int P, int64_t M, in
     }
 #endif
     wait_vm<0>();  // the dummy DMAs past the last K-tile land before the workgroup's LDS is released
-}
-
-template <bool AT, bool BT, int BM, int BN, int NBUF, int EK, int BK>
-__global__ __launch_bounds__((GeoP<BM, BN, NBUF, BK>::THREADS), (GeoP<BM, BN, NBUF, BK>::OCC))
-__attribute__((amdgpu_waves_per_eu(1, GeoP<BM, BN, NBUF, BK>::WPE)))
-void k_gemm_pk(int64_t M, int64_t N, int64_t K, const bf16_t* __restrict__ A, int64_t lda,
-               const bf16_t* __restrict__ B, int64_t ldb, void* __restrict__ Cv, int c_dtype, int64_t ldc,
-               EpiArgs epi, int split_k, int64_t kchunk, float* __restrict__ ws, int flags, RedJobs red) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    pk_body<AT, BT, BM, BN, NBUF, EK, BK>(smem, blockIdx.x, gridDim.x, M, N, K, A, lda, B, ldb, Cv, c_dtype, ldc, epi,
-                                          split_k, kchunk, ws, flags);
     // a deferred split-K reduce of an earlier launch (gemm_common.h): on the blocks beyond the items
     // when the launch has them (launch_p), else in every block's tail
-    const int nitems = (int)(M / BM) * (int)(N / BN) * split_k, P = gridDim.x;
     if (red.n || red.na) red_tail(red, P > nitems ? nitems : 0);
 }
 
-
-// Two products in ONE persistent launch (cg_gemm_pair): a Linear's input gradient (dgrad, NT, fixed
-// epilogue kind EK1) and its split-K weight gradient (TT slabs, EK2) -- the backward's independent pair
-// that both read dY (GPT1.py:111-112,136,143,145 backward).  The items of the two products form one
-// sequence [dgrad items | weight-gradient items]; block b takes b, b + P, ... of it, so the blocks the
-// dgrad leaves idle (384 of its 128x128 tiles on 512 slots at C2) start on weight-gradient items at
-// once, and the pair pays one launch / prologue / drain instead of two.  Each block runs its dgrad
-// items, drains, then its weight-gradient items: per item the same arithmetic as k_gemm_pk (same
-// bits).  The dgrad item count is a multiple of 8 at every shape it takes (XCD-aligned remap).
-struct PkProb {
-    int64_t M, N, K;
-    const bf16_t* A;
-    int64_t lda;
-    const bf16_t* B;
-    int64_t ldb;
-    void* C;
-    int c_dtype;
-    int64_t ldc;
-    EpiArgs epi;
-    int split_k;
-    int64_t kchunk;
-    float* ws;
-    int flags;
-};
-
-template <int EK1, int EK2>
-__global__ __launch_bounds__((GeoP<128, 128, 2, FBK>::THREADS), (GeoP<128, 128, 2, FBK>::OCC))
-__attribute__((amdgpu_waves_per_eu(1, GeoP<128, 128, 2, FBK>::WPE)))
-void k_gemm_pk_pair(PkProb p1, PkProb p2, RedJobs red) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int P = gridDim.x, b = blockIdx.x;
-    const int n1 = (int)(p1.M / 128) * (int)(p1.N / 128) * p1.split_k;
-    pk_body<false, true, 128, 128, 2, EK1, FBK>(smem, b, P, p1.M, p1.N, p1.K, p1.A, p1.lda, p1.B, p1.ldb, p1.C,
-                                                p1.c_dtype, p1.ldc, p1.epi, p1.split_k, p1.kchunk, p1.ws, p1.flags);
-    // every wave's last fragment reads of the dgrad are done before the weight gradient's first
-    // LDS-DMA rewrites the stages
-    __syncthreads();
-    const int j2 = b >= n1 ? 0 : (n1 - b + P - 1) / P;   // this block's first item past the dgrad's
-    pk_body<true, true, 128, 128, 2, EK2, FBK>(smem, b + j2 * P - n1, P, p2.M, p2.N, p2.K, p2.A, p2.lda, p2.B, p2.ldb,
-                                               p2.C, p2.c_dtype, p2.ldc, p2.epi, p2.split_k, p2.kchunk, p2.ws,
-                                               p2.flags);
-    // deferred reduces / AdamW jobs of earlier launches: in every block's tail
-    if (red.n || red.na) red_tail(red, 0);
-}
 
 int cu_count() {
     static int n = 0;
@@ -1034,45 +976,6 @@ bool pk_gemm_launch(int v, int at, int bt, int64_t M, int64_t N, int64_t K, cons
 #endif
         default: return false;
     }
-}
-
-// cg_gemm_pair's launch (gemm_bf16.hip pair_gemm_launch validates both products first): d = the dgrad
-// (NT, split 1, epilogue kind ek1: STORE / RELU_BWD / STORE_ROWDOT), w = the weight gradient (TT,
-// split-K slabs).  Pending reduces / AdamW jobs of earlier launches run in every block's tail.
-void pk_pair_launch(int64_t dM, int64_t dN, int64_t dK, const bf16_t* dA, int64_t dlda, const bf16_t* dB, int64_t dldb,
-                    void* dC, int dc_dtype, int64_t dldc, const EpiArgs& de, int64_t wM, int64_t wN, int64_t wK,
-                    const bf16_t* wA, int64_t wlda, const bf16_t* wB, int64_t wldb, void* wC, int64_t wldc,
-                    const EpiArgs& we, int split_k, float* ws, hipStream_t st) {
-    using G = GeoP<128, 128, 2>;
-    const int64_t kchunk = (wK / FBK + split_k - 1) / split_k * FBK;
-    const int64_t tM = wM / 128, tN = wN / 128;
-    const int gm = g_gemm_group_pk > 0 ? g_gemm_group_pk : (tN > tM ? (int)tM : 0);
-    const PkProb p1 = {dM, dN, dK, dA, dlda, dB, dldb, dC, dc_dtype, dldc, de, 1, dK, nullptr, g_pk_flags};
-    const PkProb p2 = {wM, wN, wK, wA, wlda, wB, wldb, wC, CG_F32, wldc, we, split_k, kchunk, ws,
-                       g_pk_flags | (gm << 8)};
-    const int64_t items = (dM / 128) * (dN / 128) + tM * tN * split_k;
-    int64_t slots = (int64_t)cu_count() * G::OCC;
-    if (g_gemm_max_grid > 0 && g_gemm_max_grid < slots) slots = g_gemm_max_grid;
-    const unsigned grid = (unsigned)(items < slots ? items : slots);
-    // pending reduces, and AdamW jobs (cg_adamw_defer): in every block's tail after its items
-    const RedJobs red = take_pending_reduces(st, true);
-#define PAIR(E1, E2) k_gemm_pk_pair<E1, E2><<<grid, G::THREADS, G::LDS, st>>>(p1, p2, red)
-    const bool s16 = we.slab_bf16;
-    switch (de.kind) {
-        case CG_EPI_RELU_BWD:
-            if (s16) PAIR(CG_EPI_RELU_BWD, EK_SLAB16);
-            else PAIR(CG_EPI_RELU_BWD, EK_SLAB);
-            break;
-        case CG_EPI_STORE_ROWDOT:
-            if (s16) PAIR(CG_EPI_STORE_ROWDOT, EK_SLAB16);
-            else PAIR(CG_EPI_STORE_ROWDOT, EK_SLAB);
-            break;
-        default:
-            if (s16) PAIR(CG_EPI_STORE, EK_SLAB16);
-            else PAIR(CG_EPI_STORE, EK_SLAB);
-            break;
-    }
-#undef PAIR
 }
 
 }  // namespace cg

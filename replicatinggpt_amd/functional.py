@@ -24,7 +24,7 @@ from . import _lib as L
 from . import ops
 
 EPI = {"store": L.EPI_STORE, "bias": L.EPI_BIAS, "bias_relu": L.EPI_BIAS_RELU, "bias_resid": L.EPI_BIAS_RESID,
-       "bias_drop_resid": L.EPI_BIAS_DROP_RESID, "relu_bwd": L.EPI_RELU_BWD, "store_rowdot": L.EPI_STORE_ROWDOT}
+       "bias_drop_resid": L.EPI_BIAS_DROP_RESID, "relu_bwd": L.EPI_RELU_BWD}
 
 
 class SideStream:
@@ -149,7 +149,6 @@ class DeferredReduces:
         if self.active:
             try:
                 if exc_type is None:
-                    EARLY.release_held()   # (defined below; its updates join this flush)
                     self.flush()
                 else:
                     self.aborted_adam = self.discard()
@@ -181,7 +180,6 @@ class EarlyAdam:
     def __init__(self):
         self.enabled = os.environ.get("CHARPT_EARLY_ADAM", "1") != "0"
         self.opt = None
-        self._later = []
 
     def begin(self, opt):
         self.opt = None
@@ -198,28 +196,8 @@ class EarlyAdam:
         if self.opt is not None and g is not None and beta == 0.0 and g is region.slot:
             self.opt.early_region(region)
 
-    def region_done_after_next_gemm(self, region, g, beta):
-        """As region_done, for a weight gradient whose split-K reduce is still pending after its
-        cg_gemm_pair launch: the next persistent GEMM launch on the stream takes that reduce (in its
-        tail), so the update is queued only after it (gemm_launched) -- queued now, cg_adamw_defer
-        would launch the reduce on its own."""
-        if self.opt is not None and g is not None and beta == 0.0 and g is region.slot:
-            self._later.append(region)
-
-    def gemm_launched(self):
-        """A persistent GEMM launch just took the pending reduces: the regions held back before it are final."""
-        held, self._later = self._later, []
-        for r in held:
-            self.opt.early_region(r)
-
-    def release_held(self):
-        """End of the backward: whatever is still held back (its reduce goes out with the update)."""
-        if self.opt is not None and self._later:
-            self.gemm_launched()
-
     def end(self):
         self.opt = None
-        self._later = []
 
 
 EARLY = EarlyAdam()
@@ -458,43 +436,6 @@ def linear_wgrad(dy2, x2, out, beta, into_slot=False):
     ops.gemm(dy2, x2, out, _is_bf16(dy2.dtype), True, True, N, K, M, N, K, out.stride(0), L.EPI_STORE, None,
              None, 0, None, 0, 0.0, 0, None, 0, float(beta), split, ws, flags)
     return out
-
-
-# A Linear's backward pair -- its input gradient and its weight gradient, independent products that
-# both read dY -- as ONE persistent launch (cg_gemm_pair: the dgrad's idle slots start on
-# weight-gradient items; one launch / prologue / drain instead of two).  CHARPT_PAIR=0: two launches.
-PAIR = os.environ.get("CHARPT_PAIR", "1") != "0"
-def linear_pair(dy2, w, dout, epi, x2, gout, beta, into_slot, aux=None, colpart=None, T=0):
-    """dout = epi(dy2[M,N] @ w[N,K]) and gout[N,K] (+)= dy2^T @ x2[M,K] as one cg_gemm_pair launch --
-    inside the training backward (DEFER active) when gout is a flat gradient slot; the weight
-    gradient's split-K reduce stays pending for the next persistent GEMM launch.  epi: "store",
-    "relu_bwd" (aux = ReLU output or keep bits, colpart = b1 partials) or "store_rowdot" (aux = O,
-    T, colpart = delta).  Returns False, launching nothing, where the pair does not apply (the caller
-    runs linear_wgrad and the dgrad)."""
-    if not (PAIR and DEFER.active and into_slot and not SIDE.enabled and _is_bf16(dy2.dtype)
-            and "skip_wgrad" not in WHATIF):
-        return False
-    M, N = dy2.shape
-    K, Kd = x2.shape[1], w.shape[1]
-    if M % 64 or N % 128 or K % 128 or Kd % 128 or M % 128:
-        return False
-    # the split linear_wgrad would take, so the pair gives the two launches' bits (a split balanced for
-    # the pair's concatenated items would save ~2 us more on the C2 FFN1 pair, tools/pair_ab.py)
-    split = _wgrad_split(N, K, M, True)
-    if split < 2:
-        return False
-    ws = torch.empty(ops.gemm_workspace(N, K, split) // 4, dtype=torch.float32, device=dy2.device)
-    flags = (L.GEMM_SLAB_BF16 if SLAB_BF16 else 0) | L.GEMM_DEFER_REDUCE
-    kind = EPI[epi]
-    ld_aux = aux.stride(0) if aux is not None else 0
-    if not ops.gemm_pair_supported(dy2, w, dout, kind, aux, ld_aux, colpart, T, x2, gout, float(beta), split, ws,
-                                   flags):
-        return False
-    DEFER.keep.extend((ws, dy2, x2))   # the reduce runs after this call returns
-    DEFER.note_stream()
-    ops.gemm_pair(dy2, w, dout, kind, aux, ld_aux, colpart, T, x2, gout, float(beta), split, ws, flags)
-    EARLY.gemm_launched()   # this launch took the reduces pending before it
-    return True
 
 
 def _colpart_ok(dy2, w, aux, out_ld):
@@ -804,45 +745,32 @@ class AttnSublayerFn(torch.autograd.Function):
         # proj: dW = dy^T o, db = colsum(dy) (side stream, unless fused upstream), do = dy W
         g_pw, beta_pw, f_pw = proj_w.grad_target()
         g_pb, beta_pb, f_pb = proj_b.grad_target()
-        do = torch.empty((B * T, C), dtype=act, device=x2.device)
-        wp = proj_w.operand(act)
-        delta = None
-        rowdot = rowdot_ok(dy, wp, o, T, lc.head_size)
-        if rowdot:
-            # dO and the attention backward's delta = rowsum(dO * O) from one epilogue (the attention
-            # kernel then loads neither O nor computes the row dots)
-            delta = torch.empty((B, lc.n_head, T), dtype=torch.float32, device=dev)
-        # dO and the projection's weight gradient as one launch where cg_gemm_pair takes them
-        paired = g_pw is not None and linear_pair(dy, wp, do, "store_rowdot" if rowdot else "store", o, g_pw, beta_pw,
-                                                  g_pw is proj_w.slot, aux=o if rowdot else None, colpart=delta,
-                                                  T=T if rowdot else 0)
         with SIDE.run(dev, dy, o):
-            if g_pw is not None and not paired:
+            if g_pw is not None:
                 linear_wgrad(dy, o, g_pw, beta_pw, g_pw is proj_w.slot)
             if g_pb is not None and not bias_done:
                 colsum_into(dy, g_pb, beta_pb)
-        if paired:
-            EARLY.region_done_after_next_gemm(proj_w, g_pw, beta_pw)
+        do = torch.empty((B * T, C), dtype=act, device=x2.device)
+        wp = proj_w.operand(act)
+        delta = None
+        if rowdot_ok(dy, wp, o, T, lc.head_size):
+            # dO and the attention backward's delta = rowsum(dO * O) from one epilogue (the attention
+            # kernel then loads neither O nor computes the row dots)
+            delta = torch.empty((B, lc.n_head, T), dtype=torch.float32, device=dev)
+            ops.gemm_store_rowdot(dy, wp, do, B * T, C, C, dy.stride(0), wp.stride(0), do.stride(0), o, o.stride(0),
+                                  T, delta)
         else:
-            if rowdot:
-                ops.gemm_store_rowdot(dy, wp, do, B * T, C, C, dy.stride(0), wp.stride(0), do.stride(0), o,
-                                      o.stride(0), T, delta)
-            else:
-                linear_dgrad(dy, wp, do)
-            EARLY.region_done(proj_w, g_pw, beta_pw)   # the projection weight's last read this step
+            linear_dgrad(dy, wp, do)
+        EARLY.region_done(proj_w, g_pw, beta_pw)   # the projection weight's last read this step
         dqkv = attention_bwd(qkv, B, T, lc.n_head, lc.head_size, o, do, lse, lc.scale, lc.p, lc.seed, lc.rng_call,
                              lc.site, ctx.mask, delta)
         g, beta, f_qkv = qkv_w.grad_target()
+        if g is not None:
+            with SIDE.run(dev, dqkv, a):
+                linear_wgrad(dqkv, a, g, beta, g is qkv_w.slot)
         da = torch.empty((B * T, C), dtype=act, device=x2.device)
-        paired = g is not None and linear_pair(dqkv, qkv_w.operand(act), da, "store", a, g, beta, g is qkv_w.slot)
-        if paired:
-            EARLY.region_done_after_next_gemm(qkv_w, g, beta)
-        else:
-            if g is not None:
-                with SIDE.run(dev, dqkv, a):
-                    linear_wgrad(dqkv, a, g, beta, g is qkv_w.slot)
-            linear_dgrad(dqkv, qkv_w.operand(act), da)
-            EARLY.region_done(qkv_w, g, beta)
+        linear_dgrad(dqkv, qkv_w.operand(act), da)
+        EARLY.region_done(qkv_w, g, beta)
         dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd, dres=d32, link=ctx.in_link)
         return (dx.view(B, T, C), None, None, None, None, None, None, *f_ln, *f_qkv(), *f_pw(), *f_pb())
 
@@ -896,41 +824,29 @@ class FFNSublayerFn(torch.autograd.Function):
         dev = x2.device
         g_w2, beta_w2, f_w2 = w2.grad_target()
         g_b2, beta_b2, f_b2 = b2.grad_target()
+        with SIDE.run(dev, dz2, h):
+            if g_w2 is not None:
+                linear_wgrad(dz2, h, g_w2, beta_w2, g_w2 is w2.slot)
+            if g_b2 is not None and not bias_done:
+                colsum_into(dz2, g_b2, beta_b2)
         dz1 = torch.empty_like(h)
         g_w1, beta_w1, f_w1 = w1.grad_target()
         g_b1, beta_b1, f_b1 = b1.grad_target()
         part = None
-        wt = w2.operand(act)
-        mk = h if bits is None else bits
-        colp = g_b1 is not None and _colpart_ok(dz2, wt, h, dz1.stride(0))
-        if colp:
+        if g_b1 is not None and _colpart_ok(dz2, w2.operand(act), h, dz1.stride(0)):
             # b1's gradient (column sums of dz1) fused into the ReLU-backward dgrad's epilogue as
             # per-64-row partials; only their fold runs on the side stream
             M, F4 = h.shape
             part = torch.empty((M // 64, F4), dtype=torch.float32, device=dev)
-        # dz1 and W2's weight gradient as one launch where cg_gemm_pair takes them
-        paired2 = g_w2 is not None and linear_pair(dz2, wt, dz1, "relu_bwd", h, g_w2, beta_w2, g_w2 is w2.slot,
-                                                   aux=mk, colpart=part)
-        with SIDE.run(dev, dz2, h):
-            if g_w2 is not None and not paired2:
-                linear_wgrad(dz2, h, g_w2, beta_w2, g_w2 is w2.slot)
-            if g_b2 is not None and not bias_done:
-                colsum_into(dz2, g_b2, beta_b2)
-        if paired2:
-            EARLY.region_done_after_next_gemm(w2, g_w2, beta_w2)
+            wt = w2.operand(act)
+            mk = h if bits is None else bits
+            ops.gemm_relu_bwd_colpart(dz2, wt, dz1, M, F4, dz2.shape[1], dz2.stride(0), wt.stride(0), dz1.stride(0),
+                                      mk, mk.stride(0), part)
         else:
-            if colp:
-                M, F4 = h.shape
-                ops.gemm_relu_bwd_colpart(dz2, wt, dz1, M, F4, dz2.shape[1], dz2.stride(0), wt.stride(0),
-                                          dz1.stride(0), mk, mk.stride(0), part)
-            else:
-                linear_dgrad(dz2, wt, dz1, "relu_bwd", aux=mk)
-            EARLY.region_done(w2, g_w2, beta_w2)   # W2's gradient is final (its reduce went with this dgrad)
-        da = torch.empty((B * T, C), dtype=act, device=x2.device)
-        paired1 = g_w1 is not None and linear_pair(dz1, w1.operand(act), da, "store", a, g_w1, beta_w1,
-                                                   g_w1 is w1.slot)
+            linear_dgrad(dz2, w2.operand(act), dz1, "relu_bwd", aux=h if bits is None else bits)
+        EARLY.region_done(w2, g_w2, beta_w2)   # W2's gradient is final (its reduce went with this dgrad)
         with SIDE.run(dev, dz1, a, part):
-            if g_w1 is not None and not paired1:
+            if g_w1 is not None:
                 linear_wgrad(dz1, a, g_w1, beta_w1, g_w1 is w1.slot)
             if g_b1 is not None:
                 if part is not None:
@@ -938,11 +854,9 @@ class FFNSublayerFn(torch.autograd.Function):
                         ops.reduce_rows(part, part.shape[0], part.shape[1], g_b1, bool(beta_b1), queued)
                 else:
                     colsum_into(dz1, g_b1, beta_b1)
-        if paired1:
-            EARLY.region_done_after_next_gemm(w1, g_w1, beta_w1)
-        else:
-            linear_dgrad(dz1, w1.operand(act), da)
-            EARLY.region_done(w1, g_w1, beta_w1)
+        da = torch.empty((B * T, C), dtype=act, device=x2.device)
+        linear_dgrad(dz1, w1.operand(act), da)
+        EARLY.region_done(w1, g_w1, beta_w1)
         dx, _, f_ln = layernorm_bwd(da, x2, ln_w, ln_b, mean, rstd, dres=d32, link=ctx.in_link)
         return (dx.view(B, T, C), None, None, None, None, None, None, None, *f_ln, *f_w1(), *f_b1(), *f_w2(),
                 *f_b2())

@@ -6,7 +6,6 @@ current stream (so whole training steps are capturable into a hipGraph).  Ops ar
 the "cuda" (= HIP on ROCm) device only: calling them on CPU tensors raises -- the product has no
 CPU fallback.
 """
-import ctypes
 from typing import List, Optional
 
 import torch
@@ -240,41 +239,6 @@ def gemm_resid_layernorm(a: Tensor, w: Tensor, out: Tensor, M: int, N: int, K: i
     L.check(L.load().cg_gemm_resid_layernorm(M, N, K, L.ptr(a), lda, L.ptr(w), ldw, L.ptr(out), ldc, e, L.ptr(ln_w),
                                              L.ptr(ln_b), L.ptr(y), L.ptr(mean), L.ptr(rstd), eps, _s(out)),
             "gemm_resid_layernorm")
-
-
-def _pair_descs(dy, w, dout, epi, aux, ld_aux, colpart, T, x, gout, beta, split_k, ws, wflags):
-    """cg_gemm_desc_t pair of a Linear's backward: dout[M,K] = epi(dy[M,N] @ w[N,K]) and
-    gout[N,K] (+)= dy^T x[M,K] (split-K, fp32 slabs or bf16 with wflags)."""
-    M, N = dy.shape
-    K = w.shape[1]
-    de = L.Epilogue(epi, None, None, T, L.ptr(aux), L.dtype_code(aux.dtype) if aux is not None else 0, ld_aux, 0.0, 0,
-                    None, 0, 0.0, L.ptr(colpart), 0)
-    we = L.Epilogue(L.EPI_STORE, None, None, 0, None, 0, 0, 0.0, 0, None, 0, beta, None, wflags)
-    d = L.GemmDesc(0, 1, M, K, N, L.ptr(dy), dy.stride(0), L.ptr(w), w.stride(0), L.ptr(dout),
-                   L.dtype_code(dout.dtype), dout.stride(0), ctypes.pointer(de), 1, None)
-    g = L.GemmDesc(1, 1, N, x.shape[1], M, L.ptr(dy), dy.stride(0), L.ptr(x), x.stride(0), L.ptr(gout),
-                   L.dtype_code(gout.dtype), gout.stride(0), ctypes.pointer(we), split_k, L.ptr(ws))
-    return d, g, (de, we)
-
-
-@_op("gemm_pair", ("dout", "colpart", "gout", "ws"))
-def gemm_pair(dy: Tensor, w: Tensor, dout: Tensor, epi: int, aux: Optional[Tensor], ld_aux: int,
-              colpart: Optional[Tensor], T: int, x: Tensor, gout: Tensor, beta: float, split_k: int, ws: Tensor,
-              wflags: int) -> None:
-    """A Linear's backward pair in one persistent launch (cg_gemm_pair; else the two cg_gemm calls, same
-    results): dout = epi(dy @ w) -- epi CG_EPI_STORE, CG_EPI_RELU_BWD (aux: ReLU output or keep bits,
-    colpart: b1-gradient partials) or CG_EPI_STORE_ROWDOT (aux = O, T, colpart = delta) -- and
-    gout (+)= dy^T x through split_k slabs in ws (wflags: L.GEMM_SLAB_BF16 | L.GEMM_DEFER_REDUCE)."""
-    M, N = dy.shape
-    _gemm_extents(dy, w, dout, False, True, M, w.shape[1], N, dy.stride(0), w.stride(0), dout.stride(0), "gemm_pair")
-    _gemm_extents(dy, x, gout, True, True, N, x.shape[1], M, dy.stride(0), x.stride(0), gout.stride(0), "gemm_pair")
-    d, g, keep = _pair_descs(dy, w, dout, epi, aux, ld_aux, colpart, T, x, gout, beta, split_k, ws, wflags)
-    L.check(L.load().cg_gemm_pair(ctypes.byref(d), ctypes.byref(g), _s(dout)), "gemm_pair")
-
-
-def gemm_pair_supported(dy, w, dout, epi, aux, ld_aux, colpart, T, x, gout, beta, split_k, ws, wflags):
-    d, g, keep = _pair_descs(dy, w, dout, epi, aux, ld_aux, colpart, T, x, gout, beta, split_k, ws, wflags)
-    return bool(L.load().cg_gemm_pair_supported(ctypes.byref(d), ctypes.byref(g)))
 
 
 def gemm_resid_layernorm_supported(M, N, K):

@@ -262,9 +262,7 @@ def test_failed_backward_with_early_adamw(fail_at):
         return [t.detach().clone() for t in (m.flat.master, opt._m, opt._v, opt._step_t, m.flat.shadow)]
 
     before = snap()
-    # the backward's weight-gradient launches: linear_wgrad, or linear_pair (a Linear's dgrad + weight
-    # gradient as one cg_gemm_pair launch) -- the fail_at-th of them raises
-    real, real_pair, calls = Fn.linear_wgrad, Fn.linear_pair, [0]
+    real, calls = Fn.linear_wgrad, [0]
 
     def failing(*a, **k):
         calls[0] += 1
@@ -272,21 +270,12 @@ def test_failed_backward_with_early_adamw(fail_at):
             raise RuntimeError("injected")
         return real(*a, **k)
 
-    def failing_pair(*a, **k):
-        calls[0] += 1
-        if calls[0] == fail_at:
-            raise RuntimeError("injected")
-        if real_pair(*a, **k):
-            return True
-        calls[0] -= 1   # not paired: the linear_wgrad that follows counts
-        return False
-
-    Fn.linear_wgrad, Fn.linear_pair = failing, failing_pair
+    Fn.linear_wgrad = failing
     try:
         with pytest.raises(RuntimeError, match="injected"):
             st._eager()
     finally:
-        Fn.linear_wgrad, Fn.linear_pair = real, real_pair
+        Fn.linear_wgrad = real
     after = snap()
     same = all(torch.equal(a, b) for a, b in zip(before, after))
     if fail_at == 1:
@@ -390,84 +379,3 @@ def test_deferred_work_on_a_non_current_device():
         res.append((losses, m.flat.master.detach().cpu()))
     assert res[0][0] == res[1][0]
     assert torch.equal(res[0][1], res[1][1])
-
-
-def test_gemm_pair_step_bit_identical():
-    """cg_gemm_pair (functional.linear_pair): each Linear's backward dgrad + weight gradient as one
-    persistent launch, the weight gradient's reduce left for the next launch and its early AdamW
-    released after that launch -- losses, weights, moments, step count and shadow bit for bit the
-    two-launch step (CHARPT_PAIR=0), graph replay and eager (C2 width, two layers, dropout 0.2)."""
-    from replicatinggpt_amd import functional as Fn
-    from replicatinggpt_amd.engine import TrainStep
-    cfg = _cfg(block_size=256, n_embd=384, n_head=6, n_layers=2, batch_size=64)
-    runs = []
-    saved = Fn.PAIR
-    try:
-        for pair, graph in ((False, True), (True, True), (True, False)):
-            Fn.PAIR = pair
-            m, opt, s = _setup(cfg)
-            st = TrainStep(m, opt, s, use_graph=graph)
-            st.capture(restore=True)
-            losses = [float(st.step().detach()) for _ in range(3)]
-            torch.cuda.synchronize()
-            runs.append((losses, m.flat.master.detach().cpu().clone(), opt._m.cpu().clone(), opt._v.cpu().clone(),
-                         int(opt._step_t.item()), m.flat.shadow.view(torch.int16).cpu().clone()))
-    finally:
-        Fn.PAIR = saved
-    for r in runs[1:]:
-        assert r[0] == runs[0][0]
-        for a, b in zip(r[1:], runs[0][1:]):
-            if isinstance(a, torch.Tensor):
-                assert torch.equal(a, b)
-            else:
-                assert a == b
-
-
-def test_gemm_pair_ops_match_two_calls():
-    """cg_gemm_pair against cg_gemm(dgrad) + cg_gemm(weight gradient) with the same split, at the C2
-    backward shapes and their epilogues (projection dO with the attention delta, FFN2 ReLU-backward from
-    keep bits with the b1 partials, plain dgrads; bf16 slabs, with and without a deferred reduce):
-    dO / dz1 / da, the partials and the weight gradient bit for bit.  The pair must take every case."""
-    from replicatinggpt_amd import _lib as L, ops
-    dev = torch.device("cuda:0")
-    M = 16384
-    for name, N, K, epi, split in (("proj", 384, 384, L.EPI_STORE_ROWDOT, 32), ("qkv", 1152, 384, L.EPI_STORE, 18),
-                                   ("ffn2", 384, 1536, L.EPI_RELU_BWD, 14), ("ffn1", 1536, 384, L.EPI_STORE, 14)):
-        g = torch.Generator(device=dev).manual_seed(5)
-        dy = torch.randn(M, N, device=dev, generator=g).to(torch.bfloat16)
-        w = (torch.randn(N, K, device=dev, generator=g) * N ** -0.5).to(torch.bfloat16)
-        x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
-        aux, ld_aux, colpart, T = None, 0, None, 0
-        if epi == L.EPI_RELU_BWD:
-            aux = torch.randint(-2 ** 31, 2 ** 31 - 1, (M, K // 32), dtype=torch.int32, device=dev)
-            ld_aux, colpart = aux.stride(0), torch.empty(M // 64, K, device=dev)
-        elif epi == L.EPI_STORE_ROWDOT:
-            aux = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
-            ld_aux, T, colpart = K, 256, torch.empty(M * K // 64, device=dev)
-        for defer in (False, True):
-            wflags = L.GEMM_SLAB_BF16 | (L.GEMM_DEFER_REDUCE if defer else 0)
-            outs = []
-            for pair in (False, True):
-                dout = torch.full((M, K), float("nan"), dtype=torch.bfloat16, device=dev)
-                gout = torch.full((N, K), float("nan"), device=dev)
-                cp = None if colpart is None else torch.full_like(colpart, float("nan"))
-                ws = torch.empty(ops.gemm_workspace(N, K, split) // 4, dtype=torch.float32, device=dev)
-                if pair:
-                    assert ops.gemm_pair_supported(dy, w, dout, epi, aux, ld_aux, cp, T, x, gout, 0.0, split, ws,
-                                                   wflags), name
-                    ops.gemm_pair(dy, w, dout, epi, aux, ld_aux, cp, T, x, gout, 0.0, split, ws, wflags)
-                else:
-                    e = L.Epilogue(epi, None, None, T, L.ptr(aux), L.dtype_code(aux.dtype) if aux is not None else 0,
-                                   ld_aux, 0.0, 0, None, 0, 0.0, L.ptr(cp), 0)
-                    L.check(L.load().cg_gemm(L.CG_BF16, 0, 1, M, K, N, L.ptr(dy), N, L.ptr(w), K, L.ptr(dout),
-                                             L.CG_BF16, K, e, 1, None, L.stream_ptr()), "dgrad")
-                    ops.gemm(dy, x, gout, True, True, True, N, K, M, N, K, K, 0, None, None, 0, None, 0, 0.0, 0, None,
-                             0, 0.0, split, ws, wflags)
-                if defer:
-                    L.check(L.load().cg_flush_deferred(L.stream_ptr()), "flush")
-                torch.cuda.synchronize()
-                outs.append((dout, gout, cp))
-            for a, b in zip(*outs):
-                if a is not None:
-                    assert not torch.isnan(a.float()).any(), name
-                    assert torch.equal(a, b), (name, defer)
