@@ -412,6 +412,155 @@ __global__ __launch_bounds__(256, 1) void k_gemm_f32r(int64_t M, int64_t N, int6
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Persistent fp32 forward (NT) GEMM for many rows (M > 2048: generate()'s sliding-window products,
+// M = 65536, N = 126-504, K = 126 / 504).  k_gemm_f32's 128 x 64 grid runs 2.4-3.2 rounds of
+// 5 blocks per CU there (1024-4096 blocks), each block's 8-16 K-steps behind two barriers and its
+// own prologue load, at ~55 % of the f32 MFMA rate (profiles/r5_gemm_f32_pmc.txt).  Here 2 blocks
+// per CU own equal contiguous runs of 128 x 128 tiles (row-band-major: a run's tiles share the A row
+// panel, read once into the XCD's L2), K in 32-deep steps through a 2-stage [k][row] LDS ring with
+// one barrier per step, the next K-tile (or the next tile's first one) loaded to registers as float2
+// along K during the current step's MFMAs, so the ring never drains at a tile seam.  4 waves of
+// 64 x 64 = 2 x 2 v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulation, 4 independent
+// chains per wave).  An f32 MFMA accumulates as a k-ordered fma chain (cdna guide §3 'FP32-input
+// MFMA'), so the 32x32x2 chain over k = 0..kpad-1 (kpad = K rounded up to 16, zero padding, the
+// 32-deep step's second half skipped past kpad) is k_gemm_f32's 16x16x4 chain, and the epilogue is
+// its beta-0 arithmetic: bitwise k_gemm_f32 (test_gemm_f32_persistent_matches_128x64_bitwise).
+// Needs K even, lda / ldb even and 8-B aligned A / B (float2 loads).
+typedef float fv16f __attribute__((ext_vector_type(16)));
+constexpr int PBM = 128, PBN = 128, PBK = 32, PLD = PBM + 4;   // LDS row stride over k (floats)
+
+template <int EK>
+__global__ __launch_bounds__(256, 2) void k_gemm_f32p(int64_t M, int64_t N, int64_t K, const float* __restrict__ A,
+                                                      int64_t lda, const float* __restrict__ B, int64_t ldb,
+                                                      float* __restrict__ C, int64_t ldc, EpiArgs epi) {
+    __shared__ __attribute__((aligned(16))) float sm[2][2][PBK * PLD];   // [stage][A | B][k][row]: 66 KB
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
+    const int wm = w >> 1, wn = w & 1;
+    const int64_t tilesN = (N + PBN - 1) / PBN, ntiles = (M + PBM - 1) / PBM * tilesN;
+    const int64_t kpad = (K + 15) / 16 * 16;
+    const int nks = (int)((kpad + PBK - 1) / PBK);
+    const int64_t G = gridDim.x, bid = blockIdx.x;
+    const int64_t t_begin = bid * ntiles / G, t_end = (bid + 1) * ntiles / G;
+    // loads: rows lr + 16 i (i = 0..7) of the A and B tiles, k pair lc (a wave: 4 rows x 128 B)
+    const int lr = tid >> 4, lc = tid & 15;
+    float2 ra[8], rb[8];
+    auto load = [&](int64_t t, int ks) {
+        const int64_t m0 = t / tilesN * PBM, n0 = t % tilesN * PBN;
+        const int64_t k = (int64_t)ks * PBK + 2 * lc;
+        const bool kin = k < K;   // K even: k + 1 < K as well
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int64_t ma = m0 + lr + 16 * i, nb = n0 + lr + 16 * i;
+            ra[i] = (kin && ma < M) ? *(const float2*)(A + ma * lda + k) : make_float2(0.f, 0.f);
+            rb[i] = (kin && nb < N) ? *(const float2*)(B + nb * ldb + k) : make_float2(0.f, 0.f);
+        }
+    };
+    auto store = [&](int st) {
+        float* As = sm[st][0];
+        float* Bs = sm[st][1];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int r = lr + 16 * i;
+            As[2 * lc * PLD + r] = ra[i].x;
+            As[(2 * lc + 1) * PLD + r] = ra[i].y;
+            Bs[2 * lc * PLD + r] = rb[i].x;
+            Bs[(2 * lc + 1) * PLD + r] = rb[i].y;
+        }
+    };
+    constexpr bool BIAS = EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_BIAS_RESID;
+    const bool hb = BIAS && epi.bias, hr = EK == CG_EPI_BIAS_RESID && epi.resid;
+    int stc = 0;
+    if (t_begin < t_end) load(t_begin, 0);
+#pragma unroll 1
+    for (int64_t t = t_begin; t < t_end; ++t) {
+        fv16f acc[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = fv16f{};
+#pragma unroll 1
+        for (int ks = 0; ks < nks; ++ks) {
+            const int st = stc & 1;
+            ++stc;
+            store(st);   // stage st was last read two steps ago, before the previous step's barrier
+            __syncthreads();
+            if (ks + 1 < nks) load(t, ks + 1);
+            else if (t + 1 < t_end) load(t + 1, 0);
+            const float* As = sm[st][0] + h * PLD + 64 * wm + l32;
+            const float* Bs = sm[st][1] + h * PLD + 64 * wn + l32;
+            auto k2 = [&](int s) {
+                const float a0 = As[2 * s * PLD], a1 = As[2 * s * PLD + 32];
+                const float b0 = Bs[2 * s * PLD], b1 = Bs[2 * s * PLD + 32];
+                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+            };
+#pragma unroll
+            for (int s = 0; s < 8; ++s) k2(s);
+            if (kpad - (int64_t)ks * PBK > 16) {   // wave-uniform: the step's second 16 k are inside kpad
+#pragma unroll
+                for (int s = 8; s < 16; ++s) k2(s);
+            }
+        }
+        // epilogue (k_gemm_f32's beta-0 arithmetic): bias, ReLU, resid + v; every operand loaded
+        // before the first store.  Lane column n = l32; register r holds row (r & 3) + 8 (r >> 2) + 4 h.
+        const int64_t m0 = t / tilesN * PBM + 64 * wm, n0 = t % tilesN * PBN + 64 * wn;
+        float bv[2] = {0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int64_t n = n0 + 32 * j + l32;
+            if (hb && n < N) bv[j] = epi.bias[n];
+        }
+        float rv[2][2][16];
+        if (hr) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int64_t m = m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, n = n0 + 32 * j + l32;
+                        rv[i][j][r] = (m < M && n < N) ? epi.resid[m * epi.ld_resid + n] : 0.f;
+                    }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t m = m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, n = n0 + 32 * j + l32;
+                    float v = acc[i][j][r];
+                    if (hb) v += bv[j];
+                    if (EK == CG_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
+                    if (hr) v = rv[i][j][r] + v;
+                    if (m < M && n < N) C[m * ldc + n] = v;
+                }
+    }
+}
+
+bool launch_f32p(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
+                 int64_t ldc, const EpiArgs& e, hipStream_t st) {
+    // 96 forces this kernel at any M (tests); 98 / 97 leave the fp32 products to k_gemm_f32 / the small-M kernels
+    if (g_gemm_variant == 98 || g_gemm_variant == 97 || e.beta != 0.f || (M <= 2048 && g_gemm_variant != 96) ||
+        M <= 0 || N <= 0 || K <= 0 || K % 2 || lda % 2 || ldb % 2 || (((uintptr_t)A | (uintptr_t)B) & 7))
+        return false;
+    if (e.kind != CG_EPI_STORE && e.kind != CG_EPI_BIAS && e.kind != CG_EPI_BIAS_RELU && e.kind != CG_EPI_BIAS_RESID)
+        return false;
+    const int64_t ntiles = (M + PBM - 1) / PBM * ((N + PBN - 1) / PBN);
+    const int64_t slots = 2 * (int64_t)gemm_cu_count();
+    const unsigned grid = (unsigned)(ntiles < slots ? ntiles : slots);
+#define KP(EK_) k_gemm_f32p<EK_><<<grid, 256, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e)
+    switch (e.kind) {
+        case CG_EPI_STORE: KP(CG_EPI_STORE); break;
+        case CG_EPI_BIAS: KP(CG_EPI_BIAS); break;
+        case CG_EPI_BIAS_RELU: KP(CG_EPI_BIAS_RELU); break;
+        default: KP(CG_EPI_BIAS_RESID); break;
+    }
+#undef KP
+    return true;
+}
+
 // the small-M kernel's conditions (else k_gemm_f32); gemm_variant 98 forces k_gemm_f32,
 // 97 k_gemm_f32s (A/B, tests)
 bool launch_f32s(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
@@ -457,7 +606,9 @@ bool launch_f32s(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, c
 void launch_f32(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                 const float* B, int64_t ldb, float* C, int64_t ldc, const EpiArgs& e, int split_k, float* ws,
                 hipStream_t st) {
-    if (!a_trans && !b_trans && split_k == 1 && launch_f32s(M, N, K, A, lda, B, ldb, C, ldc, e, st)) return;
+    if (!a_trans && !b_trans && split_k == 1 &&
+        (launch_f32p(M, N, K, A, lda, B, ldb, C, ldc, e, st) || launch_f32s(M, N, K, A, lda, B, ldb, C, ldc, e, st)))
+        return;
     int64_t kchunk = (K + split_k - 1) / split_k;
     kchunk = (kchunk + FBKK - 1) / FBKK * FBKK;
     dim3 grid((unsigned)(((M + FBM - 1) / FBM) * ((N + FBN - 1) / FBN)), (unsigned)split_k);
@@ -828,13 +979,14 @@ extern "C" int cg_set_tuning(const char* key, int value) {
     CG_REQUIRE(key, "cg_set_tuning: null key");
     if (!strcmp(key, "gemm_variant")) {
         // default build: automatic (0), the register-staged fallback (2), the persistent 128x128 (9)
-        // and 256x256 (24) tiles, k_gemm_f32 for every fp32 product (98: not the small-M
-        // kernels; 97: k_gemm_f32s, not the K-resident one), the generic kernels (99); the
+        // and 256x256 (24) tiles, k_gemm_f32 for every fp32 product (98: not the small-M or
+        // persistent kernels; 97: k_gemm_f32s, not the K-resident one; 96: the persistent
+        // k_gemm_f32p at any M), the generic kernels (99); the
         // measured-slower A/B tiles (among
         // them 26, the 256x256 tile on the staggered 8-phase schedule) only in
         // libcharpt_hip_ab.so (`make ab`, CG_AB_VARIANTS)
 #ifndef CG_AB_VARIANTS
-        CG_REQUIRE(value == 0 || value == 2 || value == 9 || value == 24 || value == 97 || value == 98 || value == 99,
+        CG_REQUIRE(value == 0 || value == 2 || value == 9 || value == 24 || value == 96 || value == 97 || value == 98 || value == 99,
                    "cg_set_tuning: gemm_variant %d is an A/B variant, not in this build (make ab)", value);
 #endif
         g_gemm_variant = value;

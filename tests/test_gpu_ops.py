@@ -1240,6 +1240,47 @@ def test_gemm_f32_small_m_matches_128x64_bitwise(kind, M, N, K):
     assert torch.equal(outs[0].view(torch.int32), outs[2].view(torch.int32))
 
 
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+@pytest.mark.parametrize("M,N,K,variant", [(65536, 378, 126, 0), (65536, 504, 126, 0), (65536, 126, 126, 0),
+                                           (65536, 126, 504, 0), (4129, 70, 200, 0), (2049, 129, 34, 0),
+                                           (256, 378, 126, 96), (33, 70, 6, 96), (300, 65, 48, 96), (130, 257, 2, 96),
+                                           (4097, 126, 624, 0)])
+def test_gemm_f32_persistent_matches_128x64_bitwise(kind, M, N, K, variant):
+    """The persistent fp32 forward kernel (k_gemm_f32p: M > 2048 by default, gemm_variant 96 at any M;
+    v_mfma_f32_32x32x2_f32 over 32-deep steps) against k_gemm_f32 (gemm_variant 98, 16x16x4 over 16-deep
+    steps): both k-ordered f32 fma chains over the same zero-padded depth, same epilogue -> bitwise equal,
+    at generate()'s window shapes (M = 65536), ragged M / N, K with a half-used last 32-deep step."""
+    from replicatinggpt_amd import _lib as L
+    lib = L.load()
+    torch.manual_seed(41)
+    A = torch.randn(M, K, device=DEV)
+    B = torch.randn(N, K, device=DEV)
+    bias = torch.randn(N, device=DEV)
+    resid = torch.randn(M, N, device=DEV)
+    outs = []
+    for v in (98, variant):
+        L.check(lib.cg_set_tuning(b"gemm_variant", v))
+        try:
+            out = torch.full((M, N), float("nan"), device=DEV)
+            ops().gemm(A, B, out, False, False, False, M, N, K, K, K, N, kind, bias if kind else None,
+                       resid if kind == 3 else None, N if kind == 3 else 0, None, 0, 0.0, 0, None, 0, 0.0, 1, None)
+            torch.cuda.synchronize()
+        finally:
+            L.check(lib.cg_set_tuning(b"gemm_variant", 0))
+        outs.append(out)
+    rows = slice(0, min(M, 2048))   # fp64 reference on a row sample
+    ref = A[rows].double().cpu() @ B.double().cpu().T
+    if kind:
+        ref = ref + bias.double().cpu()
+    if kind == 2:
+        ref = torch.relu(ref)
+    if kind == 3:
+        ref = ref + resid[rows].double().cpu()
+    assert relerr(outs[1][rows], ref) < 1e-5
+    assert not torch.isnan(outs[1]).any()
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+
+
 def test_adamw_matches_torch():
     n = 1000
     torch.manual_seed(8)

@@ -1,8 +1,8 @@
-"""fp32 forward GEMM A/B: k_gemm_f32 (gemm_variant 98) against the NT forward kernel k_gemm_f32n
-(default) at the C5 generate() window shapes (256 x 256 rows, C1 width 126), per-launch time from a
+"""fp32 forward GEMM A/B: k_gemm_f32 (gemm_variant 98) against the default dispatch (round 6: the
+persistent k_gemm_f32p for M > 2048; outputs compared bitwise) at the C5 generate() window shapes (256 x 256 rows, C1 width 126), per-launch time from a
 hipGraph replay of 20 launches (HIP events), rounds interleaved; then, with `gen`, one C5 generate
 (256 x 500 greedy, fp32, C1 golden weights) timed under the variant named second.
-usage: python tools/f32_fwd_ab.py [rounds]            (kernel A/B; needs the trial kernel, not in the tree)
+usage: python tools/f32_fwd_ab.py [rounds]            (kernel A/B, 98 vs 0)
        python tools/f32_fwd_ab.py now [rounds]        (the current library's fp32 products at those shapes)
        python tools/f32_fwd_ab.py small [variant]     (the 256-row products of generate()'s steps)
        python tools/f32_fwd_ab.py gen <98|0> [knob]   (generate with cg_set_tuning(knob, value), knob
@@ -23,7 +23,8 @@ SMALL = [("qkv", 256, 378, 126, 0), ("proj", 256, 126, 126, 3), ("ffn1", 256, 50
          ("ffn2", 256, 126, 504, 3), ("head", 256, 65, 126, 1)]
 
 
-def launch_fn(M, N, K, kind, dev):
+def launch_fn(M, N, K, kind, dev, outs=None):
+    torch.manual_seed(5)
     A = torch.randn(M, K, device=dev)
     B = torch.randn(N, K, device=dev)
     out = torch.empty(M, N, device=dev)
@@ -33,6 +34,10 @@ def launch_fn(M, N, K, kind, dev):
     def run():
         ops.gemm(A, B, out, False, False, False, M, N, K, K, K, N, kind, bias if kind else None,
                  resid if kind == 3 else None, N if kind == 3 else 0, None, 0, 0.0, 0, None, 0, 0.0, 1, None)
+    if outs is not None:
+        run()
+        torch.cuda.synchronize()
+        outs.append(out.clone())
     return run
 
 
@@ -57,6 +62,14 @@ def kernels(rounds):
     lib = L.load()
     dev = torch.device("cuda")
     t = {(n, v): [] for n, *_ in SHAPES for v in (98, 0)}
+    for name, M, N, K, kind in SHAPES:
+        outs = []
+        for v in (98, 0):
+            L.check(lib.cg_set_tuning(b"gemm_variant", v))
+            launch_fn(M, N, K, kind, dev, outs)
+        same = torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+        print(f"{name:5s} bitwise 98 vs 0: {'equal' if same else 'DIFFERENT'}", flush=True)
+        del outs
     for _ in range(rounds):
         for name, M, N, K, kind in SHAPES:
             for v in (98, 0):
@@ -68,7 +81,7 @@ def kernels(rounds):
         a, b = statistics.median(t[(name, 98)]), statistics.median(t[(name, 0)])
         tf = 2 * M * N * K / 1e12
         print(f"{name:5s} M={M} N={N} K={K} epi {kind}: k_gemm_f32 {a:7.1f} us ({tf / a * 1e6:6.1f} TF/s)  "
-              f"k_gemm_f32n {b:7.1f} us ({tf / b * 1e6:6.1f} TF/s)  {b / a - 1:+.1%}", flush=True)
+              f"default {b:7.1f} us ({tf / b * 1e6:6.1f} TF/s)  {b / a - 1:+.1%}", flush=True)
 
 
 def gen(variant, knob="gemm_variant"):
