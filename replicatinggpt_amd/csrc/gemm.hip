@@ -438,22 +438,39 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32p(int64_t M, int64_t N, int6
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
     const int wm = w >> 1, wn = w & 1;
     const int64_t tilesN = (N + PBN - 1) / PBN, ntiles = (M + PBM - 1) / PBM * tilesN;
-    const int64_t kpad = (K + 15) / 16 * 16;
-    const int nks = (int)((kpad + PBK - 1) / PBK);
+    const int kpad = (int)((K + 15) / 16 * 16);
+    const int nks = (kpad + PBK - 1) / PBK;
     const int64_t G = gridDim.x, bid = blockIdx.x;
     const int64_t t_begin = bid * ntiles / G, t_end = (bid + 1) * ntiles / G;
-    // loads: rows lr + 16 i (i = 0..7) of the A and B tiles, k pair lc (a wave: 4 rows x 128 B)
+    // loads: rows lr + 16 i (i = 0..7) of the A and B tiles, k pair lc (a wave: 4 rows x 128 B).  Rows
+    // past M / N read row M-1 / N-1 instead (they only reach outputs that are not stored), k past K reads
+    // k = K-2 and is zeroed (the padded depth must add exact zeros) -- no branches around the loads.
     const int lr = tid >> 4, lc = tid & 15;
-    float2 ra[8], rb[8];
-    auto load = [&](int64_t t, int ks) {
-        const int64_t m0 = t / tilesN * PBM, n0 = t % tilesN * PBN;
-        const int64_t k = (int64_t)ks * PBK + 2 * lc;
-        const bool kin = k < K;   // K even: k + 1 < K as well
+    const char* ta = nullptr;   // the tile's row m0 / n0 (wave-uniform), 32-bit byte offsets per lane
+    const char* tb = nullptr;
+    uint32_t oa[8], ob[8];
+    auto rows_of = [&](int64_t m0, int64_t n0) {
+        ta = (const char*)(A + m0 * lda);
+        tb = (const char*)(B + n0 * ldb);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const int64_t ma = m0 + lr + 16 * i, nb = n0 + lr + 16 * i;
-            ra[i] = (kin && ma < M) ? *(const float2*)(A + ma * lda + k) : make_float2(0.f, 0.f);
-            rb[i] = (kin && nb < N) ? *(const float2*)(B + nb * ldb + k) : make_float2(0.f, 0.f);
+            const int64_t ma = m0 + lr + 16 * i < M ? lr + 16 * i : M - 1 - m0;
+            const int64_t nb = n0 + lr + 16 * i < N ? lr + 16 * i : N - 1 - n0;
+            oa[i] = (uint32_t)(ma * lda * 4);
+            ob[i] = (uint32_t)(nb * ldb * 4);
+        }
+    };
+    float2 ra[8], rb[8];
+    bool rk = true;   // the loaded k pair is inside K (else it is stored as zeros: a select at the LDS
+                      // write, not a write to the load's registers, which would wait for the load)
+    auto load = [&](int ks) {
+        const int k = ks * PBK + 2 * lc;
+        rk = k < (int)K;
+        const uint32_t kc = 4u * (uint32_t)(rk ? k : (int)K - 2);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            ra[i] = *(const float2*)(ta + (oa[i] + kc));
+            rb[i] = *(const float2*)(tb + (ob[i] + kc));
         }
     };
     auto store = [&](int st) {
@@ -462,18 +479,28 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32p(int64_t M, int64_t N, int6
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int r = lr + 16 * i;
-            As[2 * lc * PLD + r] = ra[i].x;
-            As[(2 * lc + 1) * PLD + r] = ra[i].y;
-            Bs[2 * lc * PLD + r] = rb[i].x;
-            Bs[(2 * lc + 1) * PLD + r] = rb[i].y;
+            As[2 * lc * PLD + r] = rk ? ra[i].x : 0.f;
+            As[(2 * lc + 1) * PLD + r] = rk ? ra[i].y : 0.f;
+            Bs[2 * lc * PLD + r] = rk ? rb[i].x : 0.f;
+            Bs[(2 * lc + 1) * PLD + r] = rk ? rb[i].y : 0.f;
         }
     };
     constexpr bool BIAS = EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_BIAS_RESID;
     const bool hb = BIAS && epi.bias, hr = EK == CG_EPI_BIAS_RESID && epi.resid;
+    // tile coordinates advance without division: a block's tiles are consecutive in row-band-major order
+    int64_t tm = t_begin / tilesN, tn = t_begin - tm * tilesN;
     int stc = 0;
-    if (t_begin < t_end) load(t_begin, 0);
+    if (t_begin < t_end) {
+        rows_of(tm * PBM, tn * PBN);
+        load(0);
+    }
 #pragma unroll 1
     for (int64_t t = t_begin; t < t_end; ++t) {
+        const int64_t m0t = tm * PBM, n0t = tn * PBN;
+        if (++tn == tilesN) {
+            tn = 0;
+            ++tm;
+        }
         fv16f acc[2][2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = fv16f{};
@@ -483,59 +510,70 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32p(int64_t M, int64_t N, int6
             ++stc;
             store(st);   // stage st was last read two steps ago, before the previous step's barrier
             __syncthreads();
-            if (ks + 1 < nks) load(t, ks + 1);
-            else if (t + 1 < t_end) load(t + 1, 0);
+            if (ks + 1 < nks) load(ks + 1);
+            else if (t + 1 < t_end) {
+                rows_of(tm * PBM, tn * PBN);
+                load(0);
+            }
             const float* As = sm[st][0] + h * PLD + 64 * wm + l32;
             const float* Bs = sm[st][1] + h * PLD + 64 * wn + l32;
-            auto k2 = [&](int s) {
-                const float a0 = As[2 * s * PLD], a1 = As[2 * s * PLD + 32];
-                const float b0 = Bs[2 * s * PLD], b1 = Bs[2 * s * PLD + 32];
-                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-            };
+            const bool full = kpad - ks * PBK > 16;   // wave-uniform: the step's second 16 k are inside kpad
+            // a half step's fragments (8 k2-steps, 32 registers) read before its MFMAs: one LDS round
+            // trip per 32 MFMAs instead of one per 4
 #pragma unroll
-            for (int s = 0; s < 8; ++s) k2(s);
-            if (kpad - (int64_t)ks * PBK > 16) {   // wave-uniform: the step's second 16 k are inside kpad
+            for (int hs = 0; hs < 2; ++hs) {
+                if (hs == 1 && !full) break;
+                float fa[8][2], fb[8][2];
 #pragma unroll
-                for (int s = 8; s < 16; ++s) k2(s);
+                for (int s = 0; s < 8; ++s) {
+                    const int o = 2 * (8 * hs + s) * PLD;
+                    fa[s][0] = As[o];
+                    fa[s][1] = As[o + 32];
+                    fb[s][0] = Bs[o];
+                    fb[s][1] = Bs[o + 32];
+                }
+                __builtin_amdgcn_sched_barrier(0);   // keep the batch together (hipcc sinks each read to its MFMAs)
+#pragma unroll
+                for (int s = 0; s < 8; ++s) {
+                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s][0], fb[s][0], acc[0][0], 0, 0, 0);
+                    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s][0], fb[s][1], acc[0][1], 0, 0, 0);
+                    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s][1], fb[s][0], acc[1][0], 0, 0, 0);
+                    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s][1], fb[s][1], acc[1][1], 0, 0, 0);
+                }
             }
         }
-        // epilogue (k_gemm_f32's beta-0 arithmetic): bias, ReLU, resid + v; every operand loaded
-        // before the first store.  Lane column n = l32; register r holds row (r & 3) + 8 (r >> 2) + 4 h.
-        const int64_t m0 = t / tilesN * PBM + 64 * wm, n0 = t % tilesN * PBN + 64 * wn;
+        // epilogue (k_gemm_f32's beta-0 arithmetic): bias, ReLU, resid + v, per 32-row half i, the
+        // half's residuals loaded before its stores.  Lane column
+        // n = l32; register r holds row (r & 3) + 8 (r >> 2) + 4 h of the 32 x 32 fragment.
+        const int64_t m0 = m0t + 64 * wm + 4 * h, n0 = n0t + 64 * wn + l32;
         float bv[2] = {0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int64_t n = n0 + 32 * j + l32;
-            if (hb && n < N) bv[j] = epi.bias[n];
-        }
-        float rv[2][2][16];
-        if (hr) {
+        for (int j = 0; j < 2; ++j)
+            if (hb && n0 + 32 * j < N) bv[j] = epi.bias[n0 + 32 * j];
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i) {
+            float rv[2][16];
+            if (hr) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
-                        const int64_t m = m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, n = n0 + 32 * j + l32;
-                        rv[i][j][r] = (m < M && n < N) ? epi.resid[m * epi.ld_resid + n] : 0.f;
+                        const int64_t m = m0 + 32 * i + (r & 3) + 8 * (r >> 2), n = n0 + 32 * j;
+                        rv[j][r] = (m < M && n < N) ? epi.resid[m * epi.ld_resid + n] : 0.f;
                     }
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
+            }
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const int64_t m = m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, n = n0 + 32 * j + l32;
+                    const int64_t m = m0 + 32 * i + (r & 3) + 8 * (r >> 2), n = n0 + 32 * j;
                     float v = acc[i][j][r];
                     if (hb) v += bv[j];
                     if (EK == CG_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
-                    if (hr) v = rv[i][j][r] + v;
+                    if (hr) v = rv[j][r] + v;
                     if (m < M && n < N) C[m * ldc + n] = v;
                 }
+        }
     }
 }
 
@@ -547,6 +585,8 @@ bool launch_f32p(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, c
         return false;
     if (e.kind != CG_EPI_STORE && e.kind != CG_EPI_BIAS && e.kind != CG_EPI_BIAS_RELU && e.kind != CG_EPI_BIAS_RESID)
         return false;
+    // the kernel's 32-bit lane offsets within a 128-row tile (rows_of): 128 rows of lda floats under 4 GB
+    if (lda >= ((int64_t)1 << 22) || ldb >= ((int64_t)1 << 22) || K >= ((int64_t)1 << 22)) return false;
     const int64_t ntiles = (M + PBM - 1) / PBM * ((N + PBN - 1) / PBN);
     const int64_t slots = 2 * (int64_t)gemm_cu_count();
     const unsigned grid = (unsigned)(ntiles < slots ? ntiles : slots);
