@@ -433,8 +433,16 @@ constexpr int PBM = 128, PBN = 128, PBK = 32, PLD = PBM + 4;   // LDS row stride
 template <int EK>
 __global__ __launch_bounds__(256, 2) void k_gemm_f32p(int64_t M, int64_t N, int64_t K, const float* __restrict__ A,
                                                       int64_t lda, const float* __restrict__ B, int64_t ldb,
-                                                      float* __restrict__ C, int64_t ldc, EpiArgs epi) {
+                                                      float* __restrict__ C, int64_t ldc, EpiArgs epi,
+                                                      int wflags) {
     __shared__ __attribute__((aligned(16))) float sm[2][2][PBK * PLD];   // [stage][A | B][k][row]: 66 KB
+#ifdef CG_F32P_WHATIF
+    // diagnostic build only (make whatif; tools/f32p_whatif.py): pk_flags bit 4 skips the in-loop loads
+    // after each tile's first K-step, bit 5 the MFMAs, bit 6 the epilogue stores -- timing only
+    const bool WI_NOLOAD = wflags & 16, WI_NOMFMA = wflags & 32, WI_NOEPI = wflags & 64;
+#else
+    constexpr bool WI_NOLOAD = false, WI_NOMFMA = false, WI_NOEPI = false;
+#endif
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
     const int wm = w >> 1, wn = w & 1;
     const int64_t tilesN = (N + PBN - 1) / PBN, ntiles = (M + PBM - 1) / PBM * tilesN;
@@ -510,8 +518,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32p(int64_t M, int64_t N, int6
             ++stc;
             store(st);   // stage st was last read two steps ago, before the previous step's barrier
             __syncthreads();
-            if (ks + 1 < nks) load(ks + 1);
-            else if (t + 1 < t_end) {
+            if (ks + 1 < nks) {
+                if (!WI_NOLOAD) load(ks + 1);
+            } else if (t + 1 < t_end) {
                 rows_of(tm * PBM, tn * PBN);
                 load(0);
             }
@@ -522,7 +531,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32p(int64_t M, int64_t N, int6
             // trip per 32 MFMAs instead of one per 4
 #pragma unroll
             for (int hs = 0; hs < 2; ++hs) {
-                if (hs == 1 && !full) break;
+                if ((hs == 1 && !full) || WI_NOMFMA) break;
                 float fa[8][2], fb[8][2];
 #pragma unroll
                 for (int s = 0; s < 8; ++s) {
@@ -571,7 +580,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32p(int64_t M, int64_t N, int6
                     if (hb) v += bv[j];
                     if (EK == CG_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
                     if (hr) v = rv[j][r] + v;
-                    if (m < M && n < N) C[m * ldc + n] = v;
+                    if (m < M && n < N && !WI_NOEPI) C[m * ldc + n] = v;
                 }
         }
     }
@@ -590,7 +599,7 @@ bool launch_f32p(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, c
     const int64_t ntiles = (M + PBM - 1) / PBM * ((N + PBN - 1) / PBN);
     const int64_t slots = 2 * (int64_t)gemm_cu_count();
     const unsigned grid = (unsigned)(ntiles < slots ? ntiles : slots);
-#define KP(EK_) k_gemm_f32p<EK_><<<grid, 256, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e)
+#define KP(EK_) k_gemm_f32p<EK_><<<grid, 256, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, g_pk_flags)
     switch (e.kind) {
         case CG_EPI_STORE: KP(CG_EPI_STORE); break;
         case CG_EPI_BIAS: KP(CG_EPI_BIAS); break;
