@@ -438,8 +438,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32p(int64_t M, int64_t N, int6
     __shared__ __attribute__((aligned(16))) float sm[2][2][PBK * PLD];   // [stage][A | B][k][row]: 66 KB
 #ifdef CG_F32P_WHATIF
     // diagnostic build only (make whatif; tools/f32p_whatif.py): pk_flags bit 4 skips the in-loop loads
-    // after each tile's first K-step, bit 5 the MFMAs, bit 6 the epilogue stores, bit 7 delays the start
-    // of blocks 256-511 -- timing only
+    // after each tile's first K-step, bit 5 the MFMAs, bit 6 the epilogue stores -- timing only
     const bool WI_NOLOAD = wflags & 16, WI_NOMFMA = wflags & 32, WI_NOEPI = wflags & 64;
 #else
     constexpr bool WI_NOLOAD = false, WI_NOMFMA = false, WI_NOEPI = false;
@@ -498,58 +497,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32p(int64_t M, int64_t N, int6
     const bool hb = BIAS && epi.bias, hr = EK == CG_EPI_BIAS_RESID && epi.resid;
     // tile coordinates advance without division: a block's tiles are consecutive in row-band-major order
     int64_t tm = t_begin / tilesN, tn = t_begin - tm * tilesN;
-    // epilogue (k_gemm_f32's beta-0 arithmetic): bias, ReLU, resid + v, per 32-row half i, the half's
-    // residuals loaded before its stores.  Lane column n = l32; register r holds row
-    // (r & 3) + 8 (r >> 2) + 4 h of the 32 x 32 fragment.
-    fv16f acc[2][2];
-    // addresses: a wave-uniform tile base + a 32-bit lane offset (row 64 wm + 4 h, column 64 wn + l32)
-    // + uniform per-register row / column steps (launch_f32p: 128 rows of ldc / ld_resid floats < 2 GB)
-    const int lrow = 64 * wm + 4 * h, lcol = 64 * wn + l32;
-    const int ldc32 = (int)ldc, ldr32 = hr ? (int)epi.ld_resid : 0;
-    const int offc = lrow * ldc32 + lcol, offr = lrow * ldr32 + lcol;
-    auto epilogue = [&](int64_t m0t, int64_t n0t) {
-        // laundered per call: otherwise LICM hoists all 64 store offsets out of the tile loop (64 VGPRs)
-        int oc = offc, orr = offr, lc32 = ldc32, lr32 = ldr32;
-        asm volatile("" : "+v"(oc), "+v"(orr), "+s"(lc32), "+s"(lr32));
-        float* Ct = C + m0t * ldc + n0t;
-        const float* Rt = hr ? epi.resid + m0t * epi.ld_resid + n0t : nullptr;
-        const int rows = (int)(M - m0t < 128 ? M - m0t : 128) - lrow;   // rows of this lane's tile part
-        const int cols = (int)(N - n0t < 128 ? N - n0t : 128) - lcol;
-        float bv[2] = {0.f, 0.f};
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-            if (hb && 32 * j < cols) bv[j] = epi.bias[n0t + lcol + 32 * j];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            float rv[2][16];
-            if (hr) {
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int dr = 32 * i + (r & 3) + 8 * (r >> 2);
-                        rv[j][r] = (dr < rows && 32 * j < cols) ? Rt[orr + dr * lr32 + 32 * j] : 0.f;
-                    }
-            }
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int dr = 32 * i + (r & 3) + 8 * (r >> 2);
-                    float v = acc[i][j][r];
-                    if (hb) v += bv[j];
-                    if (EK == CG_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
-                    if (hr) v = rv[j][r] + v;
-                    if (dr < rows && 32 * j < cols && !WI_NOEPI) Ct[oc + dr * lc32 + 32 * j] = v;
-                }
-        }
-    };
-#ifdef CG_F32P_WHATIF
-    if ((wflags & 128) && ((bid >> 8) & 1))   // what-if: half the blocks start ~half a K-step late
-        for (int z = 0; z < 4; ++z) __builtin_amdgcn_s_sleep(8);
-#endif
     int stc = 0;
-    int64_t pm = -1, pn = 0;   // the previous tile, whose epilogue is still to run
     if (t_begin < t_end) {
         rows_of(tm * PBM, tn * PBN);
         load(0);
@@ -561,6 +509,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32p(int64_t M, int64_t N, int6
             tn = 0;
             ++tm;
         }
+        fv16f acc[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = fv16f{};
 #pragma unroll 1
         for (int ks = 0; ks < nks; ++ks) {
             const int st = stc & 1;
@@ -572,15 +523,6 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32p(int64_t M, int64_t N, int6
             } else if (t + 1 < t_end) {
                 rows_of(tm * PBM, tn * PBN);
                 load(0);
-            }
-            if (ks == 0) {
-                // the previous tile's stores go out here, after this tile's second K-tile load: that
-                // load's wait (next step) need not drain them -- vmcnt retires loads and stores in
-                // issue order -- so the store burst every block issues at a tile seam has two K-steps
-                // of MFMAs to drain behind instead of one
-                if (pm >= 0) epilogue(pm, pn);
-#pragma unroll
-                for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = fv16f{};
             }
             const float* As = sm[st][0] + h * PLD + 64 * wm + l32;
             const float* Bs = sm[st][1] + h * PLD + 64 * wn + l32;
@@ -609,10 +551,39 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32p(int64_t M, int64_t N, int6
                 }
             }
         }
-        pm = m0t;
-        pn = n0t;
+        // epilogue (k_gemm_f32's beta-0 arithmetic): bias, ReLU, resid + v, per 32-row half i, the
+        // half's residuals loaded before its stores.  Lane column
+        // n = l32; register r holds row (r & 3) + 8 (r >> 2) + 4 h of the 32 x 32 fragment.
+        const int64_t m0 = m0t + 64 * wm + 4 * h, n0 = n0t + 64 * wn + l32;
+        float bv[2] = {0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            if (hb && n0 + 32 * j < N) bv[j] = epi.bias[n0 + 32 * j];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            float rv[2][16];
+            if (hr) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int64_t m = m0 + 32 * i + (r & 3) + 8 * (r >> 2), n = n0 + 32 * j;
+                        rv[j][r] = (m < M && n < N) ? epi.resid[m * epi.ld_resid + n] : 0.f;
+                    }
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t m = m0 + 32 * i + (r & 3) + 8 * (r >> 2), n = n0 + 32 * j;
+                    float v = acc[i][j][r];
+                    if (hb) v += bv[j];
+                    if (EK == CG_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
+                    if (hr) v = rv[j][r] + v;
+                    if (m < M && n < N && !WI_NOEPI) C[m * ldc + n] = v;
+                }
+        }
     }
-    if (pm >= 0) epilogue(pm, pn);
 }
 
 bool launch_f32p(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
@@ -625,9 +596,6 @@ bool launch_f32p(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, c
         return false;
     // the kernel's 32-bit lane offsets within a 128-row tile (rows_of): 128 rows of lda floats under 4 GB
     if (lda >= ((int64_t)1 << 22) || ldb >= ((int64_t)1 << 22) || K >= ((int64_t)1 << 22)) return false;
-    // and the epilogue's 32-bit lane offsets: 128 rows of ldc / ld_resid floats under 2 GB
-    if (ldc >= ((int64_t)1 << 21) || (e.kind == CG_EPI_BIAS_RESID && e.resid && e.ld_resid >= ((int64_t)1 << 21)))
-        return false;
     const int64_t ntiles = (M + PBM - 1) / PBM * ((N + PBN - 1) / PBN);
     const int64_t slots = 2 * (int64_t)gemm_cu_count();
     const unsigned grid = (unsigned)(ntiles < slots ? ntiles : slots);

@@ -1,7 +1,7 @@
 """Where does the persistent fp32 GEMM (k_gemm_f32p, generate()'s window products) spend its time?
 Loads the what-if build (make -C replicatinggpt_amd/csrc whatif; gemm.hip CG_F32P_WHATIF) and times the
 four C5 window shapes with pk_flags 0 (all), 16 (no in-loop loads), 32 (no MFMAs), 64 (no epilogue
-stores), 128 (blocks 256-511 start ~2000 cycles late) and combinations.  Wrong results (timing only).  GPU only.
+stores) and their combinations.  Wrong results (timing only).  GPU only.
 usage: python tools/f32p_whatif.py [rounds]"""
 import os
 import statistics
@@ -18,7 +18,7 @@ from f32_fwd_ab import SHAPES, graph_us, launch_fn  # noqa: E402
 from replicatinggpt_amd import _lib as L  # noqa: E402
 
 MODES = [("all", 0), ("noload", 16), ("noMFMA", 32), ("nostore", 64), ("noload+nostore", 80),
-         ("noMFMA+nostore", 96), ("skeleton", 112), ("skew", 128)]
+         ("noMFMA+nostore", 96), ("skeleton", 112)]
 
 
 def main(rounds):
