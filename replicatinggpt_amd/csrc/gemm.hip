@@ -439,9 +439,12 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32p(int64_t M, int64_t N, int6
 #ifdef CG_F32P_WHATIF
     // diagnostic build only (make whatif; tools/f32p_whatif.py): pk_flags bit 4 skips the in-loop loads
     // after each tile's first K-step, bit 5 the MFMAs, bit 6 the epilogue stores -- timing only
-    const bool WI_NOLOAD = wflags & 16, WI_NOMFMA = wflags & 32, WI_NOEPI = wflags & 64;
+    // bit 8: fragment reads only in each tile's first K-step (MFMAs on stale registers after it),
+    // bit 9: LDS store + barrier only in each tile's first K-step
+    const bool WI_NOLOAD = wflags & 16, WI_NOMFMA = wflags & 32, WI_NOEPI = wflags & 64, WI_NOREAD = wflags & 256,
+               WI_NOSYNC = wflags & 512;
 #else
-    constexpr bool WI_NOLOAD = false, WI_NOMFMA = false, WI_NOEPI = false;
+    constexpr bool WI_NOLOAD = false, WI_NOMFMA = false, WI_NOEPI = false, WI_NOREAD = false, WI_NOSYNC = false;
 #endif
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
     const int wm = w >> 1, wn = w & 1;
@@ -516,8 +519,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32p(int64_t M, int64_t N, int6
         for (int ks = 0; ks < nks; ++ks) {
             const int st = stc & 1;
             ++stc;
-            store(st);   // stage st was last read two steps ago, before the previous step's barrier
-            __syncthreads();
+            if (!WI_NOSYNC || ks == 0) {
+                store(st);   // stage st was last read two steps ago, before the previous step's barrier
+                __syncthreads();
+            }
             if (ks + 1 < nks) {
                 if (!WI_NOLOAD) load(ks + 1);
             } else if (t + 1 < t_end) {
@@ -529,12 +534,13 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32p(int64_t M, int64_t N, int6
             const bool full = kpad - ks * PBK > 16;   // wave-uniform: the step's second 16 k are inside kpad
             // a half step's fragments (8 k2-steps, 32 registers) read before its MFMAs: one LDS round
             // trip per 32 MFMAs instead of one per 4
+            float fa[8][2], fb[8][2];
 #pragma unroll
             for (int hs = 0; hs < 2; ++hs) {
                 if ((hs == 1 && !full) || WI_NOMFMA) break;
-                float fa[8][2], fb[8][2];
 #pragma unroll
                 for (int s = 0; s < 8; ++s) {
+                    if (WI_NOREAD && (ks > 0 || hs > 0)) break;
                     const int o = 2 * (8 * hs + s) * PLD;
                     fa[s][0] = As[o];
                     fa[s][1] = As[o + 32];

@@ -1,7 +1,8 @@
 """Where does the persistent fp32 GEMM (k_gemm_f32p, generate()'s window products) spend its time?
 Loads the what-if build (make -C replicatinggpt_amd/csrc whatif; gemm.hip CG_F32P_WHATIF) and times the
 four C5 window shapes with pk_flags 0 (all), 16 (no in-loop loads), 32 (no MFMAs), 64 (no epilogue
-stores) and their combinations.  Wrong results (timing only).  GPU only.
+stores), 256 (fragment reads only in a tile's first K-step), 512 (LDS store + barrier only
+there) and combinations.  Wrong results (timing only).  GPU only.
 usage: python tools/f32p_whatif.py [rounds]"""
 import os
 import statistics
@@ -18,7 +19,8 @@ from f32_fwd_ab import SHAPES, graph_us, launch_fn  # noqa: E402
 from replicatinggpt_amd import _lib as L  # noqa: E402
 
 MODES = [("all", 0), ("noload", 16), ("noMFMA", 32), ("nostore", 64), ("noload+nostore", 80),
-         ("noMFMA+nostore", 96), ("skeleton", 112)]
+         ("noMFMA+nostore", 96), ("skeleton", 112), ("noread", 256), ("nosync", 512), ("noread+nosync", 768),
+         ("noread+nosync+noload+nostore", 848)]
 
 
 def main(rounds):
