@@ -616,6 +616,214 @@ bool launch_f32p(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, c
     return true;
 }
 
+// ---------------------------------------------------------------------------------------
+// Fused fp32 FFN forward for inference (FeedForward GPT1.py:142-147 in eval: no dropout) --
+// generate()'s sliding-window blocks, M = 65536 rows of C = 126:
+//     out = resid + (relu(a W1^T + b1) W2^T + b2),   a [M][C], W1 [H][C], W2 [C][H]
+// without writing h (M x H fp32: 132 MB per launch at C5) to HBM and reading it back.  A block owns
+// 128 rows, each wave 32 of them, and walks the hidden units in chunks of 32:
+//   * GEMM 1 transposed, D[unit][row] = W1 a^T: its "B" operand is the wave's a rows, held in 64
+//     registers for the whole block (xr[s] = a[row][2s + h] after one v_permlane32_swap per float2),
+//     its "A" operand the chunk's 32 W1 rows (all of k) staged in LDS;
+//   * D's accumulator layout puts the row on the lane and the hidden unit on the register, which is
+//     GEMM 2's A-operand layout up to a pairing of k: two v_permlane32_swap per 8 hidden units
+//     (below) make lane half 0 hold the even and half 1 the odd units, so h = relu(D + b1) feeds
+//     out += h W2^T straight from registers; the chunk's 32 W2 columns are staged in LDS.
+// Each chunk is two 64-MFMA slices per wave (W1, then W2) through a 2-stage LDS ring -- the next
+// slice loaded to registers during the current one's MFMAs, one barrier per slice; biases in LDS.
+// Bitwise the two-GEMM path (k_gemm_f32 / k_gemm_f32p BIAS_RELU then BIAS_RESID): every h element
+// is the same k-ordered f32 fma chain over k < ceil16(C) plus b1 then max(., 0), every output the
+// chain over hidden units < ceil16(H) (zero-padded h and W2 past H) plus b2 then resid + v
+// (test_ffn_f32_fused_matches_two_gemms).  C <= 128 even, H <= 2048 even, lda / ldw1 / ldw2 even.
+constexpr int FFN_LD1 = 33, FFN_LD2 = 132, FFN_STAGE = 32 * FFN_LD2;   // W1 [128 k][32 + 1], W2 [32 unit][128 + 4]
+
+__global__ __launch_bounds__(256, 2) void k_ffn_f32(int64_t M, int C, int H, const float* __restrict__ a, int64_t lda,
+                                                    const float* __restrict__ w1, int64_t ldw1,
+                                                    const float* __restrict__ b1, const float* __restrict__ w2,
+                                                    int64_t ldw2, const float* __restrict__ b2,
+                                                    const float* resid, int64_t ldr, float* out, int64_t ldo) {
+    __shared__ __attribute__((aligned(16))) float sm[2][FFN_STAGE];   // 33.8 KB
+    __shared__ float sb1[2048], sb2[128];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
+    const int64_t mw = (int64_t)blockIdx.x * 128 + 32 * w;   // the wave's first row
+    const int kpad1 = (C + 15) / 16 * 16, kpad2 = (H + 15) / 16 * 16;
+    const int nc = (H + 31) / 32;
+    for (int i = tid; i < H; i += 256) sb1[i] = b1[i];
+    for (int i = tid; i < C; i += 256) sb2[i] = b2[i];
+
+    // the wave's a rows in GEMM 1's B-operand layout: lane (l32, h) loads a[row][4t + 2h, +1]; one
+    // swap of h1's .x with h0's .y leaves xr[2t] = a[row][4t + h], xr[2t + 1] = a[row][4t + 2 + h]
+    float xr[64];
+    {
+        const int64_t row = mw + l32 < M ? mw + l32 : M - 1;
+        const float* ar = a + row * lda;
+        float2 v[32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) {
+            const int k = 4 * t + 2 * h;
+            v[t] = *(const float2*)(ar + (k < C ? k : C - 2));
+            if (k >= C) v[t] = make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int t = 0; t < 32; ++t) {
+            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[t].x), __float_as_uint(v[t].y), false,
+                                                            false);
+            xr[2 * t] = __uint_as_float(r[0]);
+            xr[2 * t + 1] = __uint_as_float(r[1]);
+        }
+    }
+
+    // slice staging, 8 float2 per thread.  kind 0: W1 rows 32 c + (tid >> 6) + 4 i at k = 2 (tid & 63)
+    // (a wave reads one 512-B row), stored [k][unit] with row stride FFN_LD1; kind 1: W2 rows
+    // (tid >> 4) + 16 i at unit 32 c + 2 (tid & 15), stored [unit][column] with row stride FFN_LD2
+    float2 ra[8];
+    bool rk = true;
+    auto load = [&](int c, int kind) {
+        const float* base;
+        int ld, rmax, k, kmax, r0, rs;
+        if (kind == 0) {
+            base = w1, ld = (int)ldw1, rmax = H, kmax = C, k = 2 * (tid & 63), r0 = 32 * c + (tid >> 6), rs = 4;
+        } else {
+            base = w2, ld = (int)ldw2, rmax = C, kmax = H, k = 32 * c + 2 * (tid & 15), r0 = tid >> 4, rs = 16;
+        }
+        rk = k < kmax;
+        const int kc = rk ? k : kmax - 2;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {   // cg_ffn_fwd_f32 checks: rows * ld under 2^31
+            const int r = r0 + rs * i < rmax ? r0 + rs * i : rmax - 1;
+            ra[i] = *(const float2*)(base + (uint32_t)(r * ld + kc));
+        }
+    };
+    auto store = [&](int st, int kind) {   // kind: the staged slice's (that of the step storing it)
+        float* S = sm[st];
+        const int LD = kind == 0 ? FFN_LD1 : FFN_LD2;
+        const int kk = kind == 0 ? 2 * (tid & 63) : 2 * (tid & 15);
+        const int r0 = kind == 0 ? tid >> 6 : tid >> 4, rs = kind == 0 ? 4 : 16;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int r = r0 + rs * i;
+            S[kk * LD + r] = rk ? ra[i].x : 0.f;
+            S[(kk + 1) * LD + r] = rk ? ra[i].y : 0.f;
+        }
+    };
+    int stc = 0;
+    // one ring step: the staged slice (chunk c, kind) to LDS, barrier, the following slice's load;
+    // returns the stage to compute from
+    auto step = [&](int c, int kind) {
+        const int st = stc & 1;
+        ++stc;
+        store(st, kind);
+        __syncthreads();
+        if (kind == 0) load(c, 1);
+        else if (c + 1 < nc) load(c + 1, 0);
+        return st;
+    };
+
+    fv16f acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = fv16f{};
+    const int nst1 = kpad1 / 2;   // GEMM 1 k2-steps (<= 64)
+    load(0, 0);
+#pragma unroll 1
+    for (int c = 0; c < nc; ++c) {
+        // GEMM 1: D (hidden units 32 c.., the wave's rows) over k: one accumulator chain
+        fv16f D = fv16f{};
+        {
+            const float* S = sm[step(c, 0)] + h * FFN_LD1 + l32;
+#pragma unroll
+            for (int b = 0; b < 16; ++b) {   // 4 k2-steps per fragment batch
+                if (4 * b >= nst1) break;
+                float fa[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) fa[u] = S[2 * (4 * b + u) * FFN_LD1];
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) D = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[u], xr[4 * b + u], D, 0, 0, 0);
+            }
+        }
+        // h = relu(D + b1), zero past H; then lane half 0 takes the even, half 1 the odd hidden units:
+        // register 4q + t holds unit 8q + t + 4h; swapping h1's 4q+0 with h0's 4q+1 and h1's 4q+2 with
+        // h0's 4q+3 leaves h0 {8q+0, 8q+4, 8q+2, 8q+6}, h1 {8q+1, 8q+5, 8q+3, 8q+7}
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int hc = 32 * c + (r & 3) + 8 * (r >> 2) + 4 * h;
+            float v = D[r];
+            v += sb1[hc < H ? hc : 0];
+            v = fmaxf(v, 0.f);
+            D[r] = hc < H ? v : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            auto r0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(D[4 * q]), __float_as_uint(D[4 * q + 1]), false,
+                                                       false);
+            auto r1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(D[4 * q + 2]), __float_as_uint(D[4 * q + 3]),
+                                                       false, false);
+            D[4 * q] = __uint_as_float(r0[0]);
+            D[4 * q + 1] = __uint_as_float(r0[1]);
+            D[4 * q + 2] = __uint_as_float(r1[0]);
+            D[4 * q + 3] = __uint_as_float(r1[1]);
+        }
+        // GEMM 2: acc[j] (output columns 32 j.., the wave's rows) over the chunk's units; k2-step s
+        // reads register 4 (s >> 2) + {0, 2, 1, 3}[s & 3]
+        {
+            const float* S = sm[step(c, 1)] + h * FFN_LD2 + l32;
+            const int nst = kpad2 - 32 * c >= 32 ? 16 : 8;
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                if (2 * b >= nst) break;
+                float fb[2][4];
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) fb[u][j] = S[2 * (2 * b + u) * FFN_LD2 + 32 * j];
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    constexpr int perm[4] = {0, 2, 1, 3};
+                    const int sstep = 2 * b + u;
+                    const float ha = D[4 * (sstep >> 2) + perm[sstep & 3]];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ha, fb[u][j], acc[j], 0, 0, 0);
+                }
+            }
+        }
+    }
+    // out = resid + (acc + b2): lane column n = 32 j + l32, register r row (r & 3) + 8 (r >> 2) + 4 h;
+    // every residual loaded before the first store (out may alias resid); residual rows / columns
+    // clamped, not branched around, so the loads stay in flight together
+    const int64_t mr = M - 1 - mw;   // the wave's last valid row offset
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int n = 32 * j + l32 < C ? 32 * j + l32 : C - 1;
+        const float bb = sb2[n];
+        float rv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t dm = (r & 3) + 8 * (r >> 2) + 4 * h;
+            rv[r] = resid[(mw + (dm < mr ? dm : mr)) * ldr + n];
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            float v = acc[j][r];
+            v += bb;
+            acc[j][r] = rv[r] + v;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t m = mw + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int n = 32 * j + l32;
+            if (m < M && n < C) out[m * ldo + n] = acc[j][r];
+        }
+}
+
+bool ffn_f32_supported(int64_t M, int64_t C, int64_t H) {
+    return M > 0 && C >= 2 && C <= 128 && C % 2 == 0 && H >= 2 && H <= 2048 && H % 2 == 0;
+}
+
 // the small-M kernel's conditions (else k_gemm_f32); gemm_variant 98 forces k_gemm_f32,
 // 97 k_gemm_f32s (A/B, tests)
 bool launch_f32s(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
@@ -1161,6 +1369,25 @@ extern "C" int cg_gemm_rowdot_supported(int a_trans, int b_trans, int64_t M, int
 
 extern "C" int64_t cg_gemm_workspace(int64_t M, int64_t N, int split_k) {
     return split_k > 1 ? (int64_t)split_k * M * N * (int64_t)sizeof(float) : 0;
+}
+
+extern "C" int cg_ffn_fwd_f32_supported(int64_t M, int64_t C, int64_t H) { return ffn_f32_supported(M, C, H) ? 1 : 0; }
+
+extern "C" int cg_ffn_fwd_f32(int64_t M, int64_t C, int64_t H, const float* a, int64_t lda, const float* w1,
+                              int64_t ldw1, const float* b1, const float* w2, int64_t ldw2, const float* b2,
+                              const float* resid, int64_t ldr, float* out, int64_t ldo, void* stream) {
+    CG_REQUIRE(ffn_f32_supported(M, C, H),
+               "cg_ffn_fwd_f32: unsupported shape M=%lld C=%lld H=%lld (C <= 128 even, H <= 2048 even)", (long long)M,
+               (long long)C, (long long)H);
+    CG_REQUIRE(a && w1 && b1 && w2 && b2 && resid && out, "cg_ffn_fwd_f32: null pointer");
+    CG_REQUIRE(lda >= C && lda % 2 == 0 && ldw1 >= C && ldw1 % 2 == 0 && ldw2 >= H && ldw2 % 2 == 0 && ldr >= C &&
+                   ldo >= C && (int64_t)H * ldw1 < ((int64_t)1 << 31) && C * ldw2 < ((int64_t)1 << 31),
+               "cg_ffn_fwd_f32: bad leading dimensions");
+    CG_REQUIRE((((uintptr_t)a | (uintptr_t)w1 | (uintptr_t)w2) & 7) == 0, "cg_ffn_fwd_f32: a, w1, w2 must be 8-B aligned");
+    k_ffn_f32<<<(unsigned)((M + 127) / 128), 256, 0, (hipStream_t)stream>>>(M, (int)C, (int)H, a, lda, w1, ldw1, b1, w2,
+                                                                            ldw2, b2, resid, ldr, out, ldo);
+    CG_LAUNCH_CHECK("cg_ffn_fwd_f32");
+    return CG_OK;
 }
 
 extern "C" int cg_gemm_resid_layernorm_supported(int64_t M, int64_t N, int64_t K) {

@@ -775,6 +775,31 @@ class AttnSublayerFn(torch.autograd.Function):
         return (dx.view(B, T, C), None, None, None, None, None, None, *f_ln, *f_qkv(), *f_pw(), *f_pb())
 
 
+# generate()'s fp32 window blocks run the FeedForward as one fused launch (ops.ffn_fwd_f32: the hidden
+# activations never reach HBM); CHARPT_FFN_FUSED=0 keeps the two GEMMs (A/B)
+FFN_FUSED = os.environ.get("CHARPT_FFN_FUSED", "1") == "1"
+
+
+def ffn_sublayer_infer(x, lc, ln_w, ln_b, w1, b1, w2, b2):
+    """FFNSublayerFn.forward for fp32 inference without autograd (no dropout, nothing saved):
+    ln2, then x + W2 relu(W1 ln2(x) + b1) + b2 in one launch -- the bits of the two-GEMM path
+    (tests/test_gpu_ops.py::test_ffn_f32_fused_matches_two_gemms).  None where it does not apply
+    (bf16, dropout, fewer than 2049 rows -- the small-M GEMMs are faster there -- or a shape the
+    kernel does not take)."""
+    if not FFN_FUSED or lc.act != torch.float32 or lc.p > 0:
+        return None
+    B, T, C = x.shape
+    M, H = B * T, w1.master.shape[0]
+    if M <= 2048 or not ops.ffn_fwd_f32_supported(M, C, H):
+        return None
+    x2 = x.reshape(M, C)
+    pre = pre_ln(x, ln_w, ln_b, lc.act)
+    a, _, _ = pre if pre is not None else layernorm(x2, ln_w.master, ln_b.master, lc.act)
+    out = torch.empty((M, C), dtype=torch.float32, device=x.device)
+    ops.ffn_fwd_f32(a, w1.operand(lc.act), b1.master, w2.operand(lc.act), b2.master, x2, out)
+    return out.view(B, T, C)
+
+
 class FFNSublayerFn(torch.autograd.Function):
     """x + Dropout(W2 relu(W1 ln2(x) + b1) + b2)   (GPT1.py:164, 142-147)."""
 

@@ -208,6 +208,10 @@ class Block(nn.Module):
         if nxt is not None and (att is None or not (self.training and att.heads[0].dropout.p > 0)):
             lc2.next_ln = (*nxt._regions(), nxt.eps)
         w1, b1, w2, b2 = self.ffwd.regions()
+        if not torch.is_grad_enabled():   # inference: the fused fp32 FFN where it applies
+            y = Fn.ffn_sublayer_infer(x, lc2, ln2w, ln2b, w1, b1, w2, b2)
+            if y is not None:
+                return y
         return Fn.FFNSublayerFn.apply(x, lc2, ln2w, ln2b, w1, b1, w2, b2, *ln2w.params, *ln2b.params, *w1.params,
                                       *b1.params, *w2.params, *b2.params)
 

@@ -241,6 +241,31 @@ def gemm_resid_layernorm(a: Tensor, w: Tensor, out: Tensor, M: int, N: int, K: i
             "gemm_resid_layernorm")
 
 
+@_op("ffn_fwd_f32", ("out",))
+def ffn_fwd_f32(a: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, resid: Tensor, out: Tensor) -> None:
+    """out = resid + (relu(a @ w1^T + b1) @ w2^T + b2), fp32, one launch (FeedForward in eval) -- the
+    bits of gemm(..., "bias_relu") into an [M, H] buffer then gemm(..., "bias_resid").  Fails
+    (CG_EINVAL) unless ffn_fwd_f32_supported(M, C, H)."""
+    M, C = a.shape
+    H = w1.shape[0]
+    for t, name in ((a, "a"), (w1, "w1"), (b1, "b1"), (w2, "w2"), (b2, "b2"), (resid, "resid"), (out, "out")):
+        if t.dtype != torch.float32 or not t.is_cuda:
+            raise ValueError(f"ffn_fwd_f32: {name} must be a float32 device tensor")
+        if t.dim() == 2 and t.stride(1) != 1:
+            raise ValueError(f"ffn_fwd_f32: {name} must have unit column stride")
+    if tuple(w1.shape) != (H, C) or tuple(w2.shape) != (C, H) or b1.numel() != H or b2.numel() != C or \
+            tuple(resid.shape) != (M, C) or tuple(out.shape) != (M, C):
+        raise ValueError(f"ffn_fwd_f32: shapes a {tuple(a.shape)} w1 {tuple(w1.shape)} w2 {tuple(w2.shape)} "
+                         f"b1 {b1.numel()} b2 {b2.numel()} resid {tuple(resid.shape)} out {tuple(out.shape)}")
+    L.check(L.load().cg_ffn_fwd_f32(M, C, H, L.ptr(a), a.stride(0), L.ptr(w1), w1.stride(0), L.ptr(b1), L.ptr(w2),
+                                    w2.stride(0), L.ptr(b2), L.ptr(resid), resid.stride(0), L.ptr(out), out.stride(0),
+                                    _s(out)), "ffn_fwd_f32")
+
+
+def ffn_fwd_f32_supported(M, C, H):
+    return bool(L.load().cg_ffn_fwd_f32_supported(M, C, H))
+
+
 def gemm_resid_layernorm_supported(M, N, K):
     return bool(L.load().cg_gemm_resid_layernorm_supported(M, N, K))
 

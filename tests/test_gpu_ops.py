@@ -1281,6 +1281,68 @@ def test_gemm_f32_persistent_matches_128x64_bitwise(kind, M, N, K, variant):
     assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
 
 
+@pytest.mark.parametrize("M,C,H,variant", [(65536, 126, 504, 0), (65536, 126, 504, 98), (4129, 126, 504, 0),
+                                           (300, 64, 256, 98), (2049, 128, 2048, 0), (1000, 126, 130, 98),
+                                           (777, 100, 66, 0), (129, 2, 6, 98), (64, 6, 34, 0)])
+def test_ffn_f32_fused_matches_two_gemms(M, C, H, variant):
+    """The fused inference FFN (k_ffn_f32: h in registers, never in memory) against the two fp32 GEMMs
+    it replaces -- bias_relu into an [M, H] buffer, then bias_resid -- under the default dispatch
+    (k_gemm_f32p above 2048 rows) and k_gemm_f32 (gemm_variant 98): bitwise equal, and within fp32
+    rounding of an fp64 reference; ragged M, C below 16 / not a multiple of 16, H not a multiple of 32."""
+    from replicatinggpt_amd import _lib as L
+    lib = L.load()
+    torch.manual_seed(43)
+    a = torch.randn(M, C, device=DEV)
+    w1 = torch.randn(H, C, device=DEV) / C ** 0.5
+    b1 = torch.randn(H, device=DEV) * 0.1
+    w2 = torch.randn(C, H, device=DEV) / H ** 0.5
+    b2 = torch.randn(C, device=DEV) * 0.1
+    resid = torch.randn(M, C, device=DEV)
+    assert ops().ffn_fwd_f32_supported(M, C, H)
+    out = torch.full((M, C), float("nan"), device=DEV)
+    ops().ffn_fwd_f32(a, w1, b1, w2, b2, resid, out)
+    L.check(lib.cg_set_tuning(b"gemm_variant", variant))
+    try:
+        h = torch.full((M, H), float("nan"), device=DEV)
+        ops().gemm(a, w1, h, False, False, False, M, H, C, C, C, H, 2, b1, None, 0, None, 0, 0.0, 0, None, 0, 0.0, 1,
+                   None)
+        ref2 = torch.full((M, C), float("nan"), device=DEV)
+        ops().gemm(h, w2, ref2, False, False, False, M, C, H, H, H, C, 3, b2, resid, C, None, 0, 0.0, 0, None, 0, 0.0,
+                   1, None)
+        torch.cuda.synchronize()
+    finally:
+        L.check(lib.cg_set_tuning(b"gemm_variant", 0))
+    assert not torch.isnan(out).any()
+    assert torch.equal(out.view(torch.int32), ref2.view(torch.int32))
+    rows = slice(0, min(M, 2048))
+    hd = torch.relu(a[rows].double().cpu() @ w1.double().cpu().T + b1.double().cpu())
+    ref = resid[rows].double().cpu() + hd @ w2.double().cpu().T + b2.double().cpu()
+    assert relerr(out[rows], ref) < 1e-5
+
+
+def test_ffn_f32_fused_in_place_and_unsupported():
+    """out may alias resid (the residual stream updated in place); unsupported shapes fail loudly."""
+    from replicatinggpt_amd import _lib as L
+    torch.manual_seed(44)
+    M, C, H = 3000, 126, 504
+    a = torch.randn(M, C, device=DEV)
+    w1 = torch.randn(H, C, device=DEV) / C ** 0.5
+    b1 = torch.randn(H, device=DEV)
+    w2 = torch.randn(C, H, device=DEV) / H ** 0.5
+    b2 = torch.randn(C, device=DEV)
+    x = torch.randn(M, C, device=DEV)
+    out = torch.empty_like(x)
+    ops().ffn_fwd_f32(a, w1, b1, w2, b2, x, out)
+    lib = L.load()
+    L.check(lib.cg_ffn_fwd_f32(M, C, H, L.ptr(a), C, L.ptr(w1), C, L.ptr(b1), L.ptr(w2), H, L.ptr(b2), L.ptr(x), C,
+                               L.ptr(x), C, L.stream_ptr(x.device)))
+    torch.cuda.synchronize()
+    assert torch.equal(x.view(torch.int32), out.view(torch.int32))
+    assert not ops().ffn_fwd_f32_supported(M, 130, H) and not ops().ffn_fwd_f32_supported(M, 127, H)
+    assert lib.cg_ffn_fwd_f32(M, 130, H, L.ptr(a), C, L.ptr(w1), C, L.ptr(b1), L.ptr(w2), H, L.ptr(b2), L.ptr(x), C,
+                              L.ptr(x), C, L.stream_ptr(x.device)) != 0
+
+
 def test_adamw_matches_torch():
     n = 1000
     torch.manual_seed(8)
