@@ -315,6 +315,11 @@ __global__ __launch_bounds__(256) void k_attn_fwd_f32mfma(int64_t T_, int H, int
 // causal work per wave) with the per-group arithmetic of k_attn_fwd_f32mfma unchanged -- the same
 // MFMAs in the same order, the same online softmax over the same 64-key tiles -- so the outputs
 // are bitwise those of the 64-query-block kernel.
+#ifdef CG_F32RES_FASTEXP   // what-if build only (make fastexp): the hardware exp2 path, not bitwise
+#define F32RES_EXP(x) __expf(x)
+#else
+#define F32RES_EXP(x) expf(x)
+#endif
 template <int DP4>
 __global__ __launch_bounds__(512) void k_attn_fwd_f32res(int64_t T_, int H, int D, const float* __restrict__ q,
                                                          const float* __restrict__ k, const float* __restrict__ v,
@@ -396,14 +401,14 @@ __global__ __launch_bounds__(512) void k_attn_fwd_f32res(int64_t T_, int H, int 
             mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
             mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
             const float m_new = fmaxf(m_run, mx);
-            const float alpha = m_new == -INFINITY ? 1.f : expf(m_run - m_new);
+            const float alpha = m_new == -INFINITY ? 1.f : F32RES_EXP(m_run - m_new);
             float ps = 0.f;
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     if (kt < nkt) {
-                        const float p = st[kt][r] == -INFINITY ? 0.f : expf(st[kt][r] - m_new);
+                        const float p = st[kt][r] == -INFINITY ? 0.f : F32RES_EXP(st[kt][r] - m_new);
                         st[kt][r] = p;
                         ps += p;
                     }
