@@ -231,17 +231,19 @@ int cg_gemm_resid_layernorm_supported(int64_t M, int64_t N, int64_t K);
 int cg_gemm_resid_layernorm(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* W, int64_t ldw,
                             float* out, int64_t ldc, const cg_epilogue_t* epi, const float* ln_w, const float* ln_b,
                             void* y, float* mean, float* rstd, float eps, void* stream);
-/* The FeedForward sublayer's forward for inference (GPT1.py:142-147 in eval, no dropout), fp32, in
-   one launch: out = resid + (relu(a W1^T + b1) W2^T + b2), a [M][C] (lda), W1 [H][C] (ldw1),
-   W2 [C][H] (ldw2), resid / out [M][C] (ldr / ldo; out may alias resid) -- bit for bit cg_gemm
-   (fp32, CG_EPI_BIAS_RELU) into an [M][H] buffer followed by cg_gemm (CG_EPI_BIAS_RESID), without
-   the hidden activations in memory.  Only where cg_ffn_fwd_f32_supported(M, C, H) says 1
-   (C <= 128 even, H <= 2048 even); lda / ldw1 / ldw2 even, a / W1 / W2 8-B aligned; else
-   CG_EINVAL.  (Replaces, in generate()'s window, the two Linear calls of FeedForward.net.)      */
+/* The FeedForward sublayer's forward for inference (GPT1.py:142-147,164 in eval, no dropout), fp32,
+   in one launch: out = resid + (relu(a' W1^T + b1) W2^T + b2) with a' = LayerNorm(a; ln_w, ln_b,
+   eps) (ln_w, ln_b non-NULL: the block's ln2, GPT1.py:164) or a' = a (both NULL); a [M][C] (lda),
+   W1 [H][C] (ldw1), W2 [C][H] (ldw2), resid / out [M][C] (ldr / ldo; out may alias resid) -- bit for
+   bit cg_layernorm_fwd, cg_gemm (fp32, CG_EPI_BIAS_RELU) into an [M][H] buffer and cg_gemm
+   (CG_EPI_BIAS_RESID), without the normalised rows or the hidden activations in memory.  Only where
+   cg_ffn_fwd_f32_supported(M, C, H) says 1 (C <= 128 even, H <= 2048 even); lda / ldw1 / ldw2 even,
+   a / W1 / W2 8-B aligned (with the LayerNorm also ln_w / ln_b, and lda == C); else CG_EINVAL.  (Replaces, in generate()'s window, FeedForward.net's
+   two Linear calls and the ln2 before them.)                                                    */
 int cg_ffn_fwd_f32_supported(int64_t M, int64_t C, int64_t H);
-int cg_ffn_fwd_f32(int64_t M, int64_t C, int64_t H, const float* a, int64_t lda, const float* w1, int64_t ldw1,
-                   const float* b1, const float* w2, int64_t ldw2, const float* b2, const float* resid, int64_t ldr,
-                   float* out, int64_t ldo, void* stream);
+int cg_ffn_fwd_f32(int64_t M, int64_t C, int64_t H, const float* a, int64_t lda, const float* ln_w, const float* ln_b,
+                   float eps, const float* w1, int64_t ldw1, const float* b1, const float* w2, int64_t ldw2,
+                   const float* b2, const float* resid, int64_t ldr, float* out, int64_t ldo, void* stream);
 /* column sums of a [rows, N] matrix (bias gradients): out[n] (=|+=) sum_m X[m,n]            */
 int64_t cg_colsum_workspace(int64_t rows, int64_t N);
 int cg_colsum(const void* X, int x_dtype, int64_t rows, int64_t N, int64_t ldx, float* out, int accumulate,

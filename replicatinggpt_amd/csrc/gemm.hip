@@ -18,6 +18,7 @@
 
 #include "defer.h"
 #include "gemm_common.h"
+#include "ln_fwd.h"
 
 using namespace cg;
 
@@ -637,11 +638,14 @@ bool launch_f32p(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, c
 // (test_ffn_f32_fused_matches_two_gemms).  C <= 128 even, H <= 2048 even, lda / ldw1 / ldw2 even.
 constexpr int FFN_LD1 = 33, FFN_LD2 = 132, FFN_STAGE = 32 * FFN_LD2;   // W1 [128 k][32 + 1], W2 [32 unit][128 + 4]
 
+template <bool LN>
 __global__ __launch_bounds__(256, 2) void k_ffn_f32(int64_t M, int C, int H, const float* __restrict__ a, int64_t lda,
                                                     const float* __restrict__ w1, int64_t ldw1,
                                                     const float* __restrict__ b1, const float* __restrict__ w2,
                                                     int64_t ldw2, const float* __restrict__ b2,
-                                                    const float* resid, int64_t ldr, float* out, int64_t ldo) {
+                                                    const float* resid, int64_t ldr, float* out, int64_t ldo,
+                                                    const float* __restrict__ ln_w, const float* __restrict__ ln_b,
+                                                    float eps) {
     __shared__ __attribute__((aligned(16))) float sm[2][FFN_STAGE];   // 33.8 KB
     __shared__ float sb1[2048], sb2[128];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
@@ -651,10 +655,50 @@ __global__ __launch_bounds__(256, 2) void k_ffn_f32(int64_t M, int C, int H, con
     for (int i = tid; i < H; i += 256) sb1[i] = b1[i];
     for (int i = tid; i < C; i += 256) sb2[i] = b2[i];
 
-    // the wave's a rows in GEMM 1's B-operand layout: lane (l32, h) loads a[row][4t + 2h, +1]; one
-    // swap of h1's .x with h0's .y leaves xr[2t] = a[row][4t + h], xr[2t + 1] = a[row][4t + 2 + h]
     float xr[64];
-    {
+    if constexpr (LN) {
+        // a = LayerNorm(x; ln_w, ln_b) of the wave's rows, with k_ln_fwd's own row body (ln_fwd.h
+        // ln_fwd_row: one wave per row, lane l holding elements 2l, 2l+1) -- the same bits -- into a
+        // per-wave LDS scratch in the ring (16 rows per pass, row stride 130 floats), read back in
+        // GEMM 1's B-operand layout: xr[s] = a[row][2s + h]
+        constexpr int LDR = 130;
+        float* scr = &sm[0][0] + w * 16 * LDR;
+        const float invC = 1.0f / (float)C;
+        float wv[1][2] = {{0.f, 0.f}}, bv[1][2] = {{0.f, 0.f}};
+        if (2 * lane < C) {
+            wv[0][0] = ln_w[2 * lane], wv[0][1] = ln_w[2 * lane + 1];
+            bv[0][0] = ln_b[2 * lane], bv[0][1] = ln_b[2 * lane + 1];
+        }
+#pragma unroll 1
+        for (int pass = 0; pass < 2; ++pass) {
+            float v[16][1][2];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int64_t row = mw + 16 * pass + i < M ? mw + 16 * pass + i : M - 1;
+                if (2 * lane < C) {
+                    const float2 t = *(const float2*)(a + row * lda + 2 * lane);
+                    v[i][0][0] = t.x, v[i][0][1] = t.y;
+                } else {
+                    v[i][0][0] = v[i][0][1] = 0.f;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                float mu, rs;
+                ln_fwd_row<2, 1, float, false>(v[i], wv, bv, C, invC, eps, lane, scr + i * LDR, mu, rs);
+            }
+            if ((l32 >> 4) == pass) {
+#pragma unroll
+                for (int s = 0; s < 64; ++s) {
+                    const int k = 2 * s + h;
+                    xr[s] = k < C ? scr[(l32 & 15) * LDR + k] : 0.f;
+                }
+            }
+        }
+        __syncthreads();   // the scratch is the ring's first stage
+    } else {
+        // the wave's a rows in GEMM 1's B-operand layout: lane (l32, h) loads a[row][4t + 2h, +1]; one
+        // swap of h1's .x with h0's .y leaves xr[2t] = a[row][4t + h], xr[2t + 1] = a[row][4t + 2 + h]
         const int64_t row = mw + l32 < M ? mw + l32 : M - 1;
         const float* ar = a + row * lda;
         float2 v[32];
@@ -1373,9 +1417,10 @@ extern "C" int64_t cg_gemm_workspace(int64_t M, int64_t N, int split_k) {
 
 extern "C" int cg_ffn_fwd_f32_supported(int64_t M, int64_t C, int64_t H) { return ffn_f32_supported(M, C, H) ? 1 : 0; }
 
-extern "C" int cg_ffn_fwd_f32(int64_t M, int64_t C, int64_t H, const float* a, int64_t lda, const float* w1,
-                              int64_t ldw1, const float* b1, const float* w2, int64_t ldw2, const float* b2,
-                              const float* resid, int64_t ldr, float* out, int64_t ldo, void* stream) {
+extern "C" int cg_ffn_fwd_f32(int64_t M, int64_t C, int64_t H, const float* a, int64_t lda, const float* ln_w,
+                              const float* ln_b, float eps, const float* w1, int64_t ldw1, const float* b1,
+                              const float* w2, int64_t ldw2, const float* b2, const float* resid, int64_t ldr,
+                              float* out, int64_t ldo, void* stream) {
     CG_REQUIRE(ffn_f32_supported(M, C, H),
                "cg_ffn_fwd_f32: unsupported shape M=%lld C=%lld H=%lld (C <= 128 even, H <= 2048 even)", (long long)M,
                (long long)C, (long long)H);
@@ -1384,8 +1429,18 @@ extern "C" int cg_ffn_fwd_f32(int64_t M, int64_t C, int64_t H, const float* a, i
                    ldo >= C && (int64_t)H * ldw1 < ((int64_t)1 << 31) && C * ldw2 < ((int64_t)1 << 31),
                "cg_ffn_fwd_f32: bad leading dimensions");
     CG_REQUIRE((((uintptr_t)a | (uintptr_t)w1 | (uintptr_t)w2) & 7) == 0, "cg_ffn_fwd_f32: a, w1, w2 must be 8-B aligned");
-    k_ffn_f32<<<(unsigned)((M + 127) / 128), 256, 0, (hipStream_t)stream>>>(M, (int)C, (int)H, a, lda, w1, ldw1, b1, w2,
-                                                                            ldw2, b2, resid, ldr, out, ldo);
+    CG_REQUIRE(!ln_w == !ln_b, "cg_ffn_fwd_f32: ln_w and ln_b both or neither");
+    // (k_ln_fwd's narrow-row body -- the one the in-launch LayerNorm repeats -- is cg_layernorm_fwd's
+    // choice for C <= 128 even with 8-B aligned x / w / b)
+    CG_REQUIRE(!ln_w || ((((uintptr_t)ln_w | (uintptr_t)ln_b) & 7) == 0 && lda == C),
+               "cg_ffn_fwd_f32: ln_w / ln_b must be 8-B aligned and a dense (lda == C) with the LayerNorm");
+    const dim3 grid((unsigned)((M + 127) / 128));
+    if (ln_w)
+        k_ffn_f32<true><<<grid, 256, 0, (hipStream_t)stream>>>(M, (int)C, (int)H, a, lda, w1, ldw1, b1, w2, ldw2, b2,
+                                                                resid, ldr, out, ldo, ln_w, ln_b, eps);
+    else
+        k_ffn_f32<false><<<grid, 256, 0, (hipStream_t)stream>>>(M, (int)C, (int)H, a, lda, w1, ldw1, b1, w2, ldw2, b2,
+                                                                 resid, ldr, out, ldo, nullptr, nullptr, 0.f);
     CG_LAUNCH_CHECK("cg_ffn_fwd_f32");
     return CG_OK;
 }

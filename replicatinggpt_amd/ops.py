@@ -242,24 +242,31 @@ def gemm_resid_layernorm(a: Tensor, w: Tensor, out: Tensor, M: int, N: int, K: i
 
 
 @_op("ffn_fwd_f32", ("out",))
-def ffn_fwd_f32(a: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, resid: Tensor, out: Tensor) -> None:
-    """out = resid + (relu(a @ w1^T + b1) @ w2^T + b2), fp32, one launch (FeedForward in eval) -- the
-    bits of gemm(..., "bias_relu") into an [M, H] buffer then gemm(..., "bias_resid").  Fails
-    (CG_EINVAL) unless ffn_fwd_f32_supported(M, C, H)."""
+def ffn_fwd_f32(a: Tensor, ln_w: Optional[Tensor], ln_b: Optional[Tensor], eps: float, w1: Tensor, b1: Tensor,
+                w2: Tensor, b2: Tensor, resid: Tensor, out: Tensor) -> None:
+    """out = resid + (relu(a' @ w1^T + b1) @ w2^T + b2), a' = LayerNorm(a; ln_w, ln_b, eps) (or a when
+    ln_w is None), fp32, one launch (FeedForward + its ln2 in eval) -- the bits of layernorm_fwd, then
+    gemm(..., "bias_relu") into an [M, H] buffer, then gemm(..., "bias_resid").  Fails (CG_EINVAL)
+    unless ffn_fwd_f32_supported(M, C, H)."""
     M, C = a.shape
     H = w1.shape[0]
-    for t, name in ((a, "a"), (w1, "w1"), (b1, "b1"), (w2, "w2"), (b2, "b2"), (resid, "resid"), (out, "out")):
+    for t, name in ((a, "a"), (w1, "w1"), (b1, "b1"), (w2, "w2"), (b2, "b2"), (resid, "resid"), (out, "out"),
+                    (ln_w, "ln_w"), (ln_b, "ln_b")):
+        if t is None:
+            continue
         if t.dtype != torch.float32 or not t.is_cuda:
             raise ValueError(f"ffn_fwd_f32: {name} must be a float32 device tensor")
         if t.dim() == 2 and t.stride(1) != 1:
             raise ValueError(f"ffn_fwd_f32: {name} must have unit column stride")
+    if (ln_w is None) != (ln_b is None) or (ln_w is not None and (ln_w.numel() != C or ln_b.numel() != C)):
+        raise ValueError("ffn_fwd_f32: ln_w and ln_b both [C] or both None")
     if tuple(w1.shape) != (H, C) or tuple(w2.shape) != (C, H) or b1.numel() != H or b2.numel() != C or \
             tuple(resid.shape) != (M, C) or tuple(out.shape) != (M, C):
         raise ValueError(f"ffn_fwd_f32: shapes a {tuple(a.shape)} w1 {tuple(w1.shape)} w2 {tuple(w2.shape)} "
                          f"b1 {b1.numel()} b2 {b2.numel()} resid {tuple(resid.shape)} out {tuple(out.shape)}")
-    L.check(L.load().cg_ffn_fwd_f32(M, C, H, L.ptr(a), a.stride(0), L.ptr(w1), w1.stride(0), L.ptr(b1), L.ptr(w2),
-                                    w2.stride(0), L.ptr(b2), L.ptr(resid), resid.stride(0), L.ptr(out), out.stride(0),
-                                    _s(out)), "ffn_fwd_f32")
+    L.check(L.load().cg_ffn_fwd_f32(M, C, H, L.ptr(a), a.stride(0), L.ptr(ln_w), L.ptr(ln_b), eps, L.ptr(w1),
+                                    w1.stride(0), L.ptr(b1), L.ptr(w2), w2.stride(0), L.ptr(b2), L.ptr(resid),
+                                    resid.stride(0), L.ptr(out), out.stride(0), _s(out)), "ffn_fwd_f32")
 
 
 def ffn_fwd_f32_supported(M, C, H):

@@ -1281,26 +1281,35 @@ def test_gemm_f32_persistent_matches_128x64_bitwise(kind, M, N, K, variant):
     assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
 
 
+@pytest.mark.parametrize("ln", [False, True])
 @pytest.mark.parametrize("M,C,H,variant", [(65536, 126, 504, 0), (65536, 126, 504, 98), (4129, 126, 504, 0),
                                            (300, 64, 256, 98), (2049, 128, 2048, 0), (1000, 126, 130, 98),
                                            (777, 100, 66, 0), (129, 2, 6, 98), (64, 6, 34, 0)])
-def test_ffn_f32_fused_matches_two_gemms(M, C, H, variant):
-    """The fused inference FFN (k_ffn_f32: h in registers, never in memory) against the two fp32 GEMMs
-    it replaces -- bias_relu into an [M, H] buffer, then bias_resid -- under the default dispatch
-    (k_gemm_f32p above 2048 rows) and k_gemm_f32 (gemm_variant 98): bitwise equal, and within fp32
-    rounding of an fp64 reference; ragged M, C below 16 / not a multiple of 16, H not a multiple of 32."""
+def test_ffn_f32_fused_matches_two_gemms(M, C, H, variant, ln):
+    """The fused inference FFN (k_ffn_f32: h in registers, never in memory; with ln, the block's ln2
+    computed in the launch with k_ln_fwd's row body) against what it replaces -- [layernorm_fwd,]
+    bias_relu GEMM into an [M, H] buffer, bias_resid GEMM -- under the default dispatch (k_gemm_f32p
+    above 2048 rows) and k_gemm_f32 (gemm_variant 98): bitwise equal, and within fp32 rounding of an
+    fp64 reference; ragged M, C below 16 / not a multiple of 16, H not a multiple of 32."""
     from replicatinggpt_amd import _lib as L
     lib = L.load()
     torch.manual_seed(43)
-    a = torch.randn(M, C, device=DEV)
+    x = torch.randn(M, C, device=DEV)
     w1 = torch.randn(H, C, device=DEV) / C ** 0.5
     b1 = torch.randn(H, device=DEV) * 0.1
     w2 = torch.randn(C, H, device=DEV) / H ** 0.5
     b2 = torch.randn(C, device=DEV) * 0.1
     resid = torch.randn(M, C, device=DEV)
+    lw = 1.0 + 0.1 * torch.randn(C, device=DEV)
+    lb = 0.1 * torch.randn(C, device=DEV)
     assert ops().ffn_fwd_f32_supported(M, C, H)
     out = torch.full((M, C), float("nan"), device=DEV)
-    ops().ffn_fwd_f32(a, w1, b1, w2, b2, resid, out)
+    ops().ffn_fwd_f32(x, lw if ln else None, lb if ln else None, 1e-5, w1, b1, w2, b2, resid, out)
+    if ln:
+        a = torch.full((M, C), float("nan"), device=DEV)
+        ops().layernorm_fwd(x, lw, lb, a, torch.empty(M, device=DEV), torch.empty(M, device=DEV), 1e-5)
+    else:
+        a = x
     L.check(lib.cg_set_tuning(b"gemm_variant", variant))
     try:
         h = torch.full((M, H), float("nan"), device=DEV)
@@ -1315,7 +1324,10 @@ def test_ffn_f32_fused_matches_two_gemms(M, C, H, variant):
     assert not torch.isnan(out).any()
     assert torch.equal(out.view(torch.int32), ref2.view(torch.int32))
     rows = slice(0, min(M, 2048))
-    hd = torch.relu(a[rows].double().cpu() @ w1.double().cpu().T + b1.double().cpu())
+    ad = x[rows].double().cpu()
+    if ln:
+        ad = torch.nn.functional.layer_norm(ad, (C,), lw.double().cpu(), lb.double().cpu(), 1e-5)
+    hd = torch.relu(ad @ w1.double().cpu().T + b1.double().cpu())
     ref = resid[rows].double().cpu() + hd @ w2.double().cpu().T + b2.double().cpu()
     assert relerr(out[rows], ref) < 1e-5
 
@@ -1332,15 +1344,15 @@ def test_ffn_f32_fused_in_place_and_unsupported():
     b2 = torch.randn(C, device=DEV)
     x = torch.randn(M, C, device=DEV)
     out = torch.empty_like(x)
-    ops().ffn_fwd_f32(a, w1, b1, w2, b2, x, out)
+    ops().ffn_fwd_f32(a, None, None, 0.0, w1, b1, w2, b2, x, out)
     lib = L.load()
-    L.check(lib.cg_ffn_fwd_f32(M, C, H, L.ptr(a), C, L.ptr(w1), C, L.ptr(b1), L.ptr(w2), H, L.ptr(b2), L.ptr(x), C,
-                               L.ptr(x), C, L.stream_ptr(x.device)))
+    L.check(lib.cg_ffn_fwd_f32(M, C, H, L.ptr(a), C, None, None, 0.0, L.ptr(w1), C, L.ptr(b1), L.ptr(w2), H,
+                               L.ptr(b2), L.ptr(x), C, L.ptr(x), C, L.stream_ptr(x.device)))
     torch.cuda.synchronize()
     assert torch.equal(x.view(torch.int32), out.view(torch.int32))
     assert not ops().ffn_fwd_f32_supported(M, 130, H) and not ops().ffn_fwd_f32_supported(M, 127, H)
-    assert lib.cg_ffn_fwd_f32(M, 130, H, L.ptr(a), C, L.ptr(w1), C, L.ptr(b1), L.ptr(w2), H, L.ptr(b2), L.ptr(x), C,
-                              L.ptr(x), C, L.stream_ptr(x.device)) != 0
+    assert lib.cg_ffn_fwd_f32(M, 130, H, L.ptr(a), C, None, None, 0.0, L.ptr(w1), C, L.ptr(b1), L.ptr(w2), H,
+                              L.ptr(b2), L.ptr(x), C, L.ptr(x), C, L.stream_ptr(x.device)) != 0
 
 
 def test_adamw_matches_torch():
