@@ -655,68 +655,6 @@ __global__ __launch_bounds__(256, 2) void k_ffn_f32(int64_t M, int C, int H, con
     for (int i = tid; i < H; i += 256) sb1[i] = b1[i];
     for (int i = tid; i < C; i += 256) sb2[i] = b2[i];
 
-    float xr[64];
-    if constexpr (LN) {
-        // a = LayerNorm(x; ln_w, ln_b) of the wave's rows, with k_ln_fwd's own row body (ln_fwd.h
-        // ln_fwd_row: one wave per row, lane l holding elements 2l, 2l+1) -- the same bits -- into a
-        // per-wave LDS scratch in the ring (16 rows per pass, row stride 130 floats), read back in
-        // GEMM 1's B-operand layout: xr[s] = a[row][2s + h]
-        constexpr int LDR = 130;
-        float* scr = &sm[0][0] + w * 16 * LDR;
-        const float invC = 1.0f / (float)C;
-        float wv[1][2] = {{0.f, 0.f}}, bv[1][2] = {{0.f, 0.f}};
-        if (2 * lane < C) {
-            wv[0][0] = ln_w[2 * lane], wv[0][1] = ln_w[2 * lane + 1];
-            bv[0][0] = ln_b[2 * lane], bv[0][1] = ln_b[2 * lane + 1];
-        }
-#pragma unroll 1
-        for (int pass = 0; pass < 2; ++pass) {
-            float v[16][1][2];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int64_t row = mw + 16 * pass + i < M ? mw + 16 * pass + i : M - 1;
-                if (2 * lane < C) {
-                    const float2 t = *(const float2*)(a + row * lda + 2 * lane);
-                    v[i][0][0] = t.x, v[i][0][1] = t.y;
-                } else {
-                    v[i][0][0] = v[i][0][1] = 0.f;
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                float mu, rs;
-                ln_fwd_row<2, 1, float, false>(v[i], wv, bv, C, invC, eps, lane, scr + i * LDR, mu, rs);
-            }
-            if ((l32 >> 4) == pass) {
-#pragma unroll
-                for (int s = 0; s < 64; ++s) {
-                    const int k = 2 * s + h;
-                    xr[s] = k < C ? scr[(l32 & 15) * LDR + k] : 0.f;
-                }
-            }
-        }
-        __syncthreads();   // the scratch is the ring's first stage
-    } else {
-        // the wave's a rows in GEMM 1's B-operand layout: lane (l32, h) loads a[row][4t + 2h, +1]; one
-        // swap of h1's .x with h0's .y leaves xr[2t] = a[row][4t + h], xr[2t + 1] = a[row][4t + 2 + h]
-        const int64_t row = mw + l32 < M ? mw + l32 : M - 1;
-        const float* ar = a + row * lda;
-        float2 v[32];
-#pragma unroll
-        for (int t = 0; t < 32; ++t) {
-            const int k = 4 * t + 2 * h;
-            v[t] = *(const float2*)(ar + (k < C ? k : C - 2));
-            if (k >= C) v[t] = make_float2(0.f, 0.f);
-        }
-#pragma unroll
-        for (int t = 0; t < 32; ++t) {
-            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[t].x), __float_as_uint(v[t].y), false,
-                                                            false);
-            xr[2 * t] = __uint_as_float(r[0]);
-            xr[2 * t + 1] = __uint_as_float(r[1]);
-        }
-    }
-
     // slice staging, 8 float2 per thread.  kind 0: W1 rows 32 c + (tid >> 6) + 4 i at k = 2 (tid & 63)
     // (a wave reads one 512-B row), stored [k][unit] with row stride FFN_LD1; kind 1: W2 rows
     // (tid >> 4) + 16 i at unit 32 c + 2 (tid & 15), stored [unit][column] with row stride FFN_LD2
@@ -750,6 +688,67 @@ __global__ __launch_bounds__(256, 2) void k_ffn_f32(int64_t M, int C, int H, con
             S[(kk + 1) * LD + r] = rk ? ra[i].y : 0.f;
         }
     };
+    load(0, 0);   // the first W1 slice in flight under the a / LayerNorm prologue
+
+    float xr[64];
+    if constexpr (LN) {
+        // a = LayerNorm(x; ln_w, ln_b) of the wave's rows, with k_ln_fwd's own row body (ln_fwd.h
+        // ln_fwd_row: one wave per row, lane l holding elements 2l, 2l+1) -- the same bits -- into a
+        // per-wave LDS scratch in the ring (16 rows per pass, row stride 130 floats), read back in
+        // GEMM 1's B-operand layout: xr[s] = a[row][2s + h]
+        constexpr int LDR = 130;
+        float* scr = &sm[0][0] + w * 16 * LDR;
+        const float invC = 1.0f / (float)C;
+        float wv[1][2] = {{0.f, 0.f}}, bv[1][2] = {{0.f, 0.f}};
+        if (2 * lane < C) {
+            wv[0][0] = ln_w[2 * lane], wv[0][1] = ln_w[2 * lane + 1];
+            bv[0][0] = ln_b[2 * lane], bv[0][1] = ln_b[2 * lane + 1];
+        }
+        float v[32][1][2];   // all 32 rows in flight at once (one load latency, not two)
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            const int64_t row = mw + i < M ? mw + i : M - 1;
+            const float2 t = *(const float2*)(a + row * lda + (2 * lane < C ? 2 * lane : 0));
+            v[i][0][0] = 2 * lane < C ? t.x : 0.f;
+            v[i][0][1] = 2 * lane < C ? t.y : 0.f;
+        }
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                float mu, rs;
+                ln_fwd_row<2, 1, float, false>(v[16 * pass + i], wv, bv, C, invC, eps, lane, scr + i * LDR, mu, rs);
+            }
+            if ((l32 >> 4) == pass) {
+#pragma unroll
+                for (int s = 0; s < 64; ++s) {
+                    const int k = 2 * s + h;
+                    xr[s] = k < C ? scr[(l32 & 15) * LDR + k] : 0.f;
+                }
+            }
+        }
+        __syncthreads();   // the scratch is the ring's first stage
+    } else {
+        // the wave's a rows in GEMM 1's B-operand layout: lane (l32, h) loads a[row][4t + 2h, +1]; one
+        // swap of h1's .x with h0's .y leaves xr[2t] = a[row][4t + h], xr[2t + 1] = a[row][4t + 2 + h]
+        const int64_t row = mw + l32 < M ? mw + l32 : M - 1;
+        const float* ar = a + row * lda;
+        float2 v[32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) {
+            const int k = 4 * t + 2 * h;
+            v[t] = *(const float2*)(ar + (k < C ? k : C - 2));
+            if (k >= C) v[t] = make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int t = 0; t < 32; ++t) {
+            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[t].x), __float_as_uint(v[t].y), false,
+                                                            false);
+            xr[2 * t] = __uint_as_float(r[0]);
+            xr[2 * t + 1] = __uint_as_float(r[1]);
+        }
+    }
+
     int stc = 0;
     // one ring step: the staged slice (chunk c, kind) to LDS, barrier, the following slice's load;
     // returns the stage to compute from
@@ -767,7 +766,6 @@ __global__ __launch_bounds__(256, 2) void k_ffn_f32(int64_t M, int C, int H, con
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[j] = fv16f{};
     const int nst1 = kpad1 / 2;   // GEMM 1 k2-steps (<= 64)
-    load(0, 0);
 #pragma unroll 1
     for (int c = 0; c < nc; ++c) {
         // GEMM 1: D (hidden units 32 c.., the wave's rows) over k: one accumulator chain
