@@ -778,6 +778,7 @@ class AttnSublayerFn(torch.autograd.Function):
 # generate()'s fp32 window blocks run the FeedForward as one fused launch (ops.ffn_fwd_f32: the hidden
 # activations never reach HBM); CHARPT_FFN_FUSED=0 keeps the two GEMMs (A/B)
 FFN_FUSED = os.environ.get("CHARPT_FFN_FUSED", "1") == "1"
+FFN_LN = os.environ.get("CHARPT_FFN_LN", "1") == "1"   # ln2 inside that launch (0: its own launch)
 
 
 def ffn_sublayer_infer(x, lc, ln_w, ln_b, w1, b1, w2, b2):
@@ -796,7 +797,7 @@ def ffn_sublayer_infer(x, lc, ln_w, ln_b, w1, b1, w2, b2):
     out = torch.empty((M, C), dtype=torch.float32, device=x.device)
     pre = pre_ln(x, ln_w, ln_b, lc.act)
     lw, lb = ln_w.master, ln_b.master
-    if pre is None and ((lw.data_ptr() | lb.data_ptr() | x2.data_ptr()) & 7) == 0:
+    if FFN_LN and pre is None and ((lw.data_ptr() | lb.data_ptr() | x2.data_ptr()) & 7) == 0:
         # ln2 inside the launch: k_ln_fwd's narrow-row body, cg_layernorm_fwd's choice for these pointers
         ops.ffn_fwd_f32(x2, lw, lb, 1e-5, w1.operand(lc.act), b1.master, w2.operand(lc.act), b2.master, x2, out)
     else:
