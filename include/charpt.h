@@ -231,6 +231,18 @@ int cg_gemm_resid_layernorm_supported(int64_t M, int64_t N, int64_t K);
 int cg_gemm_resid_layernorm(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* W, int64_t ldw,
                             float* out, int64_t ldc, const cg_epilogue_t* epi, const float* ln_w, const float* ln_b,
                             void* y, float* mean, float* rstd, float eps, void* stream);
+/* A Linear over rows of K <= 128 for inference, fp32, optionally with the LayerNorm before it in the
+   same launch: out = [resid +] (a' W^T [+ bias]), a' = LayerNorm(a; ln_w, ln_b, eps) (ln_w, ln_b
+   non-NULL: the block's ln1 before the QKV product, GPT1.py:111-112,163) or a' = a; a [M][K] (lda),
+   W [N][K] (ldw), resid / out [M][N] (ldr / ldo) -- bit for bit [cg_layernorm_fwd +] cg_gemm (fp32,
+   CG_EPI_STORE / CG_EPI_BIAS / CG_EPI_BIAS_RESID), without the normalised rows in memory.  Only where
+   cg_linear_rows_f32_supported(M, N, K) says 1 (K <= 128 even, N <= 2048 even); lda / ldw / ldo /
+   ldr even, a / W / out / resid 8-B aligned (with the LayerNorm also ln_w / ln_b, lda == K); else
+   CG_EINVAL.                                                                                     */
+int cg_linear_rows_f32_supported(int64_t M, int64_t N, int64_t K);
+int cg_linear_rows_f32(int64_t M, int64_t N, int64_t K, const float* a, int64_t lda, const float* ln_w,
+                       const float* ln_b, float eps, const float* w, int64_t ldw, const float* bias, const float* resid,
+                       int64_t ldr, float* out, int64_t ldo, void* stream);
 /* The FeedForward sublayer's forward for inference (GPT1.py:142-147,164 in eval, no dropout), fp32,
    in one launch: out = resid + (relu(a' W1^T + b1) W2^T + b2) with a' = LayerNorm(a; ln_w, ln_b,
    eps) (ln_w, ln_b non-NULL: the block's ln2, GPT1.py:164) or a' = a (both NULL); a [M][C] (lda),

@@ -636,6 +636,77 @@ bool launch_f32p(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, c
 // is the same k-ordered f32 fma chain over k < ceil16(C) plus b1 then max(., 0), every output the
 // chain over hidden units < ceil16(H) (zero-padded h and W2 past H) plus b2 then resid + v
 // (test_ffn_f32_fused_matches_two_gemms).  C <= 128 even, H <= 2048 even, lda / ldw1 / ldw2 even.
+// The B operand of a transposed row GEMM held in registers for a whole block (k_ffn_f32 GEMM 1,
+// k_linear_f32t): the wave's 32 rows of a [M][C] (C <= 128 even), xr[s] = a'[row mw + l32][2s + h]
+// with a' = a or (LN) LayerNorm(a; ln_w, ln_b, eps) computed with k_ln_fwd's own row body --
+// cg_layernorm_fwd's choice for C <= 128 even and 8-B aligned pointers, so the same bits -- through
+// a per-wave scratch at the start of the caller's LDS ring (>= 4 x 16 x 130 floats; the LN form ends
+// in a block barrier).
+template <bool LN>
+__device__ __forceinline__ void rows_b_operand(float (&xr)[64], float* ring, const float* __restrict__ a, int64_t lda,
+                                               int64_t M, int C, int64_t mw, const float* __restrict__ ln_w,
+                                               const float* __restrict__ ln_b, float eps, int lane, int w) {
+    const int h = lane >> 5, l32 = lane & 31;
+    if constexpr (LN) {
+        // a = LayerNorm(x; ln_w, ln_b) of the wave's rows, with k_ln_fwd's own row body (ln_fwd.h
+        // ln_fwd_row: one wave per row, lane l holding elements 2l, 2l+1) -- the same bits -- into a
+        // per-wave LDS scratch in the ring (16 rows per pass, row stride 130 floats), read back in
+        // GEMM 1's B-operand layout: xr[s] = a[row][2s + h]
+        constexpr int LDR = 130;
+        float* scr = ring + w * 16 * LDR;
+        const float invC = 1.0f / (float)C;
+        float wv[1][2] = {{0.f, 0.f}}, bv[1][2] = {{0.f, 0.f}};
+        if (2 * lane < C) {
+            wv[0][0] = ln_w[2 * lane], wv[0][1] = ln_w[2 * lane + 1];
+            bv[0][0] = ln_b[2 * lane], bv[0][1] = ln_b[2 * lane + 1];
+        }
+        float v[32][1][2];   // all 32 rows in flight at once (one load latency, not two)
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            const int64_t row = mw + i < M ? mw + i : M - 1;
+            const float2 t = *(const float2*)(a + row * lda + (2 * lane < C ? 2 * lane : 0));
+            v[i][0][0] = 2 * lane < C ? t.x : 0.f;
+            v[i][0][1] = 2 * lane < C ? t.y : 0.f;
+        }
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                float mu, rs;
+                ln_fwd_row<2, 1, float, false>(v[16 * pass + i], wv, bv, C, invC, eps, lane, scr + i * LDR, mu, rs);
+            }
+            if ((l32 >> 4) == pass) {
+#pragma unroll
+                for (int s = 0; s < 64; ++s) {
+                    const int k = 2 * s + h;
+                    xr[s] = k < C ? scr[(l32 & 15) * LDR + k] : 0.f;
+                }
+            }
+        }
+        __syncthreads();   // the scratch is the caller's LDS ring
+    } else {
+        // the wave's a rows in GEMM 1's B-operand layout: lane (l32, h) loads a[row][4t + 2h, +1]; one
+        // swap of h1's .x with h0's .y leaves xr[2t] = a[row][4t + h], xr[2t + 1] = a[row][4t + 2 + h]
+        const int64_t row = mw + l32 < M ? mw + l32 : M - 1;
+        const float* ar = a + row * lda;
+        float2 v[32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) {
+            const int k = 4 * t + 2 * h;
+            v[t] = *(const float2*)(ar + (k < C ? k : C - 2));
+            if (k >= C) v[t] = make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int t = 0; t < 32; ++t) {
+            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[t].x), __float_as_uint(v[t].y), false,
+                                                            false);
+            xr[2 * t] = __uint_as_float(r[0]);
+            xr[2 * t + 1] = __uint_as_float(r[1]);
+        }
+    }
+
+}
+
 constexpr int FFN_LD1 = 33, FFN_LD2 = 132, FFN_STAGE = 32 * FFN_LD2;   // W1 [128 k][32 + 1], W2 [32 unit][128 + 4]
 
 template <bool LN>
@@ -691,63 +762,7 @@ __global__ __launch_bounds__(256, 2) void k_ffn_f32(int64_t M, int C, int H, con
     load(0, 0);   // the first W1 slice in flight under the a / LayerNorm prologue
 
     float xr[64];
-    if constexpr (LN) {
-        // a = LayerNorm(x; ln_w, ln_b) of the wave's rows, with k_ln_fwd's own row body (ln_fwd.h
-        // ln_fwd_row: one wave per row, lane l holding elements 2l, 2l+1) -- the same bits -- into a
-        // per-wave LDS scratch in the ring (16 rows per pass, row stride 130 floats), read back in
-        // GEMM 1's B-operand layout: xr[s] = a[row][2s + h]
-        constexpr int LDR = 130;
-        float* scr = &sm[0][0] + w * 16 * LDR;
-        const float invC = 1.0f / (float)C;
-        float wv[1][2] = {{0.f, 0.f}}, bv[1][2] = {{0.f, 0.f}};
-        if (2 * lane < C) {
-            wv[0][0] = ln_w[2 * lane], wv[0][1] = ln_w[2 * lane + 1];
-            bv[0][0] = ln_b[2 * lane], bv[0][1] = ln_b[2 * lane + 1];
-        }
-        float v[32][1][2];   // all 32 rows in flight at once (one load latency, not two)
-#pragma unroll
-        for (int i = 0; i < 32; ++i) {
-            const int64_t row = mw + i < M ? mw + i : M - 1;
-            const float2 t = *(const float2*)(a + row * lda + (2 * lane < C ? 2 * lane : 0));
-            v[i][0][0] = 2 * lane < C ? t.x : 0.f;
-            v[i][0][1] = 2 * lane < C ? t.y : 0.f;
-        }
-#pragma unroll
-        for (int pass = 0; pass < 2; ++pass) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                float mu, rs;
-                ln_fwd_row<2, 1, float, false>(v[16 * pass + i], wv, bv, C, invC, eps, lane, scr + i * LDR, mu, rs);
-            }
-            if ((l32 >> 4) == pass) {
-#pragma unroll
-                for (int s = 0; s < 64; ++s) {
-                    const int k = 2 * s + h;
-                    xr[s] = k < C ? scr[(l32 & 15) * LDR + k] : 0.f;
-                }
-            }
-        }
-        __syncthreads();   // the scratch is the ring's first stage
-    } else {
-        // the wave's a rows in GEMM 1's B-operand layout: lane (l32, h) loads a[row][4t + 2h, +1]; one
-        // swap of h1's .x with h0's .y leaves xr[2t] = a[row][4t + h], xr[2t + 1] = a[row][4t + 2 + h]
-        const int64_t row = mw + l32 < M ? mw + l32 : M - 1;
-        const float* ar = a + row * lda;
-        float2 v[32];
-#pragma unroll
-        for (int t = 0; t < 32; ++t) {
-            const int k = 4 * t + 2 * h;
-            v[t] = *(const float2*)(ar + (k < C ? k : C - 2));
-            if (k >= C) v[t] = make_float2(0.f, 0.f);
-        }
-#pragma unroll
-        for (int t = 0; t < 32; ++t) {
-            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[t].x), __float_as_uint(v[t].y), false,
-                                                            false);
-            xr[2 * t] = __uint_as_float(r[0]);
-            xr[2 * t + 1] = __uint_as_float(r[1]);
-        }
-    }
+    rows_b_operand<LN>(xr, &sm[0][0], a, lda, M, C, mw, ln_w, ln_b, eps, lane, w);
 
     int stc = 0;
     // one ring step: the staged slice (chunk c, kind) to LDS, barrier, the following slice's load;
@@ -860,6 +875,118 @@ __global__ __launch_bounds__(256, 2) void k_ffn_f32(int64_t M, int C, int H, con
             const int n = 32 * j + l32;
             if (m < M && n < C) out[m * ldo + n] = acc[j][r];
         }
+}
+
+// ---------------------------------------------------------------------------------------
+// Row-resident fp32 forward for K <= 128 (generate()'s window: the QKV product with its ln1
+// inside, GPT1.py:111-112,163; the projection with its residual, :136): out[m][n] =
+// epi(a'[m] . W[n]) with a' = a or LayerNorm(a) (rows_b_operand: the wave's 32 rows in 64 registers
+// for the whole block, the LayerNorm with k_ln_fwd's row body).  Computed transposed, D[n][m] =
+// W a'^T, 32 output columns per slice: the W slice (32 rows x all of K) through a 2-stage LDS ring,
+// 64 MFMAs per wave per slice in one accumulator chain, then the slice's epilogue -- each lane holds
+// 4 consecutive columns of its row per 8 (registers 4q..4q+3 = columns 8q + 4h + 0..3), stored as two
+// float2 -- with its residuals loaded under the slice's MFMAs.  Same k-ordered f32 fma chain over
+// ceil16(K) and the same beta-0 epilogue as k_gemm_f32 / k_gemm_f32p: bitwise
+// (test_linear_rows_f32_matches_gemm).  K even <= 128, N even <= 2048.
+template <bool LN, int EK>
+__global__ __launch_bounds__(256, 2) void k_linear_f32t(int64_t M, int C, int N, const float* __restrict__ a,
+                                                        int64_t lda, const float* __restrict__ w, int64_t ldw,
+                                                        const float* __restrict__ bias, const float* resid,
+                                                        int64_t ldr, float* out, int64_t ldo,
+                                                        const float* __restrict__ ln_w,
+                                                        const float* __restrict__ ln_b, float eps) {
+    __shared__ __attribute__((aligned(16))) float sm[2][FFN_STAGE];   // W slices [128 k][32 + 1]
+    __shared__ float sbias[2048];
+    constexpr bool BIAS = EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_BIAS_RESID;
+    const bool hb = BIAS && bias, hr = EK == CG_EPI_BIAS_RESID && resid;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
+    const int64_t mw = (int64_t)blockIdx.x * 128 + 32 * wv;   // the wave's first row
+    const int nst = (C + 15) / 16 * 8;                          // k2-steps over ceil16(K) (<= 64)
+    const int nc = (N + 31) / 32;
+    if (hb)
+        for (int i = tid; i < N; i += 256) sbias[i] = bias[i];
+    // W slice c: rows 32 c + (tid >> 6) + 4 i, k = 2 (tid & 63) (a wave reads one row), stored [k][row]
+    float2 ra[8];
+    bool rk = true;
+    auto load = [&](int c) {
+        const int k = 2 * (tid & 63), r0 = 32 * c + (tid >> 6);
+        rk = k < C;
+        const int kc = rk ? k : C - 2;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {   // cg_linear_rows_f32 checks: rows * ldw under 2^31
+            const int r = r0 + 4 * i < N ? r0 + 4 * i : N - 1;
+            ra[i] = *(const float2*)(w + (uint32_t)(r * (int)ldw + kc));
+        }
+    };
+    auto store = [&](int st) {
+        float* S = sm[st];
+        const int kk = 2 * (tid & 63), r0 = tid >> 6;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            S[kk * FFN_LD1 + r0 + 4 * i] = rk ? ra[i].x : 0.f;
+            S[(kk + 1) * FFN_LD1 + r0 + 4 * i] = rk ? ra[i].y : 0.f;
+        }
+    };
+    load(0);   // in flight under the row / LayerNorm prologue
+    float xr[64];
+    rows_b_operand<LN>(xr, &sm[0][0], a, lda, M, C, mw, ln_w, ln_b, eps, lane, wv);
+    const int64_t m = mw + l32;
+    const int64_t mc = m < M ? m : M - 1;   // residual row, clamped (not branched around)
+    int stc = 0;
+#pragma unroll 1
+    for (int c = 0; c < nc; ++c) {
+        const int st = stc & 1;
+        ++stc;
+        store(st);   // stage st was last read two slices ago, before the previous slice's barrier
+        __syncthreads();
+        if (c + 1 < nc) load(c + 1);
+        float2 rv[4][2];
+        if (hr) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int n = 32 * c + 8 * q + 4 * h + 2 * e;
+                    rv[q][e] = *(const float2*)(resid + mc * ldr + (n < N ? n : N - 2));
+                }
+        }
+        fv16f D = fv16f{};
+        const float* S = sm[st] + h * FFN_LD1 + l32;
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {   // 4 k2-steps per fragment batch
+            if (4 * b >= nst) break;
+            float fa[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) fa[u] = S[2 * (4 * b + u) * FFN_LD1];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) D = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[u], xr[4 * b + u], D, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int n = 32 * c + 8 * q + 4 * h + 2 * e;
+                float v0 = D[4 * q + 2 * e], v1 = D[4 * q + 2 * e + 1];
+                if (hb) {
+                    v0 += sbias[n < N ? n : 0];
+                    v1 += sbias[n + 1 < N ? n + 1 : 0];
+                }
+                if (EK == CG_EPI_BIAS_RELU) {
+                    v0 = fmaxf(v0, 0.f);
+                    v1 = fmaxf(v1, 0.f);
+                }
+                if (hr) {
+                    v0 = rv[q][e].x + v0;
+                    v1 = rv[q][e].y + v1;
+                }
+                if (m < M && n < N) *(float2*)(out + m * ldo + n) = make_float2(v0, v1);
+            }
+    }
+}
+
+bool linear_rows_f32_supported(int64_t M, int64_t N, int64_t K) {
+    return M > 0 && K >= 2 && K <= 128 && K % 2 == 0 && N >= 2 && N <= 2048 && N % 2 == 0;
 }
 
 bool ffn_f32_supported(int64_t M, int64_t C, int64_t H) {
@@ -1411,6 +1538,42 @@ extern "C" int cg_gemm_rowdot_supported(int a_trans, int b_trans, int64_t M, int
 
 extern "C" int64_t cg_gemm_workspace(int64_t M, int64_t N, int split_k) {
     return split_k > 1 ? (int64_t)split_k * M * N * (int64_t)sizeof(float) : 0;
+}
+
+extern "C" int cg_linear_rows_f32_supported(int64_t M, int64_t N, int64_t K) {
+    return linear_rows_f32_supported(M, N, K) ? 1 : 0;
+}
+
+extern "C" int cg_linear_rows_f32(int64_t M, int64_t N, int64_t K, const float* a, int64_t lda, const float* ln_w,
+                                  const float* ln_b, float eps, const float* w, int64_t ldw, const float* bias,
+                                  const float* resid, int64_t ldr, float* out, int64_t ldo, void* stream) {
+    CG_REQUIRE(linear_rows_f32_supported(M, N, K),
+               "cg_linear_rows_f32: unsupported shape M=%lld N=%lld K=%lld (K <= 128 even, N <= 2048 even)",
+               (long long)M, (long long)N, (long long)K);
+    CG_REQUIRE(a && w && out, "cg_linear_rows_f32: null pointer");
+    CG_REQUIRE(lda >= K && lda % 2 == 0 && ldw >= K && ldw % 2 == 0 && ldo >= N && ldo % 2 == 0 &&
+                   (!resid || (ldr >= N && ldr % 2 == 0)) && N * ldw < ((int64_t)1 << 31),
+               "cg_linear_rows_f32: bad leading dimensions");
+    CG_REQUIRE((((uintptr_t)a | (uintptr_t)w | (uintptr_t)out | (uintptr_t)(resid ? resid : out)) & 7) == 0,
+               "cg_linear_rows_f32: a, w, out, resid must be 8-B aligned");
+    CG_REQUIRE(!ln_w == !ln_b, "cg_linear_rows_f32: ln_w and ln_b both or neither");
+    CG_REQUIRE(!ln_w || ((((uintptr_t)ln_w | (uintptr_t)ln_b) & 7) == 0 && lda == K),
+               "cg_linear_rows_f32: ln_w / ln_b must be 8-B aligned and a dense (lda == K) with the LayerNorm");
+    const dim3 grid((unsigned)((M + 127) / 128));
+    hipStream_t st = (hipStream_t)stream;
+#define KL(LN_, EK_) k_linear_f32t<LN_, EK_><<<grid, 256, 0, st>>>(M, (int)K, (int)N, a, lda, w, ldw, bias, resid, ldr, \
+                                                                out, ldo, ln_w, ln_b, eps)
+    const bool ln = ln_w != nullptr;
+    if (resid) {
+        if (ln) KL(true, CG_EPI_BIAS_RESID); else KL(false, CG_EPI_BIAS_RESID);
+    } else if (bias) {
+        if (ln) KL(true, CG_EPI_BIAS); else KL(false, CG_EPI_BIAS);
+    } else {
+        if (ln) KL(true, CG_EPI_STORE); else KL(false, CG_EPI_STORE);
+    }
+#undef KL
+    CG_LAUNCH_CHECK("cg_linear_rows_f32");
+    return CG_OK;
 }
 
 extern "C" int cg_ffn_fwd_f32_supported(int64_t M, int64_t C, int64_t H) { return ffn_f32_supported(M, C, H) ? 1 : 0; }

@@ -114,9 +114,14 @@ class DecodeEngine:
         # last block: K/V for every row, everything else for the final row only
         l = self.L - 1
         x2 = x.reshape(B * T, C)
-        a = self._ln(x2, f"{l}.ln1")
         qkv = torch.empty((B * T, 3 * C), dtype=self.act, device=self.dev)
-        Fn.linear_fwd(a, self._w(f"{l}.qkv"), qkv)
+        lw, lb = self._b(f"{l}.ln1_w"), self._b(f"{l}.ln1_b")
+        if (self.act == torch.float32 and Fn.ATTN_ROWS and Fn.FFN_LN and B * T > 2048
+                and ops.linear_rows_f32_supported(B * T, 3 * C, C)
+                and ((lw.data_ptr() | lb.data_ptr() | x2.data_ptr()) & 7) == 0):
+            ops.linear_rows_f32(x2, lw, lb, 1e-5, self._w(f"{l}.qkv"), None, None, qkv)   # ln1 inside
+        else:
+            Fn.linear_fwd(self._ln(x2, f"{l}.ln1"), self._w(f"{l}.qkv"), qkv)
         qkv32 = qkv if qkv.dtype == torch.float32 else qkv.float()
         qlast = qkv32.view(B, T, 3 * C)[:, T - 1, :]
         o = torch.empty((B, C), dtype=torch.float32, device=self.dev)

@@ -806,6 +806,41 @@ def ffn_sublayer_infer(x, lc, ln_w, ln_b, w1, b1, w2, b2):
     return out.view(B, T, C)
 
 
+# generate()'s fp32 window blocks run the attention sublayer's two Linears as row-resident launches
+# (ops.linear_rows_f32: ln1 inside the QKV launch, the residual inside the projection's);
+# CHARPT_ATTN_ROWS=0 keeps the LayerNorm + GEMM launches (A/B)
+ATTN_ROWS = os.environ.get("CHARPT_ATTN_ROWS", "1") == "1"
+
+
+def attn_sublayer_infer(x, lc, ln_w, ln_b, qkv_w, proj_w, proj_b):
+    """AttnSublayerFn.forward for fp32 inference without autograd (no dropout, nothing saved):
+    ln1 + the QKV product in one launch, the attention, the projection + residual in one launch --
+    the bits of the LayerNorm + GEMM path (tests/test_gpu_model.py::test_fp32_eval_forward_fused_*).
+    None where it does not apply (bf16, dropout, fewer than 2049 rows, a shape the kernel does not
+    take)."""
+    if not ATTN_ROWS or lc.act != torch.float32 or lc.p > 0 or lc.premask is not None:
+        return None
+    B, T, C = x.shape
+    M = B * T
+    if M <= 2048 or not ops.linear_rows_f32_supported(M, 3 * C, C) or not ops.linear_rows_f32_supported(M, C, C):
+        return None
+    act = lc.act
+    x2 = x.reshape(M, C)
+    lw, lb = ln_w.master, ln_b.master
+    qkv = torch.empty((M, 3 * C), dtype=act, device=x.device)
+    pre = pre_ln(x, ln_w, ln_b, act)
+    if FFN_LN and pre is None and ((lw.data_ptr() | lb.data_ptr() | x2.data_ptr()) & 7) == 0:
+        ops.linear_rows_f32(x2, lw, lb, 1e-5, qkv_w.operand(act), None, None, qkv)   # ln1 inside
+    else:
+        a = pre[0] if pre is not None else layernorm(x2, lw, lb, act)[0]
+        ops.linear_rows_f32(a, None, None, 0.0, qkv_w.operand(act), None, None, qkv)
+    o = torch.empty((M, C), dtype=act, device=x.device)
+    attention_fwd(qkv, B, T, lc.n_head, lc.head_size, o, lc.scale, lc.p, lc.seed, lc.rng_call, lc.site, None)
+    out = torch.empty((M, C), dtype=torch.float32, device=x.device)
+    ops.linear_rows_f32(o, None, None, 0.0, proj_w.operand(act), proj_b.master, x2, out)
+    return out.view(B, T, C)
+
+
 class FFNSublayerFn(torch.autograd.Function):
     """x + Dropout(W2 relu(W1 ln2(x) + b1) + b2)   (GPT1.py:164, 142-147)."""
 

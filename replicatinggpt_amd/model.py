@@ -198,8 +198,12 @@ class Block(nn.Module):
         pw, pb = self.sa_heads.proj_regions()
         ln2w, ln2b = self.ln2._regions()
         lc.next_ln = (ln2w, ln2b, self.ln2.eps)   # the projection GEMM also computes ln2 (functional.pre_ln)
-        x = Fn.AttnSublayerFn.apply(x, lc, ln1w, ln1b, qkv, pw, pb, *ln1w.params, *ln1b.params, *qkv.params,
-                                    *pw.params, *pb.params)
+        y = Fn.attn_sublayer_infer(x, lc, ln1w, ln1b, qkv, pw, pb) if not torch.is_grad_enabled() else None
+        if y is not None:   # inference: the row-resident fp32 Linears where they apply
+            x = y
+        else:
+            x = Fn.AttnSublayerFn.apply(x, lc, ln1w, ln1b, qkv, pw, pb, *ln1w.params, *ln1b.params, *qkv.params,
+                                        *pw.params, *pb.params)
         lc2 = self.ffwd.layer_ctx(x)
         # the next block's ln1 or the model's ln_f, from the FFN GEMM's epilogue -- not ln1 when that
         # block's attention drops out: its LayerNorm launch also makes the keep bits (functional.

@@ -241,6 +241,37 @@ def gemm_resid_layernorm(a: Tensor, w: Tensor, out: Tensor, M: int, N: int, K: i
             "gemm_resid_layernorm")
 
 
+@_op("linear_rows_f32", ("out",))
+def linear_rows_f32(a: Tensor, ln_w: Optional[Tensor], ln_b: Optional[Tensor], eps: float, w: Tensor,
+                    bias: Optional[Tensor], resid: Optional[Tensor], out: Tensor) -> None:
+    """out = [resid +] (a' @ w^T [+ bias]), a' = LayerNorm(a; ln_w, ln_b, eps) (or a when ln_w is None),
+    fp32, K <= 128, one launch -- the bits of [layernorm_fwd +] gemm(..., "store" / "bias" /
+    "bias_resid").  Fails (CG_EINVAL) unless linear_rows_f32_supported(M, N, K)."""
+    M, K = a.shape
+    N = w.shape[0]
+    for t, name in ((a, "a"), (w, "w"), (bias, "bias"), (resid, "resid"), (out, "out"), (ln_w, "ln_w"),
+                    (ln_b, "ln_b")):
+        if t is None:
+            continue
+        if t.dtype != torch.float32 or not t.is_cuda:
+            raise ValueError(f"linear_rows_f32: {name} must be a float32 device tensor")
+        if t.dim() == 2 and t.stride(1) != 1:
+            raise ValueError(f"linear_rows_f32: {name} must have unit column stride")
+    if (ln_w is None) != (ln_b is None) or (ln_w is not None and (ln_w.numel() != K or ln_b.numel() != K)):
+        raise ValueError("linear_rows_f32: ln_w and ln_b both [K] or both None")
+    if tuple(w.shape) != (N, K) or (bias is not None and bias.numel() != N) or tuple(out.shape) != (M, N) or \
+            (resid is not None and tuple(resid.shape) != (M, N)):
+        raise ValueError(f"linear_rows_f32: shapes a {tuple(a.shape)} w {tuple(w.shape)} out {tuple(out.shape)}")
+    L.check(L.load().cg_linear_rows_f32(M, N, K, L.ptr(a), a.stride(0), L.ptr(ln_w), L.ptr(ln_b), eps, L.ptr(w),
+                                        w.stride(0), L.ptr(bias), L.ptr(resid),
+                                        resid.stride(0) if resid is not None else 0, L.ptr(out), out.stride(0),
+                                        _s(out)), "linear_rows_f32")
+
+
+def linear_rows_f32_supported(M, N, K):
+    return bool(L.load().cg_linear_rows_f32_supported(M, N, K))
+
+
 @_op("ffn_fwd_f32", ("out",))
 def ffn_fwd_f32(a: Tensor, ln_w: Optional[Tensor], ln_b: Optional[Tensor], eps: float, w1: Tensor, b1: Tensor,
                 w2: Tensor, b2: Tensor, resid: Tensor, out: Tensor) -> None:

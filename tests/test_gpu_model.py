@@ -541,8 +541,10 @@ def test_decode_engine_c5_batch_matches_reference_loop():
 def test_fp32_eval_forward_fused_ffn_bitwise(ffn_ln):
     """The fp32 model's no-grad forward above 2048 rows (generate()'s window, the evaluation forward)
     takes the fused FeedForward launch (functional.ffn_sublayer_infer: ln2 + both Linears, h never in
-    memory); its logits are bitwise those of the LayerNorm + two-GEMM path (CHARPT_FFN_FUSED=0), and
-    the with-grad forward (the training path, h saved) is untouched."""
+    memory) and the row-resident attention Linears (functional.attn_sublayer_infer: ln1 + QKV, the
+    projection + residual); its logits are bitwise those of the LayerNorm + GEMM path
+    (CHARPT_FFN_FUSED=0, CHARPT_ATTN_ROWS=0), and the with-grad forward (the training path) is
+    untouched."""
     from safetensors.torch import load_file
     from replicatinggpt_amd import BigramLanguageModel, GPTConfig
     from replicatinggpt_amd import functional as Fn
@@ -552,16 +554,16 @@ def test_fp32_eval_forward_fused_ffn_bitwise(ffn_ln):
     m = m.to(DEV).eval()
     g = torch.Generator().manual_seed(5)
     idx = torch.randint(0, 65, (12, 256), generator=g).to(DEV)   # 3072 rows
-    saved = (Fn.FFN_FUSED, Fn.FFN_LN)
+    saved = (Fn.FFN_FUSED, Fn.FFN_LN, Fn.ATTN_ROWS)
     outs = []
     try:
         for fused in (True, False):
-            Fn.FFN_FUSED, Fn.FFN_LN = fused, ffn_ln
+            Fn.FFN_FUSED, Fn.FFN_LN, Fn.ATTN_ROWS = fused, ffn_ln, fused
             with torch.no_grad():
                 logits, _ = m(idx)
             outs.append(logits.float().clone())
     finally:
-        Fn.FFN_FUSED, Fn.FFN_LN = saved
+        Fn.FFN_FUSED, Fn.FFN_LN, Fn.ATTN_ROWS = saved
     assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
     logits_g, _ = m(idx)   # autograd forward: the FFNSublayerFn path
     assert torch.equal(logits_g.detach().float().view(torch.int32), outs[1].view(torch.int32))

@@ -1332,6 +1332,54 @@ def test_ffn_f32_fused_matches_two_gemms(M, C, H, variant, ln):
     assert relerr(out[rows], ref) < 1e-5
 
 
+@pytest.mark.parametrize("ln", [False, True])
+@pytest.mark.parametrize("kind", [0, 1, 3])
+@pytest.mark.parametrize("M,N,K,variant", [(65536, 378, 126, 0), (65536, 126, 126, 98), (4129, 70, 128, 0),
+                                           (300, 2, 2, 98), (2049, 2048, 64, 0), (777, 130, 100, 98)])
+def test_linear_rows_f32_matches_gemm(M, N, K, variant, kind, ln):
+    """The row-resident fp32 Linear (k_linear_f32t: the wave's rows in registers, W streamed in 32-column
+    slices; with ln, the LayerNorm before it in the launch) against [layernorm_fwd +] the fp32 GEMM with
+    the same epilogue (store / bias / bias_resid) under the default dispatch (k_gemm_f32p above 2048 rows)
+    and k_gemm_f32 (gemm_variant 98): bitwise equal, and within fp32 rounding of fp64."""
+    from replicatinggpt_amd import _lib as L
+    lib = L.load()
+    torch.manual_seed(45)
+    x = torch.randn(M, K, device=DEV)
+    w = torch.randn(N, K, device=DEV) / K ** 0.5
+    bias = torch.randn(N, device=DEV) if kind else None
+    resid = torch.randn(M, N, device=DEV) if kind == 3 else None
+    lw = 1.0 + 0.1 * torch.randn(K, device=DEV)
+    lb = 0.1 * torch.randn(K, device=DEV)
+    assert ops().linear_rows_f32_supported(M, N, K)
+    out = torch.full((M, N), float("nan"), device=DEV)
+    ops().linear_rows_f32(x, lw if ln else None, lb if ln else None, 1e-5, w, bias, resid, out)
+    if ln:
+        a = torch.full((M, K), float("nan"), device=DEV)
+        ops().layernorm_fwd(x, lw, lb, a, torch.empty(M, device=DEV), torch.empty(M, device=DEV), 1e-5)
+    else:
+        a = x
+    L.check(lib.cg_set_tuning(b"gemm_variant", variant))
+    try:
+        ref2 = torch.full((M, N), float("nan"), device=DEV)
+        ops().gemm(a, w, ref2, False, False, False, M, N, K, K, K, N, kind, bias, resid, N if kind == 3 else 0, None,
+                   0, 0.0, 0, None, 0, 0.0, 1, None)
+        torch.cuda.synchronize()
+    finally:
+        L.check(lib.cg_set_tuning(b"gemm_variant", 0))
+    assert not torch.isnan(out).any()
+    assert torch.equal(out.view(torch.int32), ref2.view(torch.int32))
+    rows = slice(0, min(M, 2048))
+    ad = x[rows].double().cpu()
+    if ln:
+        ad = torch.nn.functional.layer_norm(ad, (K,), lw.double().cpu(), lb.double().cpu(), 1e-5)
+    ref = ad @ w.double().cpu().T
+    if kind:
+        ref = ref + bias.double().cpu()
+    if kind == 3:
+        ref = ref + resid[rows].double().cpu()
+    assert relerr(out[rows], ref) < 1e-5
+
+
 def test_ffn_f32_fused_in_place_and_unsupported():
     """out may alias resid (the residual stream updated in place); unsupported shapes fail loudly."""
     from replicatinggpt_amd import _lib as L
