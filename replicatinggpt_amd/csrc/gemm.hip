@@ -888,32 +888,33 @@ __global__ __launch_bounds__(256, 2) void k_ffn_f32(int64_t M, int C, int H, con
 // float2 -- with its residuals loaded under the slice's MFMAs.  Same k-ordered f32 fma chain over
 // ceil16(K) and the same beta-0 epilogue as k_gemm_f32 / k_gemm_f32p: bitwise
 // (test_linear_rows_f32_matches_gemm).  K even <= 128, N even <= 2048.
-template <bool LN, int EK>
+template <bool LN, int EK, int NB>   // NB: 32-column blocks per slice (independent accumulator chains)
 __global__ __launch_bounds__(256, 2) void k_linear_f32t(int64_t M, int C, int N, const float* __restrict__ a,
                                                         int64_t lda, const float* __restrict__ w, int64_t ldw,
                                                         const float* __restrict__ bias, const float* resid,
                                                         int64_t ldr, float* out, int64_t ldo,
                                                         const float* __restrict__ ln_w,
                                                         const float* __restrict__ ln_b, float eps) {
-    __shared__ __attribute__((aligned(16))) float sm[2][FFN_STAGE];   // W slices [128 k][32 + 1]
+    constexpr int LDW = 32 * NB + 1;   // [128 k][32 NB + 1] per stage
+    __shared__ __attribute__((aligned(16))) float sm[2][128 * LDW];
     __shared__ float sbias[2048];
     constexpr bool BIAS = EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_BIAS_RESID;
     const bool hb = BIAS && bias, hr = EK == CG_EPI_BIAS_RESID && resid;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
     const int64_t mw = (int64_t)blockIdx.x * 128 + 32 * wv;   // the wave's first row
     const int nst = (C + 15) / 16 * 8;                          // k2-steps over ceil16(K) (<= 64)
-    const int nc = (N + 31) / 32;
+    const int nc = (N + 32 * NB - 1) / (32 * NB);
     if (hb)
         for (int i = tid; i < N; i += 256) sbias[i] = bias[i];
-    // W slice c: rows 32 c + (tid >> 6) + 4 i, k = 2 (tid & 63) (a wave reads one row), stored [k][row]
-    float2 ra[8];
+    // W slice c: rows 32 NB c + (tid >> 6) + 4 i, k = 2 (tid & 63) (a wave reads one row), stored [k][row]
+    float2 ra[8 * NB];
     bool rk = true;
     auto load = [&](int c) {
-        const int k = 2 * (tid & 63), r0 = 32 * c + (tid >> 6);
+        const int k = 2 * (tid & 63), r0 = 32 * NB * c + (tid >> 6);
         rk = k < C;
         const int kc = rk ? k : C - 2;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {   // cg_linear_rows_f32 checks: rows * ldw under 2^31
+        for (int i = 0; i < 8 * NB; ++i) {   // cg_linear_rows_f32 checks: rows * ldw under 2^31
             const int r = r0 + 4 * i < N ? r0 + 4 * i : N - 1;
             ra[i] = *(const float2*)(w + (uint32_t)(r * (int)ldw + kc));
         }
@@ -922,9 +923,9 @@ __global__ __launch_bounds__(256, 2) void k_linear_f32t(int64_t M, int C, int N,
         float* S = sm[st];
         const int kk = 2 * (tid & 63), r0 = tid >> 6;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            S[kk * FFN_LD1 + r0 + 4 * i] = rk ? ra[i].x : 0.f;
-            S[(kk + 1) * FFN_LD1 + r0 + 4 * i] = rk ? ra[i].y : 0.f;
+        for (int i = 0; i < 8 * NB; ++i) {
+            S[kk * LDW + r0 + 4 * i] = rk ? ra[i].x : 0.f;
+            S[(kk + 1) * LDW + r0 + 4 * i] = rk ? ra[i].y : 0.f;
         }
     };
     load(0);   // in flight under the row / LayerNorm prologue
@@ -940,48 +941,59 @@ __global__ __launch_bounds__(256, 2) void k_linear_f32t(int64_t M, int C, int N,
         store(st);   // stage st was last read two slices ago, before the previous slice's barrier
         __syncthreads();
         if (c + 1 < nc) load(c + 1);
-        float2 rv[4][2];
+        float2 rv[NB][4][2];
         if (hr) {
+#pragma unroll
+            for (int j = 0; j < NB; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const int n = 32 * (NB * c + j) + 8 * q + 4 * h + 2 * e;
+                        rv[j][q][e] = *(const float2*)(resid + mc * ldr + (n < N ? n : N - 2));
+                    }
+        }
+        fv16f D[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) D[j] = fv16f{};
+        const float* S = sm[st] + h * LDW + l32;
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {   // 4 k2-steps per fragment batch
+            if (4 * b >= nst) break;
+            float fa[4][NB];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < NB; ++j) fa[u][j] = S[2 * (4 * b + u) * LDW + 32 * j];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < NB; ++j)
+                    D[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[u][j], xr[4 * b + u], D[j], 0, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
 #pragma unroll
             for (int q = 0; q < 4; ++q)
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
-                    const int n = 32 * c + 8 * q + 4 * h + 2 * e;
-                    rv[q][e] = *(const float2*)(resid + mc * ldr + (n < N ? n : N - 2));
+                    const int n = 32 * (NB * c + j) + 8 * q + 4 * h + 2 * e;
+                    float v0 = D[j][4 * q + 2 * e], v1 = D[j][4 * q + 2 * e + 1];
+                    if (hb) {
+                        v0 += sbias[n < N ? n : 0];
+                        v1 += sbias[n + 1 < N ? n + 1 : 0];
+                    }
+                    if (EK == CG_EPI_BIAS_RELU) {
+                        v0 = fmaxf(v0, 0.f);
+                        v1 = fmaxf(v1, 0.f);
+                    }
+                    if (hr) {
+                        v0 = rv[j][q][e].x + v0;
+                        v1 = rv[j][q][e].y + v1;
+                    }
+                    if (m < M && n < N) *(float2*)(out + m * ldo + n) = make_float2(v0, v1);
                 }
-        }
-        fv16f D = fv16f{};
-        const float* S = sm[st] + h * FFN_LD1 + l32;
-#pragma unroll
-        for (int b = 0; b < 16; ++b) {   // 4 k2-steps per fragment batch
-            if (4 * b >= nst) break;
-            float fa[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) fa[u] = S[2 * (4 * b + u) * FFN_LD1];
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) D = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[u], xr[4 * b + u], D, 0, 0, 0);
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const int n = 32 * c + 8 * q + 4 * h + 2 * e;
-                float v0 = D[4 * q + 2 * e], v1 = D[4 * q + 2 * e + 1];
-                if (hb) {
-                    v0 += sbias[n < N ? n : 0];
-                    v1 += sbias[n + 1 < N ? n + 1 : 0];
-                }
-                if (EK == CG_EPI_BIAS_RELU) {
-                    v0 = fmaxf(v0, 0.f);
-                    v1 = fmaxf(v1, 0.f);
-                }
-                if (hr) {
-                    v0 = rv[q][e].x + v0;
-                    v1 = rv[q][e].y + v1;
-                }
-                if (m < M && n < N) *(float2*)(out + m * ldo + n) = make_float2(v0, v1);
-            }
     }
 }
 
@@ -1202,6 +1214,7 @@ int launch_generic(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, co
 
 namespace cg {
 int g_gemm_variant = 0;
+int g_linear_rows_nb = 2;   // cg_set_tuning("linear_rows_nb"): k_linear_f32t column blocks per slice (1 / 2)
 int g_gemm_max_grid = 0;
 int g_gemm_group_p8 = 0;   // persistent-kernel tile order (gemm_tile.h tile_rc), cg_set_tuning knobs
 int g_gemm_group_pk = 0;
@@ -1424,6 +1437,11 @@ extern "C" int cg_set_tuning(const char* key, int value) {
         g_gemm_variant = value;
         return CG_OK;
     }
+    if (!strcmp(key, "linear_rows_nb")) {
+        CG_REQUIRE(value == 1 || value == 2, "cg_set_tuning: linear_rows_nb must be 1 or 2");
+        g_linear_rows_nb = value;
+        return CG_OK;
+    }
     if (!strcmp(key, "gemm_max_grid")) {
         g_gemm_max_grid = value;
         return CG_OK;
@@ -1561,8 +1579,16 @@ extern "C" int cg_linear_rows_f32(int64_t M, int64_t N, int64_t K, const float* 
                "cg_linear_rows_f32: ln_w / ln_b must be 8-B aligned and a dense (lda == K) with the LayerNorm");
     const dim3 grid((unsigned)((M + 127) / 128));
     hipStream_t st = (hipStream_t)stream;
-#define KL(LN_, EK_) k_linear_f32t<LN_, EK_><<<grid, 256, 0, st>>>(M, (int)K, (int)N, a, lda, w, ldw, bias, resid, ldr, \
-                                                                out, ldo, ln_w, ln_b, eps)
+    // two 32-column chains per slice (half the barriers per MFMA) unless cg_set_tuning("linear_rows_nb", 1)
+#define KL(LN_, EK_)                                                                                              \
+    do {                                                                                                          \
+        if (g_linear_rows_nb == 1)                                                                                \
+            k_linear_f32t<LN_, EK_, 1><<<grid, 256, 0, st>>>(M, (int)K, (int)N, a, lda, w, ldw, bias, resid, ldr, \
+                                                             out, ldo, ln_w, ln_b, eps);                          \
+        else                                                                                                      \
+            k_linear_f32t<LN_, EK_, 2><<<grid, 256, 0, st>>>(M, (int)K, (int)N, a, lda, w, ldw, bias, resid, ldr, \
+                                                             out, ldo, ln_w, ln_b, eps);                          \
+    } while (0)
     const bool ln = ln_w != nullptr;
     if (resid) {
         if (ln) KL(true, CG_EPI_BIAS_RESID); else KL(false, CG_EPI_BIAS_RESID);
