@@ -997,6 +997,147 @@ __global__ __launch_bounds__(256, 2) void k_linear_f32t(int64_t M, int C, int N,
     }
 }
 
+// The same Linear with 16-row waves on v_mfma_f32_16x16x4_f32 (k_gemm_f32's own instruction):
+// 64-row blocks, 1,024 workgroups at C5 and four per CU (34 KB of LDS, <= 128 VGPRs), so four waves
+// per SIMD instead of two, and two independent 16 x 16 accumulator chains per 32-column slice.  The
+// wave's rows go through an LDS scratch (coalesced row loads, the LayerNorm with k_ln_fwd's row body
+// where asked) and come back as the B operand xr[t] = a'[row li][4t + g] (lane li + 16 g).  D[j] holds
+// output columns 32 c + 16 j + 4 g + r of row li: one float4 of consecutive columns per tile.  Same
+// k-ordered fma chain over ceil16(K) and epilogue as k_gemm_f32: bitwise.
+template <bool LN, int EK>
+__global__ __launch_bounds__(256, 4) void k_linear_f32q(int64_t M, int C, int N, const float* __restrict__ a,
+                                                        int64_t lda, const float* __restrict__ w, int64_t ldw,
+                                                        const float* __restrict__ bias, const float* resid,
+                                                        int64_t ldr, float* out, int64_t ldo,
+                                                        const float* __restrict__ ln_w,
+                                                        const float* __restrict__ ln_b, float eps) {
+    __shared__ __attribute__((aligned(16))) float sm[2][FFN_STAGE];   // W slices [128 k][32 + 1]
+    constexpr bool BIAS = EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_BIAS_RESID;
+    const bool hb = BIAS && bias, hr = EK == CG_EPI_BIAS_RESID && resid;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, li = lane & 15, g = lane >> 4;
+    const int64_t mw = (int64_t)blockIdx.x * 64 + 16 * wv;   // the wave's first row
+    const int nk4 = (C + 15) / 16 * 4;                         // k4-steps over ceil16(K) (<= 32)
+    const int nc = (N + 31) / 32;
+    float2 ra[8];
+    bool rk = true;
+    auto load = [&](int c) {
+        const int k = 2 * (tid & 63), r0 = 32 * c + (tid >> 6);
+        rk = k < C;
+        const int kc = rk ? k : C - 2;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {   // cg_linear_rows_f32 checks: rows * ldw under 2^31
+            const int r = r0 + 4 * i < N ? r0 + 4 * i : N - 1;
+            ra[i] = *(const float2*)(w + (uint32_t)(r * (int)ldw + kc));
+        }
+    };
+    auto store = [&](int st) {
+        float* S = sm[st];
+        const int kk = 2 * (tid & 63), r0 = tid >> 6;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            S[kk * FFN_LD1 + r0 + 4 * i] = rk ? ra[i].x : 0.f;
+            S[(kk + 1) * FFN_LD1 + r0 + 4 * i] = rk ? ra[i].y : 0.f;
+        }
+    };
+    load(0);
+    // the wave's 16 rows: lane l loads elements 2l, 2l+1 of each (k_ln_fwd's layout), LayerNorm in that
+    // layout where asked, into a per-wave scratch [16][130] in the ring, read back as xr
+    float xr[32];
+    {
+        constexpr int LDR = 130;
+        float* scr = &sm[0][0] + wv * 16 * LDR;
+        float v[16][1][2];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int64_t row = mw + i < M ? mw + i : M - 1;
+            const float2 t = *(const float2*)(a + row * lda + (2 * lane < C ? 2 * lane : 0));
+            v[i][0][0] = 2 * lane < C ? t.x : 0.f;
+            v[i][0][1] = 2 * lane < C ? t.y : 0.f;
+        }
+        if constexpr (LN) {
+            const float invC = 1.0f / (float)C;
+            float wl[1][2] = {{0.f, 0.f}}, bl[1][2] = {{0.f, 0.f}};
+            if (2 * lane < C) {
+                wl[0][0] = ln_w[2 * lane], wl[0][1] = ln_w[2 * lane + 1];
+                bl[0][0] = ln_b[2 * lane], bl[0][1] = ln_b[2 * lane + 1];
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                float mu, rs;
+                ln_fwd_row<2, 1, float, false>(v[i], wl, bl, C, invC, eps, lane, scr + i * LDR, mu, rs);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                if (2 * lane < C) *(float2*)(scr + i * LDR + 2 * lane) = make_float2(v[i][0][0], v[i][0][1]);
+        }
+#pragma unroll
+        for (int t = 0; t < 32; ++t) {
+            const int k = 4 * t + g;
+            xr[t] = k < C ? scr[li * LDR + k] : 0.f;
+        }
+        __syncthreads();   // the scratch is the ring's first stage
+    }
+    const int64_t m = mw + li;
+    const int64_t mc = m < M ? m : M - 1;   // residual row, clamped (not branched around)
+    int stc = 0;
+#pragma unroll 1
+    for (int c = 0; c < nc; ++c) {
+        const int st = stc & 1;
+        ++stc;
+        store(st);   // stage st was last read two slices ago, before the previous slice's barrier
+        __syncthreads();
+        if (c + 1 < nc) load(c + 1);
+        float2 rv[2][2];
+        float2 bv[2][2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int n = 32 * c + 16 * j + 4 * g + 2 * e, nn = n < N ? n : N - 2;
+                if (hr) rv[j][e] = *(const float2*)(resid + mc * ldr + nn);
+                if (hb) bv[j][e] = make_float2(bias[nn], bias[nn + 1]);
+            }
+        fv4 D[2] = {fv4{0.f, 0.f, 0.f, 0.f}, fv4{0.f, 0.f, 0.f, 0.f}};
+        const float* S = sm[st] + g * FFN_LD1 + li;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {   // 4 k4-steps per fragment batch
+            if (4 * b >= nk4) break;
+            float fa[4][2];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) fa[u][j] = S[4 * (4 * b + u) * FFN_LD1 + 16 * j];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    D[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[u][j], xr[4 * b + u], D[j], 0, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int n = 32 * c + 16 * j + 4 * g + 2 * e;
+                float v0 = D[j][2 * e], v1 = D[j][2 * e + 1];
+                if (hb) {
+                    v0 += bv[j][e].x;
+                    v1 += bv[j][e].y;
+                }
+                if (EK == CG_EPI_BIAS_RELU) {
+                    v0 = fmaxf(v0, 0.f);
+                    v1 = fmaxf(v1, 0.f);
+                }
+                if (hr) {
+                    v0 = rv[j][e].x + v0;
+                    v1 = rv[j][e].y + v1;
+                }
+                if (m < M && n < N) *(float2*)(out + m * ldo + n) = make_float2(v0, v1);
+            }
+    }
+}
+
 bool linear_rows_f32_supported(int64_t M, int64_t N, int64_t K) {
     return M > 0 && K >= 2 && K <= 128 && K % 2 == 0 && N >= 2 && N <= 2048 && N % 2 == 0;
 }
@@ -1438,7 +1579,7 @@ extern "C" int cg_set_tuning(const char* key, int value) {
         return CG_OK;
     }
     if (!strcmp(key, "linear_rows_nb")) {
-        CG_REQUIRE(value == 1 || value == 2, "cg_set_tuning: linear_rows_nb must be 1 or 2");
+        CG_REQUIRE(value >= 0 && value <= 2, "cg_set_tuning: linear_rows_nb must be 0 (16-row waves), 1 or 2");
         g_linear_rows_nb = value;
         return CG_OK;
     }
@@ -1583,7 +1724,10 @@ extern "C" int cg_linear_rows_f32(int64_t M, int64_t N, int64_t K, const float* 
     // of LDS) -- measured 2 % slower in generate (profiles/r6_linear_rows_gen.txt)
 #define KL(LN_, EK_)                                                                                              \
     do {                                                                                                          \
-        if (g_linear_rows_nb == 1)                                                                                \
+        if (g_linear_rows_nb == 0)                                                                                \
+            k_linear_f32q<LN_, EK_><<<dim3((unsigned)((M + 63) / 64)), 256, 0, st>>>(                             \
+                M, (int)K, (int)N, a, lda, w, ldw, bias, resid, ldr, out, ldo, ln_w, ln_b, eps);                  \
+        else if (g_linear_rows_nb == 1)                                                                           \
             k_linear_f32t<LN_, EK_, 1><<<grid, 256, 0, st>>>(M, (int)K, (int)N, a, lda, w, ldw, bias, resid, ldr, \
                                                              out, ldo, ln_w, ln_b, eps);                          \
         else                                                                                                      \

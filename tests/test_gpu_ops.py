@@ -1352,7 +1352,7 @@ def test_linear_rows_f32_matches_gemm(M, N, K, variant, kind, ln):
     lb = 0.1 * torch.randn(K, device=DEV)
     assert ops().linear_rows_f32_supported(M, N, K)
     outs = []
-    for nb in (2, 1):   # 32-column blocks per slice (cg_set_tuning "linear_rows_nb"; 1 is the default)
+    for nb in (2, 0, 1):   # cg_set_tuning "linear_rows_nb": 32-row waves with 1 / 2 column blocks per slice, 0 16-row waves
         L.check(lib.cg_set_tuning(b"linear_rows_nb", nb))
         try:
             o = torch.full((M, N), float("nan"), device=DEV)
@@ -1361,8 +1361,9 @@ def test_linear_rows_f32_matches_gemm(M, N, K, variant, kind, ln):
         finally:
             L.check(lib.cg_set_tuning(b"linear_rows_nb", 1))
         outs.append(o)
-    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
-    out = outs[1]
+    assert torch.equal(outs[0].view(torch.int32), outs[2].view(torch.int32))
+    assert torch.equal(outs[1].view(torch.int32), outs[2].view(torch.int32))
+    out = outs[2]
     if ln:
         a = torch.full((M, K), float("nan"), device=DEV)
         ops().layernorm_fwd(x, lw, lb, a, torch.empty(M, device=DEV), torch.empty(M, device=DEV), 1e-5)
