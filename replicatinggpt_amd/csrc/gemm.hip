@@ -1355,7 +1355,7 @@ int launch_generic(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, co
 
 namespace cg {
 int g_gemm_variant = 0;
-int g_linear_rows_nb = 1;   // cg_set_tuning("linear_rows_nb"): k_linear_f32t column blocks per slice (1 / 2)
+int g_linear_rows_nb = 0;   // cg_set_tuning("linear_rows_nb"): 0 k_linear_f32q (16-row waves), 1 / 2 k_linear_f32t
 int g_gemm_max_grid = 0;
 int g_gemm_group_p8 = 0;   // persistent-kernel tile order (gemm_tile.h tile_rc), cg_set_tuning knobs
 int g_gemm_group_pk = 0;
@@ -1720,8 +1720,9 @@ extern "C" int cg_linear_rows_f32(int64_t M, int64_t N, int64_t K, const float* 
                "cg_linear_rows_f32: ln_w / ln_b must be 8-B aligned and a dense (lda == K) with the LayerNorm");
     const dim3 grid((unsigned)((M + 127) / 128));
     hipStream_t st = (hipStream_t)stream;
-    // one 32-column chain per slice; cg_set_tuning("linear_rows_nb", 2): two (half the barriers per MFMA, 66 KB
-    // of LDS) -- measured 2 % slower in generate (profiles/r6_linear_rows_gen.txt)
+    // 16-row waves (k_linear_f32q: four waves per SIMD) by default; cg_set_tuning("linear_rows_nb", 1 / 2):
+    // 32-row waves with one / two 32-column chains per slice -- 3.3 % / 5.4 % slower in generate
+    // (profiles/r6_linear_rows_gen.txt)
 #define KL(LN_, EK_)                                                                                              \
     do {                                                                                                          \
         if (g_linear_rows_nb == 0)                                                                                \

@@ -1352,14 +1352,14 @@ def test_linear_rows_f32_matches_gemm(M, N, K, variant, kind, ln):
     lb = 0.1 * torch.randn(K, device=DEV)
     assert ops().linear_rows_f32_supported(M, N, K)
     outs = []
-    for nb in (2, 0, 1):   # cg_set_tuning "linear_rows_nb": 32-row waves with 1 / 2 column blocks per slice, 0 16-row waves
+    for nb in (2, 1, 0):   # cg_set_tuning "linear_rows_nb": 32-row waves with 2 / 1 column blocks per slice, 0 (default) 16-row waves
         L.check(lib.cg_set_tuning(b"linear_rows_nb", nb))
         try:
             o = torch.full((M, N), float("nan"), device=DEV)
             ops().linear_rows_f32(x, lw if ln else None, lb if ln else None, 1e-5, w, bias, resid, o)
             torch.cuda.synchronize()
         finally:
-            L.check(lib.cg_set_tuning(b"linear_rows_nb", 1))
+            L.check(lib.cg_set_tuning(b"linear_rows_nb", 0))
         outs.append(o)
     assert torch.equal(outs[0].view(torch.int32), outs[2].view(torch.int32))
     assert torch.equal(outs[1].view(torch.int32), outs[2].view(torch.int32))
