@@ -1150,173 +1150,6 @@ __global__ __launch_bounds__(256, 4) void k_linear_f32q(int64_t M, int C, int N,
     }
 }
 
-// The fused inference FFN with 16-row waves (H <= 512): v_mfma_f32_16x16x4_f32 (k_gemm_f32's own
-// instruction), 64-row workgroups, four per CU (36 KB of LDS), four waves per SIMD.  GEMM 1 transposed
-// leaves lane group g (lanes 16 g .. 16 g + 15, row l & 15) holding hidden units 4g..4g+3 of each
-// 16-unit tile; GEMM 2's A operand wants units g, 4+g, 8+g, 12+g -- a 4 x 4 transpose across the lane
-// groups: v_permlane32_swap of registers (0, 2) and (1, 3) swaps the off-diagonal 2 x 2 blocks, then
-// v_permlane16_swap of (0, 1) and (2, 3) the off-diagonal elements, after which register t of a tile
-// is k4-step t's operand.  Output tiles: row 4g + r, column 16 j + (l & 15).  Same chains and
-// epilogue arithmetic as k_ffn_f32: bitwise the LayerNorm + two-GEMM path.
-template <bool LN>
-__global__ __launch_bounds__(256, 4) void k_ffn_f32q(int64_t M, int C, int H, const float* __restrict__ a, int64_t lda,
-                                                     const float* __restrict__ w1, int64_t ldw1,
-                                                     const float* __restrict__ b1, const float* __restrict__ w2,
-                                                     int64_t ldw2, const float* __restrict__ b2, const float* resid,
-                                                     int64_t ldr, float* out, int64_t ldo,
-                                                     const float* __restrict__ ln_w, const float* __restrict__ ln_b,
-                                                     float eps) {
-    __shared__ __attribute__((aligned(16))) float sm[2][FFN_STAGE];   // 33.8 KB
-    __shared__ float sb1[512], sb2[128];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, li = lane & 15, g = lane >> 4;
-    const int64_t mw = (int64_t)blockIdx.x * 64 + 16 * wv;   // the wave's first row
-    const int nk1 = (C + 15) / 16 * 4, kpad2 = (H + 15) / 16 * 16;   // GEMM 1 k4-steps (<= 32)
-    const int nc = (H + 31) / 32;
-    for (int i = tid; i < H; i += 256) sb1[i] = b1[i];
-    for (int i = tid; i < C; i += 256) sb2[i] = b2[i];
-    // slice staging as k_ffn_f32: kind 0 W1 rows 32 c + (tid >> 6) + 4 i at k = 2 (tid & 63), [k][unit];
-    // kind 1 W2 rows (tid >> 4) + 16 i at unit 32 c + 2 (tid & 15), [unit][column]
-    float2 ra[8];
-    bool rk = true;
-    auto load = [&](int c, int kind) {
-        const float* base;
-        int ld, rmax, k, kmax, r0, rs;
-        if (kind == 0) {
-            base = w1, ld = (int)ldw1, rmax = H, kmax = C, k = 2 * (tid & 63), r0 = 32 * c + (tid >> 6), rs = 4;
-        } else {
-            base = w2, ld = (int)ldw2, rmax = C, kmax = H, k = 32 * c + 2 * (tid & 15), r0 = tid >> 4, rs = 16;
-        }
-        rk = k < kmax;
-        const int kc = rk ? k : kmax - 2;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {   // cg_ffn_fwd_f32 checks: rows * ld under 2^31
-            const int r = r0 + rs * i < rmax ? r0 + rs * i : rmax - 1;
-            ra[i] = *(const float2*)(base + (uint32_t)(r * ld + kc));
-        }
-    };
-    auto store = [&](int st, int kind) {
-        float* S = sm[st];
-        const int LD = kind == 0 ? FFN_LD1 : FFN_LD2;
-        const int kk = kind == 0 ? 2 * (tid & 63) : 2 * (tid & 15);
-        const int r0 = kind == 0 ? tid >> 6 : tid >> 4, rs = kind == 0 ? 4 : 16;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int r = r0 + rs * i;
-            S[kk * LD + r] = rk ? ra[i].x : 0.f;
-            S[(kk + 1) * LD + r] = rk ? ra[i].y : 0.f;
-        }
-    };
-    load(0, 0);
-    float xr[32];
-    rows16_b_operand<LN>(xr, &sm[0][0], a, lda, M, C, mw, ln_w, ln_b, eps, lane, wv);
-    int stc = 0;
-    auto step = [&](int c, int kind) {
-        const int st = stc & 1;
-        ++stc;
-        store(st, kind);
-        __syncthreads();
-        if (kind == 0) load(c, 1);
-        else if (c + 1 < nc) load(c + 1, 0);
-        return st;
-    };
-    fv4 acc[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = fv4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int c = 0; c < nc; ++c) {
-        // GEMM 1: D[j] = hidden units 32 c + 16 j + 4 g + r of row li
-        fv4 D[2] = {fv4{0.f, 0.f, 0.f, 0.f}, fv4{0.f, 0.f, 0.f, 0.f}};
-        {
-            const float* S = sm[step(c, 0)] + g * FFN_LD1 + li;
-#pragma unroll
-            for (int b = 0; b < 8; ++b) {   // 4 k4-steps per fragment batch
-                if (4 * b >= nk1) break;
-                float fa[4][2];
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) fa[u][j] = S[4 * (4 * b + u) * FFN_LD1 + 16 * j];
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j)
-                        D[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[u][j], xr[4 * b + u], D[j], 0, 0, 0);
-            }
-        }
-        // h = relu(D + b1), zero past H; then the 4 x 4 transpose across lane groups (see above)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int u = 32 * c + 16 * j + 4 * g + r;
-                float v = D[j][r];
-                v += sb1[u < H ? u : 0];
-                v = fmaxf(v, 0.f);
-                D[j][r] = u < H ? v : 0.f;
-            }
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(D[j][r]), __float_as_uint(D[j][r + 2]),
-                                                                 false, false);
-                D[j][r] = __uint_as_float(sw[0]);
-                D[j][r + 2] = __uint_as_float(sw[1]);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; r += 2) {
-                const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(D[j][r]), __float_as_uint(D[j][r + 1]),
-                                                                 false, false);
-                D[j][r] = __uint_as_float(sw[0]);
-                D[j][r + 1] = __uint_as_float(sw[1]);
-            }
-        }
-        // GEMM 2: acc[j] (row 4 g + r, column 16 j + li) over the chunk's units, k4-step t = register t & 3
-        // of tile t >> 2
-        {
-            const float* S = sm[step(c, 1)] + g * FFN_LD2 + li;
-            const int nst = kpad2 - 32 * c >= 32 ? 8 : 4;
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                if (t >= nst) break;
-                float fb[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) fb[j] = S[4 * t * FFN_LD2 + 16 * j];
-                __builtin_amdgcn_sched_barrier(0);
-                const float ha = D[t >> 2][t & 3];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ha, fb[j], acc[j], 0, 0, 0);
-            }
-        }
-    }
-    // out = resid + (acc + b2); residual rows / columns clamped, every one loaded before the stores
-    const int64_t mr = M - 1 - mw;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int n = 16 * j + li < C ? 16 * j + li : C - 1;
-        const float bb = sb2[n];
-        float rv[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int64_t dm = 4 * g + r;
-            rv[r] = resid[(mw + (dm < mr ? dm : mr)) * ldr + n];
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            float v = acc[j][r];
-            v += bb;
-            acc[j][r] = rv[r] + v;
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int64_t m = mw + 4 * g + r;
-            const int n = 16 * j + li;
-            if (m < M && n < C) out[m * ldo + n] = acc[j][r];
-        }
-}
-
 bool linear_rows_f32_supported(int64_t M, int64_t N, int64_t K) {
     return M > 0 && K >= 2 && K <= 128 && K % 2 == 0 && N >= 2 && N <= 2048 && N % 2 == 0;
 }
@@ -1534,7 +1367,6 @@ int launch_generic(int a_trans, int b_trans, int64_t M, int64_t N, int64_t K, co
 
 namespace cg {
 int g_gemm_variant = 0;
-int g_ffn_q = 1;   // cg_set_tuning("ffn_q"): 1 k_ffn_f32q (16-row waves, H <= 512), 0 k_ffn_f32
 int g_linear_rows_nb = 0;   // cg_set_tuning("linear_rows_nb"): 0 k_linear_f32q (16-row waves), 1 / 2 k_linear_f32t
 int g_gemm_max_grid = 0;
 int g_gemm_group_p8 = 0;   // persistent-kernel tile order (gemm_tile.h tile_rc), cg_set_tuning knobs
@@ -1758,11 +1590,6 @@ extern "C" int cg_set_tuning(const char* key, int value) {
         g_gemm_variant = value;
         return CG_OK;
     }
-    if (!strcmp(key, "ffn_q")) {
-        CG_REQUIRE(value == 0 || value == 1, "cg_set_tuning: ffn_q must be 0 or 1");
-        g_ffn_q = value;
-        return CG_OK;
-    }
     if (!strcmp(key, "linear_rows_nb")) {
         CG_REQUIRE(value >= 0 && value <= 2, "cg_set_tuning: linear_rows_nb must be 0 (16-row waves), 1 or 2");
         g_linear_rows_nb = value;
@@ -1952,17 +1779,6 @@ extern "C" int cg_ffn_fwd_f32(int64_t M, int64_t C, int64_t H, const float* a, i
     // choice for C <= 128 even with 8-B aligned x / w / b)
     CG_REQUIRE(!ln_w || ((((uintptr_t)ln_w | (uintptr_t)ln_b) & 7) == 0 && lda == C),
                "cg_ffn_fwd_f32: ln_w / ln_b must be 8-B aligned and a dense (lda == C) with the LayerNorm");
-    if (g_ffn_q && H <= 512) {   // 16-row waves (k_ffn_f32q); cg_set_tuning("ffn_q", 0): 32-row waves
-        const dim3 gq((unsigned)((M + 63) / 64));
-        if (ln_w)
-            k_ffn_f32q<true><<<gq, 256, 0, (hipStream_t)stream>>>(M, (int)C, (int)H, a, lda, w1, ldw1, b1, w2, ldw2,
-                                                                 b2, resid, ldr, out, ldo, ln_w, ln_b, eps);
-        else
-            k_ffn_f32q<false><<<gq, 256, 0, (hipStream_t)stream>>>(M, (int)C, (int)H, a, lda, w1, ldw1, b1, w2, ldw2,
-                                                                  b2, resid, ldr, out, ldo, nullptr, nullptr, 0.f);
-        CG_LAUNCH_CHECK("cg_ffn_fwd_f32");
-        return CG_OK;
-    }
     const dim3 grid((unsigned)((M + 127) / 128));
     if (ln_w)
         k_ffn_f32<true><<<grid, 256, 0, (hipStream_t)stream>>>(M, (int)C, (int)H, a, lda, w1, ldw1, b1, w2, ldw2, b2,
