@@ -15,6 +15,8 @@
 //   *_d64     : bf16 MFMA (16x16x32), D = 64, T % 64 == 0 -- the C2/C4 perf path.
 #include <math.h>
 
+#include <type_traits>
+
 #include "attention_common.h"
 #include "ln_fwd.h"
 
@@ -321,7 +323,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd_f32mfma(int64_t T_, int H, int
 #define F32RES_EXP(x) expf(x)
 #endif
 template <int DP4>
-__global__ __launch_bounds__(512) void k_attn_fwd_f32res(int64_t T_, int H, int D, const float* __restrict__ q,
+__global__ __launch_bounds__(512, 6) void k_attn_fwd_f32res(int64_t T_, int H, int D, const float* __restrict__ q,
                                                          const float* __restrict__ k, const float* __restrict__ v,
                                                          int64_t ld, float* __restrict__ o, int64_t ldo,
                                                          float* __restrict__ lse, float scale) {
@@ -369,14 +371,18 @@ __global__ __launch_bounds__(512) void k_attn_fwd_f32res(int64_t T_, int H, int 
         fv4 oacc[2] = {fv4{0.f, 0.f, 0.f, 0.f}, fv4{0.f, 0.f, 0.f, 0.f}};
         float m_run = -INFINITY, l_run = 0.f;
         const int nkv = (int)((qw0 + 15) / 64) + 1;   // the 64-key tiles with k0 <= qw0 + 15, in order
-        for (int kv = 0; kv < nkv; ++kv) {
-            const int64_t k0 = (int64_t)kv * 64;
+        // one 64-key tile.  FULL: every key of the tile precedes the group's first query (and T) -- no
+        // causal mask, no -inf scores, all four 16-key sub-tiles: the same arithmetic with the masking
+        // compares, the -inf tests and the sub-tile guards compiled out (int32 indices), bitwise equal
+        auto tile = [&](int kv, auto fullc) {
+            constexpr bool FULL = decltype(fullc)::value;
+            const int k0 = kv * 64;
             const float* Kt = Ks + k0 * KLD;
             const float* Vt = Vs + k0 * VLD;
             // 16-key sub-tiles past the group's last query (k0 + 16 kt > qw0 + 15) are fully masked: their
             // scores are -inf, their p exact zeros, so their S and O MFMAs and softmax terms change
             // nothing (max with -inf, + 0, MFMA products all 0) -- skipped, the result bitwise the same
-            const int nkt = (int)((qw0 + 15 - k0) / 16 + 1 < 4 ? (qw0 + 15 - k0) / 16 + 1 : 4);   // wave-uniform
+            const int nkt = FULL ? 4 : ((int)qw0 + 15 - k0) / 16 + 1 < 4 ? ((int)qw0 + 15 - k0) / 16 + 1 : 4;
             fv4 st[4];
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt) {
@@ -392,9 +398,9 @@ __global__ __launch_bounds__(512) void k_attn_fwd_f32res(int64_t T_, int H, int 
             for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int64_t key = k0 + 16 * kt + 4 * g + r;
+                    const int key = k0 + 16 * kt + 4 * g + r;
                     float x = st[kt][r] * scale;
-                    if (key > qa || key >= T_) x = -INFINITY;
+                    if (!FULL && (key > (int)qa || key >= (int)T_)) x = -INFINITY;
                     st[kt][r] = x;
                     if (kt < nkt) mx = fmaxf(mx, x);
                 }
@@ -408,7 +414,7 @@ __global__ __launch_bounds__(512) void k_attn_fwd_f32res(int64_t T_, int H, int 
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     if (kt < nkt) {
-                        const float p = st[kt][r] == -INFINITY ? 0.f : F32RES_EXP(st[kt][r] - m_new);
+                        const float p = (!FULL && st[kt][r] == -INFINITY) ? 0.f : F32RES_EXP(st[kt][r] - m_new);
                         st[kt][r] = p;
                         ps += p;
                     }
@@ -432,6 +438,10 @@ __global__ __launch_bounds__(512) void k_attn_fwd_f32res(int64_t T_, int H, int 
                     }
                 }
             }
+        };
+        for (int kv = 0; kv < nkv; ++kv) {
+            if (kv * 64 + 63 <= (int)qw0 && kv * 64 + 63 < (int)T_) tile(kv, std::true_type{});
+            else tile(kv, std::false_type{});
         }
         if (qa >= T_) continue;
         const float inv = 1.f / l_run;
