@@ -400,7 +400,8 @@ __global__ __launch_bounds__(512, 6) void k_attn_fwd_f32res(int64_t T_, int H, i
                 for (int r = 0; r < 4; ++r) {
                     const int key = k0 + 16 * kt + 4 * g + r;
                     float x = st[kt][r] * scale;
-                    if (!FULL && (key > (int)qa || key >= (int)T_)) x = -INFINITY;
+                    if constexpr (FULL) asm("" : "+v"(x));   // keep x * scale rounded: the masked path's
+                    else if (key > (int)qa || key >= (int)T_) x = -INFINITY;   // select stops its fma with - m_new
                     st[kt][r] = x;
                     if (kt < nkt) mx = fmaxf(mx, x);
                 }
