@@ -232,17 +232,27 @@ int cg_gemm_resid_layernorm(int64_t M, int64_t N, int64_t K, const void* A, int6
                             float* out, int64_t ldc, const cg_epilogue_t* epi, const float* ln_w, const float* ln_b,
                             void* y, float* mean, float* rstd, float eps, void* stream);
 /* A Linear over rows of K <= 128 for inference, fp32, optionally with the LayerNorm before it in the
-   same launch: out = [resid +] (a' W^T [+ bias]), a' = LayerNorm(a; ln_w, ln_b, eps) (ln_w, ln_b
-   non-NULL: the block's ln1 before the QKV product, GPT1.py:111-112,163) or a' = a; a [M][K] (lda),
-   W [N][K] (ldw), resid / out [M][N] (ldr / ldo) -- bit for bit [cg_layernorm_fwd +] cg_gemm (fp32,
-   CG_EPI_STORE / CG_EPI_BIAS / CG_EPI_BIAS_RESID), without the normalised rows in memory.  Only where
-   cg_linear_rows_f32_supported(M, N, K) says 1 (K <= 128 even, N <= 2048 even); lda / ldw / ldo /
-   ldr even, a / W / out / resid 8-B aligned (with the LayerNorm also ln_w / ln_b, lda == K); else
-   CG_EINVAL.                                                                                     */
+   same launch: out = [resid +] act(a' W^T [+ bias]), a' = LayerNorm(a; ln_w, ln_b, eps) (ln_w, ln_b
+   non-NULL: the block's ln1 before the QKV product, GPT1.py:111-112,163; ln2 before FFN1, lnf before
+   lm_head) or a' = a; act = relu when relu != 0 (needs bias, no resid); a [M][K] (lda), W [N][K]
+   (ldw), resid / out [M][N] (ldr / ldo) -- bit for bit [cg_layernorm_fwd +] cg_gemm (fp32,
+   CG_EPI_STORE / CG_EPI_BIAS / CG_EPI_BIAS_RELU / CG_EPI_BIAS_RESID), without the normalised rows in
+   memory.  Only where cg_linear_rows_f32_supported(M, N, K) says 1 (K <= 128 even; above 2048 rows
+   N <= 2048 even); lda / ldw even and a / W 8-B aligned; above 2048 rows also ldo / ldr even, out /
+   resid 8-B aligned and, with the LayerNorm, ln_w / ln_b 8-B aligned and lda == K; else CG_EINVAL. */
 int cg_linear_rows_f32_supported(int64_t M, int64_t N, int64_t K);
 int cg_linear_rows_f32(int64_t M, int64_t N, int64_t K, const float* a, int64_t lda, const float* ln_w,
-                       const float* ln_b, float eps, const float* w, int64_t ldw, const float* bias, const float* resid,
-                       int64_t ldr, float* out, int64_t ldo, void* stream);
+                       const float* ln_b, float eps, const float* w, int64_t ldw, const float* bias, int relu,
+                       const float* resid, int64_t ldr, float* out, int64_t ldo, void* stream);
+/* generate()'s per-token ln1 + QKV product + K/V cache append (GPT1.py:111-113,163 for the newest
+   token of each row; the decode engine's phase 1), fp32, one launch: qkv = LayerNorm(x; ln_w, ln_b,
+   eps) W^T (x [B][C] (ldx), W [3C][C] (ldw), qkv [B][3C] (ldq)), and columns C..3C-1 of row b also
+   to kcache / vcache [B][H][Tmax][C/H] at position *len_dev - 1 -- bit for bit cg_linear_rows_f32
+   (with the LayerNorm) then cg_decode_kv_append(qkv, ldq, C, 2C, ...).  B <= 2048, C <= 128 even,
+   H | C, ldx / ldw even, x / W 8-B aligned; else CG_EINVAL.                                      */
+int cg_decode_qkv_f32(int64_t B, int64_t C, int64_t H, const float* x, int64_t ldx, const float* ln_w,
+                      const float* ln_b, float eps, const float* w, int64_t ldw, float* qkv, int64_t ldq,
+                      const int64_t* len_dev, int64_t Tmax, float* kcache, float* vcache, void* stream);
 /* The FeedForward sublayer's forward for inference (GPT1.py:142-147,164 in eval, no dropout), fp32,
    in one launch: out = resid + (relu(a' W1^T + b1) W2^T + b2) with a' = LayerNorm(a; ln_w, ln_b,
    eps) (ln_w, ln_b non-NULL: the block's ln2, GPT1.py:164) or a' = a (both NULL); a [M][C] (lda),

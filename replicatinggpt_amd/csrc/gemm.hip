@@ -351,65 +351,148 @@ __global__ __launch_bounds__(64) void k_gemm_f32s(int64_t M, int64_t N, int64_t 
 // coalesced along K) into LDS, then each wave runs its 16 x 16 fragment's MFMA chain from LDS.  k_gemm_f32s
 // walked K in 128-deep register chunks, one load round trip each, on 32 waves for the C5 FFN2 (19 us).
 // Same lane / k order, padded depth and epilogue as k_gemm_f32: bitwise its result.
-template <int EK, int U>   // U = ceil(kpad / 128): float2 columns per thread and row
+// Every global load is unconditional at a clamped address (row M - 1, column K - 2), the zero selected
+// after it: a guarded load compiles to an exec-masked branch that waits for its own load (64 dependent
+// round trips per thread at K = 504).  The chain reads its operands from LDS one 4-step group ahead of
+// the MFMAs (a wait every 2 MFMAs before).
+// LN (U == 1, K <= 128): A' = LayerNorm(A; ln_w, ln_b, eps) in the launch -- wave rr holds rows rr + 4 s
+// with lane l on columns 2l, 2l + 1, k_ln_fwd's own row layout, so each row goes through its row body
+// (ln_fwd.h ln_fwd_row, cg_layernorm_fwd's choice for C <= 128 even) into the LDS slab: the same bits
+// as cg_layernorm_fwd then this GEMM (generate()'s per-token ln1 + QKV, ln2 + FFN1, lnf + lm_head).
+// KV (generate()'s per-token QKV product): columns C..3C-1 of each row also go to the layer's K / V
+// caches [rows][H][Tmax][D] at position *len - 1 -- the same values cg_decode_kv_append copies.
+struct KvAppend {
+    float* kc;
+    float* vc;
+    const int64_t* len;
+    int64_t C, H, D, Tmax;
+};
+template <int EK, int U, bool LN = false, bool KV = false>   // U = ceil(kpad / 128): float2 columns per thread and row
 __global__ __launch_bounds__(256, 1) void k_gemm_f32r(int64_t M, int64_t N, int64_t K, const float* __restrict__ A,
                                                       int64_t lda, const float* __restrict__ B, int64_t ldb,
-                                                      float* __restrict__ C, int64_t ldc, EpiArgs epi) {
+                                                      float* __restrict__ C, int64_t ldc, EpiArgs epi,
+                                                      const float* __restrict__ ln_w = nullptr,
+                                                      const float* __restrict__ ln_b = nullptr, float eps = 0.f,
+                                                      KvAppend kva = KvAppend{}) {
+    static_assert(!LN || U == 1, "k_gemm_f32r: the LayerNorm form needs K <= 128");
+    static_assert(!KV || EK == CG_EPI_STORE, "k_gemm_f32r: the K / V append goes with the plain store");
     extern __shared__ __attribute__((aligned(16))) float smr[];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
-    const int64_t kpad = (K + 15) / 16 * 16;   // k_gemm_f32's padded depth
-    const int KS = (int)kpad + 4;               // LDS row stride (floats)
+    const int kpad = (int)((K + 15) / 16 * 16);   // k_gemm_f32's padded depth
+    const int KS = kpad + 4;                       // LDS row stride (floats)
     float* As = smr;
     float* Bs = smr + 32 * KS;
     const int64_t mb = (int64_t)blockIdx.x * 32, nb = (int64_t)blockIdx.y * 32;
     const int rr = tid >> 6, c = tid & 63;      // rows rr + 4 s, float2 columns c + 64 u
+    const int Ki = (int)K;
     float2 av[8][U], bv[8][U];
 #pragma unroll
-    for (int s = 0; s < 8; ++s)
+    for (int s = 0; s < 8; ++s) {
+        const int r = rr + 4 * s;
+        const int64_t ra = mb + r < M ? mb + r : M - 1, rb = nb + r < N ? nb + r : N - 1;
+        const float* ap = A + ra * lda;
+        const float* bp = B + rb * ldb;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
+            const int k = 2 * (c + 64 * u), kc = k < Ki ? k : Ki - 2;   // K even: k + 1 < K as well
+            av[s][u] = *(const float2*)(ap + kc);
+            bv[s][u] = *(const float2*)(bp + kc);
+        }
+    }
+    if constexpr (LN) {
+        // rows past M normalise row M - 1 (their outputs are not stored); columns K..kpad-1 zero
+        const int k = 2 * c;
+        const float invC = 1.0f / (float)Ki;
+        float wl[1][2] = {{0.f, 0.f}}, bl[1][2] = {{0.f, 0.f}};
+        if (k < Ki) {
+            wl[0][0] = ln_w[k], wl[0][1] = ln_w[k + 1];
+            bl[0][0] = ln_b[k], bl[0][1] = ln_b[k + 1];
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
             const int r = rr + 4 * s;
-            const int64_t k = 2 * (c + 64 * u);
-            const bool kin = k < K;   // K even: k + 1 < K as well
-            av[s][u] = (kin && mb + r < M) ? *(const float2*)(A + (mb + r) * lda + k) : make_float2(0.f, 0.f);
-            bv[s][u] = (kin && nb + r < N) ? *(const float2*)(B + (nb + r) * ldb + k) : make_float2(0.f, 0.f);
+            float v[1][2] = {{k < Ki ? av[s][0].x : 0.f, k < Ki ? av[s][0].y : 0.f}};
+            float mu, rs;
+            ln_fwd_row<2, 1, float, false>(v, wl, bl, Ki, invC, eps, c, As + r * KS, mu, rs);
+            if (k >= Ki && k < kpad) *(float2*)(As + r * KS + k) = make_float2(0.f, 0.f);
+            if (k < kpad) *(float2*)(Bs + r * KS + k) = (k < Ki && nb + r < N) ? bv[s][0] : make_float2(0.f, 0.f);
         }
+    } else {
 #pragma unroll
-    for (int s = 0; s < 8; ++s)
+        for (int s = 0; s < 8; ++s)
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int r = rr + 4 * s, k = 2 * (c + 64 * u);
-            if (k < kpad) {
-                *(float2*)(As + r * KS + k) = av[s][u];
-                *(float2*)(Bs + r * KS + k) = bv[s][u];
+            for (int u = 0; u < U; ++u) {
+                const int r = rr + 4 * s, k = 2 * (c + 64 * u);
+                if (k < kpad) {
+                    const float2 z = make_float2(0.f, 0.f);
+                    *(float2*)(As + r * KS + k) = (k < Ki && mb + r < M) ? av[s][u] : z;
+                    *(float2*)(Bs + r * KS + k) = (k < Ki && nb + r < N) ? bv[s][u] : z;
+                }
             }
-        }
-    __syncthreads();
+    }
+    constexpr bool BIAS = EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_BIAS_RESID;
+    const bool hb = BIAS && epi.bias, hr = EK == CG_EPI_BIAS_RESID && epi.resid;
     const int i = w >> 1, j = w & 1;
+    const int64_t m0 = mb + 16 * i, n = nb + 16 * j + li, nc = n < N ? n : N - 1;
+    // the epilogue's operands in flight under the chain
+    float bb = 0.f, rv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (hb) bb = epi.bias[nc];
+    if (hr) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t m = m0 + 4 * g + r, mc = m < M ? m : M - 1;
+            rv[r] = epi.resid[mc * epi.ld_resid + nc];
+        }
+    }
+    __syncthreads();
     const float* ar = As + (16 * i + li) * KS + g;
     const float* br = Bs + (16 * j + li) * KS + g;
     fv4 acc = fv4{0.f, 0.f, 0.f, 0.f};
-    const int nt = (int)(kpad / 4);
-#pragma unroll 4
-    for (int t = 0; t < nt; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[4 * t], br[4 * t], acc, 0, 0, 0);
-    constexpr bool BIAS = EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_BIAS_RESID;
-    const bool hb = BIAS && epi.bias, hr = EK == CG_EPI_BIAS_RESID && epi.resid;
-    const int64_t m0 = mb + 16 * i, n = nb + 16 * j + li;
-    const float bb = (hb && n < N) ? epi.bias[n] : 0.f;
-    float rv[4];
+    const int nt = kpad / 4;   // a multiple of 4
+    float pa[4], pb[4], qa[4], qb[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int64_t m = m0 + 4 * g + r;
-        rv[r] = (hr && m < M && n < N) ? epi.resid[m * epi.ld_resid + n] : 0.f;
+    for (int u = 0; u < 4; ++u) {
+        pa[u] = ar[4 * u];
+        pb[u] = br[4 * u];
+    }
+    // the look-ahead reads are unconditional (clamped to the last group: no LDS op under a branch, so
+    // each wait counts only the group the MFMAs need)
+    for (int t0 = 0;; t0 += 8) {
+        const int t1 = t0 + 4 < nt ? t0 + 4 : nt - 4, t2 = t0 + 8 < nt ? t0 + 8 : nt - 4;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            qa[u] = ar[4 * (t1 + u)];
+            qb[u] = br[4 * (t1 + u)];
+        }
+        __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[u], pb[u], acc, 0, 0, 0);
+        if (t0 + 4 >= nt) break;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            pa[u] = ar[4 * (t2 + u)];
+            pb[u] = br[4 * (t2 + u)];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[u], qb[u], acc, 0, 0, 0);
+        if (t0 + 8 >= nt) break;
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int64_t m = m0 + 4 * g + r;
         float v = acc[r];
-        if (hb) v += bb;
+        if (hb) v += (n < N ? bb : 0.f);
         if (EK == CG_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
-        if (hr) v = rv[r] + v;
+        if (hr) v = ((m < M && n < N) ? rv[r] : 0.f) + v;
         if (m < M && n < N) C[m * ldc + n] = v;
+        if constexpr (KV) {
+            if (m < M && n < N && n >= kva.C) {
+                const bool isv = n >= 2 * kva.C;
+                const int64_t t = n - (isv ? 2 * kva.C : kva.C), h = t / kva.D, e = t - h * kva.D;
+                (isv ? kva.vc : kva.kc)[((m * kva.H + h) * kva.Tmax + (*kva.len - 1)) * kva.D + e] = v;
+            }
+        }
     }
 }
 
@@ -1150,8 +1233,10 @@ __global__ __launch_bounds__(256, 4) void k_linear_f32q(int64_t M, int C, int N,
     }
 }
 
+// M <= 2048: k_gemm_f32r (32 x 32 tiles, any N); above: k_linear_f32q / k_linear_f32t (N <= 2048 even)
 bool linear_rows_f32_supported(int64_t M, int64_t N, int64_t K) {
-    return M > 0 && K >= 2 && K <= 128 && K % 2 == 0 && N >= 2 && N <= 2048 && N % 2 == 0;
+    return M > 0 && K >= 2 && K <= 128 && K % 2 == 0 && N >= 1 &&
+           (M <= 2048 || (N >= 2 && N <= 2048 && N % 2 == 0));
 }
 
 bool ffn_f32_supported(int64_t M, int64_t C, int64_t H) {
@@ -1165,7 +1250,7 @@ bool launch_f32s(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, c
     if (g_gemm_variant == 98 || e.beta != 0.f || M > 2048) return false;
     const dim3 grid((unsigned)((M + 31) / 32), (unsigned)((N + 31) / 32));
     const int64_t kpad = (K + 15) / 16 * 16;
-    if (g_gemm_variant != 97 && K % 2 == 0 && kpad <= 624 && lda % 2 == 0 && ldb % 2 == 0 &&
+    if (g_gemm_variant != 97 && K >= 2 && K % 2 == 0 && kpad <= 624 && lda % 2 == 0 && ldb % 2 == 0 &&
         (((uintptr_t)A | (uintptr_t)B) & 7) == 0 &&
         (e.kind == CG_EPI_STORE || e.kind == CG_EPI_BIAS || e.kind == CG_EPI_BIAS_RELU || e.kind == CG_EPI_BIAS_RESID)) {
         const int U = (int)((kpad + 127) / 128);
@@ -1716,22 +1801,54 @@ extern "C" int cg_linear_rows_f32_supported(int64_t M, int64_t N, int64_t K) {
 }
 
 extern "C" int cg_linear_rows_f32(int64_t M, int64_t N, int64_t K, const float* a, int64_t lda, const float* ln_w,
-                                  const float* ln_b, float eps, const float* w, int64_t ldw, const float* bias,
+                                  const float* ln_b, float eps, const float* w, int64_t ldw, const float* bias, int relu,
                                   const float* resid, int64_t ldr, float* out, int64_t ldo, void* stream) {
     CG_REQUIRE(linear_rows_f32_supported(M, N, K),
-               "cg_linear_rows_f32: unsupported shape M=%lld N=%lld K=%lld (K <= 128 even, N <= 2048 even)",
+               "cg_linear_rows_f32: unsupported shape M=%lld N=%lld K=%lld (K <= 128 even; above 2048 rows N <= 2048 even)",
                (long long)M, (long long)N, (long long)K);
     CG_REQUIRE(a && w && out, "cg_linear_rows_f32: null pointer");
+    CG_REQUIRE(!relu || (bias && !resid), "cg_linear_rows_f32: relu needs a bias and no residual");
+    CG_REQUIRE(!ln_w == !ln_b, "cg_linear_rows_f32: ln_w and ln_b both or neither");
+    hipStream_t st = (hipStream_t)stream;
+    if (M <= 2048) {
+        // generate()'s per-token rows: k_gemm_f32r (the kernel cg_gemm runs there), the LayerNorm in its
+        // prologue -- the bits of [cg_layernorm_fwd +] cg_gemm at any N
+        CG_REQUIRE(lda >= K && lda % 2 == 0 && ldw >= K && ldw % 2 == 0 && ldo >= N && (!resid || ldr >= N),
+                   "cg_linear_rows_f32: bad leading dimensions");
+        CG_REQUIRE((((uintptr_t)a | (uintptr_t)w) & 7) == 0, "cg_linear_rows_f32: a, w must be 8-B aligned");
+        EpiArgs e{};
+        e.kind = resid ? CG_EPI_BIAS_RESID : relu ? CG_EPI_BIAS_RELU : bias ? CG_EPI_BIAS : CG_EPI_STORE;
+        e.bias = bias;
+        e.resid = resid;
+        e.ld_resid = ldr;
+        const dim3 grid((unsigned)((M + 31) / 32), (unsigned)((N + 31) / 32));
+        const size_t lds = (size_t)2 * 32 * ((K + 15) / 16 * 16 + 4) * sizeof(float);
+#define KR(EK_, LN_) \
+    k_gemm_f32r<EK_, 1, LN_><<<grid, 256, lds, st>>>(M, N, K, a, lda, w, ldw, out, ldo, e, ln_w, ln_b, eps)
+#define KRL(EK_)                  \
+    do {                          \
+        if (ln_w) KR(EK_, true);  \
+        else KR(EK_, false);      \
+    } while (0)
+        switch (e.kind) {
+            case CG_EPI_STORE: KRL(CG_EPI_STORE); break;
+            case CG_EPI_BIAS: KRL(CG_EPI_BIAS); break;
+            case CG_EPI_BIAS_RELU: KRL(CG_EPI_BIAS_RELU); break;
+            default: KRL(CG_EPI_BIAS_RESID); break;
+        }
+#undef KRL
+#undef KR
+        CG_LAUNCH_CHECK("cg_linear_rows_f32");
+        return CG_OK;
+    }
     CG_REQUIRE(lda >= K && lda % 2 == 0 && ldw >= K && ldw % 2 == 0 && ldo >= N && ldo % 2 == 0 &&
                    (!resid || (ldr >= N && ldr % 2 == 0)) && N * ldw < ((int64_t)1 << 31),
                "cg_linear_rows_f32: bad leading dimensions");
     CG_REQUIRE((((uintptr_t)a | (uintptr_t)w | (uintptr_t)out | (uintptr_t)(resid ? resid : out)) & 7) == 0,
                "cg_linear_rows_f32: a, w, out, resid must be 8-B aligned");
-    CG_REQUIRE(!ln_w == !ln_b, "cg_linear_rows_f32: ln_w and ln_b both or neither");
     CG_REQUIRE(!ln_w || ((((uintptr_t)ln_w | (uintptr_t)ln_b) & 7) == 0 && lda == K),
                "cg_linear_rows_f32: ln_w / ln_b must be 8-B aligned and a dense (lda == K) with the LayerNorm");
     const dim3 grid((unsigned)((M + 127) / 128));
-    hipStream_t st = (hipStream_t)stream;
     // 16-row waves (k_linear_f32q: four waves per SIMD) by default; cg_set_tuning("linear_rows_nb", 1 / 2):
     // 32-row waves with one / two 32-column chains per slice -- 3.3 % / 5.4 % slower in generate
     // (profiles/r6_linear_rows_gen.txt)
@@ -1750,6 +1867,8 @@ extern "C" int cg_linear_rows_f32(int64_t M, int64_t N, int64_t K, const float* 
     const bool ln = ln_w != nullptr;
     if (resid) {
         if (ln) KL(true, CG_EPI_BIAS_RESID); else KL(false, CG_EPI_BIAS_RESID);
+    } else if (relu) {
+        if (ln) KL(true, CG_EPI_BIAS_RELU); else KL(false, CG_EPI_BIAS_RELU);
     } else if (bias) {
         if (ln) KL(true, CG_EPI_BIAS); else KL(false, CG_EPI_BIAS);
     } else {
@@ -1757,6 +1876,28 @@ extern "C" int cg_linear_rows_f32(int64_t M, int64_t N, int64_t K, const float* 
     }
 #undef KL
     CG_LAUNCH_CHECK("cg_linear_rows_f32");
+    return CG_OK;
+}
+
+extern "C" int cg_decode_qkv_f32(int64_t B, int64_t C, int64_t H, const float* x, int64_t ldx, const float* ln_w,
+                                 const float* ln_b, float eps, const float* w, int64_t ldw, float* qkv, int64_t ldq,
+                                 const int64_t* len_dev, int64_t Tmax, float* kcache, float* vcache, void* stream) {
+    CG_REQUIRE(B > 0 && B <= 2048 && C >= 2 && C <= 128 && C % 2 == 0 && H > 0 && C % H == 0 && Tmax > 0,
+               "cg_decode_qkv_f32: needs 0 < B <= 2048, C <= 128 even, H | C (B=%lld C=%lld H=%lld)", (long long)B,
+               (long long)C, (long long)H);
+    CG_REQUIRE(x && ln_w && ln_b && w && qkv && len_dev && kcache && vcache, "cg_decode_qkv_f32: null pointer");
+    CG_REQUIRE(ldx >= C && ldx % 2 == 0 && ldw >= C && ldw % 2 == 0 && ldq >= 3 * C,
+               "cg_decode_qkv_f32: bad leading dimensions");
+    CG_REQUIRE((((uintptr_t)x | (uintptr_t)w) & 7) == 0, "cg_decode_qkv_f32: x, w must be 8-B aligned");
+    EpiArgs e{};
+    e.kind = CG_EPI_STORE;
+    const KvAppend kva{kcache, vcache, len_dev, C, H, C / H, Tmax};
+    const int64_t N = 3 * C;
+    const dim3 grid((unsigned)((B + 31) / 32), (unsigned)((N + 31) / 32));
+    const size_t lds = (size_t)2 * 32 * ((C + 15) / 16 * 16 + 4) * sizeof(float);
+    k_gemm_f32r<CG_EPI_STORE, 1, true, true><<<grid, 256, lds, (hipStream_t)stream>>>(B, N, C, x, ldx, w, ldw, qkv, ldq,
+                                                                                     e, ln_w, ln_b, eps, kva);
+    CG_LAUNCH_CHECK("cg_decode_qkv_f32");
     return CG_OK;
 }
 

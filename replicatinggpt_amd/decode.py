@@ -22,10 +22,15 @@ The current length lives in a device int64, so each phase's step is one static-s
 captured once and replayed per token (prefill of a longer prompt replays the phase-1 graph without
 sampling).  fp32 models give the reference's greedy stream (tests/test_gpu_model.py).
 """
+import os
+
 import torch
 
 from . import functional as Fn
 from . import ops
+
+# CHARPT_DECODE_ROWS=0: the per-token LayerNorms in their own launches before ln1/ln2/lnf's Linears (A/B)
+DECODE_ROWS = os.environ.get("CHARPT_DECODE_ROWS", "1") == "1"
 
 
 class DecodeEngine:
@@ -66,18 +71,33 @@ class DecodeEngine:
         y, _, _ = Fn.layernorm(x2, self._b(key + "_w"), self._b(key + "_b"), self.act)
         return y
 
+    def _ln_linear(self, x2, key, w, out, bias=None, relu=False):
+        """out = act(LayerNorm_key(x2) @ w^T [+ bias]): fp32 per-token rows in one launch
+        (ops.linear_rows_f32, k_gemm_f32r with the LayerNorm in its prologue -- the bits of the two
+        launches); else the LayerNorm launch and the GEMM."""
+        lw, lb = self._b(key + "_w"), self._b(key + "_b")
+        M, K = x2.shape
+        if (DECODE_ROWS and self.act == torch.float32 and M <= 2048 and x2.stride(0) % 2 == 0
+                and ops.linear_rows_f32_supported(M, w.shape[0], K) and w.stride(0) % 2 == 0
+                and ((x2.data_ptr() | w.data_ptr()) & 7) == 0):
+            ops.linear_rows_f32(x2, lw, lb, 1e-5, w, bias, None, out, relu)
+            return
+        a = self._ln(x2, key)
+        if bias is None:
+            Fn.linear_fwd(a, w, out)
+        else:
+            Fn.linear_fwd(a, w, out, "bias_relu" if relu else "bias", bias=bias)
+
     def _ffn_tail(self, l, x2):
         """x + W2 relu(W1 ln2(x) + b1) + b2 for rows x2 [R, C] (eval: no dropout)."""
-        a = self._ln(x2, f"{l}.ln2")
         h = torch.empty((x2.shape[0], 4 * self.C), dtype=self.act, device=self.dev)
-        Fn.linear_fwd(a, self._w(f"{l}.w1"), h, "bias_relu", bias=self._b(f"{l}.b1"))
+        self._ln_linear(x2, f"{l}.ln2", self._w(f"{l}.w1"), h, bias=self._b(f"{l}.b1"), relu=True)
         out = torch.empty_like(x2)
         Fn.linear_fwd(h, self._w(f"{l}.w2"), out, "bias_resid", bias=self._b(f"{l}.b2"), resid=x2)
         return out
 
     def _head(self, x2):
-        a = self._ln(x2, "lnf")
-        Fn.linear_fwd(a, self._R("lm_w").operand(self.act), self.logits, "bias", bias=self._b("lm_b"))
+        self._ln_linear(x2, "lnf", self._R("lm_w").operand(self.act), self.logits, bias=self._b("lm_b"))
 
     # -- phase 1: one token against the K/V caches ---------------------------------------------
     def _step1(self, sample):
@@ -85,11 +105,18 @@ class DecodeEngine:
         ops.decode_embed(self.idx, self._b("wte"), self._b("wpe"), self.len, self.x1)
         x = self.x1
         for l in range(self.L):
-            a = self._ln(x, f"{l}.ln1")
             qkv = torch.empty((B, 3 * C), dtype=self.act, device=self.dev)
-            Fn.linear_fwd(a, self._w(f"{l}.qkv"), qkv)
-            qkv32 = qkv if qkv.dtype == torch.float32 else qkv.float()
-            ops.decode_kv_append(qkv32, C, 2 * C, self.len, self.kc[l], self.vc[l])
+            wq = self._w(f"{l}.qkv")
+            if (DECODE_ROWS and self.act == torch.float32 and B <= 2048 and C <= 128 and C % 2 == 0
+                    and x.stride(0) % 2 == 0 and wq.stride(0) % 2 == 0 and ((x.data_ptr() | wq.data_ptr()) & 7) == 0):
+                # ln1 + QKV + the K / V append in one launch
+                ops.decode_qkv_f32(x, self._b(f"{l}.ln1_w"), self._b(f"{l}.ln1_b"), 1e-5, wq, qkv, self.len,
+                                   self.kc[l], self.vc[l])
+                qkv32 = qkv
+            else:
+                self._ln_linear(x, f"{l}.ln1", wq, qkv)
+                qkv32 = qkv if qkv.dtype == torch.float32 else qkv.float()
+                ops.decode_kv_append(qkv32, C, 2 * C, self.len, self.kc[l], self.vc[l])
             o = torch.empty((B, C), dtype=torch.float32, device=self.dev)
             T, H, D = self.T, self.H, self.D
             ops.decode_attn(qkv32, qkv32.stride(0), self.kc[l], 0, self.vc[l], 0, H * T * D, T * D, D, B, H, D,

@@ -243,10 +243,11 @@ def gemm_resid_layernorm(a: Tensor, w: Tensor, out: Tensor, M: int, N: int, K: i
 
 @_op("linear_rows_f32", ("out",))
 def linear_rows_f32(a: Tensor, ln_w: Optional[Tensor], ln_b: Optional[Tensor], eps: float, w: Tensor,
-                    bias: Optional[Tensor], resid: Optional[Tensor], out: Tensor) -> None:
-    """out = [resid +] (a' @ w^T [+ bias]), a' = LayerNorm(a; ln_w, ln_b, eps) (or a when ln_w is None),
-    fp32, K <= 128, one launch -- the bits of [layernorm_fwd +] gemm(..., "store" / "bias" /
-    "bias_resid").  Fails (CG_EINVAL) unless linear_rows_f32_supported(M, N, K)."""
+                    bias: Optional[Tensor], resid: Optional[Tensor], out: Tensor, relu: bool = False) -> None:
+    """out = [resid +] act(a' @ w^T [+ bias]), a' = LayerNorm(a; ln_w, ln_b, eps) (or a when ln_w is None),
+    act = relu when relu (bias, no resid), fp32, K <= 128, one launch -- the bits of [layernorm_fwd +]
+    gemm(..., "store" / "bias" / "bias_relu" / "bias_resid").  Fails (CG_EINVAL) unless
+    linear_rows_f32_supported(M, N, K)."""
     M, K = a.shape
     N = w.shape[0]
     for t, name in ((a, "a"), (w, "w"), (bias, "bias"), (resid, "resid"), (out, "out"), (ln_w, "ln_w"),
@@ -263,7 +264,7 @@ def linear_rows_f32(a: Tensor, ln_w: Optional[Tensor], ln_b: Optional[Tensor], e
             (resid is not None and tuple(resid.shape) != (M, N)):
         raise ValueError(f"linear_rows_f32: shapes a {tuple(a.shape)} w {tuple(w.shape)} out {tuple(out.shape)}")
     L.check(L.load().cg_linear_rows_f32(M, N, K, L.ptr(a), a.stride(0), L.ptr(ln_w), L.ptr(ln_b), eps, L.ptr(w),
-                                        w.stride(0), L.ptr(bias), L.ptr(resid),
+                                        w.stride(0), L.ptr(bias), int(relu), L.ptr(resid),
                                         resid.stride(0) if resid is not None else 0, L.ptr(out), out.stride(0),
                                         _s(out)), "linear_rows_f32")
 
@@ -441,6 +442,25 @@ def decode_kv_append(qkv: Tensor, k_off: int, v_off: int, len_dev: Tensor, kcach
     B, H, Tmax, D = kcache.shape
     L.check(L.load().cg_decode_kv_append(L.ptr(qkv), qkv.stride(0), k_off, v_off, B, H, D, Tmax, L.ptr(len_dev),
                                          L.ptr(kcache), L.ptr(vcache), _s(qkv)), "decode_kv_append")
+
+
+@_op("decode_qkv_f32", ("qkv", "kcache", "vcache"))
+def decode_qkv_f32(x: Tensor, ln_w: Tensor, ln_b: Tensor, eps: float, w: Tensor, qkv: Tensor, len_dev: Tensor,
+                   kcache: Tensor, vcache: Tensor) -> None:
+    """qkv = LayerNorm(x) @ w^T and its K / V columns appended to the caches at position len - 1, fp32,
+    one launch -- the bits of linear_rows_f32(x, ln_w, ln_b, eps, w, ...) then decode_kv_append."""
+    B, C = x.shape
+    _, H, Tmax, D = kcache.shape
+    for t, name in ((x, "x"), (w, "w"), (qkv, "qkv"), (kcache, "kcache"), (vcache, "vcache")):
+        if t.dtype != torch.float32 or not t.is_cuda or t.stride(-1) != 1:
+            raise ValueError(f"decode_qkv_f32: {name} must be a float32 device tensor with unit column stride")
+    if tuple(w.shape) != (3 * C, C) or tuple(qkv.shape) != (B, 3 * C) or H * D != C or \
+            tuple(kcache.shape) != (B, H, Tmax, D) or not kcache.is_contiguous() or \
+            tuple(vcache.shape) != tuple(kcache.shape) or not vcache.is_contiguous():
+        raise ValueError(f"decode_qkv_f32: shapes x {tuple(x.shape)} w {tuple(w.shape)} kcache {tuple(kcache.shape)}")
+    L.check(L.load().cg_decode_qkv_f32(B, C, H, L.ptr(x), x.stride(0), L.ptr(ln_w), L.ptr(ln_b), eps, L.ptr(w),
+                                       w.stride(0), L.ptr(qkv), qkv.stride(0), L.ptr(len_dev), Tmax, L.ptr(kcache),
+                                       L.ptr(vcache), _s(x)), "decode_qkv_f32")
 
 
 @_op("decode_attn", ("o",))

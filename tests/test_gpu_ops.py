@@ -1333,14 +1333,18 @@ def test_ffn_f32_fused_matches_two_gemms(M, C, H, variant, ln):
 
 
 @pytest.mark.parametrize("ln", [False, True])
-@pytest.mark.parametrize("kind", [0, 1, 3])
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
 @pytest.mark.parametrize("M,N,K,variant", [(65536, 378, 126, 0), (65536, 126, 126, 98), (4129, 70, 128, 0),
-                                           (300, 2, 2, 98), (2049, 2048, 64, 0), (777, 130, 100, 98)])
+                                           (300, 2, 2, 98), (2049, 2048, 64, 0), (777, 130, 100, 98),
+                                           (256, 378, 126, 98), (256, 504, 126, 0), (256, 65, 126, 98),
+                                           (1, 65, 126, 0), (2048, 17, 6, 98)])
 def test_linear_rows_f32_matches_gemm(M, N, K, variant, kind, ln):
-    """The row-resident fp32 Linear (k_linear_f32t: the wave's rows in registers, W streamed in 32-column
-    slices; with ln, the LayerNorm before it in the launch) against [layernorm_fwd +] the fp32 GEMM with
-    the same epilogue (store / bias / bias_resid) under the default dispatch (k_gemm_f32p above 2048 rows)
-    and k_gemm_f32 (gemm_variant 98): bitwise equal, and within fp32 rounding of fp64."""
+    """The row-resident fp32 Linear (above 2048 rows k_linear_f32q / k_linear_f32t: the wave's rows in
+    registers, W streamed in column slices; up to 2048 rows -- generate()'s per-token steps --
+    k_gemm_f32r with the A slab in LDS, any N; with ln, the LayerNorm before it in the launch) against
+    [layernorm_fwd +] the fp32 GEMM with the same epilogue (store / bias / bias_relu / bias_resid) under
+    the default dispatch and k_gemm_f32 (gemm_variant 98): bitwise equal, and within fp32 rounding of
+    fp64."""
     from replicatinggpt_amd import _lib as L
     lib = L.load()
     torch.manual_seed(45)
@@ -1356,7 +1360,7 @@ def test_linear_rows_f32_matches_gemm(M, N, K, variant, kind, ln):
         L.check(lib.cg_set_tuning(b"linear_rows_nb", nb))
         try:
             o = torch.full((M, N), float("nan"), device=DEV)
-            ops().linear_rows_f32(x, lw if ln else None, lb if ln else None, 1e-5, w, bias, resid, o)
+            ops().linear_rows_f32(x, lw if ln else None, lb if ln else None, 1e-5, w, bias, resid, o, kind == 2)
             torch.cuda.synchronize()
         finally:
             L.check(lib.cg_set_tuning(b"linear_rows_nb", 0))
@@ -1386,6 +1390,8 @@ def test_linear_rows_f32_matches_gemm(M, N, K, variant, kind, ln):
     ref = ad @ w.double().cpu().T
     if kind:
         ref = ref + bias.double().cpu()
+    if kind == 2:
+        ref = torch.relu(ref)
     if kind == 3:
         ref = ref + resid[rows].double().cpu()
     assert relerr(out[rows], ref) < 1e-5
@@ -1561,3 +1567,35 @@ def test_layernorm_fwd_narrow_row_paths_bitwise(C):
         n = y.shape[0]
         assert torch.equal(y, outs[0][0][:n]) and torch.equal(mean, outs[0][1][:n])
         assert torch.equal(rstd, outs[0][2][:n])
+
+
+@pytest.mark.parametrize("B,C,H,Tmax,pos", [(256, 126, 6, 256, 1), (256, 126, 6, 256, 200), (33, 64, 4, 20, 20),
+                                            (1, 6, 2, 4, 3)])
+def test_decode_qkv_f32_matches_ln_linear_and_append(B, C, H, Tmax, pos):
+    """generate()'s per-token ln1 + QKV + K/V append in one launch (k_gemm_f32r with the LayerNorm in its
+    prologue and the cache writes in its epilogue) against layernorm_fwd + gemm + decode_kv_append:
+    qkv and both caches bitwise equal (cache rows other than pos untouched)."""
+    torch.manual_seed(46)
+    D = C // H
+    x = torch.randn(B, C, device=DEV)
+    w = torch.randn(3 * C, C, device=DEV) / C ** 0.5
+    lw = 1.0 + 0.1 * torch.randn(C, device=DEV)
+    lb = 0.1 * torch.randn(C, device=DEV)
+    ln = torch.full((1,), pos, dtype=torch.int64, device=DEV)
+    kc0 = torch.randn(B, H, Tmax, D, device=DEV)
+    vc0 = torch.randn(B, H, Tmax, D, device=DEV)
+    kc, vc = kc0.clone(), vc0.clone()
+    qkv = torch.full((B, 3 * C), float("nan"), device=DEV)
+    ops().decode_qkv_f32(x, lw, lb, 1e-5, w, qkv, ln, kc, vc)
+    a = torch.full((B, C), float("nan"), device=DEV)
+    ops().layernorm_fwd(x, lw, lb, a, torch.empty(B, device=DEV), torch.empty(B, device=DEV), 1e-5)
+    ref = torch.full((B, 3 * C), float("nan"), device=DEV)
+    ops().gemm(a, w, ref, False, False, False, B, 3 * C, C, C, C, 3 * C, 0, None, None, 0, None, 0, 0.0, 0, None, 0,
+               0.0, 1, None)
+    kr, vr = kc0.clone(), vc0.clone()
+    ops().decode_kv_append(ref, C, 2 * C, ln, kr, vr)
+    torch.cuda.synchronize()
+    assert torch.equal(qkv.view(torch.int32), ref.view(torch.int32))
+    assert torch.equal(kc.view(torch.int32), kr.view(torch.int32))
+    assert torch.equal(vc.view(torch.int32), vr.view(torch.int32))
+    assert not torch.equal(kc[:, :, pos - 1], kc0[:, :, pos - 1])
