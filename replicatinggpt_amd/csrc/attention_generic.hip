@@ -323,7 +323,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd_f32mfma(int64_t T_, int H, int
 #define F32RES_EXP(x) expf(x)
 #endif
 template <int DP4>
-__global__ __launch_bounds__(512, 6) void k_attn_fwd_f32res(int64_t T_, int H, int D, const float* __restrict__ q,
+__global__ __launch_bounds__(512, 4) void k_attn_fwd_f32res(int64_t T_, int H, int D, const float* __restrict__ q,
                                                          const float* __restrict__ k, const float* __restrict__ v,
                                                          int64_t ld, float* __restrict__ o, int64_t ldo,
                                                          float* __restrict__ lse, float scale) {
@@ -333,7 +333,7 @@ __global__ __launch_bounds__(512, 6) void k_attn_fwd_f32res(int64_t T_, int H, i
     constexpr int KLD = DP4 + 1, VLD = DP4 + 1;
     __shared__ float Ks[256 * KLD];
     __shared__ float Vs[256 * VLD];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, li = lane & 15;
     const int bh = blockIdx.x, b = bh / H, h = bh % H;
     const float* qb = q + (int64_t)b * T_ * ld + h * D;
@@ -383,13 +383,33 @@ __global__ __launch_bounds__(512, 6) void k_attn_fwd_f32res(int64_t T_, int H, i
             // scores are -inf, their p exact zeros, so their S and O MFMAs and softmax terms change
             // nothing (max with -inf, + 0, MFMA products all 0) -- skipped, the result bitwise the same
             const int nkt = FULL ? 4 : ((int)qw0 + 15 - k0) / 16 + 1 < 4 ? ((int)qw0 + 15 - k0) / 16 + 1 : 4;
+            // operands read one 16-key sub-tile ahead of their MFMAs, unconditionally (rows < 256 of the
+            // staged sequence): K for the S products, then V's first sub-tile under the softmax and
+            // each next one under the current one's O MFMAs -- not one LDS round trip per MFMA
+            auto rdk = [&](float (&kr)[KS], int kt) {
+#pragma unroll
+                for (int t = 0; t < KS; ++t) kr[t] = Kt[(16 * kt + li) * KLD + 4 * t + g];
+            };
+            auto rdv = [&](float (&vr)[4][2], int kt) {
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int et = 0; et < 2; ++et) {
+                        const int e = 16 * et + li;
+                        vr[s][et] = e < DP4 ? Vt[(16 * kt + 4 * g + s) * VLD + e] : 0.f;
+                    }
+            };
             fv4 st[4];
+            float kr[2][KS];
+            rdk(kr[0], 0);
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt) {
+                if (kt < 3) rdk(kr[(kt + 1) & 1], kt + 1);
+                __builtin_amdgcn_sched_barrier(0);
                 fv4 c = {0.f, 0.f, 0.f, 0.f};
                 if (kt < nkt) {
 #pragma unroll
-                    for (int t = 0; t < KS; ++t) c = mfma_f32x4(Kt[(16 * kt + li) * KLD + 4 * t + g], qf[t], c);
+                    for (int t = 0; t < KS; ++t) c = mfma_f32x4(kr[kt & 1][t], qf[t], c);
                 }
                 st[kt] = c;
             }
@@ -426,18 +446,17 @@ __global__ __launch_bounds__(512, 6) void k_attn_fwd_f32res(int64_t T_, int H, i
             m_run = m_new;
             oacc[0] *= alpha;
             oacc[1] *= alpha;
+            float vr[2][4][2];
+            rdv(vr[0], 0);
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt) {
                 if (kt >= nkt) break;
+                if (kt < 3) rdv(vr[(kt + 1) & 1], kt + 1);
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    const int key = 16 * kt + 4 * g + s;
+                for (int s = 0; s < 4; ++s)
 #pragma unroll
-                    for (int et = 0; et < 2; ++et) {
-                        const int e = 16 * et + li;
-                        oacc[et] = mfma_f32x4(e < DP4 ? Vt[key * VLD + e] : 0.f, st[kt][s], oacc[et]);
-                    }
-                }
+                    for (int et = 0; et < 2; ++et) oacc[et] = mfma_f32x4(vr[kt & 1][s][et], st[kt][s], oacc[et]);
             }
         };
         for (int kv = 0; kv < nkv; ++kv) {
