@@ -329,7 +329,7 @@ __global__ __launch_bounds__(512, 4) void k_attn_fwd_f32res(int64_t T_, int H, i
                                                          float* __restrict__ lse, float scale) {
     constexpr int KS = DP4 / 4;
     // V rows hold only the DP4 padded dimensions (the O^T MFMAs' dims DP4..31 read zeros): 51 KB of
-    // LDS at DP4 = 24, three blocks per CU
+    // LDS at DP4 = 24; the operand look-ahead's 93 VGPRs make it two blocks per CU
     constexpr int KLD = DP4 + 1, VLD = DP4 + 1;
     __shared__ float Ks[256 * KLD];
     __shared__ float Vs[256 * VLD];
