@@ -31,6 +31,8 @@ from . import ops
 
 # CHARPT_DECODE_ROWS=0: the per-token LayerNorms in their own launches before ln1/ln2/lnf's Linears (A/B)
 DECODE_ROWS = os.environ.get("CHARPT_DECODE_ROWS", "1") == "1"
+# CHARPT_LAST_KV_SPLIT=0: the window step's last block computes Q for every row too (A/B)
+LAST_KV_SPLIT = os.environ.get("CHARPT_LAST_KV_SPLIT", "1") == "1"
 
 
 class DecodeEngine:
@@ -141,21 +143,29 @@ class DecodeEngine:
         # last block: K/V for every row, everything else for the final row only
         l = self.L - 1
         x2 = x.reshape(B * T, C)
-        qkv = torch.empty((B * T, 3 * C), dtype=self.act, device=self.dev)
         lw, lb = self._b(f"{l}.ln1_w"), self._b(f"{l}.ln1_b")
-        if (self.act == torch.float32 and Fn.ATTN_ROWS and Fn.FFN_LN and B * T > 2048
-                and ops.linear_rows_f32_supported(B * T, 3 * C, C)
-                and ((lw.data_ptr() | lb.data_ptr() | x2.data_ptr()) & 7) == 0):
-            ops.linear_rows_f32(x2, lw, lb, 1e-5, self._w(f"{l}.qkv"), None, None, qkv)   # ln1 inside
-        else:
-            Fn.linear_fwd(self._ln(x2, f"{l}.ln1"), self._w(f"{l}.qkv"), qkv)
-        qkv32 = qkv if qkv.dtype == torch.float32 else qkv.float()
-        qlast = qkv32.view(B, T, 3 * C)[:, T - 1, :]
+        wq = self._w(f"{l}.qkv")   # [3C, C]: Q rows, then K, then V
         o = torch.empty((B, C), dtype=torch.float32, device=self.dev)
-        ld = qkv32.stride(0)
-        ops.decode_attn(qlast, qlast.stride(0), qkv32, C, qkv32, 2 * C, T * ld, D, ld, B, H, D, None, T, self.scale, o)
+        xl = x[:, T - 1, :]        # the final rows in place (row stride T C)
+        if (LAST_KV_SPLIT and self.act == torch.float32 and Fn.ATTN_ROWS and Fn.FFN_LN and B * T > 2048
+                and ops.linear_rows_f32_supported(B * T, 2 * C, C) and C % 2 == 0
+                and ((lw.data_ptr() | lb.data_ptr() | x2.data_ptr() | wq.data_ptr()) & 7) == 0):
+            # ln1 + the K / V columns for every row, ln1 + Q for the final rows only: each value the
+            # same k-ordered chain as in the full QKV product, a third of its MFMAs skipped
+            kv = torch.empty((B * T, 2 * C), dtype=torch.float32, device=self.dev)
+            ops.linear_rows_f32(x2, lw, lb, 1e-5, wq[C:], None, None, kv)
+            q = torch.empty((B, C), dtype=torch.float32, device=self.dev)
+            self._ln_linear(xl, f"{l}.ln1", wq[:C], q)
+            ops.decode_attn(q, q.stride(0), kv, 0, kv, C, T * 2 * C, D, 2 * C, B, H, D, None, T, self.scale, o)
+        else:
+            qkv = torch.empty((B * T, 3 * C), dtype=self.act, device=self.dev)
+            Fn.linear_fwd(self._ln(x2, f"{l}.ln1"), wq, qkv)
+            qkv32 = qkv if qkv.dtype == torch.float32 else qkv.float()
+            qlast = qkv32.view(B, T, 3 * C)[:, T - 1, :]
+            ld = qkv32.stride(0)
+            ops.decode_attn(qlast, qlast.stride(0), qkv32, C, qkv32, 2 * C, T * ld, D, ld, B, H, D, None, T,
+                            self.scale, o)
         o = o if self.act == torch.float32 else o.to(self.act)
-        xl = x[:, T - 1, :].contiguous()
         x3 = torch.empty((B, C), dtype=torch.float32, device=self.dev)
         Fn.linear_fwd(o, self._w(f"{l}.proj_w"), x3, "bias_resid", bias=self._b(f"{l}.proj_b"), resid=xl)
         x4 = self._ffn_tail(l, x3)
