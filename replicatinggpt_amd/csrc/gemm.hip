@@ -1142,7 +1142,7 @@ struct KvHeads {
     int T, H, D;
     float* vout;
 };
-template <bool LN, int EK, bool HM = false>
+template <bool LN, int EK>
 __global__ __launch_bounds__(256, 4) void k_linear_f32q(int64_t M, int C, int N, const float* __restrict__ a,
                                                         int64_t lda, const float* __restrict__ w, int64_t ldw,
                                                         const float* __restrict__ bias, const float* resid,
@@ -1183,17 +1183,6 @@ __global__ __launch_bounds__(256, 4) void k_linear_f32q(int64_t M, int C, int N,
     rows16_b_operand<LN>(xr, &sm[0][0], a, lda, M, C, mw, ln_w, ln_b, eps, lane, wv);
     const int64_t m = mw + li;
     const int64_t mc = m < M ? m : M - 1;   // residual row, clamped (not branched around)
-    // HM: row m's head-major base -- batch m / T, position m % T -- and the per-head stride
-    int hc = 0;
-    float invD = 0.f;
-    int64_t hrow = 0, hstride = 0;
-    if constexpr (HM) {
-        const int64_t bq = mc / kvh.T, tq = mc - bq * kvh.T;
-        hc = kvh.H * kvh.D;
-        invD = 1.0f / (float)kvh.D;
-        hstride = (int64_t)kvh.T * kvh.D;
-        hrow = (bq * kvh.H * kvh.T + tq) * kvh.D;
-    }
     int stc = 0;
 #pragma unroll 1
     for (int c = 0; c < nc; ++c) {
@@ -1247,18 +1236,16 @@ __global__ __launch_bounds__(256, 4) void k_linear_f32q(int64_t M, int C, int N,
                     v0 = rv[j][e].x + v0;
                     v1 = rv[j][e].y + v1;
                 }
-                if constexpr (HM) {
+                if (kvh.D > 0) {   // wave-uniform
                     if (m < M) {
+                        const int64_t bq = m / kvh.T, tq = m - bq * kvh.T, hc = (int64_t)kvh.H * kvh.D;
 #pragma unroll
                         for (int q = 0; q < 2; ++q) {
                             const int nq = n + q;
                             if (nq < N) {
                                 const bool isv = nq >= hc;
-                                const int t = isv ? nq - hc : nq;
-                                // t / D in fp32: t < 2048, D <= 2048, the quotient's fraction >= 1 / (2 D)
-                                // from an integer boundary at t + 0.5 -- far above the rounding error
-                                const int h = (int)(((float)t + 0.5f) * invD), d = t - h * kvh.D;
-                                (isv ? kvh.vout : out)[hrow + (int64_t)h * hstride + d] = q ? v1 : v0;
+                                const int t = isv ? nq - (int)hc : nq, h = t / kvh.D, d = t - h * kvh.D;
+                                (isv ? kvh.vout : out)[((bq * kvh.H + h) * kvh.T + tq) * kvh.D + d] = q ? v1 : v0;
                             }
                         }
                     }
@@ -1919,7 +1906,7 @@ extern "C" int cg_linear_rows_f32_kv(int64_t M, int64_t C, int64_t H, int64_t T,
                                      const float* ln_w, const float* ln_b, float eps, const float* w, int64_t ldw,
                                      float* kout, float* vout, void* stream) {
     CG_REQUIRE(M > 0 && T > 0 && M % T == 0 && H > 0 && C % H == 0 && linear_rows_f32_supported(M, 2 * C, C) &&
-                   2 * C <= 2048 && M * C < ((int64_t)1 << 40),
+                   2 * C <= 2048,
                "cg_linear_rows_f32_kv: unsupported shape M=%lld C=%lld H=%lld T=%lld", (long long)M, (long long)C,
                (long long)H, (long long)T);
     CG_REQUIRE(a && w && kout && vout && ln_w && ln_b, "cg_linear_rows_f32_kv: null pointer");
@@ -1928,7 +1915,7 @@ extern "C" int cg_linear_rows_f32_kv(int64_t M, int64_t C, int64_t H, int64_t T,
     CG_REQUIRE((((uintptr_t)a | (uintptr_t)w | (uintptr_t)ln_w | (uintptr_t)ln_b) & 7) == 0,
                "cg_linear_rows_f32_kv: a, w, ln_w, ln_b must be 8-B aligned");
     const KvHeads kvh{(int)T, (int)H, (int)(C / H), vout};
-    k_linear_f32q<true, CG_EPI_STORE, true><<<dim3((unsigned)((M + 63) / 64)), 256, 0, (hipStream_t)stream>>>(
+    k_linear_f32q<true, CG_EPI_STORE><<<dim3((unsigned)((M + 63) / 64)), 256, 0, (hipStream_t)stream>>>(
         M, (int)C, (int)(2 * C), a, lda, w, ldw, nullptr, nullptr, 0, kout, 2 * C, ln_w, ln_b, eps, kvh);
     CG_LAUNCH_CHECK("cg_linear_rows_f32_kv");
     return CG_OK;
