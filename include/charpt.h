@@ -244,15 +244,6 @@ int cg_linear_rows_f32_supported(int64_t M, int64_t N, int64_t K);
 int cg_linear_rows_f32(int64_t M, int64_t N, int64_t K, const float* a, int64_t lda, const float* ln_w,
                        const float* ln_b, float eps, const float* w, int64_t ldw, const float* bias, int relu,
                        const float* resid, int64_t ldr, float* out, int64_t ldo, void* stream);
-/* The window step's last-block K / V product (generate() past block_size; GPT1.py:111-113,163 for
-   every row of the window), fp32, one launch: [K | V] = LayerNorm(a; ln_w, ln_b, eps) W^T with W the
-   [2C][C] K and V rows of the QKV weight (ldw), a [M][C] dense (M = batches x T), K and V stored
-   head-major, kout / vout [M/T][H][T][C/H] -- bit for bit cg_linear_rows_f32 (with the LayerNorm)
-   then the same values rearranged.  Needs cg_linear_rows_f32_supported(M, 2C, C), M % T == 0,
-   H | C, lda == C, a / W / ln_w / ln_b 8-B aligned; else CG_EINVAL.                             */
-int cg_linear_rows_f32_kv(int64_t M, int64_t C, int64_t H, int64_t T, const float* a, int64_t lda,
-                          const float* ln_w, const float* ln_b, float eps, const float* w, int64_t ldw, float* kout,
-                          float* vout, void* stream);
 /* generate()'s per-token ln1 + QKV product + K/V cache append (GPT1.py:111-113,163 for the newest
    token of each row; the decode engine's phase 1), fp32, one launch: qkv = LayerNorm(x; ln_w, ln_b,
    eps) W^T (x [B][C] (ldx), W [3C][C] (ldw), qkv [B][3C] (ldq)), and columns C..3C-1 of row b also

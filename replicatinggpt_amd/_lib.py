@@ -57,7 +57,6 @@ _SIGS = {
     "cg_gemm_relu_bits_supported": (c_int, [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64]),
     "cg_gemm_rowdot_supported": (c_int, [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64]),
     "cg_linear_rows_f32_supported": (c_int, [c_i64, c_i64, c_i64]),
-    "cg_linear_rows_f32_kv": (c_int, [c_i64, c_i64, c_i64, c_i64, P, c_i64, P, P, c_flt, P, c_i64, P, P, P]),
     "cg_decode_qkv_f32": (c_int, [c_i64, c_i64, c_i64, P, c_i64, P, P, c_flt, P, c_i64, P, c_i64, P, c_i64, P, P, P]),
     "cg_linear_rows_f32": (c_int, [c_i64, c_i64, c_i64, P, c_i64, P, P, c_flt, P, c_i64, P, c_int, P, c_i64, P, c_i64, P]),
     "cg_ffn_fwd_f32_supported": (c_int, [c_i64, c_i64, c_i64]),

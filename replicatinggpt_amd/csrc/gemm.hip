@@ -1135,21 +1135,13 @@ __device__ __forceinline__ void rows16_b_operand(float (&xr)[32], float* ring, c
 // where asked) and come back as the B operand xr[t] = a'[row li][4t + g] (lane li + 16 g).  D[j] holds
 // output columns 32 c + 16 j + 4 g + r of row li: one float4 of consecutive columns per tile.  Same
 // k-ordered fma chain over ceil16(K) and epilogue as k_gemm_f32: bitwise.
-// KvHeads (D > 0; the window step's last-block K / V product, N = 2 C): columns n < C are K, the rest
-// V, each stored head-major -- [rows / T][H][T][D] at kout / vout -- the K/V cache layout the per-token
-// attention reads with float4 chunks (cg_decode_attn's coalesced-row kernel) instead of row-strided dwords.
-struct KvHeads {
-    int T, H, D;
-    float* vout;
-};
 template <bool LN, int EK>
 __global__ __launch_bounds__(256, 4) void k_linear_f32q(int64_t M, int C, int N, const float* __restrict__ a,
                                                         int64_t lda, const float* __restrict__ w, int64_t ldw,
                                                         const float* __restrict__ bias, const float* resid,
                                                         int64_t ldr, float* out, int64_t ldo,
                                                         const float* __restrict__ ln_w,
-                                                        const float* __restrict__ ln_b, float eps,
-                                                        KvHeads kvh = KvHeads{}) {
+                                                        const float* __restrict__ ln_b, float eps) {
     __shared__ __attribute__((aligned(16))) float sm[2][FFN_STAGE];   // W slices [128 k][32 + 1]
     constexpr bool BIAS = EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_BIAS_RESID;
     const bool hb = BIAS && bias, hr = EK == CG_EPI_BIAS_RESID && resid;
@@ -1236,22 +1228,7 @@ __global__ __launch_bounds__(256, 4) void k_linear_f32q(int64_t M, int C, int N,
                     v0 = rv[j][e].x + v0;
                     v1 = rv[j][e].y + v1;
                 }
-                if (kvh.D > 0) {   // wave-uniform
-                    if (m < M) {
-                        const int64_t bq = m / kvh.T, tq = m - bq * kvh.T, hc = (int64_t)kvh.H * kvh.D;
-#pragma unroll
-                        for (int q = 0; q < 2; ++q) {
-                            const int nq = n + q;
-                            if (nq < N) {
-                                const bool isv = nq >= hc;
-                                const int t = isv ? nq - (int)hc : nq, h = t / kvh.D, d = t - h * kvh.D;
-                                (isv ? kvh.vout : out)[((bq * kvh.H + h) * kvh.T + tq) * kvh.D + d] = q ? v1 : v0;
-                            }
-                        }
-                    }
-                } else if (m < M && n < N) {
-                    *(float2*)(out + m * ldo + n) = make_float2(v0, v1);
-                }
+                if (m < M && n < N) *(float2*)(out + m * ldo + n) = make_float2(v0, v1);
             }
     }
 }
@@ -1899,25 +1876,6 @@ extern "C" int cg_linear_rows_f32(int64_t M, int64_t N, int64_t K, const float* 
     }
 #undef KL
     CG_LAUNCH_CHECK("cg_linear_rows_f32");
-    return CG_OK;
-}
-
-extern "C" int cg_linear_rows_f32_kv(int64_t M, int64_t C, int64_t H, int64_t T, const float* a, int64_t lda,
-                                     const float* ln_w, const float* ln_b, float eps, const float* w, int64_t ldw,
-                                     float* kout, float* vout, void* stream) {
-    CG_REQUIRE(M > 0 && T > 0 && M % T == 0 && H > 0 && C % H == 0 && linear_rows_f32_supported(M, 2 * C, C) &&
-                   2 * C <= 2048,
-               "cg_linear_rows_f32_kv: unsupported shape M=%lld C=%lld H=%lld T=%lld", (long long)M, (long long)C,
-               (long long)H, (long long)T);
-    CG_REQUIRE(a && w && kout && vout && ln_w && ln_b, "cg_linear_rows_f32_kv: null pointer");
-    CG_REQUIRE(lda == C && C % 2 == 0 && ldw >= C && ldw % 2 == 0 && 2 * C * ldw < ((int64_t)1 << 31),
-               "cg_linear_rows_f32_kv: bad leading dimensions");
-    CG_REQUIRE((((uintptr_t)a | (uintptr_t)w | (uintptr_t)ln_w | (uintptr_t)ln_b) & 7) == 0,
-               "cg_linear_rows_f32_kv: a, w, ln_w, ln_b must be 8-B aligned");
-    const KvHeads kvh{(int)T, (int)H, (int)(C / H), vout};
-    k_linear_f32q<true, CG_EPI_STORE><<<dim3((unsigned)((M + 63) / 64)), 256, 0, (hipStream_t)stream>>>(
-        M, (int)C, (int)(2 * C), a, lda, w, ldw, nullptr, nullptr, 0, kout, 2 * C, ln_w, ln_b, eps, kvh);
-    CG_LAUNCH_CHECK("cg_linear_rows_f32_kv");
     return CG_OK;
 }
 

@@ -33,8 +33,6 @@ from . import ops
 DECODE_ROWS = os.environ.get("CHARPT_DECODE_ROWS", "1") == "1"
 # CHARPT_LAST_KV_SPLIT=0: the window step's last block computes Q for every row too (A/B)
 LAST_KV_SPLIT = os.environ.get("CHARPT_LAST_KV_SPLIT", "1") == "1"
-# CHARPT_LAST_KV_HEADS=0: that K / V product row-major (the attention then reads row-strided dwords) (A/B)
-LAST_KV_HEADS = os.environ.get("CHARPT_LAST_KV_HEADS", "1") == "1"
 
 
 class DecodeEngine:
@@ -154,19 +152,11 @@ class DecodeEngine:
                 and ((lw.data_ptr() | lb.data_ptr() | x2.data_ptr() | wq.data_ptr()) & 7) == 0):
             # ln1 + the K / V columns for every row, ln1 + Q for the final rows only: each value the
             # same k-ordered chain as in the full QKV product, a third of its MFMAs skipped
+            kv = torch.empty((B * T, 2 * C), dtype=torch.float32, device=self.dev)
+            ops.linear_rows_f32(x2, lw, lb, 1e-5, wq[C:], None, None, kv)
             q = torch.empty((B, C), dtype=torch.float32, device=self.dev)
             self._ln_linear(xl, f"{l}.ln1", wq[:C], q)
-            if LAST_KV_HEADS and x2.stride(0) == C:
-                # K and V written head-major ([B, H, T, D], the phase-1 cache layout): the attention
-                # reads 64-key chunks as float4s
-                kh = torch.empty((B, H, T, D), dtype=torch.float32, device=self.dev)
-                vh = torch.empty_like(kh)
-                ops.linear_rows_f32_kv(x2, lw, lb, 1e-5, wq[C:], kh, vh)
-                ops.decode_attn(q, q.stride(0), kh, 0, vh, 0, H * T * D, T * D, D, B, H, D, None, T, self.scale, o)
-            else:
-                kv = torch.empty((B * T, 2 * C), dtype=torch.float32, device=self.dev)
-                ops.linear_rows_f32(x2, lw, lb, 1e-5, wq[C:], None, None, kv)
-                ops.decode_attn(q, q.stride(0), kv, 0, kv, C, T * 2 * C, D, 2 * C, B, H, D, None, T, self.scale, o)
+            ops.decode_attn(q, q.stride(0), kv, 0, kv, C, T * 2 * C, D, 2 * C, B, H, D, None, T, self.scale, o)
         else:
             qkv = torch.empty((B * T, 3 * C), dtype=self.act, device=self.dev)
             Fn.linear_fwd(self._ln(x2, f"{l}.ln1"), wq, qkv)

@@ -444,25 +444,6 @@ def decode_kv_append(qkv: Tensor, k_off: int, v_off: int, len_dev: Tensor, kcach
                                          L.ptr(kcache), L.ptr(vcache), _s(qkv)), "decode_kv_append")
 
 
-@_op("linear_rows_f32_kv", ("kout", "vout"))
-def linear_rows_f32_kv(a: Tensor, ln_w: Tensor, ln_b: Tensor, eps: float, w: Tensor, kout: Tensor,
-                       vout: Tensor) -> None:
-    """[K | V] = LayerNorm(a) @ w^T (w: the [2C, C] K and V rows of a QKV weight), K and V stored head-major
-    into kout / vout [M / T, H, T, C / H], fp32, one launch -- the values of linear_rows_f32(a, ln_w, ln_b,
-    eps, w, None, None, kv) rearranged."""
-    M, C = a.shape
-    Bq, H, T, D = kout.shape
-    for t, name in ((a, "a"), (w, "w"), (kout, "kout"), (vout, "vout"), (ln_w, "ln_w"), (ln_b, "ln_b")):
-        if t.dtype != torch.float32 or not t.is_cuda or t.stride(-1) != 1:
-            raise ValueError(f"linear_rows_f32_kv: {name} must be a float32 device tensor with unit column stride")
-    if tuple(w.shape) != (2 * C, C) or Bq * T != M or H * D != C or not kout.is_contiguous() or \
-            tuple(vout.shape) != tuple(kout.shape) or not vout.is_contiguous():
-        raise ValueError(f"linear_rows_f32_kv: shapes a {tuple(a.shape)} w {tuple(w.shape)} kout {tuple(kout.shape)}")
-    L.check(L.load().cg_linear_rows_f32_kv(M, C, H, T, L.ptr(a), a.stride(0), L.ptr(ln_w), L.ptr(ln_b), eps,
-                                           L.ptr(w), w.stride(0), L.ptr(kout), L.ptr(vout), _s(a)),
-            "linear_rows_f32_kv")
-
-
 @_op("decode_qkv_f32", ("qkv", "kcache", "vcache"))
 def decode_qkv_f32(x: Tensor, ln_w: Tensor, ln_b: Tensor, eps: float, w: Tensor, qkv: Tensor, len_dev: Tensor,
                    kcache: Tensor, vcache: Tensor) -> None:

@@ -1599,36 +1599,3 @@ def test_decode_qkv_f32_matches_ln_linear_and_append(B, C, H, Tmax, pos):
     assert torch.equal(kc.view(torch.int32), kr.view(torch.int32))
     assert torch.equal(vc.view(torch.int32), vr.view(torch.int32))
     assert not torch.equal(kc[:, :, pos - 1], kc0[:, :, pos - 1])
-
-
-@pytest.mark.parametrize("Bq,T,C,H", [(256, 256, 126, 6), (3, 100, 64, 4), (9, 256, 6, 2)])
-def test_linear_rows_f32_kv_head_major(Bq, T, C, H):
-    """The window step's last-block K / V product written head-major (k_linear_f32q's KvHeads stores)
-    against linear_rows_f32 into [M, 2C] rearranged: bitwise; and the per-token attention over the
-    head-major K / V (the coalesced-row kernel) against the row-strided read of the [M, 2C] buffer
-    (the dword kernel): bitwise."""
-    torch.manual_seed(47)
-    M, D = Bq * T, C // H
-    x = torch.randn(M, C, device=DEV)
-    w = torch.randn(2 * C, C, device=DEV) / C ** 0.5
-    lw = 1.0 + 0.1 * torch.randn(C, device=DEV)
-    lb = 0.1 * torch.randn(C, device=DEV)
-    kh = torch.full((Bq, H, T, D), float("nan"), device=DEV)
-    vh = torch.full((Bq, H, T, D), float("nan"), device=DEV)
-    ops().linear_rows_f32_kv(x, lw, lb, 1e-5, w, kh, vh)
-    kv = torch.full((M, 2 * C), float("nan"), device=DEV)
-    ops().linear_rows_f32(x, lw, lb, 1e-5, w, None, None, kv)
-    torch.cuda.synchronize()
-    kr = kv[:, :C].reshape(Bq, T, H, D).permute(0, 2, 1, 3).contiguous()
-    vr = kv[:, C:].reshape(Bq, T, H, D).permute(0, 2, 1, 3).contiguous()
-    assert torch.equal(kh.view(torch.int32), kr.view(torch.int32))
-    assert torch.equal(vh.view(torch.int32), vr.view(torch.int32))
-    if D <= 24:
-        q = torch.randn(Bq, C, device=DEV)
-        o1 = torch.full((Bq, C), float("nan"), device=DEV)
-        o2 = torch.full((Bq, C), float("nan"), device=DEV)
-        scale = D ** -0.5
-        ops().decode_attn(q, C, kh, 0, vh, 0, H * T * D, T * D, D, Bq, H, D, None, T, scale, o1)
-        ops().decode_attn(q, C, kv, 0, kv, C, T * 2 * C, D, 2 * C, Bq, H, D, None, T, scale, o2)
-        torch.cuda.synchronize()
-        assert torch.equal(o1.view(torch.int32), o2.view(torch.int32))
