@@ -1,6 +1,6 @@
 """Per-phase kernel breakdown of a generate() kernel trace (rocprofv3 --kernel-trace csv of
 tools/f32_fwd_ab.py gen, which runs generate twice): the LAST generate, split at its first window
-(k_ffn_f32) launch into phase 1 (per-token decode against the K/V caches) and phase 2 (window steps).
+window launch (k_decode_window) into phase 1 (per-token steps against the K/V caches) and phase 2.
 usage: python tools/gen_trace_phases.py <kernel_trace.csv> [top]"""
 import collections
 import csv
@@ -9,15 +9,15 @@ import sys
 
 def main(path, top=14):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    st = [int(r["Start_Timestamp"]) for r in rows]
-    en = [int(r["End_Timestamp"]) for r in rows]
-    # generate boundaries: gaps > 20 ms between kernels
-    cuts = [0] + [i for i in range(1, len(rows)) if st[i] - en[i - 1] > 20e6] + [len(rows)]
-    segs = [(cuts[i], cuts[i + 1]) for i in range(len(cuts) - 1)]
-    a, b = [s for s in segs if s[1] - s[0] > 1000][-1]   # the last generate (> 1000 launches)
-    g = rows[a:b]
-    first_win = next((i for i, r in enumerate(g) if "k_ffn_f32" in r["Kernel_Name"]), len(g))
-    for name, rs in (("phase 1 (decode)", g[:first_win]), ("phase 2 (window)", g[first_win:])):
+    emb = [i for i, r in enumerate(rows) if "k_decode_embed" in r["Kernel_Name"]]
+    # the last generate: its 256 phase-1 steps each start with k_decode_embed (phase 2: k_decode_window)
+    p1 = emb[-256] if len(emb) >= 256 else (emb[0] if emb else 0)
+    win = [i for i, r in enumerate(rows) if "k_decode_window" in r["Kernel_Name"] and i > p1]
+    p2 = win[0] if win else len(rows)
+    cnt = [i for i, r in enumerate(rows) if "k_counter_add" in r["Kernel_Name"]]
+    end = cnt[-1] + 1 if cnt else len(rows)
+    g1, g2 = rows[p1:p2], rows[p2:end]
+    for name, rs in (("phase 1 (per-token steps)", g1), ("phase 2 (window steps)", g2)):
         if not rs:
             continue
         span = (int(rs[-1]["End_Timestamp"]) - int(rs[0]["Start_Timestamp"])) / 1e6
