@@ -335,7 +335,13 @@ __global__ __launch_bounds__(512, 4) void k_attn_fwd_f32res(int64_t T_, int H, i
     __shared__ float Vs[256 * VLD];
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, li = lane & 15;
-    const int bh = blockIdx.x, b = bh / H, h = bh % H;
+    // XCD-contiguous (b, h): the dispatcher deals block i to XCD i % 8, so XCD x runs the x-th eighth of
+    // the (b, h) range in order and a sequence's heads share its L2 -- each head reads 84 of a row's
+    // 1512 B, so with the heads spread over 6 XCDs every row's lines came from HBM ~6 times (234 MB read
+    // per launch against the 99 MB of q / k / v)
+    const int nblk = (int)gridDim.x, id = (int)blockIdx.x, qb = nblk >> 3, rb = nblk & 7, xcd = id & 7;
+    const int bh = (xcd < rb ? xcd * (qb + 1) : rb * (qb + 1) + (xcd - rb) * qb) + (id >> 3);
+    const int b = bh / H, h = bh % H;
     const float* qb = q + (int64_t)b * T_ * ld + h * D;
     const float* kb = k + (int64_t)b * T_ * ld + h * D;
     const float* vb = v + (int64_t)b * T_ * ld + h * D;
