@@ -339,8 +339,8 @@ __global__ __launch_bounds__(512, 4) void k_attn_fwd_f32res(int64_t T_, int H, i
     // the (b, h) range in order and a sequence's heads share its L2 -- each head reads 84 of a row's
     // 1512 B, so with the heads spread over 6 XCDs every row's lines came from HBM ~6 times (234 MB read
     // per launch against the 99 MB of q / k / v)
-    const int nblk = (int)gridDim.x, id = (int)blockIdx.x, qb = nblk >> 3, rb = nblk & 7, xcd = id & 7;
-    const int bh = (xcd < rb ? xcd * (qb + 1) : rb * (qb + 1) + (xcd - rb) * qb) + (id >> 3);
+    const int nblk = (int)gridDim.x, id = (int)blockIdx.x, nq = nblk >> 3, nr = nblk & 7, xcd = id & 7;
+    const int bh = (xcd < nr ? xcd * (nq + 1) : nr * (nq + 1) + (xcd - nr) * nq) + (id >> 3);
     const int b = bh / H, h = bh % H;
     const float* qb = q + (int64_t)b * T_ * ld + h * D;
     const float* kb = k + (int64_t)b * T_ * ld + h * D;
