@@ -144,7 +144,10 @@ __global__ __launch_bounds__(64) void k_decode_attn_rows(const float* __restrict
     const float* ks = (const float*)ks4;
     const float* vs = (const float*)vs4;
     const int lane = threadIdx.x;
-    const int64_t bh = blockIdx.x;
+    // XCD-contiguous (b, h) (block i runs on XCD i % 8): a sequence's heads share one L2 -- with the
+    // window's row-strided K / V (SJ) each head reads 84 B of every 1 KB row
+    const int nblk = (int)gridDim.x, id = (int)blockIdx.x, nq = nblk >> 3, nr = nblk & 7, xcd = id & 7;
+    const int64_t bh = (xcd < nr ? xcd * (nq + 1) : nr * (nq + 1) + (xcd - nr) * nq) + (id >> 3);
     const int64_t b = bh / H, h = bh % H;
     const int64_t n = len_dev ? *len_dev : nfix;  // keys 0..n-1
     const float4* K4 = (const float4*)(kc + b * sb + h * sh);
