@@ -5,7 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD
 mkdir -p gpurun_out/pmcx
-timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_model.py -x -q --timeout 200 --timeout-method thread -k "fp32 or generate or decode" > gpurun_out/xcd_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/xcd_tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_model.py -x -q --timeout 200 --timeout-method thread -k "fp32 or generate or decode or decode_attn" > gpurun_out/xcd_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/xcd_tests.log; exit 1; }
 : > gpurun_out/xcd_ab.txt
 for r in 1 2 3; do for l in base cur; do
   if [ $l = cur ]; then unset CHARPT_LIB; else export CHARPT_LIB=$R/replicatinggpt_amd/libcharpt_hip_$l.so; fi
