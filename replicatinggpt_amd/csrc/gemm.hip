@@ -487,10 +487,11 @@ __global__ __launch_bounds__(256, 1) void k_gemm_f32r(int64_t M, int64_t N, int6
         if (hr) v = ((m < M && n < N) ? rv[r] : 0.f) + v;
         if (m < M && n < N) C[m * ldc + n] = v;
         if constexpr (KV) {
-            if (m < M && n < N && n >= kva.C) {
+            const int64_t pos = *kva.len - 1;   // a position outside the cache writes nothing
+            if (m < M && n < N && n >= kva.C && pos >= 0 && pos < kva.Tmax) {
                 const bool isv = n >= 2 * kva.C;
                 const int64_t t = n - (isv ? 2 * kva.C : kva.C), h = t / kva.D, e = t - h * kva.D;
-                (isv ? kva.vc : kva.kc)[((m * kva.H + h) * kva.Tmax + (*kva.len - 1)) * kva.D + e] = v;
+                (isv ? kva.vc : kva.kc)[((m * kva.H + h) * kva.Tmax + pos) * kva.D + e] = v;
             }
         }
     }
