@@ -138,10 +138,6 @@ int cg_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, void* stream);
 /* x[b,t] = data[ix[b]+t], y[b,t] = data[ix[b]+t+1]; data is the token stream (int64 or uint8) */
 int cg_gather_batch(const void* data, int data_is_u8, const int64_t* ix, int64_t* x, int64_t* y,
                     int64_t B, int64_t T, void* stream);
-/* the same with ix a HOST array of B <= 256 offsets, copied into the launch's kernel arguments (no
-   device staging buffer or H2D copy; ix may be reused as soon as the call returns)                  */
-int cg_gather_batch_host(const void* data, int data_is_u8, const int64_t* ix_host, int64_t* x, int64_t* y,
-                         int64_t B, int64_t T, void* stream);
 
 /* ---- embeddings (GPT1.py:179-181) ------------------------------------------------------ */
 /* x[b,t,:] = wte[idx[b,t],:] + wpe[t,:]  (fp32)                                          */

@@ -40,7 +40,6 @@ _SIGS = {
     "cg_sum_f32": (c_int, [P, c_i64, c_flt, P, P, P]),
     "cg_cast_f32_bf16": (c_int, [P, P, c_i64, P]),
     "cg_gather_batch": (c_int, [P, c_int, P, P, P, c_i64, c_i64, P]),
-    "cg_gather_batch_host": (c_int, [P, c_int, P, P, P, c_i64, c_i64, P]),
     "cg_embed_fwd": (c_int, [P, P, P, P, c_i64, c_i64, c_i64, c_i64, P]),
     "cg_embed_bwd_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
     "cg_embed_bwd": (c_int, [P, P, P, P, c_i64, c_i64, c_i64, c_i64, c_int, P, P]),

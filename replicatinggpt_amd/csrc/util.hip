@@ -349,38 +349,6 @@ __global__ void k_gather_batch(const D* data, const int64_t* ix, int64_t* x, int
     }
 }
 
-// The same windows with the B <= 256 offsets passed by value in the kernel arguments (the launch carries
-// them): get_batch's per-step offsets, drawn on the host, need no pinned staging buffer, H2D copy
-// (a runtime blit kernel and its dispatch gaps: ~15 us of idle per C2 step) or stream event.
-struct GatherIx {
-    int64_t ix[256];
-};
-template <typename D>
-__global__ void k_gather_batch_args(const D* data, GatherIx a, int64_t* x, int64_t* y, int64_t B, int64_t T) {
-    const int64_t b = blockIdx.y;
-    const int64_t base = a.ix[b];
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < T; t += (int64_t)gridDim.x * blockDim.x) {
-        x[b * T + t] = (int64_t)data[base + t];
-        y[b * T + t] = (int64_t)data[base + t + 1];
-    }
-}
-
-extern "C" int cg_gather_batch_host(const void* data, int data_is_u8, const int64_t* ix_host, int64_t* x, int64_t* y,
-                                    int64_t B, int64_t T, void* stream) {
-    CG_REQUIRE(B > 0 && B <= 256 && T > 0, "cg_gather_batch_host: needs 0 < B <= 256 (got %lld)", (long long)B);
-    CG_REQUIRE(data && ix_host && x && y, "cg_gather_batch_host: null pointer");
-    GatherIx a;
-    for (int64_t b = 0; b < B; ++b) a.ix[b] = ix_host[b];
-    for (int64_t b = B; b < 256; ++b) a.ix[b] = 0;
-    dim3 grid(ceil_div(T, 256), (unsigned)B);
-    if (data_is_u8)
-        k_gather_batch_args<uint8_t><<<grid, 256, 0, (hipStream_t)stream>>>((const uint8_t*)data, a, x, y, B, T);
-    else
-        k_gather_batch_args<int64_t><<<grid, 256, 0, (hipStream_t)stream>>>((const int64_t*)data, a, x, y, B, T);
-    CG_LAUNCH_CHECK("cg_gather_batch_host");
-    return CG_OK;
-}
-
 extern "C" int cg_gather_batch(const void* data, int data_is_u8, const int64_t* ix, int64_t* x, int64_t* y,
                                int64_t B, int64_t T, void* stream) {
     CG_REQUIRE(B > 0 && T > 0 && B < 65536, "cg_gather_batch: bad shape");

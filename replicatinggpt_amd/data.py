@@ -16,9 +16,6 @@ import os
 
 import torch
 
-# CHARPT_GATHER_ARGS=0: get_batch stages the offsets through a pinned ring and an H2D copy (A/B)
-GATHER_ARGS = os.environ.get("CHARPT_GATHER_ARGS", "1") == "1"
-
 from . import ops
 
 DEFAULT_INPUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data", "input.txt")
@@ -107,15 +104,6 @@ class BatchSampler:
         ix = self.draw_ix(split)
         data = self.s.train_dev if split == "train" else self.s.val_dev
         dev = data.device
-        if GATHER_ARGS and dev.type == "cuda" and self.B <= 256:
-            # the offsets travel in the gather launch's kernel arguments: no staging copy
-            if out is None:
-                x = torch.empty((self.B, self.T), dtype=torch.int64, device=dev)
-                y = torch.empty((self.B, self.T), dtype=torch.int64, device=dev)
-            else:
-                x, y = out
-            ops.gather_batch_host(data, ix.contiguous(), x, y)
-            return x, y
         i, buf = self._staging(dev)
         buf.copy_(ix)
         ix_dev = buf.to(dev, non_blocking=True)

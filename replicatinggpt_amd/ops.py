@@ -58,16 +58,6 @@ def cast_bf16(x: Tensor, out: Tensor) -> None:
     L.check(L.load().cg_cast_f32_bf16(L.ptr(x), L.ptr(out), x.numel(), _s(x)), "cast_f32_bf16")
 
 
-def gather_batch_host(data: Tensor, ix: Tensor, x: Tensor, y: Tensor) -> None:
-    """gather_batch with ix a contiguous int64 CPU tensor of B <= 256 offsets, passed in the launch's
-    kernel arguments (data loading only: not a traced op)."""
-    B, T = x.shape
-    if ix.device.type != "cpu" or ix.dtype != torch.int64 or not ix.is_contiguous() or ix.numel() != B:
-        raise ValueError("gather_batch_host: ix must be a contiguous int64 CPU tensor of B offsets")
-    L.check(L.load().cg_gather_batch_host(L.ptr(data), int(data.dtype == torch.uint8), ix.data_ptr(), L.ptr(x),
-                                          L.ptr(y), B, T, _s(x)), "gather_batch_host")
-
-
 @_op("gather_batch", ("x", "y"))
 def gather_batch(data: Tensor, ix: Tensor, x: Tensor, y: Tensor) -> None:
     B, T = x.shape

@@ -1599,24 +1599,3 @@ def test_decode_qkv_f32_matches_ln_linear_and_append(B, C, H, Tmax, pos):
     assert torch.equal(kc.view(torch.int32), kr.view(torch.int32))
     assert torch.equal(vc.view(torch.int32), vr.view(torch.int32))
     assert not torch.equal(kc[:, :, pos - 1], kc0[:, :, pos - 1])
-
-
-@pytest.mark.parametrize("u8,B,T", [(True, 64, 256), (False, 5, 100), (True, 256, 17), (False, 1, 1)])
-def test_gather_batch_host_offsets_match_device_offsets(u8, B, T):
-    """get_batch's gather with the offsets in the kernel arguments (cg_gather_batch_host) against the
-    device-offset kernel and CPU indexing (GPT1.py:79-80): bit-exact."""
-    torch.manual_seed(48)
-    n = 5000
-    data = torch.randint(65, (n,), dtype=torch.uint8 if u8 else torch.int64)
-    ix = torch.randint(n - T - 1, (B,))
-    dd = data.to(DEV)
-    x1 = torch.full((B, T), -1, dtype=torch.int64, device=DEV)
-    y1 = torch.full((B, T), -1, dtype=torch.int64, device=DEV)
-    x2, y2 = x1.clone(), y1.clone()
-    ops().gather_batch_host(dd, ix, x1, y1)
-    ops().gather_batch(dd, ix.to(DEV), x2, y2)
-    torch.cuda.synchronize()
-    xr = torch.stack([data[i:i + T] for i in ix.tolist()]).long()
-    yr = torch.stack([data[i + 1:i + T + 1] for i in ix.tolist()]).long()
-    assert torch.equal(x1.cpu(), xr) and torch.equal(y1.cpu(), yr)
-    assert torch.equal(x1, x2) and torch.equal(y1, y2)
