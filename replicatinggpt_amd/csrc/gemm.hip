@@ -1682,7 +1682,7 @@ extern "C" int cg_set_tuning(const char* key, int value) {
         return CG_OK;
     }
     if (!strcmp(key, "linear_rows_nb")) {
-        CG_REQUIRE(value >= 0 && value <= 3, "cg_set_tuning: linear_rows_nb must be 0 (16-row waves), 1, 2 or 3");
+        CG_REQUIRE(value >= 0 && value <= 2, "cg_set_tuning: linear_rows_nb must be 0 (16-row waves), 1 or 2");
         g_linear_rows_nb = value;
         return CG_OK;
     }
