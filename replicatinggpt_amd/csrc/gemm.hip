@@ -1136,49 +1136,44 @@ __device__ __forceinline__ void rows16_b_operand(float (&xr)[32], float* ring, c
 // where asked) and come back as the B operand xr[t] = a'[row li][4t + g] (lane li + 16 g).  D[j] holds
 // output columns 32 c + 16 j + 4 g + r of row li: one float4 of consecutive columns per tile.  Same
 // k-ordered fma chain over ceil16(K) and epilogue as k_gemm_f32: bitwise.
-// NW = 8 (cg_set_tuning "linear_rows_nb" 3): 128-row workgroups of 8 waves, two per CU -- each W slice
-// staged once per 128 rows instead of 64 (A/B)
-template <bool LN, int EK, int NW = 4>
-__global__ __launch_bounds__(64 * NW, NW == 4 ? 4 : 2) void k_linear_f32q(int64_t M, int C, int N, const float* __restrict__ a,
+template <bool LN, int EK>
+__global__ __launch_bounds__(256, 4) void k_linear_f32q(int64_t M, int C, int N, const float* __restrict__ a,
                                                         int64_t lda, const float* __restrict__ w, int64_t ldw,
                                                         const float* __restrict__ bias, const float* resid,
                                                         int64_t ldr, float* out, int64_t ldo,
                                                         const float* __restrict__ ln_w,
                                                         const float* __restrict__ ln_b, float eps) {
-    // W slices [128 k][32 + 1] x 2 stages; the rows' LayerNorm scratch (NW x 16 x 130) shares it
-    constexpr int SMF = 2 * FFN_STAGE > NW * 16 * 130 ? 2 * FFN_STAGE : NW * 16 * 130;
-    constexpr int RPT = 32 / NW;   // W rows per thread per slice
-    __shared__ __attribute__((aligned(16))) float smem[SMF];
+    __shared__ __attribute__((aligned(16))) float sm[2][FFN_STAGE];   // W slices [128 k][32 + 1]
     constexpr bool BIAS = EK == CG_EPI_BIAS || EK == CG_EPI_BIAS_RELU || EK == CG_EPI_BIAS_RESID;
     const bool hb = BIAS && bias, hr = EK == CG_EPI_BIAS_RESID && resid;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, li = lane & 15, g = lane >> 4;
-    const int64_t mw = (int64_t)blockIdx.x * (16 * NW) + 16 * wv;   // the wave's first row
+    const int64_t mw = (int64_t)blockIdx.x * 64 + 16 * wv;   // the wave's first row
     const int nk4 = (C + 15) / 16 * 4;                         // k4-steps over ceil16(K) (<= 32)
     const int nc = (N + 31) / 32;
-    float2 ra[RPT];
+    float2 ra[8];
     bool rk = true;
     auto load = [&](int c) {
         const int k = 2 * (tid & 63), r0 = 32 * c + (tid >> 6);
         rk = k < C;
         const int kc = rk ? k : C - 2;
 #pragma unroll
-        for (int i = 0; i < RPT; ++i) {   // cg_linear_rows_f32 checks: rows * ldw under 2^31
-            const int r = r0 + NW * i < N ? r0 + NW * i : N - 1;
+        for (int i = 0; i < 8; ++i) {   // cg_linear_rows_f32 checks: rows * ldw under 2^31
+            const int r = r0 + 4 * i < N ? r0 + 4 * i : N - 1;
             ra[i] = *(const float2*)(w + (uint32_t)(r * (int)ldw + kc));
         }
     };
     auto store = [&](int st) {
-        float* S = smem + st * FFN_STAGE;
+        float* S = sm[st];
         const int kk = 2 * (tid & 63), r0 = tid >> 6;
 #pragma unroll
-        for (int i = 0; i < RPT; ++i) {
-            S[kk * FFN_LD1 + r0 + NW * i] = rk ? ra[i].x : 0.f;
-            S[(kk + 1) * FFN_LD1 + r0 + NW * i] = rk ? ra[i].y : 0.f;
+        for (int i = 0; i < 8; ++i) {
+            S[kk * FFN_LD1 + r0 + 4 * i] = rk ? ra[i].x : 0.f;
+            S[(kk + 1) * FFN_LD1 + r0 + 4 * i] = rk ? ra[i].y : 0.f;
         }
     };
     load(0);
     float xr[32];
-    rows16_b_operand<LN>(xr, smem, a, lda, M, C, mw, ln_w, ln_b, eps, lane, wv);
+    rows16_b_operand<LN>(xr, &sm[0][0], a, lda, M, C, mw, ln_w, ln_b, eps, lane, wv);
     const int64_t m = mw + li;
     const int64_t mc = m < M ? m : M - 1;   // residual row, clamped (not branched around)
     int stc = 0;
@@ -1200,7 +1195,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 4 : 2) void k_linear_f32q(int64_
                 if (hb) bv[j][e] = make_float2(bias[nn], bias[nn + 1]);
             }
         fv4 D[2] = {fv4{0.f, 0.f, 0.f, 0.f}, fv4{0.f, 0.f, 0.f, 0.f}};
-        const float* S = smem + st * FFN_STAGE + g * FFN_LD1 + li;
+        const float* S = sm[st] + g * FFN_LD1 + li;
 #pragma unroll
         for (int b = 0; b < 8; ++b) {   // 4 k4-steps per fragment batch
             if (4 * b >= nk4) break;
@@ -1862,9 +1857,6 @@ extern "C" int cg_linear_rows_f32(int64_t M, int64_t N, int64_t K, const float* 
     do {                                                                                                          \
         if (g_linear_rows_nb == 0)                                                                                \
             k_linear_f32q<LN_, EK_><<<dim3((unsigned)((M + 63) / 64)), 256, 0, st>>>(                             \
-                M, (int)K, (int)N, a, lda, w, ldw, bias, resid, ldr, out, ldo, ln_w, ln_b, eps);                  \
-        else if (g_linear_rows_nb == 3)                                                                           \
-            k_linear_f32q<LN_, EK_, 8><<<dim3((unsigned)((M + 127) / 128)), 512, 0, st>>>(                        \
                 M, (int)K, (int)N, a, lda, w, ldw, bias, resid, ldr, out, ldo, ln_w, ln_b, eps);                  \
         else if (g_linear_rows_nb == 1)                                                                           \
             k_linear_f32t<LN_, EK_, 1><<<grid, 256, 0, st>>>(M, (int)K, (int)N, a, lda, w, ldw, bias, resid, ldr, \
